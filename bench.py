@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): RAG queries/sec + p50 TTFT with
+Qwen2-7B over a 10M-vector index, plus ingest docs/sec.
+
+Config (BASELINE config 3): Qwen2-7B TP=1 per GPU + bge-large-en-v1.5 encoder,
+10M x 1024-d IVF index sharded data-parallel over the N GPUs, per-shard top-k
+merged with one RCCL all-gather over xGMI.  Weights are random-init of the
+real architectures; data is synthetic (no network): clustered unit vectors for
+the index, generated code/prose chunk texts addressed by row id, generated
+questions.
+
+One timed step = one batch of B RAG queries per GPU, end to end:
+  encode questions (bge-large, HIP encoder) -> sharded IVF search
+  (fused score+top-k kernels + all-gather merge) -> prompt from the top-5
+  blocks (reference synthesize(), agent_graph.py:448-476) -> Qwen2-7B
+  prefill + decode of gen_len tokens with the reference worker's sampling
+  (temperature 0.4, top_p 0.8, repetition_penalty 1.2; qwen_llm.py:107-113).
+Scaling is weak (B queries per GPU fixed).  `value` = total queries/s over
+all ranks (B * N / max-over-ranks step time).  p50 TTFT = submission -> first
+generated token per query.  The ingest phase (split -> LLM summary+keywords ->
+embed -> index upsert over a synthetic repo) runs after the timed steps and is
+reported separately as ingest_docs_per_s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="qwen2-7b")
+    ap.add_argument("--encoder", default="bge-large-en-v1.5")
+    ap.add_argument("--index-size", type=int, default=10_000_000)
+    ap.add_argument("--index-kind", default="ivf", choices=["ivf", "flat"])
+    ap.add_argument("--nlist", type=int, default=4096)
+    ap.add_argument("--nprobe", type=int, default=32)
+    ap.add_argument("--batch", type=int, default=64, help="queries per GPU per step")
+    ap.add_argument("--prompt-len", type=int, default=1024)
+    ap.add_argument("--gen-len", type=int, default=128)
+    ap.add_argument("--top-k", type=int, default=10)
+    ap.add_argument("--ingest-files", type=int, default=48)
+    ap.add_argument("--no-ingest", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+
+    from githubrepostorag_amd.parallel import comm
+
+    info = comm.init_distributed()
+    rank, world = info.rank, info.world_size
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = torch.device("cuda", info.local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    group = comm.world_group()
+
+    from githubrepostorag_amd.embed.service import Embedder
+    from githubrepostorag_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from githubrepostorag_amd.engine.sequence import SamplingParams
+    from githubrepostorag_amd.engine.tokenizer import load_tokenizer
+    from githubrepostorag_amd.index.sharded import ShardedIndex
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import Qwen2Model
+    from githubrepostorag_amd.utils import synthetic
+
+    def log(*a):
+        if rank == 0:
+            print("[bench]", *a, file=sys.stderr, flush=True)
+
+    t_setup = time.perf_counter()
+    dcfg = decoder_config(args.model)
+    model = Qwen2Model(dcfg, device=dev, seed=1)
+    tok = load_tokenizer(None, dcfg.vocab_size)
+    emb = Embedder.from_name(args.encoder, device=dev, seed=2)
+    log(f"models ready {time.perf_counter() - t_setup:.1f}s  decoder={model.param_bytes() / 1e9:.1f} GB")
+
+    # ---- index shard: N / world rows of d-dim clustered vectors
+    n_local = args.index_size // world + (1 if rank < args.index_size % world else 0)
+    t0 = time.perf_counter()
+    X = synthetic.clustered_vectors(n_local, emb.dim, seed=1000 + rank, device=dev)
+    index = ShardedIndex(emb.dim, group, dev, kind=args.index_kind, nlist=args.nlist, nprobe=args.nprobe)
+    index.build(X, seed=7)
+    del X
+    torch.cuda.synchronize() if dev.type == "cuda" else None
+    log(f"index shard ready: {n_local} rows ({args.index_kind}) in {time.perf_counter() - t0:.1f}s")
+
+    max_len = args.prompt_len + args.gen_len + 64
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max(args.batch, 8), max_num_batched_tokens=16384,
+                                             max_model_len=max_len, use_cuda_graph=not args.no_graph,
+                                             seed=rank))
+    sp = SamplingParams(max_tokens=args.gen_len, temperature=0.4, top_p=0.8, repetition_penalty=1.2,
+                        ignore_eos=True)
+    sys_prompt = ("You are a senior developer assistant. Answer using the provided context blocks. "
+                  "Cite blocks as [1], [2]. If the specific information needed is not in the context, "
+                  "say so clearly and suggest looking in specific repos/modules that might contain the answer.")
+
+    qcounter = [rank * 1_000_000]
+
+    def run_step():
+        """One batch of B RAG queries on this rank; returns per-query TTFTs (s)."""
+        B = args.batch
+        t_sub = time.perf_counter()
+        qs = [synthetic.question(qcounter[0] + i) for i in range(B)]
+        qcounter[0] += B
+        qv = emb.embed_queries(qs)
+        scores, ids = index.search(qv, args.top_k)
+        ids = ids.cpu().tolist()
+        prompts = []
+        for q, row in zip(qs, ids):
+            blocks = [f"[{j + 1}] repo=synthetic module=m{d % 97} file=f{d}.py\n{synthetic.chunk_text(d)}"
+                      for j, d in enumerate([x for x in row if x >= 0][:5])]
+            text = tok.apply_chat_template([{"role": "user", "content": f"{sys_prompt}\n\nQuestion: {q}\n\n"
+                                             "Context:\n" + "\n\n".join(blocks) + "\n\nAnswer:"}])
+            pid = tok.encode(text)
+            pid = (pid * (args.prompt_len // max(1, len(pid)) + 1))[: args.prompt_len] if len(pid) < args.prompt_len \
+                else pid[-args.prompt_len:]
+            prompts.append(pid)
+        rids = [eng.add_request(p, sp) for p in prompts]
+        while eng.has_unfinished():
+            eng.step()
+        ttft = []
+        for r in rids:
+            s = eng.pop(r)
+            ttft.append(s.first_token_time - t_sub)
+            assert len(s.output_ids) == args.gen_len, (len(s.output_ids), s.finish_reason)
+        return ttft
+
+    log("warmup")
+    for _ in range(args.warmup):
+        run_step()
+    comm.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    ttfts = []
+    for _ in range(args.steps):
+        ttfts += run_step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    elapsed = time.perf_counter() - t_start
+    ttfts_all = [ttfts]
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tt = torch.tensor(ttfts, dtype=torch.float64, device=dev)
+        g = torch.empty(world, tt.numel(), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(g, tt)
+        ttfts_all = g.cpu().tolist()
+    elapsed = float(t.item())
+    total_q = args.batch * args.steps * world
+    qps = total_q / elapsed
+    p50 = statistics.median([x for r in ttfts_all for x in r]) * 1000.0
+    ms_step = elapsed / args.steps * 1000.0
+
+    # ---- ingest phase (reported separately)
+    ingest_dps = None
+    if not args.no_ingest and args.ingest_files > 0:
+        from githubrepostorag_amd.ingest.bench_ingest import run_ingest_bench
+
+        dps = run_ingest_bench(eng, emb, args.ingest_files, seed=rank)
+        tt = torch.tensor([dps], dtype=torch.float64, device=dev)
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(tt)
+        ingest_dps = float(tt.item())
+
+    if rank == 0:
+        res = {
+            "metric": "RAG queries/sec + p50 TTFT (Qwen2-7B, 10M-vec index); ingest docs/sec",
+            "value": round(qps, 3),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init weights, clustered synthetic vectors, generated chunk texts/questions)",
+            "p50_ttft_ms": round(p50, 2),
+            "ingest_docs_per_s": None if ingest_dps is None else round(ingest_dps, 3),
+            "config": {
+                "model": f"{args.model} TP=1 + {args.encoder}, {args.index_size}-vec {args.index_kind} index "
+                         f"(nlist={args.nlist}, nprobe={args.nprobe}) sharded dp{world}",
+                "global_batch": args.batch * world,
+                "seq_len": args.prompt_len,
+                "gen_len": args.gen_len,
+                "top_k": args.top_k,
+                "parallelism": f"dp{world}",
+            },
+            "engine": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()},
+        }
+        line = json.dumps(res)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,366 @@
+// Unified MFMA flash-attention forward for gfx950.
+//
+// One kernel template serves three ops of SURVEY §2.7:
+//   N1f  causal GQA prefill over the paged KV cache (chunked prefill too),
+//   N1g  paged decode (q_len = 1) with split-KV ("flash-decoding") + combine,
+//   N2c  bidirectional encoder attention over contiguous packed QKV with
+//        per-sequence lengths (padding mask).
+//
+// Work decomposition.  Query rows are GQA-packed: for kv head h of sequence s
+// the rows are (position p, group g) flattened as r = p*G + g, so the G query
+// heads that share one KV head read every K/V tile once.  A wave owns 16 rows,
+// a workgroup NW waves.  Keys stream through LDS in 64-key tiles.
+//
+// MFMA formulation (cdna_hip_programming.md §B attention, "swapped QK^T"):
+//   S^T[key][q] = K · Q^T      A = K tile from LDS (ds_read_b128, XOR-swizzled
+//                              rows, T2), B = Q^T held in registers.
+//   The accumulator puts all keys of one query row in one lane's registers, so
+//   the row max/sum need only 2 cross-lane steps (xor 16, xor 32).
+//   O^T[d][q] += V^T · P^T     A = V^T via ds_read_b64_tr_b16 (T10) from a
+//                              swizzled V image, B = P^T taken straight from
+//                              the S^T accumulators (k-slot permutation chosen
+//                              so no lane movement is needed).
+// Both products use v_mfma_f32_16x16x32_bf16.  Online softmax runs in the
+// log2 domain (exp2).
+#include "common.h"
+
+using namespace grag;
+
+namespace {
+
+constexpr int KT = 64;  // keys per tile
+
+struct AttnParams {
+  const bf16* q;
+  const bf16* k;
+  const bf16* v;
+  bf16* out;
+  float* part_o;   // [nsplit, T, Hq, D] (split mode only)
+  float* part_ml;  // [nsplit, T, Hq, 2]
+  const int32_t* block_tables;
+  const int32_t* q_start;  // [nseq+1]
+  const int32_t* ctx_len;  // [nseq]
+  int q_stride, kv_stride, out_stride;
+  int Hq, Hkv, G, BS, bt_stride;
+  int tiles_per_seq, num_splits, split_len, total_q;
+  float scale_log2;
+  int causal;
+};
+
+// Chunk (16 B) swizzle for the K image read as row fragments by ds_read_b128.
+template <int D>
+__device__ __forceinline__ int kswz(int row) {
+  if constexpr (D == 128) return row & 15;
+  else if constexpr (D == 64) return (row >> 1) & 7;
+  else return (row >> 2) & 3;
+}
+// Chunk (16 B) swizzle for the V image read with ds_read_b64_tr_b16: a 32-lane
+// half reads 8 consecutive rows x 4 8-byte units; these XORs spread them over
+// all 64 banks (derivation in docs/kernels.md).
+template <int D>
+__device__ __forceinline__ int vswz(int row) {
+  if constexpr (D == 128) return (row & 7) << 1;
+  else if constexpr (D == 64) return ((row >> 1) & 3) << 1;
+  else return ((row >> 2) & 1) << 1;
+}
+
+typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4_t;
+
+template <int D, int NW, bool PAGED>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
+  constexpr int CPR = D / 8;      // 16-B chunks per K/V row
+  constexpr int RB = 2 * D;       // bytes per K/V row
+  constexpr int NC = D / 32;      // k-chunks of the QK^T product
+  constexpr int ND = D / 16;      // 16-dim output tiles
+  __shared__ __attribute__((aligned(16))) char smem[2 * KT * RB];
+  char* k_lds = smem;
+  char* v_lds = smem + KT * RB;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h4 = lane >> 4, li = lane & 15;
+  const int seq = blockIdx.x / p.tiles_per_seq, tile = blockIdx.x % p.tiles_per_seq;
+  const int kvh = blockIdx.y, split = blockIdx.z;
+  const int q0 = p.q_start[seq], qlen = p.q_start[seq + 1] - q0;
+  const int ctx = p.ctx_len[seq];
+  const int G = p.G;
+  const int nrows = qlen * G;
+  const int row_base = tile * 16 * NW;
+  if (row_base >= nrows) return;
+  const int my_row = row_base + wave * 16 + li;
+  const bool row_valid = my_row < nrows;
+  const int pq = row_valid ? my_row / G : 0;
+  const int g = row_valid ? my_row % G : 0;
+
+  int kv_lo = split * p.split_len;
+  int kv_hi = min(ctx, kv_lo + p.split_len);
+  if (p.causal) {
+    const int last_row = min(row_base + 16 * NW, nrows) - 1;
+    kv_hi = min(kv_hi, ctx - qlen + last_row / G + 1);
+  }
+  if (kv_lo >= kv_hi && p.num_splits > 1) return;  // combine skips empty splits
+
+  // Q^T fragments: lane holds Q[row li][32c + 8*h4 .. +8]
+  bf16x8_t qf[NC];
+  {
+    const bf16* qp = p.q + (size_t)(q0 + pq) * p.q_stride + (size_t)(kvh * G + g) * D + 8 * h4;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (row_valid) qf[c] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * c);
+      else qf[c] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  const int key_lim = p.causal ? (ctx - qlen + pq + 1) : ctx;  // keys j < key_lim visible
+
+  float m = -INFINITY, lsum = 0.f;
+  f32x4_t o[ND];
+#pragma unroll
+  for (int n = 0; n < ND; ++n) o[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int kt0 = kv_lo; kt0 < kv_hi; kt0 += KT) {
+    __syncthreads();  // previous tile fully consumed
+    // cooperative K/V tile load: global (16 B/lane) -> swizzled LDS image
+    for (int c = threadIdx.x; c < KT * CPR; c += 64 * NW) {
+      const int r = c / CPR, ch = c % CPR;
+      const int j = kt0 + r;
+      bf16x8_t kk = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      bf16x8_t vv = kk;
+      if (j < kv_hi) {
+        size_t off;
+        if constexpr (PAGED) {
+          const int blk = p.block_tables[(size_t)seq * p.bt_stride + j / p.BS];
+          off = (((size_t)blk * p.Hkv + kvh) * p.BS + (j % p.BS)) * D + ch * 8;
+        } else {
+          off = (size_t)(q0 + j) * p.kv_stride + (size_t)kvh * D + ch * 8;
+        }
+        kk = *reinterpret_cast<const bf16x8_t*>(p.k + off);
+        vv = *reinterpret_cast<const bf16x8_t*>(p.v + off);
+      }
+      *reinterpret_cast<bf16x8_t*>(k_lds + r * RB + ((ch ^ kswz<D>(r)) << 4)) = kk;
+      *reinterpret_cast<bf16x8_t*>(v_lds + r * RB + ((ch ^ vswz<D>(r)) << 4)) = vv;
+    }
+    __syncthreads();
+
+    // S^T = K Q^T for 4 key sub-tiles of 16
+    f32x4_t s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int row = 16 * t + li;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const bf16x8_t a =
+            *reinterpret_cast<const bf16x8_t*>(k_lds + row * RB + (((4 * c + h4) ^ kswz<D>(row)) << 4));
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[c], s[t], 0, 0, 0);
+      }
+    }
+    // scale + mask; this lane holds keys kt0 + 16t + 4*h4 + r of query row li
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt0 + 16 * t + 4 * h4 + r;
+        float x = s[t][r] * p.scale_log2;
+        if (key >= key_lim || key >= kv_hi) x = -INFINITY;
+        s[t][r] = x;
+        tmax = fmaxf(tmax, x);
+      }
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m, tmax);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = exp2f(m - m_use);
+    m = m_new;
+    lsum *= alpha;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) o[n] *= alpha;
+    float pr[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pr[t][r] = exp2f(s[t][r] - m_use);
+        lsum += pr[t][r];
+      }
+
+    // O^T += V^T P^T over two 32-key chunks
+    const int tq = li >> 2, tp = li & 3;  // tr-read: this lane addresses row tq, unit tp
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      bf16x8_t bp;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bp[r] = f2bits(pr[2 * cc][r]);
+        bp[4 + r] = f2bits(pr[2 * cc + 1][r]);
+      }
+      const int r0 = 32 * cc + 4 * h4 + tq;  // row of first block
+      const int r1 = r0 + 16;                // row of second block
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+        const int unit = 4 * n + tp;  // 8-byte unit within the row
+        const int b0 = r0 * RB + ((unit ^ (vswz<D>(r0) << 1)) << 3);
+        const int b1 = r1 * RB + ((unit ^ (vswz<D>(r1) << 1)) << 3);
+        const bf16x4_t a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(v_lds + b0));
+        const bf16x4_t a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(v_lds + b1));
+        const bf16x8_t a = bf16x8_t{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bp, o[n], 0, 0, 0);
+      }
+    }
+  }
+
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (!row_valid) return;
+  const int tok = q0 + pq, head = kvh * G + g;
+  if (p.num_splits > 1) {
+    float* po = p.part_o + (((size_t)split * p.total_q + tok) * p.Hq + head) * D;
+#pragma unroll
+    for (int n = 0; n < ND; ++n)
+      *reinterpret_cast<float4*>(po + 16 * n + 4 * h4) = make_float4(o[n][0], o[n][1], o[n][2], o[n][3]);
+    if (h4 == 0) {
+      float* pm = p.part_ml + (((size_t)split * p.total_q + tok) * p.Hq + head) * 2;
+      pm[0] = m;
+      pm[1] = lsum;
+    }
+  } else {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16* op = p.out + (size_t)tok * p.out_stride + (size_t)head * D;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+      bf16x4_t w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = f2bits(o[n][r] * inv);
+      *reinterpret_cast<bf16x4_t*>(op + 16 * n + 4 * h4) = w;
+    }
+  }
+}
+
+// Combine split-KV partials of decode (q_len == 1 per sequence: token == seq).
+template <int D>
+__global__ __launch_bounds__(D) void attn_combine_kernel(AttnParams p) {
+  const int tok = blockIdx.x, head = blockIdx.y, d = threadIdx.x;
+  const int ctx = p.ctx_len[tok];
+  int nvalid = (ctx + p.split_len - 1) / p.split_len;
+  nvalid = max(1, min(nvalid, p.num_splits));
+  float M = -INFINITY;
+  for (int s = 0; s < nvalid; ++s)
+    M = fmaxf(M, p.part_ml[(((size_t)s * p.total_q + tok) * p.Hq + head) * 2]);
+  const float Mu = M == -INFINITY ? 0.f : M;
+  float L = 0.f, acc = 0.f;
+  for (int s = 0; s < nvalid; ++s) {
+    const size_t base = ((size_t)s * p.total_q + tok) * p.Hq + head;
+    const float w = exp2f(p.part_ml[base * 2] - Mu);
+    L += p.part_ml[base * 2 + 1] * w;
+    acc += p.part_o[base * D + d] * w;
+  }
+  p.out[(size_t)tok * p.out_stride + (size_t)head * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+}
+
+template <int D, int NW, bool PAGED>
+int launch(const AttnParams& prm, int nseq, hipStream_t stream) {
+  dim3 grid(nseq * prm.tiles_per_seq, prm.Hkv, prm.num_splits);
+  attn_fwd_kernel<D, NW, PAGED><<<grid, 64 * NW, 0, stream>>>(prm);
+  int err = (int)hipGetLastError();
+  if (err) return err;
+  if (prm.num_splits > 1) {
+    dim3 g2(prm.total_q, prm.Hq);
+    attn_combine_kernel<D><<<g2, D, 0, stream>>>(prm);
+    err = (int)hipGetLastError();
+  }
+  return err;
+}
+
+template <int D>
+int dispatch_nw(const AttnParams& prm, int nseq, int nw, bool paged, hipStream_t stream) {
+  if (paged) {
+    return nw == 1 ? launch<D, 1, true>(prm, nseq, stream) : launch<D, 4, true>(prm, nseq, stream);
+  }
+  return nw == 1 ? launch<D, 1, false>(prm, nseq, stream) : launch<D, 4, false>(prm, nseq, stream);
+}
+
+}  // namespace
+
+// Paged attention (prefill / decode).  q: [T, Hq, D] token-major rows of
+// stride q_stride; caches [blocks, Hkv, BS, D]; out [T, Hq*D] (stride
+// out_stride).  max_q_len bounds the per-sequence q length (tiles are implicit
+// so the launch is graph-capturable).  num_splits > 1 (decode only) needs
+// workspaces part_o [num_splits, T, Hq, D] f32 and part_ml [num_splits, T, Hq, 2].
+GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cache,
+                                  const void* v_cache, void* out, int out_stride,
+                                  const int32_t* block_tables, int bt_stride,
+                                  const int32_t* q_start, const int32_t* ctx_len, int nseq,
+                                  int total_q, int max_q_len, int Hq, int Hkv, int D, int BS,
+                                  float scale, int causal, int num_splits, int split_len,
+                                  float* part_o, float* part_ml, int nw, hipStream_t stream) {
+  if (nseq <= 0) return 0;
+  if (Hq % Hkv != 0 || BS <= 0 || (nw != 1 && nw != 4)) return (int)hipErrorInvalidValue;
+  if (num_splits > 1 && (max_q_len != 1 || !part_o || !part_ml || split_len % KT != 0))
+    return (int)hipErrorInvalidValue;
+  AttnParams prm{};
+  prm.q = (const bf16*)q;
+  prm.k = (const bf16*)k_cache;
+  prm.v = (const bf16*)v_cache;
+  prm.out = (bf16*)out;
+  prm.part_o = part_o;
+  prm.part_ml = part_ml;
+  prm.block_tables = block_tables;
+  prm.q_start = q_start;
+  prm.ctx_len = ctx_len;
+  prm.q_stride = q_stride;
+  prm.kv_stride = 0;
+  prm.out_stride = out_stride;
+  prm.Hq = Hq;
+  prm.Hkv = Hkv;
+  prm.G = Hq / Hkv;
+  prm.BS = BS;
+  prm.bt_stride = bt_stride;
+  prm.tiles_per_seq = (max_q_len * prm.G + 16 * nw - 1) / (16 * nw);
+  prm.num_splits = num_splits < 1 ? 1 : num_splits;
+  prm.split_len = prm.num_splits > 1 ? split_len : (1 << 30);
+  prm.total_q = total_q;
+  prm.scale_log2 = scale * 1.4426950408889634f;
+  prm.causal = causal;
+  switch (D) {
+    case 128: return dispatch_nw<128>(prm, nseq, nw, true, stream);
+    case 64: return dispatch_nw<64>(prm, nseq, nw, true, stream);
+    case 32: return dispatch_nw<32>(prm, nseq, nw, true, stream);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// Contiguous (varlen) self-attention over packed QKV rows, e.g. encoder
+// layers: q/k/v point at the first element of each tensor inside the packed
+// row (row stride qkv_stride); seq_start [nseq+1] gives token offsets.
+GRAG_API int grag_varlen_attention(const void* q, const void* k, const void* v, int qkv_stride,
+                                   void* out, int out_stride, const int32_t* seq_start,
+                                   const int32_t* seq_len, int nseq, int max_len, int H, int Hkv,
+                                   int D, float scale, int causal, hipStream_t stream) {
+  if (nseq <= 0) return 0;
+  if (H % Hkv != 0) return (int)hipErrorInvalidValue;
+  AttnParams prm{};
+  prm.q = (const bf16*)q;
+  prm.k = (const bf16*)k;
+  prm.v = (const bf16*)v;
+  prm.out = (bf16*)out;
+  prm.q_start = seq_start;
+  prm.ctx_len = seq_len;
+  prm.q_stride = qkv_stride;
+  prm.kv_stride = qkv_stride;
+  prm.out_stride = out_stride;
+  prm.Hq = H;
+  prm.Hkv = Hkv;
+  prm.G = H / Hkv;
+  prm.BS = 1;
+  prm.tiles_per_seq = (max_len * prm.G + 63) / 64;
+  prm.num_splits = 1;
+  prm.split_len = 1 << 30;
+  prm.scale_log2 = scale * 1.4426950408889634f;
+  prm.causal = causal;
+  switch (D) {
+    case 128: return dispatch_nw<128>(prm, nseq, 4, false, stream);
+    case 64: return dispatch_nw<64>(prm, nseq, 4, false, stream);
+    case 32: return dispatch_nw<32>(prm, nseq, 4, false, stream);
+    default: return (int)hipErrorInvalidValue;
+  }
+}

@@ -1,0 +1,97 @@
+// Common device helpers for the gfx950 (CDNA4 / MI355X) kernel library.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * bf16 storage is clang's __bf16; conversions go through plain casts so
+//     hipcc emits v_cvt_pk_bf16_f32 (NaN-preserving, RNE) — see
+//     MI355X_MICROARCH.md "Correctness boundaries".
+//   * wave = 64 lanes; block sizes are multiples of 64.
+//   * every global load of bf16 data is vectorised to 16 B/lane (bf16x8).
+//   * exported entry points are extern "C", take raw device pointers plus the
+//     caller's hipStream_t (PyTorch's current stream), and return hipError_t
+//     so the Python side can raise loudly.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GRAG_API extern "C" __attribute__((visibility("default")))
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+typedef __bf16 bf16;
+
+namespace grag {
+
+__device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
+__device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
+
+__device__ __forceinline__ float bits2f(short s) {
+  return __uint_as_float(((uint32_t)(uint16_t)s) << 16);
+}
+__device__ __forceinline__ short f2bits(float f) {
+  bf16 b = (bf16)f;
+  return __builtin_bit_cast(short, b);
+}
+
+// Unpack a 16-byte bf16x8 vector into 8 floats.
+__device__ __forceinline__ void unpack8(const bf16x8_t& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = bits2f(v[i]);
+}
+__device__ __forceinline__ bf16x8_t pack8(const float* f) {
+  bf16x8_t v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = f2bits(f[i]);
+  return v;
+}
+
+// ---- wave / block reductions (wave64) ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum; `red` must hold >= blockDim.x/64 floats of LDS.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+__device__ __forceinline__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+// XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle
+// must be bijective"): blocks that the dispatcher deals to one XCD
+// (orig % 8 equal) get a contiguous range of logical tile ids so neighbouring
+// tiles share that XCD's L2.  Speed-only; correctness never depends on it.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = orig % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + orig / 8;
+}
+
+}  // namespace grag

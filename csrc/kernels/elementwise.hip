@@ -1,0 +1,252 @@
+// Fused elementwise kernels:
+//   * qkv_bias_rope_kvstore  (N1c epilogue + N1d + N1e): QKV bias add, NeoX
+//     rotary embedding on q/k, q written token-major for attention, k/v
+//     scattered straight into the paged KV cache [blocks, Hkv, BS, D].
+//   * silu_mul (N1i epilogue), gelu_bias (N2d FFN1 epilogue), bias_add.
+//   * pool_l2norm (N2e): masked-mean or CLS pooling + L2 normalisation,
+//     writing fp32 (index staging) and optionally bf16.
+// All HBM-bound; every access is 16 B per lane.
+#include "common.h"
+
+using namespace grag;
+
+namespace {
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+}
+
+// One block per token.  Work units (16 B each):
+//   [0, (Hq+Hkv)*D/16)           rotary units: 8 pairs (i..i+7, i+D/2..i+D/2+7)
+//   [.., + Hkv*D/8)              v copy units
+__global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
+    const bf16* __restrict__ qkv, int ld, const bf16* __restrict__ bias,
+    const int32_t* __restrict__ positions, const float* __restrict__ cos_sin,
+    const int32_t* __restrict__ slot_mapping, bf16* __restrict__ q_out, bf16* __restrict__ k_cache,
+    bf16* __restrict__ v_cache, int Hq, int Hkv, int D, int BS) {
+  const int t = blockIdx.x;
+  const int half = D >> 1;
+  const int upp = half >> 3;  // rotary units per head
+  const int n_rot = (Hq + Hkv) * upp;
+  const int n_v = Hkv * (D >> 3);
+  const bf16* row = qkv + (size_t)t * ld;
+  const int pos = positions[t];
+  const int slot = slot_mapping ? slot_mapping[t] : -1;
+  const float* cs = cos_sin + (size_t)pos * D;
+  const int blk = slot >= 0 ? slot / BS : 0;
+  const int off = slot >= 0 ? slot % BS : 0;
+  for (int u = threadIdx.x; u < n_rot + n_v; u += kThreads) {
+    if (u < n_rot) {
+      const int head = u / upp;  // 0..Hq-1 are q heads, then k heads
+      const int i0 = (u % upp) * 8;
+      const int col = head * D + i0;
+      float x1[8], x2[8];
+      unpack8(*reinterpret_cast<const bf16x8_t*>(row + col), x1);
+      unpack8(*reinterpret_cast<const bf16x8_t*>(row + col + half), x2);
+      if (bias) {
+        float b1[8], b2[8];
+        unpack8(*reinterpret_cast<const bf16x8_t*>(bias + col), b1);
+        unpack8(*reinterpret_cast<const bf16x8_t*>(bias + col + half), b2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // match the unfused path: bias add rounds to bf16 before rotary
+          x1[j] = bits2f(f2bits(x1[j] + b1[j]));
+          x2[j] = bits2f(f2bits(x2[j] + b2[j]));
+        }
+      }
+      float o1[8], o2[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = cs[i0 + j], s = cs[half + i0 + j];
+        o1[j] = x1[j] * c - x2[j] * s;
+        o2[j] = x2[j] * c + x1[j] * s;
+      }
+      if (head < Hq) {
+        bf16* qo = q_out + ((size_t)t * Hq + head) * D + i0;
+        *reinterpret_cast<bf16x8_t*>(qo) = pack8(o1);
+        *reinterpret_cast<bf16x8_t*>(qo + half) = pack8(o2);
+      } else if (slot >= 0) {
+        const int kh = head - Hq;
+        bf16* ko = k_cache + (((size_t)blk * Hkv + kh) * BS + off) * D + i0;
+        *reinterpret_cast<bf16x8_t*>(ko) = pack8(o1);
+        *reinterpret_cast<bf16x8_t*>(ko + half) = pack8(o2);
+      }
+    } else if (slot >= 0) {
+      const int vu = u - n_rot;
+      const int vh = vu / (D >> 3);
+      const int i0 = (vu % (D >> 3)) * 8;
+      const int col = (Hq + Hkv + vh) * D + i0;
+      bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(row + col);
+      if (bias) {
+        float a[8], b[8];
+        unpack8(v, a);
+        unpack8(*reinterpret_cast<const bf16x8_t*>(bias + col), b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += b[j];
+        v = pack8(a);
+      }
+      *reinterpret_cast<bf16x8_t*>(v_cache + (((size_t)blk * Hkv + vh) * BS + off) * D + i0) = v;
+    }
+  }
+}
+
+// out[t, i] = silu(gu[t, i]) * gu[t, I + i]
+__global__ __launch_bounds__(kThreads) void silu_mul_kernel(const bf16* __restrict__ gu,
+                                                            bf16* __restrict__ out, int T, int I) {
+  const int nvec = I >> 3;
+  const size_t total = (size_t)T * nvec;
+  for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * kThreads) {
+    const int t = (int)(i / nvec), v = (int)(i % nvec);
+    const bf16* r = gu + (size_t)t * 2 * I;
+    float g[8], u[8], o[8];
+    unpack8(reinterpret_cast<const bf16x8_t*>(r)[v], g);
+    unpack8(reinterpret_cast<const bf16x8_t*>(r + I)[v], u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = silu(g[j]) * u[j];
+    reinterpret_cast<bf16x8_t*>(out + (size_t)t * I)[v] = pack8(o);
+  }
+}
+
+// y = act(x + b); act 0 = identity, 1 = gelu(erf), 2 = silu.  In place allowed.
+__global__ __launch_bounds__(kThreads) void bias_act_kernel(const bf16* __restrict__ x,
+                                                            const bf16* __restrict__ b,
+                                                            bf16* __restrict__ y, int T, int N,
+                                                            int act) {
+  const int nvec = N >> 3;
+  const size_t total = (size_t)T * nvec;
+  for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * kThreads) {
+    const int v = (int)(i % nvec);
+    float a[8], c[8];
+    unpack8(reinterpret_cast<const bf16x8_t*>(x)[i], a);
+    if (b) {
+      unpack8(reinterpret_cast<const bf16x8_t*>(b)[v], c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += c[j];
+    }
+    if (act == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = gelu_erf(a[j]);
+    } else if (act == 2) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = silu(a[j]);
+    }
+    reinterpret_cast<bf16x8_t*>(y)[i] = pack8(a);
+  }
+}
+
+// Pool sequences of token-major hidden rows: sequence b starts at row
+// starts[b] (packed varlen layout) or b*S when starts is null (padded layout),
+// with lengths[b] valid tokens.  mode 0 = masked mean, 1 = CLS (token 0).
+// Writes L2-normalised fp32 [B, H] and optionally bf16 [B, H].
+__global__ __launch_bounds__(kThreads) void pool_l2norm_kernel(
+    const bf16* __restrict__ hidden, const int32_t* __restrict__ starts,
+    const int32_t* __restrict__ lengths, float* __restrict__ outf, bf16* __restrict__ outb, int S,
+    int H, int mode, int normalize) {
+  __shared__ float red[kThreads / 64];
+  const int b = blockIdx.x;
+  const int len = lengths[b] > 0 ? lengths[b] : 1;
+  const int nvec = H >> 3;
+  const bf16* base = hidden + (size_t)(starts ? starts[b] : b * S) * H;
+  // each thread owns up to 2 vectors of the output row (H <= 4096)
+  float acc[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+  const int ntok = mode == 1 ? 1 : len;
+  for (int t = 0; t < ntok; ++t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = threadIdx.x + i * kThreads;
+      if (idx < nvec) {
+        float a[8];
+        unpack8(reinterpret_cast<const bf16x8_t*>(base + (size_t)t * H)[idx], a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] += a[j];
+      }
+    }
+  }
+  float ss = 0.f;
+  const float scale = 1.f / (float)ntok;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc[i][j] *= scale;
+        ss += acc[i][j] * acc[i][j];
+      }
+    }
+  }
+  ss = block_sum(ss, red);
+  const float inv = normalize ? 1.f / fmaxf(sqrtf(ss), 1e-12f) : 1.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = acc[i][j] * inv;
+      if (outf) {
+        float4* of = reinterpret_cast<float4*>(outf + (size_t)b * H + idx * 8);
+        of[0] = make_float4(o[0], o[1], o[2], o[3]);
+        of[1] = make_float4(o[4], o[5], o[6], o[7]);
+      }
+      if (outb) reinterpret_cast<bf16x8_t*>(outb + (size_t)b * H)[idx] = pack8(o);
+    }
+  }
+}
+
+int grid_for(size_t total) {
+  size_t g = (total + kThreads - 1) / kThreads;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+GRAG_API int grag_qkv_rope_kvstore(const void* qkv, int ld, const void* bias,
+                                   const int32_t* positions, const float* cos_sin,
+                                   const int32_t* slot_mapping, void* q_out, void* k_cache,
+                                   void* v_cache, int T, int Hq, int Hkv, int D, int BS,
+                                   hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (D % 16 != 0 || ld % 8 != 0) return (int)hipErrorInvalidValue;
+  qkv_rope_kernel<<<T, kThreads, 0, stream>>>((const bf16*)qkv, ld, (const bf16*)bias, positions,
+                                              cos_sin, slot_mapping, (bf16*)q_out,
+                                              (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, D, BS);
+  return (int)hipGetLastError();
+}
+
+GRAG_API int grag_silu_mul(const void* gu, void* out, int T, int I, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (I % 8 != 0) return (int)hipErrorInvalidValue;
+  silu_mul_kernel<<<grid_for((size_t)T * I / 8), kThreads, 0, stream>>>((const bf16*)gu,
+                                                                         (bf16*)out, T, I);
+  return (int)hipGetLastError();
+}
+
+GRAG_API int grag_bias_act(const void* x, const void* b, void* y, int T, int N, int act,
+                           hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (N % 8 != 0) return (int)hipErrorInvalidValue;
+  bias_act_kernel<<<grid_for((size_t)T * N / 8), kThreads, 0, stream>>>(
+      (const bf16*)x, (const bf16*)b, (bf16*)y, T, N, act);
+  return (int)hipGetLastError();
+}
+
+GRAG_API int grag_pool_l2norm(const void* hidden, const int32_t* starts, const int32_t* lengths,
+                              float* outf, void* outb, int B, int S, int H, int mode, int normalize,
+                              hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (H % 8 != 0 || H > 16 * kThreads) return (int)hipErrorInvalidValue;
+  pool_l2norm_kernel<<<B, kThreads, 0, stream>>>((const bf16*)hidden, starts, lengths, outf,
+                                                 (bf16*)outb, S, H, mode, normalize);
+  return (int)hipGetLastError();
+}

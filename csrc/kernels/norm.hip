@@ -1,0 +1,293 @@
+// Normalisation kernels: fused residual-add + RMSNorm (Qwen2, N1b),
+// fused bias + residual + LayerNorm (BERT-family encoders, N2d),
+// fused word/pos/type embedding gather + LayerNorm (N2a) and the plain
+// token-embedding gather used by the decoder (N1a).
+//
+// Design: one 256-thread block per row, the row held in registers as 16-B
+// bf16x8 vectors (Guideline 13), fp32 statistics, one LDS round trip per
+// reduction.  These ops are HBM-bound; at H=3584 a row is 7 KB read + 7 KB
+// written (+7 KB residual each way when fused), which is why the residual add
+// is folded in instead of being a separate pass.
+#include "common.h"
+
+using namespace grag;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+template <int VPT>
+__global__ __launch_bounds__(kThreads) void rmsnorm_kernel(
+    const bf16* __restrict__ x, bf16* __restrict__ residual, const bf16* __restrict__ w,
+    bf16* __restrict__ out, int H, float eps) {
+  __shared__ float red[kThreads / 64];
+  const int row = blockIdx.x;
+  const int nvec = H >> 3;
+  const bf16x8_t* xr = reinterpret_cast<const bf16x8_t*>(x + (size_t)row * H);
+  bf16x8_t* rr = residual ? reinterpret_cast<bf16x8_t*>(residual + (size_t)row * H) : nullptr;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) {
+      float a[8];
+      unpack8(xr[idx], a);
+      if (rr) {
+        float b[8];
+        unpack8(rr[idx], b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += b[j];
+        // the residual stream is kept in bf16, so normalise the rounded sum
+        bf16x8_t s = pack8(a);
+        rr[idx] = s;
+        unpack8(s, a);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = a[j];
+        ss += a[j] * a[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  ss = block_sum(ss, red);
+  const float inv = rsqrtf(ss / (float)H + eps);
+  const bf16x8_t* wr = reinterpret_cast<const bf16x8_t*>(w);
+  bf16x8_t* orow = reinterpret_cast<bf16x8_t*>(out + (size_t)row * H);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) {
+      float g[8], o[8];
+      unpack8(wr[idx], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * g[j];
+      orow[idx] = pack8(o);
+    }
+  }
+}
+
+// y = LN(x [+ bias] [+ residual]) * gamma + beta
+template <int VPT>
+__global__ __launch_bounds__(kThreads) void layernorm_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ bias, const bf16* __restrict__ residual,
+    const bf16* __restrict__ gamma, const bf16* __restrict__ beta, bf16* __restrict__ out, int H,
+    float eps) {
+  __shared__ float red[kThreads / 64];
+  const int row = blockIdx.x;
+  const int nvec = H >> 3;
+  const bf16x8_t* xr = reinterpret_cast<const bf16x8_t*>(x + (size_t)row * H);
+  const bf16x8_t* rr =
+      residual ? reinterpret_cast<const bf16x8_t*>(residual + (size_t)row * H) : nullptr;
+  const bf16x8_t* br = bias ? reinterpret_cast<const bf16x8_t*>(bias) : nullptr;
+  float v[VPT][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    if (idx < nvec) {
+      unpack8(xr[idx], v[i]);
+      if (br) {
+        float b[8];
+        unpack8(br[idx], b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] += b[j];
+      }
+      if (rr) {
+        float b[8];
+        unpack8(rr[idx], b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] += b[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[i][j];
+    }
+  }
+  const float mean = block_sum(s, red) / (float)H;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[i][j] - mean;
+        s2 += d * d;
+      }
+    }
+  }
+  const float inv = rsqrtf(block_sum(s2, red) / (float)H + eps);
+  const bf16x8_t* gr = reinterpret_cast<const bf16x8_t*>(gamma);
+  const bf16x8_t* er = reinterpret_cast<const bf16x8_t*>(beta);
+  bf16x8_t* orow = reinterpret_cast<bf16x8_t*>(out + (size_t)row * H);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) {
+      float g[8], b[8], o[8];
+      unpack8(gr[idx], g);
+      unpack8(er[idx], b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * inv * g[j] + b[j];
+      orow[idx] = pack8(o);
+    }
+  }
+}
+
+// BERT embeddings: LN(word[id] + pos[p] + type[tt]) — one block per token.
+template <int VPT>
+__global__ __launch_bounds__(kThreads) void bert_embed_ln_kernel(
+    const int32_t* __restrict__ ids, const int32_t* __restrict__ pos_ids,
+    const int32_t* __restrict__ type_ids, const bf16* __restrict__ word,
+    const bf16* __restrict__ pos, const bf16* __restrict__ type, const bf16* __restrict__ gamma,
+    const bf16* __restrict__ beta, bf16* __restrict__ out, int H, float eps) {
+  __shared__ float red[kThreads / 64];
+  const int t = blockIdx.x;
+  const int nvec = H >> 3;
+  const bf16x8_t* wr = reinterpret_cast<const bf16x8_t*>(word + (size_t)ids[t] * H);
+  const bf16x8_t* pr = reinterpret_cast<const bf16x8_t*>(pos + (size_t)pos_ids[t] * H);
+  const bf16x8_t* tr =
+      reinterpret_cast<const bf16x8_t*>(type + (size_t)(type_ids ? type_ids[t] : 0) * H);
+  float v[VPT][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    if (idx < nvec) {
+      float a[8], b[8], c[8];
+      unpack8(wr[idx], a);
+      unpack8(pr[idx], b);
+      unpack8(tr[idx], c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = a[j] + b[j] + c[j];
+        s += v[i][j];
+      }
+    }
+  }
+  const float mean = block_sum(s, red) / (float)H;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[i][j] - mean;
+        s2 += d * d;
+      }
+    }
+  }
+  const float inv = rsqrtf(block_sum(s2, red) / (float)H + eps);
+  const bf16x8_t* gr = reinterpret_cast<const bf16x8_t*>(gamma);
+  const bf16x8_t* er = reinterpret_cast<const bf16x8_t*>(beta);
+  bf16x8_t* orow = reinterpret_cast<bf16x8_t*>(out + (size_t)t * H);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) {
+      float g[8], b[8], o[8];
+      unpack8(gr[idx], g);
+      unpack8(er[idx], b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * inv * g[j] + b[j];
+      orow[idx] = pack8(o);
+    }
+  }
+}
+
+// out[t] = table[ids[t]] — 16 B per lane, grid-stride over (token, vec).
+__global__ __launch_bounds__(kThreads) void embed_gather_kernel(const int32_t* __restrict__ ids,
+                                                                const bf16* __restrict__ table,
+                                                                bf16* __restrict__ out, int T,
+                                                                int H) {
+  const int nvec = H >> 3;
+  const size_t total = (size_t)T * nvec;
+  for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * kThreads) {
+    const int t = (int)(i / nvec), v = (int)(i % nvec);
+    reinterpret_cast<bf16x8_t*>(out + (size_t)t * H)[v] =
+        reinterpret_cast<const bf16x8_t*>(table + (size_t)ids[t] * H)[v];
+  }
+}
+
+int vpt_for(int H) {
+  const int nvec = H / 8;
+  if (nvec <= kThreads) return 1;
+  if (nvec <= 2 * kThreads) return 2;
+  if (nvec <= 4 * kThreads) return 4;
+  return 8;
+}
+
+}  // namespace
+
+GRAG_API int grag_rmsnorm(const void* x, void* residual, const void* w, void* out, int T, int H,
+                          float eps, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8 != 0 || H > 8 * 8 * kThreads) return (int)hipErrorInvalidValue;
+  const bf16* xp = (const bf16*)x;
+  bf16* rp = (bf16*)residual;
+  switch (vpt_for(H)) {
+    case 1: rmsnorm_kernel<1><<<T, kThreads, 0, stream>>>(xp, rp, (const bf16*)w, (bf16*)out, H, eps); break;
+    case 2: rmsnorm_kernel<2><<<T, kThreads, 0, stream>>>(xp, rp, (const bf16*)w, (bf16*)out, H, eps); break;
+    case 4: rmsnorm_kernel<4><<<T, kThreads, 0, stream>>>(xp, rp, (const bf16*)w, (bf16*)out, H, eps); break;
+    default: rmsnorm_kernel<8><<<T, kThreads, 0, stream>>>(xp, rp, (const bf16*)w, (bf16*)out, H, eps); break;
+  }
+  return (int)hipGetLastError();
+}
+
+GRAG_API int grag_layernorm(const void* x, const void* bias, const void* residual,
+                            const void* gamma, const void* beta, void* out, int T, int H,
+                            float eps, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8 != 0 || H > 8 * 8 * kThreads) return (int)hipErrorInvalidValue;
+  auto args = [&](auto kern) {
+    kern<<<T, kThreads, 0, stream>>>((const bf16*)x, (const bf16*)bias, (const bf16*)residual,
+                                     (const bf16*)gamma, (const bf16*)beta, (bf16*)out, H, eps);
+  };
+  switch (vpt_for(H)) {
+    case 1: args(layernorm_kernel<1>); break;
+    case 2: args(layernorm_kernel<2>); break;
+    case 4: args(layernorm_kernel<4>); break;
+    default: args(layernorm_kernel<8>); break;
+  }
+  return (int)hipGetLastError();
+}
+
+GRAG_API int grag_bert_embed_ln(const int32_t* ids, const int32_t* pos_ids,
+                                const int32_t* type_ids, const void* word, const void* pos,
+                                const void* type, const void* gamma, const void* beta, void* out,
+                                int T, int H, float eps, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8 != 0 || H > 8 * 8 * kThreads) return (int)hipErrorInvalidValue;
+  auto args = [&](auto kern) {
+    kern<<<T, kThreads, 0, stream>>>(ids, pos_ids, type_ids, (const bf16*)word, (const bf16*)pos,
+                                     (const bf16*)type, (const bf16*)gamma, (const bf16*)beta,
+                                     (bf16*)out, H, eps);
+  };
+  switch (vpt_for(H)) {
+    case 1: args(bert_embed_ln_kernel<1>); break;
+    case 2: args(bert_embed_ln_kernel<2>); break;
+    case 4: args(bert_embed_ln_kernel<4>); break;
+    default: args(bert_embed_ln_kernel<8>); break;
+  }
+  return (int)hipGetLastError();
+}
+
+GRAG_API int grag_embed_gather(const int32_t* ids, const void* table, void* out, int T, int H,
+                               hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8 != 0) return (int)hipErrorInvalidValue;
+  const size_t total = (size_t)T * (H / 8);
+  int grid = (int)((total + kThreads - 1) / kThreads);
+  if (grid > 4096) grid = 4096;
+  embed_gather_kernel<<<grid, kThreads, 0, stream>>>(ids, (const bf16*)table, (bf16*)out, T, H);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,419 @@
+"""In-process LLM engine: continuous batching over the paged KV cache,
+chunked prefill, prefix caching, fused sampler and hipGraph-captured decode.
+
+Replaces the reference's external vLLM container (helm/templates/
+qwen-deployment.yaml:20-71, ``--max-num-seqs 4 --max-model-len 11712``) with
+an engine that lives in the worker process next to the index and encoder.
+
+Decode steps are captured per (batch bucket, split plan) into
+``torch.cuda.CUDAGraph`` objects (hipGraphs on ROCm): embed -> 28 layers ->
+LM head -> sampler replay as one graph launch; the only host round trip per
+step is one H2D copy of a packed int32 control buffer and one D2H copy of
+the sampled token ids.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+import uuid
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..ops.attention import KV_TILE, AttnMetadata
+from ..ops.sampling import SamplerState, sample
+from .scheduler import KVCacheManager, Scheduler
+from .sequence import Completion, SamplingParams, Sequence
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class EngineConfig:
+    max_num_seqs: int = 64
+    max_num_batched_tokens: int = 16384
+    max_model_len: int = 11712  # reference --max-model-len (helm/values.yaml:74)
+    block_size: int = 16
+    num_blocks: int | None = None
+    kv_cache_gb: float | None = None
+    gpu_memory_fraction: float = 0.5
+    enable_prefix_caching: bool = True
+    use_cuda_graph: bool = True
+    graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
+    seed: int = 0
+
+
+def _split_len_for(batch: int) -> int:
+    if batch >= 32:
+        return 4 * KV_TILE
+    if batch >= 8:
+        return 2 * KV_TILE
+    return KV_TILE
+
+
+def _pow2_at_least(n: int) -> int:
+    p = 1
+    while p < n:
+        p *= 2
+    return p
+
+
+class _DecodeGraph:
+    def __init__(self, graph, out_tokens, batch, nsplit, split_len):
+        self.graph = graph
+        self.out_tokens = out_tokens
+        self.batch = batch
+        self.nsplit = nsplit
+        self.split_len = split_len
+
+
+class LLMEngine:
+    def __init__(self, model, tokenizer, config: EngineConfig | None = None):
+        self.model = model
+        self.tok = tokenizer
+        self.cfg = config or EngineConfig()
+        self.device = model.device
+        self.on_gpu = self.device.type == "cuda"
+        cfg = self.cfg
+        cfg.max_model_len = min(cfg.max_model_len, model.cfg.max_position)
+        bs = cfg.block_size
+        nblocks = cfg.num_blocks or self._plan_blocks()
+        self.kv = KVCacheManager(nblocks, bs, cfg.enable_prefix_caching)
+        self.kv_caches = model.allocate_kv_cache(nblocks, bs)
+        self.sched = Scheduler(self.kv, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
+        self.scratch_slot = cfg.max_num_seqs
+        self.sampler = SamplerState(cfg.max_num_seqs + 1, model.cfg.vocab_size, self.device, seed=cfg.seed)
+        self.max_blocks_per_seq = -(-cfg.max_model_len // bs)
+        self._seqs: dict[str, Sequence] = {}
+        self._graphs: dict[tuple, _DecodeGraph] = {}
+        self._graph_pool = None
+        self._static = None
+        self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0, "steps": 0,
+                      "graph_replays": 0, "graph_captures": 0}
+        self._eos = set(getattr(tokenizer, "eos_token_ids", set()))
+        self._lock = threading.RLock()
+        max_split = -(-cfg.max_model_len // KV_TILE)
+        self._max_b = max(cfg.graph_batch_sizes) if cfg.use_cuda_graph else cfg.max_num_seqs
+        self._max_b = max(self._max_b, cfg.max_num_seqs)
+        if self.on_gpu:
+            hq, d = model.hq, model.head_dim
+            self._part_o = torch.empty(max_split * self._max_b * hq * d, dtype=torch.float32, device=self.device)
+            self._part_ml = torch.empty(max_split * self._max_b * hq * 2, dtype=torch.float32, device=self.device)
+
+    # ------------------------------------------------------------------ setup
+    def _plan_blocks(self) -> int:
+        cfg = self.cfg
+        per_block = self.model.kv_bytes_per_block(cfg.block_size)
+        want_tokens = cfg.max_num_seqs * cfg.max_model_len
+        want = -(-want_tokens // cfg.block_size) + 1
+        if self.device.type != "cuda":
+            return min(want, 4096)
+        if cfg.kv_cache_gb:
+            cap = int(cfg.kv_cache_gb * (1 << 30) // per_block)
+        else:
+            free, _ = torch.cuda.mem_get_info(self.device)
+            cap = int(free * cfg.gpu_memory_fraction // per_block)
+        return max(64, min(want, cap))
+
+    # ------------------------------------------------------------------ API
+    def add_request(self, prompt, params: SamplingParams | None = None, req_id: str | None = None,
+                    on_token=None) -> str:
+        params = params or SamplingParams()
+        ids = self.tok.encode(prompt) if isinstance(prompt, str) else list(prompt)
+        if not ids:
+            ids = [self.tok.pad_token_id] if hasattr(self.tok, "pad_token_id") else [0]
+        if len(ids) >= self.cfg.max_model_len:  # keep the tail (most recent context) like a sliding truncation
+            ids = ids[-(self.cfg.max_model_len - 1):]
+        req_id = req_id or uuid.uuid4().hex
+        seq = Sequence(req_id, ids, params, on_token=on_token)
+        with self._lock:
+            self._seqs[req_id] = seq
+        self.sched.add(seq)
+        return req_id
+
+    def abort(self, req_id: str) -> None:
+        seq = self._seqs.get(req_id)
+        if seq is not None:
+            seq.cancelled = True
+
+    def has_unfinished(self) -> bool:
+        return self.sched.has_work()
+
+    def get(self, req_id: str) -> Sequence | None:
+        return self._seqs.get(req_id)
+
+    def pop(self, req_id: str) -> Sequence | None:
+        with self._lock:
+            return self._seqs.pop(req_id, None)
+
+    def generate(self, prompts, params: SamplingParams | list | None = None) -> list[Completion]:
+        if isinstance(params, list):
+            ids = [self.add_request(p, sp) for p, sp in zip(prompts, params)]
+        else:
+            ids = [self.add_request(p, params) for p in prompts]
+        while self.has_unfinished():
+            self.step()
+        return [self.completion(self.pop(r)) for r in ids]
+
+    def completion(self, seq: Sequence) -> Completion:
+        return Completion(seq.req_id, seq.text, list(seq.output_ids), seq.finish_reason, len(seq.prompt_ids),
+                          seq.ttft, None if seq.finish_time is None else seq.finish_time - seq.arrival,
+                          seq.cached_prefix)
+
+    # ------------------------------------------------------------------ step
+    @torch.inference_mode()
+    def step(self) -> list[Sequence]:
+        """Run one scheduler step; returns sequences that finished in it."""
+        finished = self.sched.reap_cancelled()
+        for s in finished:
+            self._notify(s, None, True)
+        kind, items = self.sched.schedule()
+        for s in getattr(self.sched, "last_rejected", []):
+            s.finish_time = time.perf_counter()
+            self._notify(s, None, True)
+            finished.append(s)
+        for s in getattr(self.sched, "last_admitted", []):
+            self.sampler.reset_slot(s.slot, s.params.temperature, s.params.top_p, s.params.top_k,
+                                    s.params.repetition_penalty, s.all_ids, seed=s.params.seed)
+        if not items:
+            return finished
+        self.stats["steps"] += 1
+        if kind == "prefill":
+            finished += self._run_prefill(items)
+        else:
+            finished += self._run_decode([s for s, _, _ in items])
+        return finished
+
+    # ------------------------------------------------------------------ helpers
+    def _slots_of(self, seq: Sequence, start: int, end: int) -> np.ndarray:
+        bs = self.cfg.block_size
+        pos = np.arange(start, end)
+        blocks = np.asarray(seq.blocks, dtype=np.int64)
+        return (blocks[pos // bs] * bs + pos % bs).astype(np.int32)
+
+    def _block_table(self, seqs, width: int) -> np.ndarray:
+        bt = np.zeros((len(seqs), width), dtype=np.int32)
+        for i, s in enumerate(seqs):
+            n = min(len(s.blocks), width)
+            bt[i, :n] = s.blocks[:n]
+        return bt
+
+    def _to_dev(self, arr: np.ndarray) -> torch.Tensor:
+        t = torch.from_numpy(arr)
+        if self.on_gpu:
+            return t.pin_memory().to(self.device, non_blocking=True)
+        return t
+
+    # ------------------------------------------------------------------ prefill
+    def _run_prefill(self, items) -> list[Sequence]:
+        t0 = time.perf_counter()
+        seqs = [s for s, _, _ in items]
+        ids, pos, slots, q_start, ctx = [], [], [], [0], []
+        for s, a, b in items:
+            ids.append(np.asarray(s.all_ids[a:b], dtype=np.int32))
+            pos.append(np.arange(a, b, dtype=np.int32))
+            slots.append(self._slots_of(s, a, b))
+            q_start.append(q_start[-1] + (b - a))
+            ctx.append(b)
+        width = max(len(s.blocks) for s in seqs)
+        packed = np.concatenate([np.concatenate(ids), np.concatenate(pos), np.concatenate(slots),
+                                 np.asarray(q_start, dtype=np.int32), np.asarray(ctx, dtype=np.int32),
+                                 self._block_table(seqs, width).reshape(-1)])
+        dev = self._to_dev(packed)
+        T, n = q_start[-1], len(seqs)
+        o = 0
+        d_ids = dev[o:o + T]; o += T
+        d_pos = dev[o:o + T]; o += T
+        d_slot = dev[o:o + T]; o += T
+        d_qs = dev[o:o + n + 1]; o += n + 1
+        d_ctx = dev[o:o + n]; o += n
+        d_bt = dev[o:o + n * width].view(n, width)
+        meta = AttnMetadata(q_start=d_qs, ctx_len=d_ctx, block_tables=d_bt, slot_mapping=d_slot,
+                            max_q_len=max(b - a for _, a, b in items), num_seqs=n, num_tokens=T)
+        hidden = self.model.forward(d_ids, d_pos, meta, self.kv_caches)
+        # sample for sequences whose prompt is now complete and have no pending token
+        samp_rows, samp_seqs = [], []
+        for i, (s, a, b) in enumerate(items):
+            s.num_computed = b
+            self.kv.register_full_blocks(s)
+            if b == s.total_len and not s.output_ids:
+                samp_rows.append(q_start[i + 1] - 1)
+                samp_seqs.append(s)
+        finished = []
+        if samp_seqs:
+            rows = torch.as_tensor(samp_rows, dtype=torch.long, device=self.device)
+            logits = self.model.compute_logits(hidden.index_select(0, rows))
+            slot_t = self._to_dev(np.asarray([s.slot for s in samp_seqs], dtype=np.int32))
+            toks = sample(logits, self.sampler, slot_t).tolist()
+            now = time.perf_counter()
+            for s, t in zip(samp_seqs, toks):
+                if self._append(s, int(t), now):
+                    finished.append(s)
+        self.stats["prefill_tokens"] += T
+        self.stats["prefill_s"] += time.perf_counter() - t0
+        return finished
+
+    # ------------------------------------------------------------------ decode
+    def _decode_inputs(self, seqs, B: int, width: int) -> np.ndarray:
+        n = len(seqs)
+        ids = np.zeros(B, dtype=np.int32)
+        pos = np.zeros(B, dtype=np.int32)
+        slot = np.full(B, -1, dtype=np.int32)
+        ctx = np.ones(B, dtype=np.int32)
+        sl = np.full(B, self.scratch_slot, dtype=np.int32)
+        bs = self.cfg.block_size
+        for i, s in enumerate(seqs):
+            p = s.total_len - 1
+            ids[i] = s.all_ids[-1]
+            pos[i] = p
+            slot[i] = s.blocks[p // bs] * bs + p % bs
+            ctx[i] = s.total_len
+            sl[i] = s.slot
+        bt = np.zeros((B, width), dtype=np.int32)
+        bt[:n] = self._block_table(seqs, width)
+        qs = np.arange(B + 1, dtype=np.int32)
+        return np.concatenate([ids, pos, slot, ctx, sl, qs, bt.reshape(-1)])
+
+    def _views(self, buf: torch.Tensor, B: int, width: int):
+        o = 0
+        out = {}
+        for name, n in (("ids", B), ("pos", B), ("slot", B), ("ctx", B), ("slots", B), ("qs", B + 1)):
+            out[name] = buf[o:o + n]
+            o += n
+        out["bt"] = buf[o:o + B * width].view(B, width)
+        return out
+
+    def _decode_forward(self, v, B, nsplit, split_len, out_tokens):
+        hq, d = self.model.hq, self.model.head_dim
+        part_o = self._part_o[: nsplit * B * hq * d] if self.on_gpu else None
+        part_ml = self._part_ml[: nsplit * B * hq * 2] if self.on_gpu else None
+        meta = AttnMetadata(q_start=v["qs"], ctx_len=v["ctx"], block_tables=v["bt"], slot_mapping=v["slot"],
+                            max_q_len=1, num_seqs=B, num_tokens=B, is_decode=True, num_splits=nsplit,
+                            split_len=split_len, part_o=part_o, part_ml=part_ml)
+        hidden = self.model.forward(v["ids"], v["pos"], meta, self.kv_caches)
+        logits = self.model.compute_logits(hidden)
+        return sample(logits, self.sampler, v["slots"], out=out_tokens)
+
+    def _run_decode(self, seqs) -> list[Sequence]:
+        t0 = time.perf_counter()
+        n = len(seqs)
+        max_ctx = max(s.total_len for s in seqs)
+        width = self.max_blocks_per_seq
+        use_graph = (self.on_gpu and self.cfg.use_cuda_graph and self.model.tp.trivial
+                     and n <= max(self.cfg.graph_batch_sizes))
+        if use_graph:
+            B = next(b for b in self.cfg.graph_batch_sizes if b >= n)
+            split_len = _split_len_for(B)
+            nsplit = min(_pow2_at_least(-(-max_ctx // split_len)), -(-self.cfg.max_model_len // split_len))
+            g = self._graphs.get((B, nsplit, split_len))
+            if g is None:
+                g = self._capture(B, nsplit, split_len)
+            packed = self._decode_inputs(seqs, B, width)
+            self._static_host[: packed.size] = torch.from_numpy(packed)
+            self._static_dev[: packed.size].copy_(self._static_host[: packed.size], non_blocking=True)
+            g.graph.replay()
+            toks = g.out_tokens[:n].tolist()
+            self.stats["graph_replays"] += 1
+        else:
+            split_len = _split_len_for(n)
+            nsplit = max(1, -(-max_ctx // split_len))
+            width = max(len(s.blocks) for s in seqs)
+            dev = self._to_dev(self._decode_inputs(seqs, n, width))
+            out = torch.empty(n, dtype=torch.int32, device=self.device)
+            toks = self._decode_forward(self._views(dev, n, width), n, nsplit, split_len, out).tolist()
+        now = time.perf_counter()
+        finished = []
+        for s, t in zip(seqs, toks):
+            s.num_computed = s.total_len
+            if self._append(s, int(t), now):
+                finished.append(s)
+        self.stats["decode_tokens"] += n
+        self.stats["decode_s"] += now - t0
+        return finished
+
+    def _ensure_static(self):
+        if self._static is None:
+            W = self.max_blocks_per_seq
+            size = 6 * self._max_b + 1 + self._max_b * W
+            self._static_dev = torch.zeros(size, dtype=torch.int32, device=self.device)
+            self._static_host = torch.zeros(size, dtype=torch.int32).pin_memory()
+            self._static = True
+            self._graph_pool = torch.cuda.graph_pool_handle()
+
+    def _capture(self, B, nsplit, split_len) -> _DecodeGraph:
+        self._ensure_static()
+        W = self.max_blocks_per_seq
+        # a benign batch: every row is a padding row (scratch block, scratch slot)
+        dummy = self._decode_inputs([], B, W)
+        self._static_dev[: dummy.size].copy_(torch.from_numpy(dummy))
+        v = self._views(self._static_dev, B, W)
+        out = torch.empty(B, dtype=torch.int32, device=self.device)
+        rng_save = self.sampler.rng.clone()
+        seen_save = self.sampler.seen[self.scratch_slot].clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._decode_forward(v, B, nsplit, split_len, out)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, pool=self._graph_pool):
+            self._decode_forward(v, B, nsplit, split_len, out)
+        torch.cuda.synchronize()
+        self.sampler.rng.copy_(rng_save)
+        self.sampler.seen[self.scratch_slot].copy_(seen_save)
+        g = _DecodeGraph(graph, out, B, nsplit, split_len)
+        self._graphs[(B, nsplit, split_len)] = g
+        self.stats["graph_captures"] += 1
+        return g
+
+    def warmup_graphs(self, batch_sizes=None, max_ctx: int = 2048) -> None:
+        if not (self.on_gpu and self.cfg.use_cuda_graph and self.model.tp.trivial):
+            return
+        for B in batch_sizes or self.cfg.graph_batch_sizes:
+            split_len = _split_len_for(B)
+            nsplit = _pow2_at_least(-(-max_ctx // split_len))
+            if (B, nsplit, split_len) not in self._graphs:
+                self._capture(B, nsplit, split_len)
+
+    # ------------------------------------------------------------------ outputs
+    def _append(self, s: Sequence, tok: int, now: float) -> bool:
+        if s.first_token_time is None:
+            s.first_token_time = now
+        s.output_ids.append(tok)
+        p = s.params
+        reason = None
+        if not p.ignore_eos and tok in self._eos and len(s.output_ids) > p.min_tokens:
+            reason = "stop"
+        elif tok in p.stop_token_ids:
+            reason = "stop"
+        elif len(s.output_ids) >= p.max_tokens:
+            reason = "length"
+        elif s.total_len >= self.cfg.max_model_len:
+            reason = "length"
+        delta = ""
+        if reason != "stop" or tok not in self._eos:
+            delta = self.tok.decode([tok])
+            s.text += delta
+        if p.stop and reason is None:
+            for st in p.stop:
+                idx = s.text.find(st, max(0, len(s.text) - len(delta) - len(st)))
+                if idx >= 0:
+                    s.text = s.text[:idx]
+                    reason = "stop"
+                    break
+        if reason is not None:
+            s.finish_reason = reason
+            s.finish_time = now
+            self.sched.finish(s)
+        self._notify(s, delta, reason is not None)
+        return reason is not None
+
+    def _notify(self, s: Sequence, delta, finished: bool) -> None:
+        if s.on_token is not None:
+            try:
+                s.on_token(s, delta, finished)
+            except Exception:  # a slow/broken consumer must never kill the engine loop
+                log.exception("on_token callback failed for %s", s.req_id)

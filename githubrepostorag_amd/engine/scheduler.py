@@ -1,0 +1,233 @@
+"""KV-cache manager (over the C++ block allocator) and the continuous-batching
+scheduler.
+
+Policy (what vLLM gave the reference at ``--max-num-seqs 4``, generalised):
+* waiting requests are admitted FCFS while a sampler slot, token budget and
+  KV blocks are available; long prompts are split into chunks
+  (chunked prefill) so one request never blocks the batch;
+* prompt prefixes already in the cache (same chained block hash) are reused
+  instead of recomputed — the agent's repeated instructions and the ingest
+  extractor prompts share long prefixes;
+* when decode runs out of blocks the youngest running sequence is preempted
+  (blocks freed, recomputed later).
+"""
+from __future__ import annotations
+
+import collections
+import threading
+
+import numpy as np
+
+from ..utils.runtime import rt
+from .sequence import Sequence, SeqStatus
+
+
+class KVCacheManager:
+    SCRATCH_BLOCK = 0  # never handed out: padding rows of graph-captured batches point here
+
+    def __init__(self, num_blocks: int, block_size: int, enable_prefix_caching: bool = True):
+        self.num_blocks = num_blocks
+        self.block_size = block_size
+        self.prefix_caching = enable_prefix_caching
+        self._h = rt().grag_alloc_create(num_blocks, block_size)
+        buf = np.zeros(1, dtype=np.int32)
+        assert rt().grag_alloc_allocate(self._h, 1, buf.ctypes.data) == 0 and buf[0] == self.SCRATCH_BLOCK
+
+    def __del__(self):
+        try:
+            rt().grag_alloc_destroy(self._h)
+        except Exception:
+            pass
+
+    @property
+    def num_free(self) -> int:
+        return rt().grag_alloc_num_free(self._h)
+
+    def usage(self) -> float:
+        return 1.0 - self.num_free / max(1, self.num_blocks - 1)
+
+    def stats(self) -> dict:
+        out = np.zeros(3, dtype=np.int64)
+        rt().grag_alloc_stats(self._h, out.ctypes.data)
+        return {"prefix_hits": int(out[0]), "prefix_queries": int(out[1]), "cached_blocks": int(out[2])}
+
+    def blocks_needed(self, seq: Sequence, upto: int) -> int:
+        need = -(-upto // self.block_size)
+        return max(0, need - len(seq.blocks))
+
+    def ensure(self, seq: Sequence, upto: int) -> bool:
+        n = self.blocks_needed(seq, upto)
+        if n == 0:
+            return True
+        buf = np.zeros(n, dtype=np.int32)
+        if rt().grag_alloc_allocate(self._h, n, buf.ctypes.data) != 0:
+            return False
+        seq.blocks.extend(buf.tolist())
+        return True
+
+    def match_prefix(self, seq: Sequence) -> int:
+        """Reuse cached full blocks of the prompt (keeping >= 1 token to compute)."""
+        if not self.prefix_caching or seq.blocks:
+            return 0
+        usable = (len(seq.prompt_ids) - 1) // self.block_size * self.block_size
+        if usable <= 0:
+            return 0
+        toks = np.asarray(seq.prompt_ids[:usable], dtype=np.int32)
+        nb = usable // self.block_size
+        out = np.zeros(nb, dtype=np.int32)
+        hashes = np.zeros(nb, dtype=np.uint64)
+        m = rt().grag_alloc_match_prefix(self._h, toks.ctypes.data, usable, out.ctypes.data, hashes.ctypes.data)
+        if m:
+            seq.blocks = out[:m].tolist()
+            seq.block_hashes = [int(h) for h in hashes[:m]]
+            seq.num_computed = m * self.block_size
+            seq.cached_prefix = seq.num_computed
+        return m * self.block_size
+
+    def register_full_blocks(self, seq: Sequence) -> None:
+        if not self.prefix_caching:
+            return
+        full = min(seq.num_computed, len(seq.prompt_ids)) // self.block_size
+        if len(seq.block_hashes) >= full:
+            return
+        ids = seq.prompt_ids
+        parent = seq.block_hashes[-1] if seq.block_hashes else 0
+        for b in range(len(seq.block_hashes), full):
+            chunk = np.asarray(ids[b * self.block_size:(b + 1) * self.block_size], dtype=np.int32)
+            h = int(rt().grag_hash_block(parent, chunk.ctypes.data, self.block_size))
+            rt().grag_alloc_register(self._h, seq.blocks[b], h)
+            seq.block_hashes.append(h)
+            parent = h
+
+    def free(self, seq: Sequence) -> None:
+        if seq.blocks:
+            arr = np.asarray(seq.blocks, dtype=np.int32)
+            rt().grag_alloc_free(self._h, len(arr), arr.ctypes.data)
+        seq.blocks = []
+        seq.block_hashes = []
+        seq.num_computed = 0
+
+
+class Scheduler:
+    def __init__(self, kv: KVCacheManager, max_num_seqs: int, max_num_batched_tokens: int, max_model_len: int):
+        self.kv = kv
+        self.max_num_seqs = max_num_seqs
+        self.max_num_batched_tokens = max_num_batched_tokens
+        self.max_model_len = max_model_len
+        self.waiting: collections.deque[Sequence] = collections.deque()
+        self.running: list[Sequence] = []
+        self.free_slots = list(range(max_num_seqs - 1, -1, -1))
+        self.lock = threading.Lock()
+        self.num_preemptions = 0
+
+    def add(self, seq: Sequence) -> None:
+        with self.lock:
+            self.waiting.append(seq)
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def _finish(self, seq: Sequence) -> None:
+        self.kv.free(seq)
+        if seq.slot >= 0:
+            self.free_slots.append(seq.slot)
+            seq.slot = -1
+        seq.status = SeqStatus.FINISHED
+
+    def finish(self, seq: Sequence) -> None:
+        with self.lock:
+            if seq in self.running:
+                self.running.remove(seq)
+            self._finish(seq)
+
+    def reap_cancelled(self) -> list[Sequence]:
+        out = []
+        with self.lock:
+            for s in list(self.waiting):
+                if s.cancelled:
+                    self.waiting.remove(s)
+                    self._finish(s)
+                    s.finish_reason = "abort"
+                    out.append(s)
+            for s in list(self.running):
+                if s.cancelled:
+                    self.running.remove(s)
+                    self._finish(s)
+                    s.finish_reason = "abort"
+                    out.append(s)
+        return out
+
+    @staticmethod
+    def prefill_target(seq: Sequence) -> int:
+        return seq.total_len - (1 if seq.output_ids else 0)
+
+    def _preempt_one(self, keep: Sequence) -> bool:
+        victims = [s for s in self.running if s is not keep]
+        if not victims:
+            return False
+        v = max(victims, key=lambda s: s.arrival)
+        self.running.remove(v)
+        self.kv.free(v)
+        self.free_slots.append(v.slot)
+        v.slot = -1
+        v.status = SeqStatus.WAITING
+        v.num_preemptions += 1
+        self.num_preemptions += 1
+        self.waiting.appendleft(v)
+        return True
+
+    def schedule(self):
+        """Returns ("prefill", [(seq, start, end)]) or ("decode", [(seq, pos, pos+1)]) or (None, [])."""
+        with self.lock:
+            budget = self.max_num_batched_tokens
+            items = []
+            # continue partially prefilled running sequences
+            for seq in self.running:
+                if budget <= 0:
+                    break
+                if seq.is_prefill:
+                    tgt = self.prefill_target(seq)
+                    n = min(tgt - seq.num_computed, budget)
+                    if n > 0 and self.kv.ensure(seq, seq.num_computed + n):
+                        items.append((seq, seq.num_computed, seq.num_computed + n))
+                        budget -= n
+            admitted = []
+            while self.waiting and budget > 0 and self.free_slots and len(self.running) < self.max_num_seqs:
+                seq = self.waiting[0]
+                if seq.total_len >= self.max_model_len:
+                    self.waiting.popleft()
+                    seq.finish_reason = "length"
+                    self._finish(seq)
+                    admitted.append(("rejected", seq))
+                    continue
+                if not seq.blocks:
+                    self.kv.match_prefix(seq)
+                tgt = self.prefill_target(seq)
+                n = min(tgt - seq.num_computed, budget)
+                if n <= 0 or not self.kv.ensure(seq, seq.num_computed + n):
+                    break
+                self.waiting.popleft()
+                seq.slot = self.free_slots.pop()
+                seq.status = SeqStatus.RUNNING
+                self.running.append(seq)
+                admitted.append(("admitted", seq))
+                items.append((seq, seq.num_computed, seq.num_computed + n))
+                budget -= n
+            self.last_admitted = [s for tag, s in admitted if tag == "admitted"]
+            self.last_rejected = [s for tag, s in admitted if tag == "rejected"]
+            if items:
+                return "prefill", items
+            # decode every running sequence (one new token each)
+            out = []
+            for seq in list(self.running):
+                if seq not in self.running or seq.is_prefill:
+                    continue
+                while not self.kv.ensure(seq, seq.total_len):
+                    if not self._preempt_one(seq):
+                        break
+                if seq in self.running and len(seq.blocks) * self.kv.block_size >= seq.total_len:
+                    out.append((seq, seq.total_len - 1, seq.total_len))
+            out = [it for it in out if it[0] in self.running]  # drop anything preempted meanwhile
+            if out:
+                return "decode", out
+            return None, []

@@ -1,0 +1,192 @@
+"""Qwen2-family decoder (Qwen2 / Qwen2.5 / Qwen2.5-Coder) for the in-process
+LLM engine — what the reference reached through the external vLLM container
+(reference call sites rag_worker/src/worker/services/
+qwen_llm.py:104-148, ingest/src/app/llm_init.py:68-143).
+
+Layer dataflow per step (T tokens, kernels in brackets):
+  embed gather [grag_embed_gather]
+  per layer:
+    residual += h ; x = RMSNorm(residual)            [grag_rmsnorm, fused]
+    qkv = x W_qkv^T                                   (hipBLASLt, plain GEMM)
+    q, K/V-cache <- bias + NeoX RoPE + paged store    [grag_qkv_rope_kvstore]
+    a = paged flash attention (GQA-packed, MFMA)      [grag_paged_attention]
+    h = a W_o^T        (+ TP all-reduce, RCCL)
+    residual += h ; x = RMSNorm(residual)            [grag_rmsnorm]
+    gu = x W_gu^T ; m = SiLU(g) * u                   [grag_silu_mul]
+    h = m W_down^T     (+ TP all-reduce, RCCL)
+  final RMSNorm ; LM head on last tokens (vocab-parallel under TP) ; fused
+  sampler [grag_sample].
+
+Tensor parallelism: q heads, kv heads (replicated when tp > num_kv_heads),
+the FFN and the vocab are sharded per rank; two all-reduces per layer.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops.attention import AttnMetadata, paged_attention
+from ..ops.elementwise import qkv_rope_kvstore, rope_cos_sin, silu_mul
+from ..ops.linear import linear
+from ..ops.norm import embed_gather, rmsnorm
+from ..parallel.comm import Group
+from .configs import DecoderConfig
+
+
+class _Layer:
+    __slots__ = ("in_norm", "qkv_w", "qkv_b", "o_w", "post_norm", "gu_w", "down_w")
+
+
+class Qwen2Model:
+    def __init__(self, cfg: DecoderConfig, device="cuda", dtype=torch.bfloat16, tp: Group | None = None,
+                 seed: int = 0, state_dict: dict | None = None, init_std: float = 0.02):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.tp = tp or Group([0])
+        ts, tr = self.tp.size, self.tp.rank
+        assert cfg.num_heads % ts == 0, "num_heads must divide by tp"
+        self.hq = cfg.num_heads // ts
+        if cfg.num_kv_heads >= ts:
+            assert cfg.num_kv_heads % ts == 0
+            self.hkv = cfg.num_kv_heads // ts
+            self.kv_head0 = tr * self.hkv
+        else:  # replicate kv heads across ranks
+            self.hkv = 1
+            self.kv_head0 = tr // (ts // cfg.num_kv_heads)
+        self.head_dim = cfg.head_dim
+        assert cfg.intermediate_size % ts == 0
+        self.inter = cfg.intermediate_size // ts
+        self.vocab_shard = -(-cfg.vocab_size // ts)
+        self.vocab0 = tr * self.vocab_shard
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.cos_sin = rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device)
+        if state_dict is not None:
+            self._load(state_dict)
+        else:
+            self._init_random(seed, init_std)
+
+    # ------------------------------------------------------------------ weights
+    def _rand(self, g, *shape, std):
+        t = torch.empty(*shape, dtype=self.dtype, device=self.device)
+        if self.device.type == "cuda":
+            t.normal_(0.0, std, generator=g)
+        else:
+            t.copy_(torch.randn(*shape, generator=g) * std)
+        return t
+
+    def _init_random(self, seed: int, std: float):
+        cfg = self.cfg
+        dev = self.device
+        g = torch.Generator(device=dev if dev.type == "cuda" else "cpu")
+        g.manual_seed(seed * 1000003 + 17)
+        H, D = cfg.hidden_size, self.head_dim
+        qkv_rows = (self.hq + 2 * self.hkv) * D
+        self.embed = self._rand(g, cfg.vocab_size, H, std=std)
+        self.layers = []
+        for _ in range(cfg.num_layers):
+            L = _Layer()
+            L.in_norm = torch.ones(H, dtype=self.dtype, device=dev)
+            L.qkv_w = self._rand(g, qkv_rows, H, std=std)
+            L.qkv_b = self._rand(g, qkv_rows, std=std) if cfg.qkv_bias else None
+            L.o_w = self._rand(g, H, self.hq * D, std=std)
+            L.post_norm = torch.ones(H, dtype=self.dtype, device=dev)
+            L.gu_w = self._rand(g, 2 * self.inter, H, std=std)
+            L.down_w = self._rand(g, H, self.inter, std=std)
+            self.layers.append(L)
+        self.norm = torch.ones(H, dtype=self.dtype, device=dev)
+        if cfg.tie_word_embeddings:
+            self.lm_head = self._pad_rows(self.embed[self.vocab0:self.vocab0 + self.vocab_shard])
+        else:
+            self.lm_head = self._pad_rows(self._rand(g, min(self.vocab_shard, cfg.vocab_size - self.vocab0), H,
+                                                     std=std))
+
+    def _pad_rows(self, t: torch.Tensor) -> torch.Tensor:
+        # equal-sized vocab shards so the TP all-gather of logits is one collective
+        if t.shape[0] == self.vocab_shard:
+            return t
+        pad = torch.zeros(self.vocab_shard - t.shape[0], t.shape[1], dtype=t.dtype, device=t.device)
+        return torch.cat([t, pad], 0)
+
+    def _load(self, sd: dict):
+        """HF Qwen2 naming -> fused, TP-sharded tensors."""
+        cfg = self.cfg
+        D = self.head_dim
+        dev, dt = self.device, self.dtype
+
+        def get(name):
+            return sd[name].to(device=dev, dtype=dt)
+
+        q0, q1 = self.tp.rank * self.hq * D, (self.tp.rank + 1) * self.hq * D
+        k0, k1 = self.kv_head0 * D, (self.kv_head0 + self.hkv) * D
+        i0, i1 = self.tp.rank * self.inter, (self.tp.rank + 1) * self.inter
+        self.embed = get("model.embed_tokens.weight")
+        self.layers = []
+        for i in range(cfg.num_layers):
+            p = f"model.layers.{i}."
+            L = _Layer()
+            L.in_norm = get(p + "input_layernorm.weight")
+            L.qkv_w = torch.cat([get(p + "self_attn.q_proj.weight")[q0:q1], get(p + "self_attn.k_proj.weight")[k0:k1],
+                                 get(p + "self_attn.v_proj.weight")[k0:k1]], 0).contiguous()
+            if cfg.qkv_bias:
+                L.qkv_b = torch.cat([get(p + "self_attn.q_proj.bias")[q0:q1], get(p + "self_attn.k_proj.bias")[k0:k1],
+                                     get(p + "self_attn.v_proj.bias")[k0:k1]], 0).contiguous()
+            else:
+                L.qkv_b = None
+            L.o_w = get(p + "self_attn.o_proj.weight")[:, q0:q1].contiguous()
+            L.post_norm = get(p + "post_attention_layernorm.weight")
+            L.gu_w = torch.cat([get(p + "mlp.gate_proj.weight")[i0:i1], get(p + "mlp.up_proj.weight")[i0:i1]],
+                               0).contiguous()
+            L.down_w = get(p + "mlp.down_proj.weight")[:, i0:i1].contiguous()
+            self.layers.append(L)
+        self.norm = get("model.norm.weight")
+        head = self.embed if cfg.tie_word_embeddings or "lm_head.weight" not in sd else get("lm_head.weight")
+        self.lm_head = self._pad_rows(head[self.vocab0:self.vocab0 + self.vocab_shard].contiguous())
+
+    def param_bytes(self) -> int:
+        n = self.embed.numel() + self.norm.numel()
+        for L in self.layers:
+            for t in (L.in_norm, L.qkv_w, L.qkv_b, L.o_w, L.post_norm, L.gu_w, L.down_w):
+                n += 0 if t is None else t.numel()
+        if not self.cfg.tie_word_embeddings:
+            n += self.lm_head.numel()
+        return n * torch.finfo(self.dtype).bits // 8
+
+    # ------------------------------------------------------------------ cache
+    def kv_bytes_per_block(self, block_size: int) -> int:
+        return 2 * self.cfg.num_layers * self.hkv * block_size * self.head_dim * torch.finfo(self.dtype).bits // 8
+
+    def allocate_kv_cache(self, num_blocks: int, block_size: int):
+        shape = (num_blocks, self.hkv, block_size, self.head_dim)
+        return [(torch.zeros(shape, dtype=self.dtype, device=self.device),
+                 torch.zeros(shape, dtype=self.dtype, device=self.device)) for _ in range(self.cfg.num_layers)]
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, input_ids: torch.Tensor, positions: torch.Tensor, meta: AttnMetadata, kv_caches) -> torch.Tensor:
+        cfg = self.cfg
+        eps = cfg.rms_norm_eps
+        h = embed_gather(input_ids, self.embed)
+        residual = None
+        for L, (kc, vc) in zip(self.layers, kv_caches):
+            if residual is None:
+                residual = h
+                x = rmsnorm(h, L.in_norm, eps)
+            else:
+                x = rmsnorm(h, L.in_norm, eps, residual=residual)
+            qkv = linear(x, L.qkv_w)
+            q = qkv_rope_kvstore(qkv, L.qkv_b, positions, self.cos_sin, meta.slot_mapping, kc, vc,
+                                 self.hq, self.hkv, self.head_dim)
+            a = paged_attention(q, kc, vc, meta, self.scale, causal=True)
+            h = self.tp.all_reduce(linear(a, L.o_w))
+            x = rmsnorm(h, L.post_norm, eps, residual=residual)
+            h = self.tp.all_reduce(linear(silu_mul(linear(x, L.gu_w)), L.down_w))
+        return rmsnorm(h, self.norm, eps, residual=residual)
+
+    def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        """hidden [B, H] -> logits [B, vocab] (bf16); vocab-parallel gather under TP."""
+        logits = linear(hidden, self.lm_head)
+        if not self.tp.trivial:
+            g = self.tp.all_gather(logits)  # [tp, B, Vs]
+            logits = g.permute(1, 0, 2).reshape(hidden.shape[0], -1)[:, : self.cfg.vocab_size]
+        return logits

@@ -1,0 +1,101 @@
+"""ctypes binding of ``libgrag_kernels.so`` (the gfx950 HIP kernel library).
+
+The library is loaded lazily, always *after* ``import torch`` so it shares
+PyTorch-ROCm's HIP runtime (same ``libamdhip64.so.7`` SONAME).  On a GPU box a
+missing or unloadable library is a hard error — ops never fall back silently
+to PyTorch on device tensors.  CPU tensors use the fp32 reference
+implementations in the individual op modules (that is what the CPU test tier
+exercises).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+_LIB_PATH = Path(__file__).resolve().parents[1] / "_lib" / "libgrag_kernels.so"
+_lock = threading.Lock()
+_lib = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+U64 = ctypes.c_uint64
+F = ctypes.c_float
+
+_SIGS = {
+    "grag_rmsnorm": [P, P, P, P, I, I, F, P],
+    "grag_layernorm": [P, P, P, P, P, P, I, I, F, P],
+    "grag_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, P],
+    "grag_embed_gather": [P, P, P, I, I, P],
+    "grag_qkv_rope_kvstore": [P, I, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grag_silu_mul": [P, P, I, I, P],
+    "grag_bias_act": [P, P, P, I, I, I, P],
+    "grag_pool_l2norm": [P, P, P, P, P, I, I, I, I, I, P],
+    "grag_paged_attention": [P, I, P, P, P, I, P, I, P, P, I, I, I, I, I, I, I, F, I, I, I, P, P, I, P],
+    "grag_varlen_attention": [P, P, P, I, P, I, P, P, I, I, I, I, I, F, I, P],
+    "grag_score_topk_flat": [P, I64, I64, I64, I, P, I, I, I, I, P, P, P, I, P, P, P, I, P, P, P, P, P],
+    "grag_score_topk_work": [P, I, P, I, I, I, I, P, P, I, P, P, P, I, P, P, P, I, P, P, P, P, P],
+    "grag_topk_num_waves": [],
+    "grag_sample": [P, I, I, I, I, P, P, P, P, P, P, I, P, U64, P, P, P],
+    "grag_mark_seen": [P, P, I, P, I, I, P],
+    "grag_gemm": [P, P, P, P, P, I, I, I, I, I, I, I, P],
+    "grag_gemm_skinny": [P, P, P, P, P, I, I, I, I, I, P],
+}
+
+
+def lib_path() -> Path:
+    return _LIB_PATH
+
+
+def available() -> bool:
+    return _LIB_PATH.exists()
+
+
+def lib():
+    """Return the loaded kernel library (building it if hipcc is present)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not _LIB_PATH.exists() or os.environ.get("GRAG_REBUILD") == "1":
+            from ..utils.native_build import build_kernels
+
+            build_kernels()
+        handle = ctypes.CDLL(str(_LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            fn = getattr(handle, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        _lib = handle
+        return _lib
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def check(err: int, name: str) -> None:
+    if err != 0:
+        raise RuntimeError(f"{name}: HIP kernel launch failed with hipError_t={err}")
+
+
+def call(name: str, *args) -> None:
+    """Call a kernel entry point; the trailing hipStream_t is appended here."""
+    fn = getattr(lib(), name)
+    check(fn(*args, stream_ptr()), name)
+
+
+def loaded_path() -> str | None:
+    return str(_LIB_PATH) if _lib is not None else None

@@ -1,0 +1,130 @@
+"""Attention ops over the paged KV cache (decoder) and packed QKV (encoder)."""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from ._lib import call, ptr
+
+KV_TILE = 64  # keys per kernel tile; split lengths must be multiples of this
+
+
+@dataclass
+class AttnMetadata:
+    """Per-step attention metadata (device int32 tensors).
+
+    q_start   [nseq+1]  cumulative query-token offsets
+    ctx_len   [nseq]    total keys visible to each sequence (cached + new)
+    block_tables [nseq, max_blocks]
+    slot_mapping [T]    cache slot of every new token (-1 = padding)
+    """
+
+    q_start: torch.Tensor
+    ctx_len: torch.Tensor
+    block_tables: torch.Tensor
+    slot_mapping: torch.Tensor
+    max_q_len: int
+    num_seqs: int
+    num_tokens: int
+    is_decode: bool = False
+    num_splits: int = 1
+    split_len: int = 1 << 30
+    part_o: torch.Tensor | None = None
+    part_ml: torch.Tensor | None = None
+    extra: dict = field(default_factory=dict)
+
+
+def choose_splits(max_ctx: int, nseq: int, hkv: int, target_wgs: int = 1024, split_min: int = 256):
+    """Split-KV plan for decode: enough workgroups to fill 256 CUs."""
+    tiles = max(1, (max_ctx + KV_TILE - 1) // KV_TILE)
+    base = max(1, nseq * hkv)
+    want = max(1, min(tiles, (target_wgs + base - 1) // base))
+    split_tiles = max(split_min // KV_TILE, (tiles + want - 1) // want)
+    split_len = split_tiles * KV_TILE
+    nsplit = (max_ctx + split_len - 1) // split_len
+    return max(1, nsplit), split_len
+
+
+def paged_attention_ref(q, k_cache, v_cache, meta: AttnMetadata, scale: float, causal: bool = True):
+    """fp32 reference: q [T, Hq, D] -> out [T, Hq, D]."""
+    T, Hq, D = q.shape
+    Hkv, BS = k_cache.shape[1], k_cache.shape[2]
+    G = Hq // Hkv
+    out = torch.zeros(T, Hq, D, dtype=torch.float32, device=q.device)
+    qs = meta.q_start.tolist()
+    cl = meta.ctx_len.tolist()
+    bt = meta.block_tables
+    for s in range(meta.num_seqs):
+        a, b = qs[s], qs[s + 1]
+        ql, ctx = b - a, cl[s]
+        if ql == 0:
+            continue
+        nblk = (ctx + BS - 1) // BS
+        blocks = bt[s, :nblk].long()
+        K = k_cache[blocks].permute(0, 2, 1, 3).reshape(-1, Hkv, D)[:ctx].float()
+        V = v_cache[blocks].permute(0, 2, 1, 3).reshape(-1, Hkv, D)[:ctx].float()
+        K = K.repeat_interleave(G, dim=1)
+        V = V.repeat_interleave(G, dim=1)
+        qq = q[a:b].float()
+        sc = torch.einsum("phd,khd->hpk", qq, K) * scale
+        if causal:
+            pos = torch.arange(ctx - ql, ctx, device=q.device)[:, None]
+            kk = torch.arange(ctx, device=q.device)[None, :]
+            sc = sc.masked_fill((kk > pos)[None], float("-inf"))
+        p = torch.softmax(sc, dim=-1)
+        out[a:b] = torch.einsum("hpk,khd->phd", p, V)
+    return out.to(q.dtype)
+
+
+def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMetadata,
+                    scale: float, causal: bool = True, out: torch.Tensor | None = None) -> torch.Tensor:
+    """q [T, Hq, D] (token-major) -> out [T, Hq*D]."""
+    if not q.is_cuda:
+        return paged_attention_ref(q, k_cache, v_cache, meta, scale, causal).reshape(q.shape[0], -1)
+    T, Hq, D = q.shape
+    Hkv, BS = k_cache.shape[1], k_cache.shape[2]
+    if out is None:
+        out = torch.empty(T, Hq * D, dtype=q.dtype, device=q.device)
+    nsplit = meta.num_splits if meta.is_decode else 1
+    nw = 1 if meta.is_decode else 4
+    call("grag_paged_attention", ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(out), out.stride(0),
+         ptr(meta.block_tables), meta.block_tables.stride(0), ptr(meta.q_start), ptr(meta.ctx_len),
+         meta.num_seqs, T, meta.max_q_len, Hq, Hkv, D, BS, float(scale), 1 if causal else 0, nsplit,
+         meta.split_len if nsplit > 1 else 0, ptr(meta.part_o) if nsplit > 1 else None,
+         ptr(meta.part_ml) if nsplit > 1 else None, nw)
+    return out
+
+
+def varlen_attention_ref(qkv, seq_start, H, D, scale, causal=False):
+    T = qkv.shape[0]
+    x = qkv.float().view(T, 3, H, D)
+    out = torch.zeros(T, H, D, dtype=torch.float32, device=qkv.device)
+    ss = seq_start.tolist()
+    for s in range(len(ss) - 1):
+        a, b = ss[s], ss[s + 1]
+        if b <= a:
+            continue
+        q, k, v = x[a:b, 0], x[a:b, 1], x[a:b, 2]
+        sc = torch.einsum("phd,khd->hpk", q, k) * scale
+        if causal:
+            L = b - a
+            sc = sc.masked_fill(torch.ones(L, L, dtype=torch.bool, device=qkv.device).triu(1)[None], float("-inf"))
+        out[a:b] = torch.einsum("hpk,khd->phd", torch.softmax(sc, -1), v)
+    return out.reshape(T, H * D).to(qkv.dtype)
+
+
+def varlen_attention(qkv: torch.Tensor, seq_start: torch.Tensor, seq_len: torch.Tensor, max_len: int,
+                     H: int, D: int, scale: float, causal: bool = False) -> torch.Tensor:
+    """Self-attention over packed QKV rows [T, 3*H*D] (encoder layers, no padding
+    tokens computed) -> [T, H*D]."""
+    if not qkv.is_cuda:
+        return varlen_attention_ref(qkv, seq_start, H, D, scale, causal)
+    T = qkv.shape[0]
+    out = torch.empty(T, H * D, dtype=qkv.dtype, device=qkv.device)
+    base = qkv.data_ptr()
+    es = qkv.element_size()
+    call("grag_varlen_attention", base, base + H * D * es, base + 2 * H * D * es, qkv.stride(0), ptr(out),
+         out.stride(0), ptr(seq_start), ptr(seq_len), seq_len.numel(), max_len, H, H, D, float(scale),
+         1 if causal else 0)
+    return out

@@ -1,0 +1,112 @@
+"""Fused sampler op + persistent per-slot sampler state."""
+from __future__ import annotations
+
+import torch
+
+from ._lib import call, ptr
+
+
+class SamplerState:
+    """Per-slot sampling parameters, seen-token bitmaps and RNG counters kept
+    on device so the decode step (forward + LM head + sampler) can be replayed
+    from a captured hipGraph with no host round trip besides the token read."""
+
+    def __init__(self, max_slots: int, vocab: int, device, seed: int = 0):
+        self.max_slots = max_slots
+        self.vocab = vocab
+        self.words = (vocab + 31) // 32
+        self.device = torch.device(device)
+        self.seed = int(seed) & ((1 << 63) - 1)
+        self.temperature = torch.ones(max_slots, dtype=torch.float32, device=device)
+        self.top_p = torch.ones(max_slots, dtype=torch.float32, device=device)
+        self.top_k = torch.zeros(max_slots, dtype=torch.int32, device=device)
+        self.penalty = torch.ones(max_slots, dtype=torch.float32, device=device)
+        self.seen = torch.zeros(max_slots, self.words, dtype=torch.int32, device=device)
+        self.rng = torch.zeros(max_slots, dtype=torch.int64, device=device)
+
+    def reset_slot(self, slot: int, temperature: float, top_p: float, top_k: int, penalty: float,
+                   prompt_ids, seed: int | None = None) -> None:
+        self.temperature[slot] = float(temperature)
+        self.top_p[slot] = float(top_p)
+        self.top_k[slot] = int(top_k)
+        self.penalty[slot] = float(penalty)
+        self.rng[slot] = int(seed) if seed is not None else 0
+        self.seen[slot].zero_()
+        if penalty != 1.0 and len(prompt_ids):
+            toks = torch.as_tensor(list(prompt_ids), dtype=torch.int32, device=self.device)
+            mark_seen(self, toks, torch.full_like(toks, slot))
+
+
+def mark_seen(state: SamplerState, tokens: torch.Tensor, slots: torch.Tensor) -> None:
+    if not tokens.is_cuda:
+        t = tokens.long()
+        ok = (t >= 0) & (t < state.vocab)
+        t, s = t[ok], slots.long()[ok]
+        words = state.seen.view(torch.int32)
+        for ti, si in zip(t.tolist(), s.tolist()):
+            w = words[si, ti >> 5].item() | (1 << (ti & 31))
+            words[si, ti >> 5] = w - (1 << 32) if w >= (1 << 31) else w
+        return
+    call("grag_mark_seen", ptr(tokens.to(torch.int32).contiguous()), ptr(slots.to(torch.int32).contiguous()),
+         tokens.numel(), ptr(state.seen), state.words, state.vocab)
+
+
+def _seen_mask(state, slot, V, device):
+    words = state.seen[slot].long() & 0xFFFFFFFF
+    idx = torch.arange(V, device=device)
+    return ((words[idx >> 5] >> (idx & 31)) & 1).bool()
+
+
+def sample_ref(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, generator=None) -> torch.Tensor:
+    """Reference sampler with identical semantics (different RNG stream)."""
+    B, V = logits.shape[0], state.vocab
+    out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    for b in range(B):
+        s = int(slots[b])
+        x = logits[b, :V].float().clone()
+        pen = float(state.penalty[s])
+        if pen != 1.0:
+            m = _seen_mask(state, s, V, logits.device)
+            x = torch.where(m, torch.where(x > 0, x / pen, x * pen), x)
+        t = float(state.temperature[s])
+        if t <= 0:
+            tok = int(torch.argmax(x))
+        else:
+            x = x / t
+            k = int(state.top_k[s])
+            keep = torch.ones(V, dtype=torch.bool, device=x.device)
+            if 0 < k < V:
+                thr = torch.topk(x, k).values[-1]
+                keep &= x >= thr
+            p = float(state.top_p[s])
+            if p < 1.0:
+                xs = torch.where(keep, x, torch.full_like(x, float("-inf")))
+                probs = torch.softmax(xs, 0)
+                sp, si = probs.sort(descending=True)
+                csum = sp.cumsum(0)
+                n = int((csum < p).sum()) + 1
+                thr = x[si[min(n, V) - 1]]
+                keep &= x >= thr
+            xs = torch.where(keep, x, torch.full_like(x, float("-inf")))
+            tok = int(torch.multinomial(torch.softmax(xs, 0), 1, generator=generator))
+        out[b] = tok
+        if True:  # the kernel always records the sampled token
+            w = int(state.seen[s, tok >> 5]) & 0xFFFFFFFF
+            w |= 1 << (tok & 31)
+            state.seen[s, tok >> 5] = w - (1 << 32) if w >= (1 << 31) else w
+        state.rng[s] += 1
+    return out
+
+
+def sample(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, out: torch.Tensor | None = None):
+    """logits [B, >=V] (fp32 or bf16) -> sampled token ids int32 [B]."""
+    if not logits.is_cuda:
+        return sample_ref(logits, state, slots)
+    B = logits.shape[0]
+    if out is None:
+        out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    dtype = 0 if logits.dtype == torch.float32 else 1
+    call("grag_sample", ptr(logits), dtype, logits.stride(0), B, state.vocab, ptr(state.temperature),
+         ptr(state.top_p), ptr(state.top_k), ptr(state.penalty), ptr(state.seen), state.words, ptr(state.rng),
+         state.seed, ptr(slots), ptr(out))
+    return out

@@ -1,0 +1,159 @@
+"""Process groups and collectives.
+
+One process per GPU; ``torch.distributed`` with backend ``"nccl"`` is RCCL on
+ROCm (collectives over xGMI), ``"gloo"`` is the CPU fallback used by the
+multi-process CPU tests.  The reference has no collectives at all (SURVEY
+§2.8); the ones here are introduced by the MI355X design:
+
+* C1  TP all-reduce of row-parallel projections (Qwen2 o_proj / down_proj)
+* C2  TP all-gather of vocab-parallel LM-head logits
+* C3  DP all-gather of per-shard top-k lists for the sharded vector index
+* C5  all-gather of scalar counts (ingest id assignment)
+* C6  all-reduce of k-means centroid sums/counts (IVF training across shards)
+
+xGMI is point-to-point (7 links per GPU), so small latency-bound messages
+(decode all-reduce [B, hidden], top-k lists of a few KB) are issued as single
+fused collectives per step rather than many small ones.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+
+_INFO = DistInfo()
+
+
+def env_world() -> tuple[int, int, int]:
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))))
+
+
+def init_distributed(backend: str | None = None, timeout_s: int = 600) -> DistInfo:
+    """Initialise the default process group from torchrun-style env vars.
+    Single-process runs get a trivial DistInfo and no process group."""
+    global _INFO
+    rank, world, local = env_world()
+    if world <= 1:
+        _INFO = DistInfo(0, 1, local, "none")
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        return _INFO
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(**kw)
+    _INFO = DistInfo(rank, world, local, backend)
+    return _INFO
+
+
+def info() -> DistInfo:
+    return _INFO
+
+
+def barrier() -> None:
+    if dist.is_available() and dist.is_initialized():
+        if _INFO.backend == "nccl":
+            dist.barrier(device_ids=[_INFO.local_rank])
+        else:
+            dist.barrier()
+
+
+class Group:
+    """A (possibly trivial) communicator over a subset of ranks."""
+
+    def __init__(self, ranks: list[int] | None = None, pg=None):
+        self.ranks = ranks or [0]
+        self.pg = pg
+        self.size = len(self.ranks)
+        me = _INFO.rank
+        self.rank = self.ranks.index(me) if me in self.ranks else 0
+
+    @property
+    def trivial(self) -> bool:
+        return self.size == 1
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if not self.trivial:
+            dist.all_reduce(t, group=self.pg)
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """[...] -> [size, ...] (one collective)."""
+        if self.trivial:
+            return t.unsqueeze(0)
+        out = torch.empty((self.size, *t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.pg)
+        return out
+
+    def all_gather_topk(self, scores: torch.Tensor, ids: torch.Tensor, k: int):
+        """C3: merge per-shard top-k lists.  scores fp32 [nq, k], ids int64
+        [nq, k] (already global ids) -> global top-k.  Packs both into one
+        fp64-sized buffer so the merge is a single all-gather."""
+        if self.trivial:
+            return scores, ids
+        nq = scores.shape[0]
+        packed = torch.empty(nq, k, 2, dtype=torch.int64, device=scores.device)
+        packed[..., 0] = ids
+        packed[..., 1] = scores.float().view(torch.int32).to(torch.int64)
+        g = self.all_gather(packed)  # [W, nq, k, 2]
+        all_ids = g[..., 0].permute(1, 0, 2).reshape(nq, -1)
+        all_s = g[..., 1].to(torch.int32).view(torch.float32).permute(1, 0, 2).reshape(nq, -1)
+        s, sel = all_s.topk(min(k, all_s.shape[1]), dim=1)
+        return s, all_ids.gather(1, sel)
+
+    def broadcast(self, t: torch.Tensor, src_local: int = 0) -> torch.Tensor:
+        if not self.trivial:
+            dist.broadcast(t, src=self.ranks[src_local], group=self.pg)
+        return t
+
+
+def world_group() -> Group:
+    if not _INFO.is_distributed:
+        return Group([0])
+    return Group(list(range(_INFO.world_size)), pg=dist.group.WORLD)
+
+
+def make_tp_dp_groups(tp: int) -> tuple[Group, Group]:
+    """Split the world into TP groups of `tp` consecutive ranks (share one
+    xGMI-connected node) and DP groups of the ranks with the same TP rank.
+    Every rank must call this (new_group is collective)."""
+    W = _INFO.world_size
+    if W == 1:
+        return Group([0]), Group([0])
+    assert W % tp == 0, f"world {W} not divisible by tp {tp}"
+    my_tp = my_dp = None
+    for s in range(0, W, tp):
+        ranks = list(range(s, s + tp))
+        pg = dist.new_group(ranks) if tp > 1 else None
+        if _INFO.rank in ranks:
+            my_tp = Group(ranks, pg)
+    for r in range(tp):
+        ranks = list(range(r, W, tp))
+        pg = dist.new_group(ranks) if len(ranks) > 1 else None
+        if _INFO.rank in ranks:
+            my_dp = Group(ranks, pg)
+    return my_tp, my_dp

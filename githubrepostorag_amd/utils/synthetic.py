@@ -1,0 +1,97 @@
+"""Deterministic synthetic data (no network on the GPU box): code-repo files,
+chunk texts addressed by id (so a 10M-row index needs no host text store),
+questions, and clustered embedding matrices for index benchmarks."""
+from __future__ import annotations
+
+import random
+
+import torch
+
+_WORDS = ("cache retry broker session token config handler queue worker index vector embed chunk module "
+          "service client request response timeout reconnect policy schema table stream event job cancel "
+          "health metrics summary parser splitter encoder decoder attention kernel batch shard gather merge "
+          "repository branch commit pipeline deploy helm redis cassandra graph traverse scope file package").split()
+_LANGS = (("py", "python"), ("java", "java"), ("ts", "typescript"), ("go", "go"), ("md", "markdown"),
+          ("yaml", "yaml"), ("sql", "sql"))
+
+
+def _rng(seed: int) -> random.Random:
+    return random.Random(seed * 2654435761 % (1 << 32))
+
+
+def words(r: random.Random, n: int) -> str:
+    return " ".join(r.choice(_WORDS) for _ in range(n))
+
+
+def code_file(r: random.Random, ext: str, n_funcs: int = 4) -> str:
+    out = []
+    for f in range(n_funcs):
+        name = f"{r.choice(_WORDS)}_{r.choice(_WORDS)}_{f}"
+        if ext == "py":
+            out.append(f"def {name}(self, {r.choice(_WORDS)}, timeout=30):\n    \"\"\"{words(r, 12)}.\"\"\"\n"
+                       f"    result = self.{r.choice(_WORDS)}.{r.choice(_WORDS)}({r.choice(_WORDS)})\n"
+                       f"    if result is None:\n        raise RuntimeError('{words(r, 5)}')\n    return result\n")
+        elif ext == "java":
+            out.append(f"public class {name.title().replace('_', '')} {{\n  // {words(r, 10)}\n"
+                       f"  public void {name}(String {r.choice(_WORDS)}) {{ log.info(\"{words(r, 4)}\"); }}\n}}\n")
+        elif ext == "ts":
+            out.append(f"export function {name}(opts: Options): Promise<Result> {{\n  // {words(r, 10)}\n"
+                       f"  return client.{r.choice(_WORDS)}(opts).then((r) => r.{r.choice(_WORDS)});\n}}\n")
+        elif ext == "go":
+            out.append(f"func {name.title().replace('_', '')}(ctx context.Context) error {{\n\t// {words(r, 10)}\n"
+                       f"\treturn nil\n}}\n")
+        elif ext == "md":
+            out.append(f"## {words(r, 3).title()}\n\n{words(r, 40)}.\n")
+        elif ext == "yaml":
+            out.append(f"{r.choice(_WORDS)}:\n  {r.choice(_WORDS)}: {r.randint(1, 100)}\n  name: {words(r, 2)}\n")
+        else:
+            out.append(f"SELECT {r.choice(_WORDS)}, {r.choice(_WORDS)} FROM {r.choice(_WORDS)} WHERE id = {f};\n")
+    return "\n".join(out)
+
+
+def synthetic_repo(seed: int, n_files: int = 24, repo: str | None = None) -> tuple[str, list[dict]]:
+    """-> (repo name, [{"file_path", "text"}]) with a README, modules and a notebook."""
+    r = _rng(seed)
+    repo = repo or f"{r.choice(_WORDS)}-{r.choice(_WORDS)}-{seed}"
+    files = [{"file_path": "README.md",
+              "text": f"# {repo}\n\nThis service handles {words(r, 30)}.\n\n## Usage\n\n{words(r, 40)}.\n"}]
+    mods = [r.choice(_WORDS) for _ in range(max(1, n_files // 6))]
+    for i in range(n_files - 1):
+        ext, _ = _LANGS[i % len(_LANGS)]
+        mod = mods[i % len(mods)]
+        files.append({"file_path": f"{mod}/{r.choice(_WORDS)}_{i}.{ext}", "text": code_file(r, ext, 3 + i % 4)})
+    files.append({"file_path": "LICENSE", "text": "MIT License\n" + words(r, 50)})
+    files.append({"file_path": "assets/logo.png", "text": "\x89PNG binary"})
+    return repo, files
+
+
+def chunk_text(doc_id: int, n_chars: int = 800) -> str:
+    """Text of synthetic index row `doc_id` (regenerated on demand)."""
+    r = _rng(doc_id + 1)
+    out = []
+    while sum(len(x) + 1 for x in out) < n_chars:
+        out.append(code_file(r, _LANGS[r.randrange(len(_LANGS))][0], 1))
+    return "\n".join(out)[:n_chars]
+
+
+def question(i: int) -> str:
+    r = _rng(10_000_019 + i)
+    return (f"How does the {r.choice(_WORDS)} {r.choice(_WORDS)} handle {r.choice(_WORDS)} "
+            f"{r.choice(_WORDS)} when the {r.choice(_WORDS)} {r.choice(_WORDS)} times out?")
+
+
+@torch.inference_mode()
+def clustered_vectors(n: int, d: int, n_centers: int = 4096, noise: float = 0.35, seed: int = 0,
+                      device="cuda", chunk: int = 1 << 20) -> torch.Tensor:
+    """bf16 [n, d] unit vectors drawn around random unit centres."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    C = torch.randn(n_centers, d, generator=g, device=device)
+    C = C / C.norm(dim=1, keepdim=True)
+    out = torch.empty(n, d, dtype=torch.bfloat16, device=device)
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        c = torch.randint(0, n_centers, (m,), generator=g, device=device)
+        x = C[c] + noise * torch.randn(m, d, generator=g, device=device) / d ** 0.5
+        out[s:s + m] = (x / x.norm(dim=1, keepdim=True)).to(torch.bfloat16)
+    return out
