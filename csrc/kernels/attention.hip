@@ -66,6 +66,28 @@ __device__ __forceinline__ int vswz(int row) {
 
 typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4_t;
 
+// One LDS-DMA wave instruction (global_load_lds_dwordx4): 16 B per lane from
+// each lane's `src` into the 1 KiB LDS block at wave-uniform `lds_dst`
+// (lane-linear).  Issued from inline asm so hipcc's waitcnt pass does not see
+// an LDS write it cannot disambiguate between ring stages (it would put a
+// vmcnt(0) in front of every ds_read); completion is tracked only by the
+// caller's explicit counted `s_waitcnt vmcnt(N)` (cdna guide §5.7 recipe:
+// M0 saved, set, used and restored inside one statement).
+__device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
+  const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds_dst;
+  const uint32_t lu = __builtin_amdgcn_readfirstlane(lds);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lu)
+      : "memory");
+}
+
 template <int D, int NW, bool PAGED>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   constexpr int CPR = D / 8;      // 16-B chunks per K/V row
@@ -236,6 +258,194 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Decode (q_len == 1) specialisation: one wave per (sequence, kv head, split).
+// The GQA group's G <= 16 query heads are the 16 MFMA columns.  K/V tiles are
+// fetched by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave instruction,
+// destination lane-linear, so the XOR swizzle of the K and V images is applied
+// to the per-lane SOURCE address — cdna guide §5.4 rule 21) into a 2-stage
+// ring; the block-table entry of every 4..16-key group is wave-uniform and
+// comes through the scalar cache, so no vector load sits between two tiles.
+// Tile t+1 is issued before tile t is computed and retired with a counted
+// vmcnt, keeping 32 KiB per wave in flight under the MFMA/softmax work.
+template <int D>
+__global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
+  constexpr int RB = 2 * D;
+  constexpr int CPR = D / 8;
+  constexpr int NC = D / 32;
+  constexpr int ND = D / 16;
+  constexpr int TILE = KT * RB;      // bytes per K (or V) tile
+  constexpr int NI = TILE / 1024;    // LDS-DMA instructions per tile per tensor
+  constexpr int RPI = 1024 / RB;     // rows per instruction
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+
+  const int lane = threadIdx.x;
+  const int h4 = lane >> 4, li = lane & 15;
+  const int seq = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
+  const int ctx = p.ctx_len[seq];
+  const int kv_lo = split * p.split_len;
+  const int kv_hi = min(ctx, kv_lo + p.split_len);
+  if (kv_lo >= kv_hi) return;
+  const int G = p.G;
+  const bool row_valid = li < G;
+  const int tok = p.q_start[seq];
+  bf16x8_t qf[NC];
+  {
+    const bf16* qp = p.q + (size_t)tok * p.q_stride + (size_t)(kvh * G + (row_valid ? li : 0)) * D + 8 * h4;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) qf[c] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * c);
+  }
+  const int32_t* bt = p.block_tables + (size_t)seq * p.bt_stride;
+  const int lrow = lane / CPR, lch = lane % CPR;
+  // Block ids of a 64-block window live one per lane; readlane with a
+  // wave-uniform index hands them to the scalar unit, so no vector load ever
+  // sits between two LDS-DMA issues (a vector load there costs a vmcnt(0)
+  // drain of the whole pipeline).
+  // A 64-key tile never straddles a window (64 blocks x BS keys, BS % 16 == 0),
+  // so the window is refreshed at most once per tile, outside the unrolled
+  // issue loop (once per split for split_len <= 64*BS).
+  const int nblk_seq = (ctx + p.BS - 1) / p.BS;
+  int win = (kv_lo / p.BS) >> 6;
+  int bvec = bt[min((win << 6) + lane, nblk_seq - 1)];
+  // Retire the Q and block-id loads with a wait hipcc understands, so its
+  // scoreboard is empty when the asm-issued LDS-DMA pipeline starts (else it
+  // re-waits vmcnt(0) for them inside every iteration).
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#pragma unroll
+  for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(qf[c]));
+  asm volatile("" : "+v"(bvec));
+
+  auto issue = [&](int kt0, int stage) {
+    char* kdst = smem + stage * 2 * TILE;
+    char* vdst = kdst + TILE;
+    const int w = (kt0 / p.BS) >> 6;
+    if (w != win) {
+      win = w;
+      bvec = bt[min((w << 6) + lane, nblk_seq - 1)];
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int key0 = min(kt0 + i * RPI, ctx - 1);        // wave-uniform
+      const int blk = __builtin_amdgcn_readlane(bvec, (key0 / p.BS) & 63);
+      const int row = i * RPI + lrow;
+      const int key = min(kt0 + row, ctx - 1);
+      const size_t off = (((size_t)blk * p.Hkv + kvh) * p.BS + (key % p.BS)) * D;
+      const bf16* ks = p.k + off + ((lch ^ kswz<D>(row)) << 3);
+      const bf16* vs = p.v + off + ((lch ^ vswz<D>(row)) << 3);
+      glds16(ks, kdst + i * 1024);
+      glds16(vs, vdst + i * 1024);
+    }
+  };
+
+  float m = -INFINITY, lsum = 0.f;
+  f32x4_t o[ND];
+#pragma unroll
+  for (int n = 0; n < ND; ++n) o[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int ntiles = (kv_hi - kv_lo + KT - 1) / KT;
+  issue(kv_lo, 0);
+  for (int t = 0; t < ntiles; ++t) {
+    const int stage = t & 1;
+    const int kt0 = kv_lo + t * KT;
+    if (t + 1 < ntiles) {
+      issue(kt0 + KT, stage ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const char* k_lds = smem + stage * 2 * TILE;
+    const char* v_lds = k_lds + TILE;
+    f32x4_t s[4];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      s[tt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int row = 16 * tt + li;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const bf16x8_t a =
+            *reinterpret_cast<const bf16x8_t*>(k_lds + row * RB + (((4 * c + h4) ^ kswz<D>(row)) << 4));
+        s[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[c], s[tt], 0, 0, 0);
+      }
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt0 + 16 * tt + 4 * h4 + r;
+        float x = s[tt][r] * p.scale_log2;
+        if (key >= kv_hi) x = -INFINITY;
+        s[tt][r] = x;
+        tmax = fmaxf(tmax, x);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m, tmax);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = exp2f(m - m_use);
+    m = m_new;
+    lsum *= alpha;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) o[n] *= alpha;
+    float pr[4][4];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pr[tt][r] = exp2f(s[tt][r] - m_use);
+        lsum += pr[tt][r];
+      }
+    const int tq = li >> 2, tp = li & 3;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      bf16x8_t bp;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bp[r] = f2bits(pr[2 * cc][r]);
+        bp[4 + r] = f2bits(pr[2 * cc + 1][r]);
+      }
+      const int r0 = 32 * cc + 4 * h4 + tq;
+      const int r1 = r0 + 16;
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+        const int unit = 4 * n + tp;
+        const int b0 = r0 * RB + ((unit ^ (vswz<D>(r0) << 1)) << 3);
+        const int b1 = r1 * RB + ((unit ^ (vswz<D>(r1) << 1)) << 3);
+        const bf16x4_t a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(v_lds + b0));
+        const bf16x4_t a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(v_lds + b1));
+        const bf16x8_t a = bf16x8_t{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bp, o[n], 0, 0, 0);
+      }
+    }
+    // every LDS read of this stage has been consumed before the next issue
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (!row_valid) return;
+  const int head = kvh * G + li;
+  if (p.num_splits > 1) {
+    float* po = p.part_o + (((size_t)split * p.total_q + tok) * p.Hq + head) * D;
+#pragma unroll
+    for (int n = 0; n < ND; ++n)
+      *reinterpret_cast<float4*>(po + 16 * n + 4 * h4) = make_float4(o[n][0], o[n][1], o[n][2], o[n][3]);
+    if (h4 == 0) {
+      float* pm = p.part_ml + (((size_t)split * p.total_q + tok) * p.Hq + head) * 2;
+      pm[0] = m;
+      pm[1] = lsum;
+    }
+  } else {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16* op = p.out + (size_t)tok * p.out_stride + (size_t)head * D;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+      bf16x4_t w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = f2bits(o[n][r] * inv);
+      *reinterpret_cast<bf16x4_t*>(op + 16 * n + 4 * h4) = w;
+    }
+  }
+}
+
 // Combine split-KV partials of decode (q_len == 1 per sequence: token == seq).
 template <int D>
 __global__ __launch_bounds__(D) void attn_combine_kernel(AttnParams p) {
@@ -272,7 +482,26 @@ int launch(const AttnParams& prm, int nseq, hipStream_t stream) {
 }
 
 template <int D>
+int launch_decode(const AttnParams& prm, int nseq, hipStream_t stream) {
+  dim3 grid(nseq, prm.Hkv, prm.num_splits);
+  paged_decode_kernel<D><<<grid, 64, 0, stream>>>(prm);
+  int err = (int)hipGetLastError();
+  if (err) return err;
+  if (prm.num_splits > 1) {
+    dim3 g2(prm.total_q, prm.Hq);
+    attn_combine_kernel<D><<<g2, D, 0, stream>>>(prm);
+    err = (int)hipGetLastError();
+  }
+  return err;
+}
+
+template <int D>
 int dispatch_nw(const AttnParams& prm, int nseq, int nw, bool paged, hipStream_t stream) {
+  // nw == 1 with q_len == 1: LDS-DMA pipelined decode kernel; nw == 2: the
+  // generic kernel with one wave per workgroup (kept for A/B comparisons)
+  if (paged && nw == 1 && prm.tiles_per_seq == 1 && prm.G <= 16 && prm.BS % 16 == 0)
+    return launch_decode<D>(prm, nseq, stream);
+  if (nw == 2) nw = 1;
   if (paged) {
     return nw == 1 ? launch<D, 1, true>(prm, nseq, stream) : launch<D, 4, true>(prm, nseq, stream);
   }
@@ -294,7 +523,7 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
                                   float scale, int causal, int num_splits, int split_len,
                                   float* part_o, float* part_ml, int nw, hipStream_t stream) {
   if (nseq <= 0) return 0;
-  if (Hq % Hkv != 0 || BS <= 0 || (nw != 1 && nw != 4)) return (int)hipErrorInvalidValue;
+  if (Hq % Hkv != 0 || BS <= 0 || (nw != 1 && nw != 2 && nw != 4)) return (int)hipErrorInvalidValue;
   if (num_splits > 1 && (max_q_len != 1 || !part_o || !part_ml || split_len % KT != 0))
     return (int)hipErrorInvalidValue;
   AttnParams prm{};
@@ -315,7 +544,9 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
   prm.G = Hq / Hkv;
   prm.BS = BS;
   prm.bt_stride = bt_stride;
-  prm.tiles_per_seq = (max_q_len * prm.G + 16 * nw - 1) / (16 * nw);
+  const int nwr = nw == 2 ? 1 : nw;
+  prm.tiles_per_seq = (max_q_len * prm.G + 16 * nwr - 1) / (16 * nwr);
+  if (nw == 1 && max_q_len != 1) return (int)hipErrorInvalidValue;
   prm.num_splits = num_splits < 1 ? 1 : num_splits;
   prm.split_len = prm.num_splits > 1 ? split_len : (1 << 30);
   prm.total_q = total_q;

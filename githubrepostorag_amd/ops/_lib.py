@@ -40,10 +40,9 @@ _SIGS = {
     "grag_score_topk_flat": [P, I64, I64, I64, I, P, I, I, I, I, P, P, P, I, P, P, P, I, P, P, P, P, P],
     "grag_score_topk_work": [P, I, P, I, I, I, I, P, P, I, P, P, P, I, P, P, P, I, P, P, P, P, P],
     "grag_topk_num_waves": [],
-    "grag_sample": [P, I, I, I, I, P, P, P, P, P, P, I, P, U64, P, P, P],
+    "grag_sample": [P, I, I, I, I, P, P, P, P, P, I, P, U64, P, P, P],
     "grag_mark_seen": [P, P, I, P, I, I, P],
-    "grag_gemm": [P, P, P, P, P, I, I, I, I, I, I, I, P],
-    "grag_gemm_skinny": [P, P, P, P, P, I, I, I, I, I, P],
+    "grag_gemm_skinny": [P, P, P, P, I, I, I, I, I, I, I, P],
 }
 
 

@@ -1,0 +1,129 @@
+"""Interleaved A/B micro-benchmarks of hot ops on the real model shapes
+(one process, several rounds, median/min per variant — cdna guide §5.4 rule 24)."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from githubrepostorag_amd.ops import attention as A
+from githubrepostorag_amd.ops import sampling as S
+from githubrepostorag_amd.ops.linear import gemm_skinny
+
+
+def timeit(fn, iters=50):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1000.0  # us
+
+
+def rounds(variants, n=5, iters=50):
+    res = {k: [] for k in variants}
+    for _ in range(n):
+        for k, fn in variants.items():
+            res[k].append(timeit(fn, iters))
+    return {k: {"median_us": round(statistics.median(v), 2), "min_us": round(min(v), 2)} for k, v in res.items()}
+
+
+def gemm_bench(M):
+    out = {}
+    dev = torch.device("cuda")
+    for name, N, K in [("qkv", 4608, 3584), ("o_proj", 3584, 3584), ("gate_up", 37888, 3584), ("down", 3584, 18944),
+                       ("lm_head", 152064, 3584)]:
+        x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+        # rotate through >= 1 GiB of weight copies: in a real decode step the
+        # other ~15 GB of weights evict each matrix from the 256 MB MALL
+        ncopy = max(2, min(16, (1 << 30) // (N * K * 2) + 1))
+        ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02 for _ in range(ncopy)]
+        it = {"i": 0}
+
+        def nxt():
+            it["i"] = (it["i"] + 1) % ncopy
+            return ws[it["i"]]
+
+        r = rounds({"hipblaslt": lambda: torch.nn.functional.linear(x, nxt()),
+                    "grag_skinny": lambda: gemm_skinny(x, nxt())})
+        del ws
+        gb = N * K * 2 / 1e9
+        for k in r:
+            r[k]["TB_s"] = round(gb / (r[k]["min_us"] * 1e-6) / 1e3, 2)
+        out[f"{name}_M{M}"] = r
+    return out
+
+
+def attn_decode_bench(B, ctx, split_len):
+    dev = torch.device("cuda")
+    Hq, Hkv, D, BS = 28, 4, 128, 16
+    nb = B * ((ctx + BS - 1) // BS) + 1
+    kc = torch.randn(nb, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    q = torch.randn(B, Hq, D, device=dev, dtype=torch.bfloat16)
+    bt = torch.randperm(nb - 1, device=dev)[: B * ((ctx + BS - 1) // BS)].view(B, -1).to(torch.int32) + 1
+    ns = (ctx + split_len - 1) // split_len
+    meta = A.AttnMetadata(q_start=torch.arange(B + 1, device=dev, dtype=torch.int32),
+                          ctx_len=torch.full((B,), ctx, device=dev, dtype=torch.int32), block_tables=bt,
+                          slot_mapping=torch.zeros(B, dtype=torch.int32, device=dev), max_q_len=1, num_seqs=B,
+                          num_tokens=B, is_decode=True, num_splits=ns, split_len=split_len,
+                          part_o=torch.empty(ns * B * Hq * D, device=dev), part_ml=torch.empty(ns * B * Hq * 2, device=dev))
+    r = rounds({f"paged_decode_split{split_len}": lambda: A.paged_attention(q, kc, vc, meta, 0.088)})
+    gb = B * ctx * Hkv * D * 2 * 2 / 1e9
+    for k in r:
+        r[k]["TB_s"] = round(gb / (r[k]["min_us"] * 1e-6) / 1e3, 2)
+    return r
+
+
+def attn_prefill_bench(nseq, L):
+    dev = torch.device("cuda")
+    Hq, Hkv, D, BS = 28, 4, 128, 16
+    nbs = (L + BS - 1) // BS
+    kc = torch.randn(nseq * nbs + 1, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    q = torch.randn(nseq * L, Hq, D, device=dev, dtype=torch.bfloat16)
+    bt = (torch.arange(nseq * nbs, device=dev, dtype=torch.int32) + 1).view(nseq, nbs)
+    meta = A.AttnMetadata(q_start=torch.arange(0, nseq * L + 1, L, device=dev, dtype=torch.int32),
+                          ctx_len=torch.full((nseq,), L, device=dev, dtype=torch.int32), block_tables=bt,
+                          slot_mapping=torch.zeros(nseq * L, dtype=torch.int32, device=dev), max_q_len=L,
+                          num_seqs=nseq, num_tokens=nseq * L)
+    r = rounds({"paged_prefill": lambda: A.paged_attention(q, kc, vc, meta, 0.088)}, n=3, iters=10)
+    fl = nseq * Hq * L * L / 2 * D * 4 / 1e12
+    for k in r:
+        r[k]["TFLOPs"] = round(fl / (r[k]["min_us"] * 1e-6), 1)
+    return r
+
+
+def sampler_bench(B):
+    dev = torch.device("cuda")
+    V = 152064
+    st = S.SamplerState(B, V, dev)
+    for i in range(B):
+        st.reset_slot(i, 0.4, 0.8, 0, 1.2, list(range(0, 2000, 7)))
+    logits = torch.randn(B, V, device=dev, dtype=torch.bfloat16) * 3
+    slots = torch.arange(B, device=dev, dtype=torch.int32)
+    return rounds({"sampler_top_p": lambda: S.sample(logits, st, slots)})
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--what", default="all")
+    args = ap.parse_args()
+    res = {}
+    if args.what in ("all", "gemm"):
+        for M in (1, 8, 64):
+            res.update(gemm_bench(M))
+    if args.what in ("all", "attn"):
+        for sl in (256, 512):
+            res[f"decode_B64_ctx1152_split{sl}"] = attn_decode_bench(64, 1152, sl)
+        res["decode_B1_ctx4096_split64"] = attn_decode_bench(1, 4096, 64)
+        res["prefill_16x1024"] = attn_prefill_bench(16, 1024)
+    if args.what in ("all", "sampler"):
+        res["sampler_B64"] = sampler_bench(64)
+    print(json.dumps(res, indent=1))

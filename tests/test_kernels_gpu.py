@@ -244,3 +244,18 @@ def test_sampler(dev):
     # bf16 logits path + seen-bit bookkeeping
     out2 = S.sample(logits.to(torch.bfloat16), st, slots)
     assert out2.shape == (3,)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 4608, 3584), (7, 3584, 3584), (33, 1000, 512), (64, 37888, 3584),
+                                   (64, 3584, 18944), (50, 2048, 128)])
+def test_gemm_skinny(dev, M, N, K):
+    from githubrepostorag_amd.ops.linear import gemm_skinny
+
+    x = rnd(M, K, dev=dev, scale=0.5)
+    w = rnd(N, K, dev=dev, scale=0.05, seed=1)
+    b = rnd(N, dev=dev, seed=2)
+    y = gemm_skinny(x, w, b)
+    ref = x.float().cpu() @ w.float().cpu().T + b.float().cpu()
+    close(y, ref, 3e-2, 2e-2)
+    for nt in (16, 32, 64):
+        close(gemm_skinny(x, w, None, nt), ref - b.float().cpu(), 3e-2, 2e-2)
