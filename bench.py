@@ -172,13 +172,19 @@ def main():
     if not args.no_ingest and args.ingest_files > 0:
         from githubrepostorag_amd.ingest.bench_ingest import run_ingest_bench
 
-        dps = run_ingest_bench(eng, emb, args.ingest_files, seed=rank)
-        tt = torch.tensor([dps], dtype=torch.float64, device=dev)
+        del eng  # release the serving engine's KV cache; ingest builds a long-context engine
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        comm.barrier()
+        n_docs, secs = run_ingest_bench(model, tok, emb, args.ingest_files, seed=rank,
+                                        use_graph=not args.no_graph)
+        tt = torch.tensor([secs], dtype=torch.float64, device=dev)
         if world > 1:
             import torch.distributed as dist
 
-            dist.all_reduce(tt)
-        ingest_dps = float(tt.item())
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ingest_dps = n_docs * world / float(tt.item())
+        log(f"ingest: {n_docs} docs/rank in {float(tt.item()):.2f}s")
 
     if rank == 0:
         res = {

@@ -1,0 +1,363 @@
+"""Agentic retrieval loop: plan_scope -> retrieve (+query expansion) -> judge
+-> rewrite_or_end -> (retrieve again | synthesize), at most ``max_iters``
+attempts — the reference's LangGraph ``GraphAgent``
+(rag_worker/src/worker/services/agent_graph.py:87-543) as a plain state
+machine with the same node semantics, prompts and fallbacks.
+
+Deliberate fixes of reference defects:
+* per-call run context: the progress callback and cancel check travel with
+  the call instead of being swapped on a shared singleton (quirk 5: with
+  max_jobs=10 events of one job could land on another job's channel);
+* ``sources`` are returned explicitly (quirk 3: they were dropped by the
+  TypedDict state) and carry real similarity scores (quirk 4);
+* cancellation is checked before every node and aborts in-flight LLM calls
+  (quirk 7: checked once before the run).
+Optional: the synthesis answer can be streamed token by token.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import re
+import threading
+from dataclasses import dataclass, field
+from typing import Any, Callable, Optional
+
+from . import prompts
+
+log = logging.getLogger(__name__)
+
+TECH_SYNONYMS = {"activemq": ["activemq", "jms", "amq", "failovertransport", "redeliverypolicy", "broker", "stomp"]}
+_CODEY = ("stacktrace", "traceback", "exception", "error", "class ", "function ", "method ", "nullpointer",
+          "undefined", "timeout", "reconnect", "retry", "activemq", "jms")
+_CONSERVATIVE = ("insufficient", "don't see enough", "can't answer", "not enough information")
+NEXT_SCOPE = {"project": "package", "package": "file", "file": "code"}
+
+
+class Cancelled(Exception):
+    pass
+
+
+def looks_codey(q: str) -> bool:
+    ql = q.lower()
+    return any(s in ql for s in _CODEY)
+
+
+def extract_repo_hint(q: str) -> Optional[str]:
+    m = re.search(r"(?:repo(?:sitory)?[:\s]+)([\w\-./]+)", q, re.I)
+    return m.group(1) if m else None
+
+
+def score_of(doc: Any) -> Optional[float]:
+    md = getattr(doc, "metadata", {}) or {}
+    for k in ("_similarity_score", "_score", "score", "similarity", "distance"):
+        v = md.get(k)
+        if isinstance(v, (int, float)):
+            return float(v)
+        try:
+            return float(v)
+        except (TypeError, ValueError):
+            pass
+    s = getattr(doc, "score", None)
+    try:
+        return float(s) if s is not None else None
+    except (TypeError, ValueError):
+        return None
+
+
+def _content(doc: Any) -> str:
+    return getattr(doc, "page_content", "") or getattr(doc, "text", "") or ""
+
+
+def doc_to_source(i: int, doc: Any) -> dict:
+    md = getattr(doc, "metadata", {}) or {}
+    return {"block": i, "score": score_of(doc),
+            "metadata": {"scope": md.get("scope", ""), "namespace": md.get("namespace", ""),
+                         "repo": md.get("repo", ""), "module": md.get("module", ""),
+                         "file_path": md.get("file_path", ""), "file_name": (md.get("file_path") or "").split("/")[-1],
+                         "topics": md.get("topics", "")},
+            "text": _content(doc)[:1200]}
+
+
+def _json_object(raw: str) -> dict:
+    raw = raw[raw.find("{"): raw.rfind("}") + 1]
+    data = json.loads(raw)
+    if not isinstance(data, dict):
+        raise ValueError("not an object")
+    return data
+
+
+def _merge_filters(filters: dict, suggested: dict | None) -> None:
+    for k, v in (suggested or {}).items():
+        if isinstance(v, str) and v:
+            filters[k] = v
+        elif isinstance(v, list) and v:
+            filters[k.rstrip("s") if k.endswith("s") else k] = v[0]
+
+
+@dataclass
+class RunContext:
+    progress_cb: Optional[Callable[[dict], None]] = None
+    cancel_check: Optional[Callable[[], bool]] = None
+    on_answer_token: Optional[Callable[[str], None]] = None
+    turns: list = field(default_factory=list)
+
+    def notify(self, payload: dict) -> None:
+        if self.progress_cb:
+            try:
+                self.progress_cb(payload)
+            except Exception:
+                log.exception("progress callback failed")
+
+    def check(self) -> None:
+        if self.cancel_check and self.cancel_check():
+            raise Cancelled()
+
+
+class GraphAgent:
+    def __init__(self, llm, retrievers: dict, namespace: str = "default", max_iters: int = 3,
+                 router_top_k: int = 5, embed_fn=None):
+        self.llm = llm
+        self.retrievers = retrievers
+        self.namespace = namespace
+        self.max_iters = max_iters
+        self.router_top_k = router_top_k
+        self.embed_fn = embed_fn
+
+    # ------------------------------------------------------------------ helpers
+    def _complete(self, prompt: str, ctx: RunContext, **kw) -> str:
+        ctx.check()
+        if ctx.cancel_check is not None:
+            kw["cancel_check"] = ctx.cancel_check
+        return self.llm.complete(prompt, **kw).text
+
+    def _expand(self, question: str, info: dict, ctx: RunContext) -> list[str]:
+        try:
+            resp = self._complete(prompts.expand_query(question, info.get("repo"), info.get("scope")), ctx).strip()
+            s, e = resp.find("["), resp.rfind("]") + 1
+            if s >= 0 and e > s:
+                qs = json.loads(resp[s:e])
+                out = [q for q in qs if isinstance(q, str) and q.strip()]
+                if out:
+                    return out
+        except Cancelled:
+            raise
+        except Exception as e:
+            log.warning("query expansion failed: %s", e)
+        ql = question.lower()
+        fb = []
+        if "auth" in ql or "login" in ql:
+            fb += ["authentication mechanism", "security configuration", "OAuth2 setup"]
+        if "cache" in ql or "caching" in ql:
+            fb += ["caching strategy", "cache configuration", "data caching implementation"]
+        if "config" in ql or "configuration" in ql:
+            fb += ["application settings", "environment configuration", "setup parameters"]
+        return fb[:3] if fb else [question]
+
+    def _search(self, scope: str, q: str, filters: dict) -> list:
+        return self.retrievers[scope].invoke(q, filter=filters) or []
+
+    # ------------------------------------------------------------------ nodes
+    def plan_scope(self, st: dict, ctx: RunContext) -> dict:
+        q = st["query"]
+        filters = dict(st.get("filters") or {})
+        if self.namespace:
+            filters.setdefault("namespace", self.namespace)
+        rh = extract_repo_hint(q)
+        if rh:
+            filters["repo"] = rh
+        try:
+            data = _json_object(self._complete(prompts.plan_scope(q), ctx).strip())
+            scope = data.get("scope") or ("code" if looks_codey(q) else "project")
+            _merge_filters(filters, data.get("filters"))
+        except Cancelled:
+            raise
+        except Exception as e:
+            log.warning("scope planning parse failed: %s", e)
+            scope = "code" if looks_codey(q) else "project"
+        if scope not in self.retrievers:
+            scope = "code" if looks_codey(q) else "project"
+        if st.get("force_level") in self.retrievers:
+            scope = st["force_level"]
+        for tech, syns in TECH_SYNONYMS.items():
+            if any(t in q.lower() for t in syns) and "topics" not in filters:
+                filters["topics"] = tech
+                break
+        ctx.turns.append({"stage": "plan", "scope": scope, "filters": dict(filters)})
+        ctx.notify({"stage": "plan", "scope": scope, "filters": dict(filters), "attempt": st.get("attempt", 0)})
+        return {**st, "scope": scope, "filters": filters, "attempt": st.get("attempt", 0)}
+
+    def retrieve(self, st: dict, ctx: RunContext) -> dict:
+        ctx.check()
+        scope, q = st["scope"], st["query"]
+        filters = st.get("filters") or {}
+        attempt = st.get("attempt", 0)
+        docs = self._search(scope, q, filters)
+        n0 = len(docs)
+        if len(docs) < 3 or attempt > 0:
+            expanded = self._expand(q, {"repo": filters.get("repo"), "scope": scope}, ctx)
+            all_docs = list(docs)
+            seen = {hash(_content(d)) for d in docs}
+            for eq in expanded:
+                if len(all_docs) >= self.router_top_k:
+                    break
+                try:
+                    for d in self._search(scope, eq, filters):
+                        if len(all_docs) >= self.router_top_k:
+                            break
+                        h = hash(_content(d))
+                        if h not in seen:
+                            all_docs.append(d)
+                            seen.add(h)
+                except Exception as e:
+                    log.warning("expanded query %r failed: %s", eq, e)
+            docs = all_docs[: self.router_top_k]
+            if len(docs) > n0:
+                ctx.notify({"stage": "retrieve_expanded", "original_hits": n0, "expanded_hits": len(docs),
+                            "expanded_queries": expanded})
+        docs = sorted(docs, key=lambda d: score_of(d) or 0.0, reverse=True)
+        ctx.turns.append({"stage": "retrieve", "scope": scope, "filters": dict(filters), "hits": len(docs),
+                          "original_hits": n0, "attempt": attempt})
+        ctx.notify({"stage": "retrieve", "scope": scope, "filters": dict(filters), "hits": len(docs)})
+        return {**st, "docs": docs}
+
+    def judge(self, st: dict, ctx: RunContext) -> dict:
+        q = st["query"]
+        docs = st.get("docs") or []
+        inv = []
+        for i, d in enumerate(docs, start=1):
+            md = getattr(d, "metadata", {}) or {}
+            c = _content(d)
+            inv.append({"i": i, "repo": md.get("repo", ""), "module": md.get("module", ""),
+                        "file": md.get("file_path", ""), "topics": md.get("topics", ""),
+                        "content_preview": c[:200] + "..." if len(c) > 200 else c, "relevance_score": score_of(d)})
+        quality = "good" if inv else "empty"
+        if inv and all(not it["content_preview"].strip() for it in inv):
+            quality = "metadata_only"
+        elif inv and any("auth" in it["content_preview"].lower() or "cache" in it["content_preview"].lower()
+                         for it in inv):
+            quality = "semantically_relevant"
+        try:
+            data = _json_object(self._complete(prompts.judge(q, quality, inv), ctx).strip())
+        except Cancelled:
+            raise
+        except Exception as e:
+            log.warning("judge parse failed: %s", e)
+            cur = st["scope"]
+            if cur == "project":
+                data = {"coverage": 0.2, "needs_more": True, "stage_down": "package"}
+            elif cur == "package":
+                data = {"coverage": 0.3, "needs_more": True, "stage_down": "file"}
+            else:
+                data = {"coverage": 0.4, "needs_more": False}
+        filters = dict(st.get("filters") or {})
+        _merge_filters(filters, data.get("suggest_filters"))
+        nxt = st["scope"]
+        sd = data.get("stage_down")
+        try:
+            cov = float(data.get("coverage", 0) or 0)
+        except (TypeError, ValueError):
+            cov = 0.0
+        if sd in ("package", "file", "code"):
+            nxt = sd
+        elif cov < 0.3 and docs:
+            nxt = NEXT_SCOPE.get(st["scope"], st["scope"])
+        ctx.turns.append({"stage": "judge", "decision": data})
+        ctx.notify({"stage": "judge", "decision": data})
+        return {**st, "needs_more": bool(data.get("needs_more")), "rewrite": data.get("rewrite"),
+                "filters": filters, "scope": nxt}
+
+    def rewrite_or_end(self, st: dict, ctx: RunContext) -> dict:
+        if not st.get("needs_more"):
+            return st
+        attempt = int(st.get("attempt", 0)) + 1
+        if attempt >= self.max_iters:
+            return {**st, "needs_more": False, "attempt": attempt}
+        docs = st.get("docs") or []
+        if attempt > 1 and docs and st.get("scope") in ("project", "package"):
+            if all(not (getattr(d, "metadata", {}) or {}).get("file_path") for d in docs):
+                return {**st, "scope": "file", "attempt": attempt}
+        base = st.get("rewrite") or st["query"]
+        filters = st.get("filters") or {}
+        if attempt == 1:
+            ctx_s = " ".join(filters[k] for k in ("repo", "module") if k in filters)
+            try:
+                sharp = self._complete(prompts.rewrite(base, ctx_s), ctx).strip().strip("\"'").strip()
+                if not sharp or len(sharp) < 10:
+                    raise ValueError("rewrite too short")
+            except Cancelled:
+                raise
+            except Exception as e:
+                log.warning("rewrite failed: %s", e)
+                sharp = " ".join([base] + ([f"in {ctx_s}"] if ctx_s else []))
+        else:
+            exp = self._expand(base, {"repo": filters.get("repo"), "scope": st.get("scope")}, ctx)
+            sharp = exp[0] if exp else base
+        ctx.turns.append({"stage": "rewrite", "attempt": attempt + 1, "query": sharp, "filters": dict(filters)})
+        ctx.notify({"stage": "rewrite", "action": "retry", "attempt": attempt + 1, "query": sharp,
+                    "filters": dict(filters)})
+        return {**st, "query": sharp, "attempt": attempt}
+
+    def synthesize(self, st: dict, ctx: RunContext) -> dict:
+        q = st["query"]
+        docs = st.get("docs") or []
+        blocks, sources = [], []
+        for i, d in enumerate(docs[:5], start=1):
+            md = getattr(d, "metadata", {}) or {}
+            blocks.append(f"[{i}] repo={md.get('repo', '')} module={md.get('module', '')} "
+                          f"file={md.get('file_path', '')}\n{_content(d)[:800]}")
+            sources.append(doc_to_source(i, d))
+        qtype = "overview" if any(w in q.lower() for w in ("projects", "repositories", "overview", "tell me about",
+                                                            "what is", "describe")) else "specific"
+        has_content = any(len(b.split("\n", 1)[-1].strip()) > 50 for b in blocks)
+        system = prompts.SYNTH_OVERVIEW if qtype == "overview" and has_content else prompts.SYNTH_SPECIFIC
+        dbg_issue = None
+        try:
+            kw = {"on_token": ctx.on_answer_token} if ctx.on_answer_token else {}
+            text = self._complete(prompts.synthesize(system, q, blocks), ctx, **kw)
+            if has_content and len(docs) >= 3 and any(p in text.lower() for p in _CONSERVATIVE):
+                try:
+                    retry = self._complete(prompts.synthesize(prompts.SYNTH_RETRY, q, blocks), ctx)
+                    if not any(p in retry.lower() for p in _CONSERVATIVE[:3]):
+                        text = retry
+                except Cancelled:
+                    raise
+                except Exception as e:
+                    log.warning("synthesis retry failed: %s", e)
+        except Cancelled:
+            raise
+        except Exception as e:
+            text = f"(LLM error) {e}"
+        if any(p in text.lower() for p in _CONSERVATIVE[:3]) and has_content and len(docs) >= 3:
+            dbg_issue = "LLM_overly_conservative"
+        ctx.notify({"stage": "synthesize", "final_ctx_blocks": len(blocks), "sources_count": len(sources),
+                    "answer_length": len(text), "synthesis_issue": dbg_issue})
+        debug = {"final_ctx_blocks": len(blocks), "sources_count": len(sources), "final_scope": st.get("scope", ""),
+                 "question_type": qtype, "has_content": has_content, "answer_length": len(text)}
+        if dbg_issue:
+            debug["synthesis_issue"] = dbg_issue
+        return {**st, "answer": text, "sources": sources, "debug": debug}
+
+    # ------------------------------------------------------------------ run
+    def run(self, question: str, *, namespace: str | None = None, progress_cb=None, cancel_check=None,
+            force_level: str | None = None, on_answer_token=None) -> dict:
+        ctx = RunContext(progress_cb, cancel_check, on_answer_token)
+        st: dict = {"query": question, "force_level": force_level}
+        ns = namespace or self.namespace
+        if ns:
+            st["filters"] = {"namespace": ns}
+        st = self.plan_scope(st, ctx)
+        while True:
+            st = self.retrieve(st, ctx)
+            st = self.judge(st, ctx)
+            st = self.rewrite_or_end(st, ctx)
+            if not st.get("needs_more"):
+                break
+        st = self.synthesize(st, ctx)
+        debug = dict(st.get("debug") or {})
+        debug["turns"] = ctx.turns
+        return {"answer": st.get("answer", ""), "sources": st.get("sources", []), "debug": debug,
+                "scope": st.get("scope", "")}
+
+
+_lock = threading.Lock()

@@ -1,0 +1,141 @@
+"""Background engine loop.
+
+Many agent jobs (the reference worker runs ``max_jobs=10`` concurrently,
+worker.py:182-187) and ingest extractor waves submit generations from their
+own threads; one loop thread owns the GPU engine and steps it whenever work
+is queued, so all of them share continuous batches.  ``generate`` blocks the
+caller (agent threads), ``submit`` returns a handle with a per-token
+callback (SSE token streaming) and supports cancellation.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+
+import torch
+
+from .llm_engine import LLMEngine
+from .sequence import Completion, SamplingParams
+
+log = logging.getLogger(__name__)
+
+
+class GenerationHandle:
+    def __init__(self, runner: "EngineRunner", req_id: str):
+        self.runner = runner
+        self.req_id = req_id
+        self.done = threading.Event()
+        self.result: Completion | None = None
+        self.error: BaseException | None = None
+
+    def wait(self, timeout: float | None = None) -> Completion:
+        if not self.done.wait(timeout):
+            self.runner.abort(self.req_id)
+            self.done.wait(5.0)
+            raise TimeoutError(f"generation {self.req_id} timed out after {timeout}s")
+        if self.error is not None:
+            raise self.error
+        return self.result
+
+    def cancel(self) -> None:
+        self.runner.abort(self.req_id)
+
+
+class EngineRunner:
+    def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005):
+        self.engine = engine
+        self.idle_sleep = idle_sleep
+        self._cv = threading.Condition()
+        self._stop = False
+        self._handles: dict[str, GenerationHandle] = {}
+        self._pending: list[tuple] = []
+        self._thread = threading.Thread(target=self._loop, name="grag-engine", daemon=True)
+        self._thread.start()
+        self.last_error: BaseException | None = None
+        self.healthy = True
+
+    # ------------------------------------------------------------------ API
+    def submit(self, prompt, params: SamplingParams | None = None, on_token=None) -> GenerationHandle:
+        import uuid
+
+        rid = uuid.uuid4().hex
+        h = GenerationHandle(self, rid)
+        with self._cv:
+            self._handles[rid] = h
+            self._pending.append((rid, prompt, params, on_token))
+            self._cv.notify()
+        return h
+
+    def generate(self, prompt, params: SamplingParams | None = None, on_token=None,
+                 timeout: float | None = None) -> Completion:
+        return self.submit(prompt, params, on_token).wait(timeout)
+
+    def abort(self, req_id: str) -> None:
+        self.engine.abort(req_id)
+        with self._cv:
+            self._cv.notify()
+
+    def shutdown(self) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        self._thread.join(timeout=10)
+
+    def stats(self) -> dict:
+        sch = self.engine.sched
+        return {"running": len(sch.running), "waiting": len(sch.waiting), "kv_usage": self.engine.kv.usage(),
+                **self.engine.stats, **self.engine.kv.stats()}
+
+    # ------------------------------------------------------------------ loop
+    def _on_token_wrapper(self, user_cb):
+        def cb(seq, delta, finished):
+            if user_cb is not None and delta:
+                user_cb(delta)
+            if finished:
+                h = self._handles.pop(seq.req_id, None)
+                self.engine.pop(seq.req_id)
+                if h is not None:
+                    h.result = self.engine.completion(seq)
+                    h.done.set()
+        return cb
+
+    def _loop(self):
+        if self.engine.on_gpu:
+            torch.cuda.set_device(self.engine.device)
+        while True:
+            with self._cv:
+                while not self._stop and not self._pending and not self.engine.has_unfinished():
+                    self._cv.wait(timeout=1.0)
+                if self._stop:
+                    break
+                pending, self._pending = self._pending, []
+            for rid, prompt, params, cb in pending:
+                try:
+                    self.engine.add_request(prompt, params, req_id=rid, on_token=self._on_token_wrapper(cb))
+                except Exception as e:  # bad request: fail just this handle
+                    h = self._handles.pop(rid, None)
+                    if h is not None:
+                        h.error = e
+                        h.done.set()
+            try:
+                self.engine.step()
+                self.healthy = True
+            except Exception as e:  # engine fault: fail every in-flight request, keep serving
+                log.exception("engine step failed")
+                self.last_error = e
+                self.healthy = False
+                self._fail_all(e)
+                time.sleep(0.05)
+
+    def _fail_all(self, err: BaseException) -> None:
+        with self._cv:
+            handles, self._handles = self._handles, {}
+        for rid, h in handles.items():
+            self.engine.abort(rid)
+            h.error = err
+            h.done.set()
+        try:  # drop the aborted sequences from the scheduler
+            self.engine.sched.reap_cancelled()
+        except Exception:
+            pass

@@ -1,0 +1,58 @@
+"""Ingest throughput benchmark (BASELINE.json secondary metric: ingest
+docs/sec).  Runs the FULL ingest_component pipeline on a synthetic repository
+of ``n_files`` source files: filter/transform -> code split -> LLM summary /
+title / keyword waves -> catalog (README check or code-summary catalog) ->
+file / module / repo roll-ups (+ their extractor passes) -> embedding of
+every scope -> upsert into the GPU store.
+
+Random-init weights essentially never emit EOS, so every LLM call would run
+to its token cap; caps are therefore set to the lengths real Qwen outputs
+have for these prompts (code summary 128, keywords 64, title 32, roll-ups
+256 tokens) and ``ignore_eos`` is not used.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..agent.llm import EngineLLM
+from ..config import Settings
+from ..engine.llm_engine import EngineConfig, LLMEngine
+from ..engine.runner import EngineRunner
+from ..index.store import VectorStore
+from ..utils.synthetic import synthetic_repo
+from .controller import IngestController
+from .readers import Document
+
+
+def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs: int = 128,
+                     max_model_len: int = 8192, use_graph: bool = True, summary_tokens: int = 128) -> tuple[int, float]:
+    """Returns (documents ingested, seconds)."""
+    dev = next(model.parameters()).device if hasattr(model, "parameters") else torch.device("cpu")
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max_num_seqs, max_num_batched_tokens=16384,
+                                             max_model_len=max_model_len, use_cuda_graph=use_graph, seed=seed))
+    if use_graph and dev.type == "cuda":
+        eng.warmup_graphs()
+    runner = EngineRunner(eng)
+    try:
+        llm = EngineLLM(runner, tok, max_tokens=summary_tokens, mode="ingest", timeout_s=1800.0, retries=0)
+        store = VectorStore(emb.dim, dev)
+        ctl = IngestController(llm=llm, store=store, embedder=emb, settings=Settings(data_dir=None),
+                               summary_tokens=summary_tokens)
+        _, files = synthetic_repo(seed, n_files, f"bench-repo-{seed}")
+        docs = [Document(f["text"], {"file_path": f["file_path"], "file_name": f["file_path"].split("/")[-1]})
+                for f in files]
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = ctl.ingest_component(repo=f"bench-repo-{seed}", namespace="bench", documents=docs, force=True)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        return res["documents"], dt
+    finally:
+        runner.shutdown()
+        del eng
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()

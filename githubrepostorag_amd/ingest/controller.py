@@ -1,0 +1,239 @@
+"""Ingest controller (ingest/src/app/ingest_controller.py:164-542).
+
+``ingest_component`` runs the same stages as the reference, each under a
+``stage_timer`` that records ``ingest_stage_run_seconds`` (and pushes it to a
+Prometheus push-gateway when one is configured and reachable):
+
+  preprocess -> code_nodes -> catalog -> file_summaries -> module_summaries
+  -> repo_summaries -> vector_write -> audit_and_clean
+
+The LLM stages go through the in-process engine (batched waves, see
+extractors.py) instead of an HTTP vLLM pod; vectors land in the GPU store.
+Additions: content-hash resume markers under ``DATA_DIR/repos/<repo>/``
+(an unchanged repo is skipped unless ``force``), audit rows appended to the
+store manifest and ``DATA_DIR/ingest_runs.jsonl`` (replaces the Cassandra
+``ingest_runs`` table), and source selection (github / local / synthetic).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import logging
+import math
+import os
+import time
+import uuid
+from datetime import datetime, timezone
+from pathlib import Path
+
+from ..config import settings as get_settings
+from ..service import metrics as M
+from .extractors import ExtractorPipeline
+from .hierarchy import HierarchyBuilder
+from .preprocess import infer_component_kind, prepare_repo_documents
+from .readers import GithubReader, LocalDirReader, SyntheticRepoReader, fetch_repositories
+from .splitters import DynamicCodeSplitter
+from .writer import VectorWriter
+
+log = logging.getLogger(__name__)
+
+DOC_TYPE_TO_SCOPE = {"catalog": "catalog", "repo": "repo", "module": "module", "file": "file"}
+
+
+class stage_timer:
+    def __init__(self, level: str, *, repo: str, namespace: str, branch: str, run_id: str, timings: dict,
+                 push_addr: str | None = None, on_stage=None):
+        self.level, self.labels = level, dict(repo=repo, namespace=namespace, branch=branch, run_id=run_id)
+        self.timings, self.push_addr, self.on_stage = timings, push_addr, on_stage
+
+    def __enter__(self):
+        self.t0 = time.perf_counter()
+        if self.on_stage:
+            self.on_stage(self.level, self.labels)
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        dt = time.perf_counter() - self.t0
+        if not math.isfinite(dt):
+            return False
+        self.timings[self.level] = dt
+        M.INGEST_STAGE_SECONDS.labels(level=self.level, **self.labels).set(dt)
+        _push("ingest_stage_run_seconds", "Duration (seconds) of a single ingest stage for a single run",
+              {"level": self.level, **self.labels}, dt, self.push_addr)
+        return False
+
+
+def _push(name: str, help_text: str, labels: dict, value: float, addr: str | None) -> None:
+    if not addr or os.environ.get("PUSHGATEWAY_ADDRESS") is None:
+        return  # only push when explicitly configured
+    try:
+        from prometheus_client import CollectorRegistry, Gauge, push_to_gateway
+
+        reg = CollectorRegistry()
+        g = Gauge(name, help_text, list(labels), registry=reg)
+        g.labels(**labels).set(value)
+        push_to_gateway(addr, job="ingest_component", registry=reg, grouping_key={"run_id": labels.get("run_id", "")},
+                        timeout=2)
+    except Exception:
+        log.debug("push-gateway push failed", exc_info=True)
+
+
+def attach_common_metadata(nodes, *, namespace, repo, branch, collection, component_kind, is_standalone, run_id,
+                           dev_forced, doc_type) -> None:
+    for n in nodes:
+        md = n.metadata
+        md.update(namespace=namespace, repo=repo, branch=branch, collection=collection, component_kind=component_kind,
+                  is_standalone=is_standalone, dev_forced_standalone=dev_forced, ingest_run_id=str(run_id))
+        md.setdefault("doc_type", doc_type)
+        md.setdefault("path", md.get("file_path"))
+        md["scope"] = DOC_TYPE_TO_SCOPE.get(doc_type, "chunk")
+
+
+def docs_digest(docs) -> str:
+    h = hashlib.sha1()
+    for d in sorted(docs, key=lambda d: d.metadata.get("file_path", "")):
+        h.update(d.metadata.get("file_path", "").encode())
+        h.update(hashlib.sha1(d.text.encode("utf-8", "replace")).digest())
+    return h.hexdigest()
+
+
+class IngestController:
+    def __init__(self, runtime=None, *, llm=None, store=None, embedder=None, settings=None, extract: bool = True,
+                 summary_tokens: int | None = None, on_event=None):
+        self.s = settings or (runtime.settings if runtime is not None else get_settings())
+        self.llm = llm or runtime.ingest_llm
+        self.store = store or runtime.store
+        self.embedder = embedder or runtime.embedder
+        self.runtime = runtime
+        self.on_event = on_event or (lambda kind, data: None)
+        toks = summary_tokens or 256
+        self.extractors = ExtractorPipeline(self.llm, title_nodes=5, summary_tokens=toks, enabled=extract)
+        self.hier = HierarchyBuilder(self.llm, ExtractorPipeline(self.llm, title_nodes=3, summary_tokens=toks,
+                                                                 enabled=extract), summary_tokens=2 * toks)
+        self.writer = VectorWriter(self.store, self.embedder)
+        self.splitter = DynamicCodeSplitter()
+
+    # ---- sources ---------------------------------------------------------
+    def _reader(self, source: str, path: str | None):
+        if source == "github":
+            return GithubReader(self.s.github_user, self.s.github_token)
+        if source == "local":
+            if not path:
+                raise ValueError("source=local needs a path")
+            return LocalDirReader(path)
+        return SyntheticRepoReader()
+
+    def _data_dir(self) -> Path | None:
+        return Path(self.s.data_dir) if self.s.data_dir else None
+
+    # ---- one component ---------------------------------------------------
+    def ingest_component(self, *, repo: str, namespace: str, branch: str | None = None, layer: str | None = None,
+                         collection: str | None = None, component_kind: str | None = None,
+                         dev_force_standalone: bool | None = None, source: str = "synthetic",
+                         path: str | None = None, documents=None, force: bool = False) -> dict:
+        t_run = time.perf_counter()
+        branch = branch or self.s.default_branch
+        collection = collection or self.s.default_collection
+        forced = bool(dev_force_standalone)
+        run_id = uuid.uuid4()
+        started = datetime.now(timezone.utc)
+        timings: dict = {}
+        self.on_event("ingest_start", {"repo": repo, "namespace": namespace, "branch": branch,
+                                       "collection": collection, "force": forced})
+
+        def timer(level):
+            return stage_timer(level, repo=repo, namespace=namespace, branch=branch, run_id=str(run_id),
+                               timings=timings, push_addr=self.s.pushgateway_address,
+                               on_stage=lambda lv, lab: self.on_event("step", {"stage": lv, **lab}))
+
+        with timer("preprocess"):
+            raw = documents if documents is not None else self._reader(source, path).load_data(repo, branch)
+            docs = prepare_repo_documents(raw)
+            kind = "standalone" if forced else (component_kind or infer_component_kind(docs))
+            is_sa = kind == "standalone"
+            digest = docs_digest(docs)
+            dd = self._data_dir()
+            marker = dd / "repos" / repo / f".ingested_{branch}" if dd else None
+            if marker is not None and marker.exists() and not force and marker.read_text().strip() == digest:
+                log.info("%s@%s unchanged since last ingest; skipping", repo, branch)
+                return {"repo": repo, "namespace": namespace, "branch": branch, "skipped": True,
+                        "nodes_written": 0, "component_kind": kind}
+            if dd:
+                (dd / "repos" / repo).mkdir(parents=True, exist_ok=True)
+                with open(dd / "repos" / repo / f"raw_documents_{branch}.json", "w") as f:
+                    json.dump([{"id": d.id, "text": d.text, "metadata": d.metadata} for d in docs], f)
+        common = dict(namespace=namespace, repo=repo, branch=branch, collection=collection, component_kind=kind,
+                      is_standalone=is_sa, dev_forced=forced)
+        with timer("code_nodes"):
+            code_nodes = self.extractors.run(self.splitter.get_nodes_from_documents(docs))
+            attach_common_metadata(code_nodes, run_id=run_id, doc_type="code", **common)
+        with timer("catalog"):
+            catalog_nodes = self.hier.catalog_nodes(repo, docs, code_nodes, collection, kind, layer)
+            attach_common_metadata(catalog_nodes, run_id=uuid.UUID(int=0), doc_type="catalog", **common)
+        with timer("file_summaries"):
+            file_nodes = self.hier.file_nodes(code_nodes, repo, namespace, branch, kind)
+            attach_common_metadata(file_nodes, run_id=run_id, doc_type="file", **common)
+        with timer("module_summaries"):
+            module_nodes = self.hier.module_nodes(file_nodes, repo, namespace, branch, kind)
+            attach_common_metadata(module_nodes, run_id=run_id, doc_type="module", **common)
+        with timer("repo_summaries"):
+            repo_nodes = self.hier.repo_nodes(docs, module_nodes, repo, namespace, branch, kind)
+            attach_common_metadata(repo_nodes, run_id=run_id, doc_type="repo", **common)
+        with timer("vector_write"):
+            written = self.writer.write_nodes_per_scope(catalog_nodes=catalog_nodes, repo_nodes=repo_nodes,
+                                                        module_nodes=module_nodes, file_nodes=file_nodes,
+                                                        chunk_nodes=code_nodes)
+        with timer("audit_and_clean"):
+            row = {"run_id": str(run_id), "namespace": namespace, "repo": repo, "branch": branch,
+                   "collection": collection, "component_kind": kind, "started_at": started.isoformat(),
+                   "finished_at": datetime.now(timezone.utc).isoformat(), "node_count": len(code_nodes),
+                   "nodes_per_scope": written}
+            self.store.audit.append(row)
+            if dd:
+                with open(dd / "ingest_runs.jsonl", "a") as f:
+                    f.write(json.dumps(row) + "\n")
+                marker.write_text(digest)
+            if self.runtime is not None and self.s.index_dir:
+                self.runtime.save_index()
+        total = time.perf_counter() - t_run
+        M.INGEST_RUN_SECONDS.labels(repo=repo, namespace=namespace, branch=branch, run_id=str(run_id)).set(total)
+        M.INGEST_DOCS.inc(len(docs))
+        _push("ingest_run_seconds", "Total duration (seconds) of a single ingest run",
+              {"repo": repo, "namespace": namespace, "branch": branch, "run_id": str(run_id)}, total,
+              self.s.pushgateway_address)
+        res = {"repo": repo, "namespace": namespace, "collection": collection, "component_kind": kind,
+               "branch": branch, "nodes_written": len(code_nodes), "is_standalone": is_sa,
+               "dev_forced_standalone": forced, "documents": len(docs), "nodes_per_scope": written,
+               "stage_seconds": {k: round(v, 4) for k, v in timings.items()}, "run_seconds": round(total, 4)}
+        self.on_event("ingest_done", res)
+        return res
+
+    # ---- batch driver (ingest_controller.py:490-542) ---------------------
+    def ingest_many(self, components, *, branch: str | None = None, dev_force_standalone: bool | None = None,
+                    source: str = "synthetic", path: str | None = None) -> list[dict]:
+        default_branch = branch or self.s.default_branch
+        items = []
+        if dev_force_standalone and source == "github":
+            for repo in fetch_repositories(self.s.github_user, self.s.github_token):
+                items.append({"repo": repo, "namespace": "default", "branch": default_branch,
+                              "dev_force_standalone": True})
+        else:
+            for it in components:
+                if isinstance(it, dict):
+                    p = dict(it)
+                    p.setdefault("branch", default_branch)
+                    p.setdefault("dev_force_standalone", dev_force_standalone)
+                else:
+                    it = list(it)
+                    p = {"repo": it[0], "namespace": it[1], "layer": it[2] if len(it) > 2 else None,
+                         "collection": it[3] if len(it) > 3 else None,
+                         "component_kind": it[4] if len(it) > 4 else None,
+                         "dev_force_standalone": it[5] if len(it) > 5 else dev_force_standalone,
+                         "branch": default_branch}
+                items.append(p)
+        out = []
+        for p in items:
+            p.setdefault("source", source)
+            p.setdefault("path", path)
+            out.append(self.ingest_component(**p))
+        return out

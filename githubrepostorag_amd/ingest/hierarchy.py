@@ -1,0 +1,112 @@
+"""Hierarchical roll-up summaries file -> module -> repo and the catalog
+document (ingest/src/app/services/hierarchy_summary_service.py:13-202,
+catalog/catalog_builder.py:8-194, services/catalog_service.py:12-39).
+
+Each level is one batched LLM wave (every file summary of a repo at once,
+then every module summary), then the "catalog pipeline"
+(SentenceSplitter(1500,100) + Summary + Title(3) + Keyword extractors,
+pipelines/catalog_pipeline.py:10-23) runs over the produced documents.
+Truncation semantics match the reference: 25 000 chars per roll-up input,
+40 files per module, 3 READMEs + 10 modules for the repo overview, README
+quality check on the first 1 000 chars, <= 10 code summaries for the catalog.
+"""
+from __future__ import annotations
+
+import logging
+
+from ..agent import prompts
+from .extractors import ExtractorPipeline, LLMWave
+from .preprocess import group_files_by_module, group_nodes_by_file, top_directory
+from .readers import Document, Node
+from .splitters import SentenceSplitter
+
+log = logging.getLogger(__name__)
+
+
+class HierarchyBuilder:
+    def __init__(self, llm, extractors: ExtractorPipeline | None = None, summary_tokens: int = 512):
+        self.wave = LLMWave(llm)
+        self.extract = extractors or ExtractorPipeline(llm, title_nodes=3)
+        self.summary_tokens = summary_tokens
+        self.splitter = SentenceSplitter(1500, 100)
+
+    def _catalog_pipeline(self, docs: list[Document]) -> list[Node]:
+        return self.extract.run(self.splitter.get_nodes_from_documents(docs))
+
+    def file_nodes(self, code_nodes: list[Node], repo: str, namespace: str, branch: str, kind: str) -> list[Node]:
+        files = [(fp, ns) for fp, ns in group_nodes_by_file(code_nodes).items() if fp]
+        concat = ["\n\n".join(n.get_content() for n in ns)[:25000] for _, ns in files]
+        texts = self.wave.map([prompts.file_summary(fp) + "\n\n" + c for (fp, _), c in zip(files, concat)],
+                              max_tokens=self.summary_tokens)
+        docs = []
+        for (fp, ns), t in zip(files, texts):
+            t = t or f"{fp} summary unavailable."
+            docs.append(Document(t, {"namespace": namespace, "repo": repo, "branch": branch, "file_path": fp,
+                                     "module": top_directory(fp, 1), "component_kind": kind, "doc_type": "file",
+                                     "rollup_of": [n.id for n in ns], "rollup_count": len(ns)}))
+        return self._catalog_pipeline(docs)
+
+    def module_nodes(self, file_nodes: list[Node], repo: str, namespace: str, branch: str, kind: str,
+                     depth: int = 1, max_files: int = 40) -> list[Node]:
+        summaries, ids = {}, {}
+        for n in file_nodes:
+            fp = (n.metadata.get("file_path") or "").strip()
+            if fp:
+                summaries.setdefault(fp, n.get_content())
+                ids.setdefault(fp, n.id)
+        mods = [(m, fs) for m, fs in group_files_by_module(list(summaries), depth).items() if m]
+        joined = ["\n\n".join(summaries[f] for f in fs[:max_files])[:25000] for _, fs in mods]
+        texts = self.wave.map([prompts.module_summary(m, repo) + "\n\n" + j for (m, _), j in zip(mods, joined)],
+                              max_tokens=self.summary_tokens)
+        docs = [Document(t or f"{m} module summary unavailable.",
+                         {"namespace": namespace, "repo": repo, "branch": branch, "module": m, "component_kind": kind,
+                          "doc_type": "module", "rollup_of": [ids[f] for f in fs[:max_files] if f in ids],
+                          "constituent_files": fs[:max_files]})
+                for (m, fs), t in zip(mods, texts)]
+        return self._catalog_pipeline(docs)
+
+    def repo_nodes(self, docs: list[Document], module_nodes: list[Node], repo: str, namespace: str, branch: str,
+                   kind: str, readme_limit: int = 3, module_limit: int = 10) -> list[Node]:
+        readmes = [d.text for d in docs if d.metadata.get("file_path", "").lower().endswith("readme.md")][:readme_limit]
+        mods = module_nodes[:module_limit]
+        seeds = "\n\n".join(readmes + [m.get_content() for m in mods])[:25000]
+        text = self.wave.map([prompts.repo_overview(repo) + "\n\n" + seeds], max_tokens=self.summary_tokens)[0]
+        doc = Document(text or f"{repo}: overview unavailable.",
+                       {"namespace": namespace, "repo": repo, "branch": branch, "component_kind": kind,
+                        "doc_type": "repo", "rollup_of": [m.id for m in mods],
+                        "constituent_modules": [m.metadata.get("module", "") for m in mods if m.metadata.get("module")]})
+        return self._catalog_pipeline([doc])
+
+    # ---- catalog (catalog_builder.make_catalog_document) ------------------
+    def catalog_nodes(self, repo: str, docs: list[Document], code_nodes: list[Node], collection: str, kind: str,
+                      layer: str | None = None) -> list[Node]:
+        readme = "\n\n".join(d.text for d in docs
+                             if d.metadata.get("file_path", "").lower().endswith(("readme.md", "readme.txt"))
+                             or d.metadata.get("file_path", "").lower() == "readme")
+        good = False
+        if readme and len(readme.strip()) >= 50:
+            verdict = self.wave.map([prompts.readme_quality(readme)], max_tokens=8)[0]
+            if verdict.startswith("Error"):
+                good = len(readme.strip()) > 200 and "todo" not in readme.lower()
+            else:
+                good = verdict.strip().upper() == "GOOD"
+        if readme and good:
+            text = f"# PROJECT OVERVIEW\n{readme}"
+        elif code_nodes:
+            sums, exts = [], set()
+            for n in code_nodes:
+                s = n.metadata.get("section_summary", "") or n.get_content()[:200]
+                fp = n.metadata.get("file_path", "unknown")
+                if s and len(s.strip()) > 20:
+                    sums.append(f"File: {fp}\nSummary: {s}")
+                if fp != "unknown" and "." in fp:
+                    exts.add(fp.rsplit(".", 1)[-1].lower())
+            tech = ", ".join(sorted(exts)) or "unknown"
+            text = self.wave.map([prompts.catalog_from_summaries(repo, tech, "\n\n---\n\n".join(sums[:10]))],
+                                 max_tokens=self.summary_tokens)[0]
+        else:
+            text = f"# PROJECT OVERVIEW\n{readme}" if readme else f"Component summary placeholder for {repo}."
+        doc = Document(text, {"doc_type": "catalog", "repo": repo, "layer": layer or "unspecified",
+                              "collection": collection, "component_kind": kind,
+                              "generated_from_code_summaries": bool(code_nodes) and not (readme and good)})
+        return self._catalog_pipeline([doc])

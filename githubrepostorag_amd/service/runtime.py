@@ -1,0 +1,94 @@
+"""Process-wide runtime: one GPU (or TP group) hosting the LLM engine, the
+encoder, the five-table vector store and the retrievers, shared by the API,
+the job workers and ingest.  Replaces the reference's five pods (api, worker,
+vLLM, Cassandra, Redis) with one process per GPU."""
+from __future__ import annotations
+
+import logging
+import time
+from pathlib import Path
+
+import torch
+
+from ..agent.graph_agent import GraphAgent
+from ..agent.llm import EngineLLM, MeteredLLM
+from ..config import Settings, settings as get_settings
+from ..embed.service import Embedder
+from ..engine.llm_engine import EngineConfig, LLMEngine
+from ..engine.runner import EngineRunner
+from ..engine.tokenizer import WordPieceTokenizer, load_tokenizer
+from ..index.store import VectorStore
+from ..models.configs import decoder_config, encoder_config
+from ..models.encoder import BertEncoder
+from ..models.qwen2 import Qwen2Model
+from ..models.weights import load_state_dict
+from ..retrieval.graph import RetrieverFactory
+
+log = logging.getLogger(__name__)
+
+
+class RAGRuntime:
+    def __init__(self, settings: Settings | None = None, device: str | None = None, llm=None, ingest_llm=None,
+                 embedder: Embedder | None = None, store: VectorStore | None = None, build_engine: bool = True):
+        self.settings = s = settings or get_settings()
+        self.device = torch.device(device or s.resolved_device())
+        self.started = time.time()
+        dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        # encoder
+        if embedder is None:
+            ecfg = encoder_config(s.embed_model)
+            sd = load_state_dict(s.encoder_dir) if s.encoder_dir else None
+            vocab = str(Path(s.encoder_dir) / "vocab.txt") if s.encoder_dir else None
+            enc = BertEncoder(ecfg, device=self.device, dtype=dtype, seed=s.seed + 2, state_dict=sd)
+            embedder = Embedder(enc, WordPieceTokenizer(ecfg.vocab_size, vocab))
+        self.embedder = embedder
+        # store
+        if store is None:
+            if s.index_dir and (Path(s.index_dir) / "manifest.json").exists():
+                store = VectorStore.load(s.index_dir, self.device)
+            else:
+                store = VectorStore(embedder.dim, self.device, s.table_names())
+        self.store = store
+        self.retrievers = RetrieverFactory(store, embedder)
+        # LLM engine
+        self.engine = self.runner = None
+        if llm is None and build_engine:
+            dcfg = decoder_config(s.qwen_model)
+            sd = load_state_dict(s.model_dir) if s.model_dir else None
+            model = Qwen2Model(dcfg, device=self.device, dtype=dtype, seed=s.seed + 1, state_dict=sd)
+            self.tokenizer = load_tokenizer(s.model_dir, dcfg.vocab_size)
+            ecfg = EngineConfig(max_num_seqs=s.max_num_seqs, max_num_batched_tokens=s.max_num_batched_tokens,
+                                max_model_len=s.max_model_len, block_size=s.kv_block,
+                                kv_cache_gb=s.kv_cache_gb or None, use_cuda_graph=s.cuda_graphs,
+                                enable_prefix_caching=s.prefix_caching, seed=s.seed)
+            self.engine = LLMEngine(model, self.tokenizer, ecfg)
+            self.runner = EngineRunner(self.engine)
+            llm = MeteredLLM(EngineLLM(self.runner, self.tokenizer, max_tokens=s.qwen_max_output,
+                                       timeout_s=s.job_timeout_s, retries=s.llm_retries))
+            ingest_llm = EngineLLM(self.runner, self.tokenizer, max_tokens=2048, mode="ingest",
+                                   allow_thinking=s.allow_thinking, timeout_s=s.job_timeout_s,
+                                   retries=s.llm_retries)
+        self.llm = llm
+        self.ingest_llm = ingest_llm or llm
+
+    def agent(self) -> GraphAgent:
+        """A fresh agent per job (cheap: it only holds references)."""
+        s = self.settings
+        return GraphAgent(self.llm, self.retrievers.scope_retrievers(), namespace=s.default_namespace,
+                          max_iters=s.max_rag_attempts, router_top_k=s.router_top_k)
+
+    def health(self) -> dict:
+        out = {"device": str(self.device), "tables": self.store.counts()}
+        if self.runner is not None:
+            out["engine"] = {"healthy": self.runner.healthy, **{k: v for k, v in self.runner.stats().items()
+                                                                 if isinstance(v, (int, float))}}
+        return out
+
+    def save_index(self, path: str | None = None) -> None:
+        p = path or self.settings.index_dir
+        if p:
+            self.store.save(p)
+
+    def close(self) -> None:
+        if self.runner is not None:
+            self.runner.shutdown()
