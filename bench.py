@@ -167,8 +167,12 @@ def main():
     p50 = statistics.median([x for r in ttfts_all for x in r]) * 1000.0
     ms_step = elapsed / args.steps * 1000.0
 
+    log(f"serving: {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms, {ms_step:.1f} ms/step")
+    eng_stats = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()}
+
     # ---- ingest phase (reported separately)
     ingest_dps = None
+    ingest_stages = None
     if not args.no_ingest and args.ingest_files > 0:
         from githubrepostorag_amd.ingest.bench_ingest import run_ingest_bench
 
@@ -176,8 +180,8 @@ def main():
         if dev.type == "cuda":
             torch.cuda.empty_cache()
         comm.barrier()
-        n_docs, secs = run_ingest_bench(model, tok, emb, args.ingest_files, seed=rank,
-                                        use_graph=not args.no_graph)
+        n_docs, secs, ingest_stages = run_ingest_bench(model, tok, emb, args.ingest_files, seed=rank,
+                                                       use_graph=not args.no_graph)
         tt = torch.tensor([secs], dtype=torch.float64, device=dev)
         if world > 1:
             import torch.distributed as dist
@@ -211,7 +215,8 @@ def main():
                 "top_k": args.top_k,
                 "parallelism": f"dp{world}",
             },
-            "engine": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()},
+            "engine": eng_stats,
+            "ingest_stage_s": ingest_stages,
         }
         line = json.dumps(res)
         print(line, flush=True)

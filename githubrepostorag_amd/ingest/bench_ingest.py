@@ -27,8 +27,8 @@ from .readers import Document
 
 
 def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs: int = 128,
-                     max_model_len: int = 8192, use_graph: bool = True, summary_tokens: int = 128) -> tuple[int, float]:
-    """Returns (documents ingested, seconds)."""
+                     max_model_len: int = 8192, use_graph: bool = True, summary_tokens: int = 128) -> tuple[int, float, dict]:
+    """Returns (documents ingested, seconds, per-stage seconds)."""
     dev = next(model.parameters()).device if hasattr(model, "parameters") else torch.device("cpu")
     eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max_num_seqs, max_num_batched_tokens=16384,
                                              max_model_len=max_model_len, use_cuda_graph=use_graph, seed=seed))
@@ -50,7 +50,7 @@ def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs:
         if dev.type == "cuda":
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        return res["documents"], dt
+        return res["documents"], dt, res["stage_seconds"]
     finally:
         runner.shutdown()
         del eng

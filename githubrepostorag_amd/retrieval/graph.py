@@ -106,20 +106,19 @@ class GraphRetriever:
     def _adjacent(self, q: torch.Tensor, pairs, base_filter) -> list[list[Hit]]:
         """All (dst_field, value) lookups of one depth in one fused launch."""
         tab = self.table
-        fields = sorted({f for f, _ in pairs})
-        cols = []
+        cols: list[tuple[str, torch.Tensor]] = []
+        col_idx: dict[str, int] = {}
         sel, vals, keep = [], [], []
         host_pairs = []
         for f, v in pairs:
             if f in FILTER_FIELDS:
                 code = tab.dicts[f].get(v)
-                if code is None:
+                if code is None:  # value never seen in this table: no row can match
                     continue
-                if f not in fields[: len(cols) + 8]:
-                    pass
-                if f not in [c[0] for c in cols]:
+                if f not in col_idx:
+                    col_idx[f] = len(cols)
                     cols.append((f, tab.columns[f]))
-                sel.append([c[0] for c in cols].index(f))
+                sel.append(col_idx[f])
                 vals.append(code)
                 keep.append((f, v))
             else:
