@@ -107,6 +107,7 @@ def main():
                   "say so clearly and suggest looking in specific repos/modules that might contain the answer.")
 
     qcounter = [rank * 1_000_000]
+    phase = {"embed": 0.0, "search": 0.0, "prompt": 0.0, "generate": 0.0}
 
     def run_step():
         """One batch of B RAG queries on this rank; returns per-query TTFTs (s)."""
@@ -115,8 +116,10 @@ def main():
         qs = [synthetic.question(qcounter[0] + i) for i in range(B)]
         qcounter[0] += B
         qv = emb.embed_queries(qs)
+        t_e = time.perf_counter()
         scores, ids = index.search(qv, args.top_k)
         ids = ids.cpu().tolist()
+        t_s = time.perf_counter()
         prompts = []
         for q, row in zip(qs, ids):
             blocks = [f"[{j + 1}] repo=synthetic module=m{d % 97} file=f{d}.py\n{synthetic.chunk_text(d)}"
@@ -127,6 +130,7 @@ def main():
             pid = (pid * (args.prompt_len // max(1, len(pid)) + 1))[: args.prompt_len] if len(pid) < args.prompt_len \
                 else pid[-args.prompt_len:]
             prompts.append(pid)
+        t_p = time.perf_counter()
         rids = [eng.add_request(p, sp) for p in prompts]
         while eng.has_unfinished():
             eng.step()
@@ -135,6 +139,9 @@ def main():
             s = eng.pop(r)
             ttft.append(s.first_token_time - t_sub)
             assert len(s.output_ids) == args.gen_len, (len(s.output_ids), s.finish_reason)
+        t_g = time.perf_counter()
+        for k, v in (("embed", t_e - t_sub), ("search", t_s - t_e), ("prompt", t_p - t_s), ("generate", t_g - t_p)):
+            phase[k] += v
         return ttft
 
     log("warmup")
@@ -169,6 +176,8 @@ def main():
 
     log(f"serving: {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms, {ms_step:.1f} ms/step")
     eng_stats = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()}
+    nstep = args.steps + args.warmup
+    log("per-step phases (ms, incl. warmup): " + ", ".join(f"{k}={v / nstep * 1000:.1f}" for k, v in phase.items()))
 
     # ---- ingest phase (reported separately)
     ingest_dps = None
