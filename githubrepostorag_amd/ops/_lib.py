@@ -43,6 +43,8 @@ _SIGS = {
     "grag_sample": [P, I, I, I, I, P, P, P, P, P, I, P, U64, P, P, P],
     "grag_mark_seen": [P, P, I, P, I, I, P],
     "grag_gemm_skinny": [P, P, P, P, I, I, I, I, I, I, I, P],
+    "grag_gemm_stream": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
+    "grag_gemm_stream_plan": [I, I, I, I, P],
 }
 
 

@@ -1,8 +1,13 @@
 """Linear layers.
 
-* decode-sized inputs (M <= SKINNY_MAX_M rows, K % 32 == 0): the hand-written
-  weight-streaming MFMA kernel ``grag_gemm_skinny`` (HBM-bound regime: every
-  weight byte read once per step, nontemporal loads, intra-workgroup split-K);
+Decode-sized inputs (the weight-streaming regime: every weight byte read once
+per step) go to hand-written MFMA kernels, chosen per shape from the cold-cache
+A/B in scripts/bench_gemm.py:
+* ``grag_gemm_skinny`` (M <= 16, and square projections up to M = 64):
+  register-streamed W, nontemporal loads, intra-workgroup split-K;
+* ``grag_gemm_stream`` (deep-K projections such as down_proj, and the LM head
+  at M <= 32): stream-K over (tile, 64-k) iterations, full-line LDS-DMA ring,
+  in-launch split-tile combine;
 * larger M (prefill, encoder batches): plain GEMMs go to hipBLASLt through
   ``torch.nn.functional.linear`` — the library is used only for plain
   (epilogue-free / bias-only) GEMMs; everything fused around them
@@ -15,7 +20,7 @@ import os
 
 import torch
 
-from ._lib import call, ptr
+from ._lib import call, lib, ptr
 
 SKINNY_MAX_M = int(os.environ.get("GRAG_SKINNY_MAX_M", "64"))
 _SKINNY_ON = os.environ.get("GRAG_SKINNY", "1") != "0"
@@ -29,16 +34,115 @@ def gemm_skinny(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
     return out
 
 
+class _StreamWorkspace:
+    """Per-device split-K scratch for ``grag_gemm_stream``: an fp32 slab and a
+    zero-initialised ticket-counter array (the kernel's last arriver resets
+    its word, so replays inside a hipGraph need no memset).  Grown only
+    outside graph capture; GEMMs on one stream reuse it in stream order."""
+
+    def __init__(self):
+        self.slab = {}
+        self.counters = {}
+        self._retired = []  # outgrown slabs stay alive: captured hipGraphs may still point at them
+
+    def ready(self, dev: torch.device, M: int, N: int, K: int) -> bool:
+        """True when a graph capture can use the stream kernel for this shape
+        (workspace already large enough: capture cannot allocate)."""
+        mt, bn, G, pmax = stream_plan(M, N, K)
+        need = -(-N // bn) * -(-M // (16 * mt)) * pmax * 16 * mt * bn
+        s = self.slab.get(dev.index)
+        return s is not None and s.numel() >= need and dev.index in self.counters
+
+    def get(self, dev: torch.device, slab_floats: int):
+        key = dev.index
+        s = self.slab.get(key)
+        if s is None or s.numel() < slab_floats:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("gemm_stream workspace must be sized before hipGraph capture")
+            if s is not None:
+                self._retired.append(s)
+            s = torch.empty(max(slab_floats, 1 << 20), dtype=torch.float32, device=dev)
+            self.slab[key] = s
+        c = self.counters.get(key)
+        if c is None:
+            c = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
+            self.counters[key] = c
+        return s, c
+
+
+_WS = _StreamWorkspace()
+_PLAN_CACHE: dict = {}
+_NCU: list = []
+STREAM_MAX_M = int(os.environ.get("GRAG_STREAM_MAX_M", "64"))
+
+
+def num_cus() -> int:
+    if not _NCU:
+        _NCU.append(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+                    if torch.cuda.is_available() else 256)
+    return _NCU[0]
+
+
+def stream_plan(M: int, N: int, K: int, mt: int | None = None, bn: int | None = None,
+                grid: int | None = None) -> tuple[int, int, int, int]:
+    """(mt, bn, grid, pmax) of the stream-K split (same rule as the library's
+    ``grag_gemm_stream_plan``): one 4-wave workgroup per CU by default, every
+    workgroup a contiguous range of (tile, 64-k step) iterations; pmax = max
+    workgroups sharing one output tile (slab slots per tile)."""
+    key = (M, N, K, mt, bn, grid)
+    p = _PLAN_CACHE.get(key)
+    if p is None:
+        mt = mt or (2 if M <= 32 else 4)
+        bn = bn or 128
+        ntm = -(-M // (16 * mt))
+        ks = -(-K // 64)
+        total = -(-N // bn) * ntm * ks
+        G = grid or num_cus()
+        if total < G * 4:
+            G = max(1, -(-total // 4))
+        per = total // G
+        pmax = -(-ks // per) + 1
+        p = _PLAN_CACHE[key] = (mt, bn, G, pmax)
+    return p
+
+
+def gemm_stream(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
+                plan: tuple | None = None) -> torch.Tensor:
+    """Stream-K weight-streaming MFMA GEMM (csrc/kernels/gemm_stream.hip) for
+    decode-batch M: y = x @ w.T (+ b).  ``plan`` = (mt, bn, grid) overrides."""
+    M, K = x.shape
+    N = w.shape[0]
+    mt, bn, G, pmax = stream_plan(M, N, K, *(plan or ()))
+    ntiles = -(-N // bn) * -(-M // (16 * mt))
+    slab, cnt = _WS.get(x.device, ntiles * pmax * 16 * mt * bn)
+    if ntiles > cnt.numel():
+        raise ValueError(f"gemm_stream: {ntiles} tiles exceed the counter array")
+    out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    call("grag_gemm_stream", ptr(x), ptr(w), ptr(b), ptr(out), x.stride(0), w.stride(0), out.stride(0), M, N, K,
+         mt, bn, G, pmax, ptr(slab), ptr(cnt))
+    return out
+
+
 def use_skinny(M: int, N: int, K: int) -> bool:
-    """Dispatch rule from the cold-cache A/B of scripts/microbench.py
-    (profiles/microbench_gemm.json): the streaming kernel wins at M <= 16
-    except for very wide outputs (N >= 8K with K <= 4K, e.g. gate_up), and at
-    M <= 64 for square-ish projections (o_proj)."""
+    """Dispatch rule from the cold-cache A/B of scripts/bench_gemm.py
+    (profiles/bench_gemm_decode.json): the register-streaming kernel wins at
+    M <= 16 except for very wide outputs (gate_up: N >= 8K, N >= 8K), and at
+    M <= 64 for square projections (o_proj)."""
     if M <= 16:
         return not (N >= 8192 and K <= 4096 and N >= 8 * K)
     if M <= SKINNY_MAX_M:
-        return N <= 4096 and K <= 4096
+        return N <= 4096 and K <= 4096 and N < 4096 + 512
     return False
+
+
+def use_stream(M: int, N: int, K: int) -> bool:
+    """Stream-K LDS-DMA kernel: deep-K projections (down_proj K = 18944: 52 us
+    vs hipBLASLt 90 us at M = 64) and, at M <= 32, the vocab-wide LM head."""
+    if M > 128:
+        return False
+    if K >= 2 * N and K >= 4096:
+        return True
+    return M <= 32 and N >= 65536
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
@@ -48,7 +152,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> t
             y = torch.nn.functional.linear(x.float(), w.float(), None if b is None else b.float())
             return y.to(x.dtype)
         return torch.nn.functional.linear(x, w, b)
-    if (_SKINNY_ON and x.dim() == 2 and x.shape[1] % 64 == 0 and use_skinny(x.shape[0], w.shape[0], x.shape[1])
-            and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.stride(1) == 1 and w.stride(1) == 1):
-        return gemm_skinny(x, w, b)
+    if (_SKINNY_ON and x.dim() == 2 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.stride(1) == 1 and w.stride(1) == 1):
+        M, K = x.shape
+        N = w.shape[0]
+        if K % 64 == 0 and use_skinny(M, N, K):
+            return gemm_skinny(x, w, b)
+        if (K % 16 == 0 and N % 4 == 0 and use_stream(M, N, K)
+                and (not torch.cuda.is_current_stream_capturing() or _WS.ready(x.device, M, N, K))):
+            return gemm_stream(x, w, b)
     return torch.nn.functional.linear(x, w, b)

@@ -259,3 +259,21 @@ def test_gemm_skinny(dev, M, N, K):
     close(y, ref, 3e-2, 2e-2)
     for nt in (16, 32, 64):
         close(gemm_skinny(x, w, None, nt), ref - b.float().cpu(), 3e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 3584, 18944), (64, 4608, 3584), (37, 1000, 512), (17, 3584, 3696),
+                                   (128, 3584, 3584), (9, 2048, 1024)])
+def test_gemm_stream(dev, M, N, K):
+    """Stream-K weight-streaming GEMM: auto plan + forced (mt, bn, grid) plans —
+    tiles split across 1..many workgroups (slab + in-launch last-arriver
+    combine), a K % 64 != 0 tail, M not a multiple of 16."""
+    from githubrepostorag_amd.ops.linear import gemm_stream
+
+    x = rnd(M, K, dev=dev, scale=0.5)
+    w = rnd(N, K, dev=dev, scale=0.05, seed=1)
+    b = rnd(N, dev=dev, seed=2)
+    ref = x.float().cpu() @ w.float().cpu().T
+    close(gemm_stream(x, w, b), ref + b.float().cpu(), 3e-2, 2e-2)
+    for plan in ((4, 128, 256), (4, 64, 100), (2, 128, 37), (2, 64, 512), (4, 256, 3), (2, 256, 1), (4, 256, 256)):
+        for _ in range(2):  # second call re-uses the ticket counters the first call reset
+            close(gemm_stream(x, w, None, plan), ref, 3e-2, 2e-2)
