@@ -5,11 +5,17 @@ Replaces the reference's external vLLM container (helm/templates/
 qwen-deployment.yaml:20-71, ``--max-num-seqs 4 --max-model-len 11712``) with
 an engine that lives in the worker process next to the index and encoder.
 
-Decode steps are captured per (batch bucket, split plan) into
-``torch.cuda.CUDAGraph`` objects (hipGraphs on ROCm): embed -> 28 layers ->
-LM head -> sampler replay as one graph launch; the only host round trip per
-step is one H2D copy of a packed int32 control buffer and one D2H copy of
-the sampled token ids.
+Decode runs in multi-step windows: K in {1, 2, 4, 8} consecutive decode steps
+(embed -> 28 layers -> LM head -> sampler, K times, each step's sampled ids
+feeding the next step's embedding gather on device) are captured per
+(batch bucket, split plan, K) into one ``torch.cuda.CUDAGraph`` (a hipGraph
+on ROCm).  The host builds the positions / slot mapping / context lengths of
+all K steps at once (KV blocks are reserved K tokens ahead), issues one H2D
+copy of a packed int32 control buffer, one replay and one D2H copy of the
+K x B sampled ids, so the per-token host work (scheduling, detokenising,
+stop checks) is amortised over K steps and the GPU is not left idle between
+tokens.  Tokens sampled after a sequence hit EOS/stop inside a window are
+discarded.
 """
 from __future__ import annotations
 
@@ -25,7 +31,7 @@ import torch
 from ..ops.attention import KV_TILE, AttnMetadata
 from ..ops.sampling import SamplerState, sample
 from .scheduler import KVCacheManager, Scheduler
-from .sequence import Completion, SamplingParams, Sequence
+from .sequence import Completion, SamplingParams, Sequence, SeqStatus
 
 log = logging.getLogger(__name__)
 
@@ -42,6 +48,7 @@ class EngineConfig:
     enable_prefix_caching: bool = True
     use_cuda_graph: bool = True
     graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
+    decode_window: int = 8  # max decode steps per graph replay (power of two)
     seed: int = 0
 
 
@@ -63,12 +70,13 @@ def _pow2_at_least(n: int) -> int:
 
 
 class _DecodeGraph:
-    def __init__(self, graph, out_tokens, batch, nsplit, split_len):
+    def __init__(self, graph, out_tokens, batch, nsplit, split_len, steps):
         self.graph = graph
-        self.out_tokens = out_tokens
+        self.out_tokens = out_tokens  # [steps, batch] int32
         self.batch = batch
         self.nsplit = nsplit
         self.split_len = split_len
+        self.steps = steps
 
 
 class LLMEngine:
@@ -93,7 +101,7 @@ class LLMEngine:
         self._graph_pool = None
         self._static = None
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0, "steps": 0,
-                      "graph_replays": 0, "graph_captures": 0}
+                      "graph_replays": 0, "graph_captures": 0, "decode_steps": 0, "decode_wait_s": 0.0}
         self._eos = set(getattr(tokenizer, "eos_token_ids", set()))
         self._lock = threading.RLock()
         max_split = -(-cfg.max_model_len // KV_TILE)
@@ -258,116 +266,162 @@ class LLMEngine:
         return finished
 
     # ------------------------------------------------------------------ decode
-    def _decode_inputs(self, seqs, B: int, width: int) -> np.ndarray:
-        n = len(seqs)
-        ids = np.zeros(B, dtype=np.int32)
-        pos = np.zeros(B, dtype=np.int32)
-        slot = np.full(B, -1, dtype=np.int32)
-        ctx = np.ones(B, dtype=np.int32)
-        sl = np.full(B, self.scratch_slot, dtype=np.int32)
-        bs = self.cfg.block_size
-        for i, s in enumerate(seqs):
-            p = s.total_len - 1
-            ids[i] = s.all_ids[-1]
-            pos[i] = p
-            slot[i] = s.blocks[p // bs] * bs + p % bs
-            ctx[i] = s.total_len
-            sl[i] = s.slot
-        bt = np.zeros((B, width), dtype=np.int32)
-        bt[:n] = self._block_table(seqs, width)
-        qs = np.arange(B + 1, dtype=np.int32)
-        return np.concatenate([ids, pos, slot, ctx, sl, qs, bt.reshape(-1)])
+    @staticmethod
+    def _last_id(s: Sequence) -> int:
+        return s.output_ids[-1] if s.output_ids else s.prompt_ids[-1]
 
-    def _views(self, buf: torch.Tensor, B: int, width: int):
+    def _decode_inputs(self, seqs, B: int, width: int, K: int = 1) -> np.ndarray:
+        """Packed int32 control buffer for a K-step decode window:
+        ids[B] | pos[K,B] | slot[K,B] | ctx[K,B] | sampler slots[B] | q_start[B+1] | block table[B,width]."""
+        n = len(seqs)
+        bs = self.cfg.block_size
+        ids = np.zeros(B, dtype=np.int32)
+        pos = np.zeros((K, B), dtype=np.int32)
+        slot = np.full((K, B), -1, dtype=np.int32)
+        ctx = np.ones((K, B), dtype=np.int32)
+        sl = np.full(B, self.scratch_slot, dtype=np.int32)
+        bt = np.zeros((B, width), dtype=np.int32)
+        steps = np.arange(K, dtype=np.int64)
+        for i, s in enumerate(seqs):
+            L = s.total_len
+            ids[i] = self._last_id(s)
+            blocks = np.asarray(s.blocks[:width], dtype=np.int64)
+            p = L - 1 + steps
+            pos[:, i] = p
+            slot[:, i] = blocks[p // bs] * bs + p % bs
+            ctx[:, i] = L + steps
+            sl[i] = s.slot
+            bt[i, : len(blocks)] = blocks
+        qs = np.arange(B + 1, dtype=np.int32)
+        del n
+        return np.concatenate([ids, pos.ravel(), slot.ravel(), ctx.ravel(), sl, qs, bt.ravel()])
+
+    def _views(self, buf: torch.Tensor, B: int, width: int, K: int = 1):
         o = 0
         out = {}
-        for name, n in (("ids", B), ("pos", B), ("slot", B), ("ctx", B), ("slots", B), ("qs", B + 1)):
-            out[name] = buf[o:o + n]
-            o += n
+        for name, shape in (("ids", (B,)), ("pos", (K, B)), ("slot", (K, B)), ("ctx", (K, B)), ("slots", (B,)),
+                            ("qs", (B + 1,))):
+            cnt = int(np.prod(shape))
+            out[name] = buf[o:o + cnt].view(*shape)
+            o += cnt
         out["bt"] = buf[o:o + B * width].view(B, width)
         return out
 
-    def _decode_forward(self, v, B, nsplit, split_len, out_tokens):
+    def _decode_forward(self, v, B, nsplit, split_len, out_tokens, K: int = 1):
+        """K chained decode steps; step j > 0 embeds the ids step j-1 sampled (on device)."""
         hq, d = self.model.hq, self.model.head_dim
         part_o = self._part_o[: nsplit * B * hq * d] if self.on_gpu else None
         part_ml = self._part_ml[: nsplit * B * hq * 2] if self.on_gpu else None
-        meta = AttnMetadata(q_start=v["qs"], ctx_len=v["ctx"], block_tables=v["bt"], slot_mapping=v["slot"],
-                            max_q_len=1, num_seqs=B, num_tokens=B, is_decode=True, num_splits=nsplit,
-                            split_len=split_len, part_o=part_o, part_ml=part_ml)
-        hidden = self.model.forward(v["ids"], v["pos"], meta, self.kv_caches)
-        logits = self.model.compute_logits(hidden)
-        return sample(logits, self.sampler, v["slots"], out=out_tokens)
+        for j in range(K):
+            ids = v["ids"] if j == 0 else out_tokens[j - 1]
+            meta = AttnMetadata(q_start=v["qs"], ctx_len=v["ctx"][j], block_tables=v["bt"], slot_mapping=v["slot"][j],
+                                max_q_len=1, num_seqs=B, num_tokens=B, is_decode=True, num_splits=nsplit,
+                                split_len=split_len, part_o=part_o, part_ml=part_ml)
+            hidden = self.model.forward(ids, v["pos"][j], meta, self.kv_caches)
+            logits = self.model.compute_logits(hidden)
+            sample(logits, self.sampler, v["slots"], out=out_tokens[j])
+        return out_tokens
+
+    def _window(self, seqs) -> int:
+        """Largest power-of-two window <= decode_window that no sequence's
+        max_tokens / max_model_len cuts short and whose KV blocks fit."""
+        K = max(1, self.cfg.decode_window)
+        for s in seqs:
+            K = min(K, s.params.max_tokens - len(s.output_ids), self.cfg.max_model_len - s.total_len)
+        K = max(1, K)
+        while K & (K - 1):
+            K &= K - 1
+        if K > 1:
+            for s in seqs:
+                if not self.kv.ensure(s, s.total_len + K - 1):
+                    return 1
+        return K
 
     def _run_decode(self, seqs) -> list[Sequence]:
         t0 = time.perf_counter()
         n = len(seqs)
-        max_ctx = max(s.total_len for s in seqs)
-        width = self.max_blocks_per_seq
         use_graph = (self.on_gpu and self.cfg.use_cuda_graph and self.model.tp.trivial
                      and n <= max(self.cfg.graph_batch_sizes))
+        K = self._window(seqs) if use_graph else 1
+        max_ctx = max(s.total_len for s in seqs) + K - 1
         if use_graph:
+            width = self.max_blocks_per_seq
             B = next(b for b in self.cfg.graph_batch_sizes if b >= n)
             split_len = _split_len_for(B)
             nsplit = min(_pow2_at_least(-(-max_ctx // split_len)), -(-self.cfg.max_model_len // split_len))
-            g = self._graphs.get((B, nsplit, split_len))
+            g = self._graphs.get((B, nsplit, split_len, K))
             if g is None:
-                g = self._capture(B, nsplit, split_len)
-            packed = self._decode_inputs(seqs, B, width)
+                g = self._capture(B, nsplit, split_len, K)
+            packed = self._decode_inputs(seqs, B, width, K)
             self._static_host[: packed.size] = torch.from_numpy(packed)
             self._static_dev[: packed.size].copy_(self._static_host[: packed.size], non_blocking=True)
             g.graph.replay()
-            toks = g.out_tokens[:n].tolist()
+            tw = time.perf_counter()
+            toks = g.out_tokens[:K, :n].cpu().numpy()
+            self.stats["decode_wait_s"] += time.perf_counter() - tw
             self.stats["graph_replays"] += 1
         else:
             split_len = _split_len_for(n)
             nsplit = max(1, -(-max_ctx // split_len))
             width = max(len(s.blocks) for s in seqs)
-            dev = self._to_dev(self._decode_inputs(seqs, n, width))
-            out = torch.empty(n, dtype=torch.int32, device=self.device)
-            toks = self._decode_forward(self._views(dev, n, width), n, nsplit, split_len, out).tolist()
+            dev = self._to_dev(self._decode_inputs(seqs, n, width, 1))
+            out = torch.empty(1, n, dtype=torch.int32, device=self.device)
+            toks = self._decode_forward(self._views(dev, n, width, 1), n, nsplit, split_len, out, 1).cpu().numpy()
         now = time.perf_counter()
         finished = []
-        for s, t in zip(seqs, toks):
-            s.num_computed = s.total_len
-            if self._append(s, int(t), now):
-                finished.append(s)
-        self.stats["decode_tokens"] += n
+        live = list(seqs)
+        for j in range(K):
+            nxt = []
+            for i, s in enumerate(seqs):
+                if s.finish_reason is not None or s.status != SeqStatus.RUNNING:
+                    continue
+                s.num_computed = s.total_len
+                if self._append(s, int(toks[j, i]), now):
+                    finished.append(s)
+                else:
+                    nxt.append(s)
+            self.stats["decode_tokens"] += len(live)
+            live = nxt
+            if not live:
+                break
+        self.stats["decode_steps"] += K
         self.stats["decode_s"] += now - t0
         return finished
 
     def _ensure_static(self):
         if self._static is None:
             W = self.max_blocks_per_seq
-            size = 6 * self._max_b + 1 + self._max_b * W
+            Kmax = max(1, self.cfg.decode_window)
+            size = (3 * Kmax + 3) * self._max_b + 1 + self._max_b * W
             self._static_dev = torch.zeros(size, dtype=torch.int32, device=self.device)
             self._static_host = torch.zeros(size, dtype=torch.int32).pin_memory()
             self._static = True
             self._graph_pool = torch.cuda.graph_pool_handle()
 
-    def _capture(self, B, nsplit, split_len) -> _DecodeGraph:
+    def _capture(self, B, nsplit, split_len, K=1) -> _DecodeGraph:
         self._ensure_static()
         W = self.max_blocks_per_seq
         # a benign batch: every row is a padding row (scratch block, scratch slot)
-        dummy = self._decode_inputs([], B, W)
+        dummy = self._decode_inputs([], B, W, K)
         self._static_dev[: dummy.size].copy_(torch.from_numpy(dummy))
-        v = self._views(self._static_dev, B, W)
-        out = torch.empty(B, dtype=torch.int32, device=self.device)
+        v = self._views(self._static_dev, B, W, K)
+        out = torch.zeros(K, B, dtype=torch.int32, device=self.device)
         rng_save = self.sampler.rng.clone()
         seen_save = self.sampler.seen[self.scratch_slot].clone()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
-                self._decode_forward(v, B, nsplit, split_len, out)
+                self._decode_forward(v, B, nsplit, split_len, out, K)
         torch.cuda.current_stream().wait_stream(s)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, pool=self._graph_pool):
-            self._decode_forward(v, B, nsplit, split_len, out)
+            self._decode_forward(v, B, nsplit, split_len, out, K)
         torch.cuda.synchronize()
         self.sampler.rng.copy_(rng_save)
         self.sampler.seen[self.scratch_slot].copy_(seen_save)
-        g = _DecodeGraph(graph, out, B, nsplit, split_len)
-        self._graphs[(B, nsplit, split_len)] = g
+        g = _DecodeGraph(graph, out, B, nsplit, split_len, K)
+        self._graphs[(B, nsplit, split_len, K)] = g
         self.stats["graph_captures"] += 1
         return g
 
@@ -377,8 +431,8 @@ class LLMEngine:
         for B in batch_sizes or self.cfg.graph_batch_sizes:
             split_len = _split_len_for(B)
             nsplit = _pow2_at_least(-(-max_ctx // split_len))
-            if (B, nsplit, split_len) not in self._graphs:
-                self._capture(B, nsplit, split_len)
+            if (B, nsplit, split_len, 1) not in self._graphs:
+                self._capture(B, nsplit, split_len, 1)
 
     # ------------------------------------------------------------------ outputs
     def _append(self, s: Sequence, tok: int, now: float) -> bool:

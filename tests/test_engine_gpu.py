@@ -63,3 +63,22 @@ def test_prefix_cache_and_sampling(setup):
     assert all(o.cached_tokens > 0 for o in outs)
     st = eng.kv.stats()
     assert st["prefix_hits"] > 0
+
+
+def test_multistep_window_sampling_and_stop(setup):
+    """K-step decode windows (one hipGraph replay per window) must sample the
+    same tokens as one-step eager decode — top-p + repetition penalty with a
+    per-request seed — and stop exactly at a stop token met inside a window."""
+    model, tok = setup
+    sp = SamplingParams(max_tokens=19, temperature=0.7, top_p=0.9, repetition_penalty=1.2, ignore_eos=True, seed=5)
+    mk = lambda g: LLMEngine(model, tok, EngineConfig(max_num_seqs=8, max_model_len=2048, num_blocks=1024,  # noqa
+                                                      use_cuda_graph=g, decode_window=8))
+    a = mk(True).generate(_prompts(tok), sp)
+    b = mk(False).generate(_prompts(tok), sp)
+    assert [x.token_ids for x in a] == [x.token_ids for x in b]
+    stop_at = a[2].token_ids[5]
+    first = a[2].token_ids.index(stop_at)
+    sp2 = SamplingParams(max_tokens=19, temperature=0.7, top_p=0.9, repetition_penalty=1.2, ignore_eos=True, seed=5,
+                         stop_token_ids=[stop_at])
+    c = mk(True).generate(_prompts(tok), sp2)
+    assert c[2].token_ids == a[2].token_ids[: first + 1] and c[2].finish_reason == "stop"
