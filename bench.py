@@ -165,9 +165,7 @@ def main():
 
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         tt = torch.tensor(ttfts, dtype=torch.float64, device=dev)
-        g = torch.empty(world, tt.numel(), dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(g, tt)
-        ttfts_all = g.cpu().tolist()
+        ttfts_all = group.all_gather(tt).cpu().tolist()
     elapsed = float(t.item())
     total_q = args.batch * args.steps * world
     qps = total_q / elapsed

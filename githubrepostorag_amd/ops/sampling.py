@@ -101,7 +101,11 @@ def sample_ref(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, g
 def sample(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, out: torch.Tensor | None = None):
     """logits [B, >=V] (fp32 or bf16) -> sampled token ids int32 [B]."""
     if not logits.is_cuda:
-        return sample_ref(logits, state, slots)
+        res = sample_ref(logits, state, slots)
+        if out is not None:
+            out.copy_(res)
+            return out
+        return res
     B = logits.shape[0]
     if out is None:
         out = torch.empty(B, dtype=torch.int32, device=logits.device)

@@ -105,9 +105,10 @@ class Group:
         """[...] -> [size, ...] (one collective)."""
         if self.trivial:
             return t.unsqueeze(0)
-        out = torch.empty((self.size, *t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous(), group=self.pg)
-        return out
+        # flat concatenated form: the only layout both RCCL and gloo accept
+        out = torch.empty(self.size * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous().view(-1), group=self.pg)
+        return out.view(self.size, *t.shape)
 
     def all_gather_topk(self, scores: torch.Tensor, ids: torch.Tensor, k: int):
         """C3: merge per-shard top-k lists.  scores fp32 [nq, k], ids int64

@@ -1,0 +1,40 @@
+"""The bench.py driver contract on CPU: single process, and two ranks under
+torch.distributed.run (gloo) with tiny models — one JSON line from rank 0
+with the whole-job aggregate, weak scaling and the BASELINE metric name."""
+import json
+import os
+import subprocess
+import sys
+
+from dist_utils import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TINY = ["--model", "qwen2-tiny", "--encoder", "encoder-tiny", "--index-size", "4000", "--index-kind", "ivf",
+        "--nlist", "16", "--nprobe", "4", "--batch", "3", "--prompt-len", "48", "--gen-len", "5",
+        "--ingest-files", "4", "--steps", "2", "--warmup", "1"]
+
+
+def _run(cmd, env):
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_single_process_cpu():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    res = _run([sys.executable, "bench.py", "--gpus", "1", *TINY], env)
+    assert res["n_gpus"] == 1 and res["steps"] == 2 and res["warmup"] == 1
+    assert res["metric"].startswith("RAG queries/sec") and res["value"] > 0 and res["higher_is_better"]
+    assert res["scaling"] == "weak" and res["config"]["global_batch"] == 3
+    assert res["ingest_docs_per_s"] > 0 and res["p50_ttft_ms"] > 0
+
+
+def test_bench_two_ranks_gloo():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    res = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", *TINY],
+               env)
+    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 6 and res["config"]["parallelism"] == "dp2"
+    assert res["value"] > 0
