@@ -57,8 +57,38 @@ def _seen_mask(state, slot, V, device):
     return ((words[idx >> 5] >> (idx & 31)) & 1).bool()
 
 
+_M64 = (1 << 64) - 1
+
+
+def _mix64(z):
+    """splitmix64 finaliser (same constants as csrc/kernels/sampling.hip); z: uint64 ndarray."""
+    import numpy as np
+
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def gumbel_noise(seed: int, counter: int, slot: int, V: int) -> torch.Tensor:
+    """G_i = -log(-log u_i) from the kernel's counter-based hash of (seed,
+    per-slot step counter, slot, token) — reproducible per request and equal
+    on CPU and GPU."""
+    import numpy as np
+
+    with np.errstate(over="ignore"):
+        inner = _mix64(np.asarray([(counter * 0x100000001B3 + slot) & _M64], dtype=np.uint64))
+        base = _mix64(np.asarray([seed & _M64], dtype=np.uint64) ^ inner)
+        h = _mix64(base + np.arange(V, dtype=np.uint64))
+    u = ((h >> np.uint64(40)).astype(np.float64) + 0.5) * (1.0 / 16777216.0)
+    return torch.from_numpy(-np.log(-np.log(u))).float()
+
+
 def sample_ref(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, generator=None) -> torch.Tensor:
-    """Reference sampler with identical semantics (different RNG stream)."""
+    """Reference sampler with the kernel's semantics and RNG stream (Gumbel-max
+    over the kept tokens with the same counter-based noise); ``generator``
+    switches to torch.multinomial for distribution tests."""
     B, V = logits.shape[0], state.vocab
     out = torch.empty(B, dtype=torch.int32, device=logits.device)
     for b in range(B):
@@ -88,7 +118,11 @@ def sample_ref(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, g
                 thr = x[si[min(n, V) - 1]]
                 keep &= x >= thr
             xs = torch.where(keep, x, torch.full_like(x, float("-inf")))
-            tok = int(torch.multinomial(torch.softmax(xs, 0), 1, generator=generator))
+            if generator is not None:
+                tok = int(torch.multinomial(torch.softmax(xs, 0), 1, generator=generator))
+            else:
+                g = gumbel_noise(state.seed, int(state.rng[s]), s, V).to(xs.device)
+                tok = int(torch.argmax(xs + g))
         out[b] = tok
         if True:  # the kernel always records the sampled token
             w = int(state.seen[s, tok >> 5]) & 0xFFFFFFFF

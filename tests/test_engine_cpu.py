@@ -1,0 +1,146 @@
+"""LLM engine on CPU (fp32 reference ops): continuous batching, chunked
+prefill, prefix cache, preemption, abort, stop handling, the native block
+allocator and the tokenizers.  The GPU tier (test_engine_gpu.py) repeats the
+numerics on the HIP kernels with hipGraph decode windows."""
+import numpy as np
+import pytest
+import torch
+
+from githubrepostorag_amd.engine.llm_engine import EngineConfig, LLMEngine
+from githubrepostorag_amd.engine.scheduler import KVCacheManager
+from githubrepostorag_amd.engine.sequence import SamplingParams, Sequence
+from githubrepostorag_amd.engine.tokenizer import IM_END, IM_START, ByteBPETokenizer, WordPieceTokenizer, chatml
+from githubrepostorag_amd.models.configs import decoder_config
+from githubrepostorag_amd.models.qwen2 import Qwen2Model
+
+
+@pytest.fixture(scope="module")
+def model():
+    return Qwen2Model(decoder_config("qwen2-tiny"), device="cpu", dtype=torch.float32, seed=0, init_std=0.05)
+
+
+@pytest.fixture(scope="module")
+def tok():
+    return ByteBPETokenizer(512)
+
+
+PROMPTS = [[5, 17, 99, 3, 250], list(range(1, 40)), [7] * 70, [300, 301, 302]]
+GREEDY = SamplingParams(max_tokens=7, temperature=0.0, ignore_eos=True)
+
+
+def _gen(model, tok, prompts=PROMPTS, sp=GREEDY, **cfg):
+    kw = dict(max_num_seqs=4, max_model_len=512, num_blocks=256, use_cuda_graph=False)
+    kw.update(cfg)
+    eng = LLMEngine(model, tok, EngineConfig(**kw))
+    return eng, eng.generate(prompts, sp)
+
+
+def test_decode_matches_full_recompute(model, tok):
+    _, outs = _gen(model, tok)
+    _, ref_eng = None, LLMEngine(model, tok, EngineConfig(max_num_seqs=1, max_model_len=512, num_blocks=256,
+                                                          use_cuda_graph=False, enable_prefix_caching=False))
+    for p, o in zip(PROMPTS, outs):
+        assert len(o.token_ids) == 7 and o.finish_reason == "length"
+        for j in range(len(o.token_ids)):
+            r = ref_eng.generate([p + o.token_ids[:j]], SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))
+            assert r[0].token_ids[0] == o.token_ids[j]
+
+
+def test_chunked_prefill_and_small_batches_identical(model, tok):
+    _, a = _gen(model, tok)
+    eng, b = _gen(model, tok, max_num_batched_tokens=16, max_num_seqs=2)
+    assert [x.token_ids for x in a] == [x.token_ids for x in b]
+    assert eng.stats["steps"] > 10
+
+
+def test_preemption_recomputes_identically(model, tok):
+    prompts = [[(7 * i + j) % 500 + 1 for j in range(31)] for i in range(4)]
+    _, a = _gen(model, tok, prompts=prompts)
+    # 16 usable blocks of 8 tokens hold the four 31-token prompts (4 blocks each) but not
+    # their growth past 32 tokens: decode must preempt the youngest and recompute it later
+    eng, b = _gen(model, tok, prompts=prompts, num_blocks=17, block_size=8, enable_prefix_caching=False)
+    assert [x.token_ids for x in a] == [x.token_ids for x in b]
+    assert eng.sched.num_preemptions > 0
+
+
+def test_prefix_cache_hit(model, tok):
+    base = list(range(10, 90))
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_model_len=512, num_blocks=256,
+                                             use_cuda_graph=False))
+    eng.generate([base + [1]], GREEDY)
+    outs = eng.generate([base + [2], base + [3]], GREEDY)
+    assert all(o.cached_tokens >= 64 for o in outs)
+    assert eng.kv.stats()["prefix_hits"] > 0
+    _, ref = _gen(model, tok, prompts=[base + [2], base + [3]], enable_prefix_caching=False)
+    assert [o.token_ids for o in outs] == [o.token_ids for o in ref]
+
+
+def test_abort_and_stop_tokens(model, tok):
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_model_len=512, num_blocks=256,
+                                             use_cuda_graph=False))
+    rid = eng.add_request(PROMPTS[0], SamplingParams(max_tokens=50, temperature=0.0, ignore_eos=True))
+    eng.step()
+    eng.abort(rid)
+    while eng.has_unfinished():
+        eng.step()
+    assert eng.get(rid).finish_reason == "abort"
+    _, full = _gen(model, tok, prompts=[PROMPTS[1]])
+    stop = full[0].token_ids[3]
+    _, cut = _gen(model, tok, prompts=[PROMPTS[1]],
+                  sp=SamplingParams(max_tokens=7, temperature=0.0, ignore_eos=True, stop_token_ids=[stop]))
+    k = full[0].token_ids.index(stop)
+    assert cut[0].token_ids == full[0].token_ids[: k + 1] and cut[0].finish_reason == "stop"
+
+
+def test_sampling_seeded_and_penalty(model, tok):
+    sp = SamplingParams(max_tokens=12, temperature=0.9, top_p=0.9, repetition_penalty=1.3, ignore_eos=True, seed=7)
+    _, a = _gen(model, tok, sp=sp)
+    _, b = _gen(model, tok, sp=sp)
+    assert [x.token_ids for x in a] == [x.token_ids for x in b]
+
+
+def test_streaming_callback(model, tok):
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=2, max_model_len=512, num_blocks=64, use_cuda_graph=False))
+    seen = []
+    eng.add_request("def retry(policy):", SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True),
+                    on_token=lambda s, d, fin: seen.append((d, fin)))
+    while eng.has_unfinished():
+        eng.step()
+    assert len(seen) == 5 and seen[-1][1] is True
+
+
+def test_block_allocator_prefix_and_free():
+    kv = KVCacheManager(num_blocks=32, block_size=4)
+    free0 = kv.num_free
+    s = Sequence("a", list(range(40)), SamplingParams())
+    assert kv.ensure(s, 40) and len(s.blocks) == 10 and kv.num_free == free0 - 10
+    assert KVCacheManager.SCRATCH_BLOCK not in s.blocks
+    s.num_computed = 40
+    kv.register_full_blocks(s)
+    t = Sequence("b", list(range(40)) + [99], SamplingParams())
+    got = kv.match_prefix(t)
+    assert got == 40 and t.blocks == s.blocks
+    kv.free(s)
+    kv.free(t)
+    assert kv.num_free == free0
+    big = Sequence("c", list(range(1000)), SamplingParams())
+    assert not kv.ensure(big, 1000)  # more blocks than exist: refused, nothing leaked
+    assert kv.num_free == free0
+
+
+def test_byte_bpe_roundtrip_and_chatml(tok):
+    for text in ["def f(x):\n    return x * 2  # ünïcode ✓", "", "   spaces\t\ttabs\n\n"]:
+        assert tok.decode(tok.encode(text)) == text
+    msg = chatml([{"role": "system", "content": "be brief"}, {"role": "user", "content": "hi"}])
+    assert msg.startswith(IM_START + "system\nbe brief" + IM_END) and msg.endswith(IM_START + "assistant\n")
+    ids = tok.encode(msg)
+    assert max(ids) < 512
+
+
+def test_wordpiece_basic():
+    wp = WordPieceTokenizer(2048)
+    ids = wp.encode("Hello, World! retry_policy", max_len=16)
+    assert ids[0] != ids[-1] and 2 < len(ids) <= 16
+    assert all(0 <= i < 2048 for i in ids)
+    assert wp.encode("hello world", 64) == wp.encode("HELLO world", 64)  # lowercasing
+    assert np.asarray(wp.encode("x " * 500, 32)).shape == (32,)

@@ -277,3 +277,25 @@ def test_gemm_stream(dev, M, N, K):
     for plan in ((4, 128, 256), (4, 64, 100), (2, 128, 37), (2, 64, 512), (4, 256, 3), (2, 256, 1), (4, 256, 256)):
         for _ in range(2):  # second call re-uses the ticket counters the first call reset
             close(gemm_stream(x, w, None, plan), ref, 3e-2, 2e-2)
+
+
+def test_sampler_matches_reference_stream(dev):
+    """The HIP sampler and the CPU reference share the counter-based Gumbel
+    stream: same logits + state -> the same token (up to rare rounding ties)."""
+    V, B = 5000, 16
+    g = torch.Generator().manual_seed(11)
+    logits = torch.randn(B, V, generator=g) * 3
+    agree = 0
+    for dev_state in (True,):
+        st_g = S.SamplerState(B, V, dev, seed=123)
+        st_c = S.SamplerState(B, V, "cpu", seed=123)
+        for i in range(B):
+            for st in (st_g, st_c):
+                st.reset_slot(i, 0.8, 0.9 if i % 2 else 1.0, 50 if i % 3 == 0 else 0, 1.3, list(range(0, 400, 3)),
+                              seed=i)
+        slots = torch.arange(B, dtype=torch.int32)
+        for _ in range(3):
+            a = S.sample(logits.to(dev), st_g, slots.to(dev)).cpu()
+            b = S.sample_ref(logits, st_c, slots)
+            agree += int((a == b).sum())
+    assert agree >= 3 * B - 2, agree
