@@ -1,0 +1,161 @@
+"""Command line entry points (``python -m githubrepostorag_amd <command>``).
+
+Replaces the reference's three process entry points — the API
+(rest_api/src/app/__main__.py:5-7, uvicorn on :8000), the ARQ worker
+(helm/templates/rag-worker-deployment.yaml:64) and the ingest batch job
+(ingest/src/app/__main__.py:7-18) — with one process per GPU that hosts the
+engine, encoder, index, job workers and API together:
+
+  serve    FastAPI app (jobs + SSE, /health, /metrics, /static UI, OpenAI /v1)
+           with the in-process job workers; the runtime (models, index) is
+           built once at startup on this process's GPU.
+  ingest   ingest repositories (github | local dir | synthetic) into the
+           index and optionally snapshot it to INDEX_DIR.
+  ask      one RAG query through the agent, printing events as they arrive.
+  build    compile the gfx950 kernel library and the host runtime in-tree.
+  config   print the resolved settings (env-compatible with the reference).
+  bench    forward to bench.py (driver contract).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import subprocess
+import sys
+
+
+def _settings(args):
+    from .config import settings
+
+    s = settings(reload=True)
+    for k in ("qwen_model", "embed_model", "device", "index_dir", "model_dir", "encoder_dir"):
+        v = getattr(args, k, None)
+        if v:
+            setattr(s, k, v)
+    return s
+
+
+def _runtime(args, build_engine=True):
+    from .service.runtime import RAGRuntime
+
+    return RAGRuntime(_settings(args), build_engine=build_engine)
+
+
+def cmd_serve(args) -> int:
+    import uvicorn
+
+    from .service.api import create_app
+
+    s = _settings(args)
+    logging.basicConfig(level=s.log_level, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    app = create_app(runtime_factory=lambda: _runtime(args))
+    uvicorn.run(app, host=args.host, port=args.port, log_level=s.log_level.lower())
+    return 0
+
+
+def cmd_ingest(args) -> int:
+    from .ingest.controller import IngestController
+
+    s = _settings(args)
+    logging.basicConfig(level=s.log_level, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    rt = _runtime(args)
+    ctl = IngestController(rt, extract=not args.no_extract)
+    if args.repos:
+        comps = [{"repo": r, "namespace": args.namespace} for r in args.repos]
+    else:
+        comps = [{"repo": "synthetic-repo", "namespace": args.namespace}] if args.source == "synthetic" else []
+    if args.source == "local" and not args.repos:
+        comps = [{"repo": os.path.basename(os.path.abspath(args.path)), "namespace": args.namespace}]
+    res = ctl.ingest_many(comps, branch=args.branch, dev_force_standalone=args.dev_force_standalone or s.dev_force_standalone,
+                          source=args.source, path=args.path)
+    for r in res:
+        print(json.dumps({k: r.get(k) for k in ("ok", "repo", "namespace", "nodes_written", "documents",
+                                                "nodes_per_scope", "run_seconds")}))
+    out = args.save or s.index_dir
+    if out:
+        rt.store.save(out)
+        print(json.dumps({"index_saved": out, "counts": rt.store.counts()}))
+    rt.close()
+    return 0 if all(r.get("ok") for r in res) else 1
+
+
+def cmd_ask(args) -> int:
+    rt = _runtime(args)
+    agent = rt.agent()
+
+    def progress(p):
+        print(json.dumps({"event": "turn", "data": p})[:400], file=sys.stderr)
+
+    res = agent.run(args.query, namespace=args.namespace, progress_cb=progress)
+    print(json.dumps({"answer": res.get("answer"), "scope": res.get("scope"),
+                      "sources": [s.get("metadata", {}) for s in res.get("sources") or []]}, indent=1))
+    rt.close()
+    return 0
+
+
+def cmd_build(args) -> int:
+    from .utils.native_build import build_all
+
+    build_all(force=args.force, verbose=args.verbose)
+    return 0
+
+
+def cmd_config(args) -> int:
+    print(json.dumps(_settings(args).to_dict(), indent=1, default=str))
+    return 0
+
+
+def cmd_bench(args, rest) -> int:
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return subprocess.call([sys.executable, os.path.join(root, "bench.py"), *rest])
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="githubrepostorag_amd", description=__doc__.split("\n\n")[0])
+    sub = ap.add_subparsers(dest="cmd", required=True)
+
+    def common(p):
+        p.add_argument("--qwen-model", dest="qwen_model")
+        p.add_argument("--embed-model", dest="embed_model")
+        p.add_argument("--device")
+        p.add_argument("--index-dir", dest="index_dir")
+        p.add_argument("--model-dir", dest="model_dir")
+        p.add_argument("--encoder-dir", dest="encoder_dir")
+
+    p = sub.add_parser("serve", help="API + workers + engine in one process")
+    common(p)
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=8000)
+    p = sub.add_parser("ingest", help="ingest repositories into the index")
+    common(p)
+    p.add_argument("--source", choices=["github", "local", "synthetic"], default="synthetic")
+    p.add_argument("--path", help="local directory (source=local)")
+    p.add_argument("--repos", nargs="*", default=[])
+    p.add_argument("--namespace", default="default")
+    p.add_argument("--branch", default=None)
+    p.add_argument("--dev-force-standalone", action="store_true")
+    p.add_argument("--no-extract", action="store_true", help="skip the LLM summary/title/keyword extractors")
+    p.add_argument("--save", help="snapshot directory (default INDEX_DIR)")
+    p = sub.add_parser("ask", help="one RAG query through the agent")
+    common(p)
+    p.add_argument("query")
+    p.add_argument("--namespace", default="default")
+    p = sub.add_parser("build", help="compile the native libraries in-tree")
+    p.add_argument("--force", action="store_true")
+    p.add_argument("-v", "--verbose", action="store_true")
+    p = sub.add_parser("config", help="print resolved settings")
+    common(p)
+    sub.add_parser("bench", help="run bench.py (remaining args are forwarded)", add_help=False)
+
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if argv and argv[0] == "bench":
+        return cmd_bench(None, argv[1:])
+    args = ap.parse_args(argv)
+    return {"serve": cmd_serve, "ingest": cmd_ingest, "ask": cmd_ask, "build": cmd_build,
+            "config": cmd_config}[args.cmd](args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

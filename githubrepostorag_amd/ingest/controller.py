@@ -201,7 +201,8 @@ class IngestController:
         _push("ingest_run_seconds", "Total duration (seconds) of a single ingest run",
               {"repo": repo, "namespace": namespace, "branch": branch, "run_id": str(run_id)}, total,
               self.s.pushgateway_address)
-        res = {"repo": repo, "namespace": namespace, "collection": collection, "component_kind": kind,
+        res = {"ok": True, "run_id": str(run_id), "repo": repo, "namespace": namespace, "collection": collection,
+               "component_kind": kind,
                "branch": branch, "nodes_written": len(code_nodes), "is_standalone": is_sa,
                "dev_forced_standalone": forced, "documents": len(docs), "nodes_per_scope": written,
                "stage_seconds": {k: round(v, 4) for k, v in timings.items()}, "run_seconds": round(total, 4)}

@@ -262,3 +262,16 @@ def test_cancel_flags_callbacks():
     f.cancel_sync("x")
     assert f.is_cancelled_sync("x") and seen == [1]
     assert not f.is_cancelled_sync("y")
+
+
+def test_static_ui_served():
+    from fastapi.testclient import TestClient
+
+    from githubrepostorag_amd.service.api import APIState, create_app
+
+    with TestClient(create_app(APIState())) as c:
+        r = c.get("/static/index.html")
+        assert r.status_code == 200 and "text/html" in r.headers["content-type"]
+        body = r.text
+        for needle in ("/rag/jobs", "EventSource", "/cancel", '"token"', '"final"'):
+            assert needle in body
