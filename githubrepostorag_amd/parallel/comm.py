@@ -126,6 +126,15 @@ class Group:
         s, sel = all_s.topk(min(k, all_s.shape[1]), dim=1)
         return s, all_ids.gather(1, sel)
 
+    def all_to_all(self, t: torch.Tensor) -> torch.Tensor:
+        """[size, ...] -> [size, ...]: slice j goes to local rank j; slice i of
+        the result came from local rank i (one all_to_all_single)."""
+        if self.trivial:
+            return t
+        out = torch.empty_like(t)
+        dist.all_to_all_single(out.view(-1), t.contiguous().view(-1), group=self.pg)
+        return out
+
     def broadcast(self, t: torch.Tensor, src_local: int = 0) -> torch.Tensor:
         if not self.trivial:
             dist.broadcast(t, src=self.ranks[src_local], group=self.pg)

@@ -102,7 +102,9 @@ def _sharded_worker(rank, world, n, d, k):
     local = X[rank::world]  # global id = local * world + rank
     idx = ShardedIndex(d, world_group(), "cpu", kind="flat")
     idx.build(local)
-    s, i = idx.search(Q, k)
+    # every rank brings different queries (rank 1 a different-sized batch)
+    mine = Q[rank:] if rank else Q
+    s, i = idx.search(mine, k)
     return s.tolist(), i.tolist()
 
 
@@ -112,11 +114,12 @@ def test_sharded_index_matches_flat():
     g = torch.Generator().manual_seed(3)
     X = torch.nn.functional.normalize(torch.randn(n, d, generator=g), dim=1)
     Q = torch.nn.functional.normalize(torch.randn(5, d, generator=g), dim=1)
-    exact = Q.to(torch.bfloat16).float() @ X.to(torch.bfloat16).float().T
-    ref = exact.topk(k, dim=1)
-    for s, i in res:
-        assert res[0][1] == i  # every rank holds the same merged answer
+    for rank, (s, i) in enumerate(res):
+        mine = Q[rank:] if rank else Q
+        exact = mine.to(torch.bfloat16).float() @ X.to(torch.bfloat16).float().T
+        ref = exact.topk(k, dim=1)
         got = torch.tensor(i)
+        assert got.shape == (mine.shape[0], k)
         assert (got >= 0).all() and len({tuple(r) for r in i}) == len(i)
         # the merged ids are a true top-k up to bf16 score ties
         assert torch.allclose(exact.gather(1, got), ref.values, atol=2e-2)
