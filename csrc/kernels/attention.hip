@@ -268,13 +268,15 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
 // comes through the scalar cache, so no vector load sits between two tiles.
 // Tile t+1 is issued before tile t is computed and retired with a counted
 // vmcnt, keeping 32 KiB per wave in flight under the MFMA/softmax work.
-template <int D>
+template <int D, int TK>
 __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
+  static_assert(TK == 32 || TK == 64, "keys per tile");
+  constexpr int NT16 = TK / 16, NCC = TK / 32;
   constexpr int RB = 2 * D;
   constexpr int CPR = D / 8;
   constexpr int NC = D / 32;
   constexpr int ND = D / 16;
-  constexpr int TILE = KT * RB;      // bytes per K (or V) tile
+  constexpr int TILE = TK * RB;      // bytes per K (or V) tile
   constexpr int NI = TILE / 1024;    // LDS-DMA instructions per tile per tensor
   constexpr int RPI = 1024 / RB;     // rows per instruction
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
@@ -341,22 +343,22 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
   f32x4_t o[ND];
 #pragma unroll
   for (int n = 0; n < ND; ++n) o[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const int ntiles = (kv_hi - kv_lo + KT - 1) / KT;
+  const int ntiles = (kv_hi - kv_lo + TK - 1) / TK;
   issue(kv_lo, 0);
   for (int t = 0; t < ntiles; ++t) {
     const int stage = t & 1;
-    const int kt0 = kv_lo + t * KT;
+    const int kt0 = kv_lo + t * TK;
     if (t + 1 < ntiles) {
-      issue(kt0 + KT, stage ^ 1);
+      issue(kt0 + TK, stage ^ 1);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     const char* k_lds = smem + stage * 2 * TILE;
     const char* v_lds = k_lds + TILE;
-    f32x4_t s[4];
+    f32x4_t s[NT16];
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
+    for (int tt = 0; tt < NT16; ++tt) {
       s[tt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       const int row = 16 * tt + li;
 #pragma unroll
@@ -368,7 +370,7 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
     }
     float tmax = -INFINITY;
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt)
+    for (int tt = 0; tt < NT16; ++tt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kt0 + 16 * tt + 4 * h4 + r;
@@ -386,9 +388,9 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
     lsum *= alpha;
 #pragma unroll
     for (int n = 0; n < ND; ++n) o[n] *= alpha;
-    float pr[4][4];
+    float pr[NT16][4];
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt)
+    for (int tt = 0; tt < NT16; ++tt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         pr[tt][r] = exp2f(s[tt][r] - m_use);
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
       }
     const int tq = li >> 2, tp = li & 3;
 #pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
+    for (int cc = 0; cc < NCC; ++cc) {
       bf16x8_t bp;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -482,9 +484,12 @@ int launch(const AttnParams& prm, int nseq, hipStream_t stream) {
 }
 
 template <int D>
-int launch_decode(const AttnParams& prm, int nseq, hipStream_t stream) {
+int launch_decode(const AttnParams& prm, int nseq, int tk, hipStream_t stream) {
   dim3 grid(nseq, prm.Hkv, prm.num_splits);
-  paged_decode_kernel<D><<<grid, 64, 0, stream>>>(prm);
+  if (tk == 32)
+    paged_decode_kernel<D, 32><<<grid, 64, 0, stream>>>(prm);
+  else
+    paged_decode_kernel<D, 64><<<grid, 64, 0, stream>>>(prm);
   int err = (int)hipGetLastError();
   if (err) return err;
   if (prm.num_splits > 1) {
@@ -497,10 +502,12 @@ int launch_decode(const AttnParams& prm, int nseq, hipStream_t stream) {
 
 template <int D>
 int dispatch_nw(const AttnParams& prm, int nseq, int nw, bool paged, hipStream_t stream) {
-  // nw == 1 with q_len == 1: LDS-DMA pipelined decode kernel; nw == 2: the
-  // generic kernel with one wave per workgroup (kept for A/B comparisons)
-  if (paged && nw == 1 && prm.tiles_per_seq == 1 && prm.G <= 16 && prm.BS % 16 == 0)
-    return launch_decode<D>(prm, nseq, stream);
+  // nw == 1 / 3 with q_len == 1: LDS-DMA pipelined decode kernel with 64- / 32-key
+  // tiles (32-key tiles halve the LDS ring so more single-wave workgroups share a
+  // CU); nw == 2: the generic kernel with one wave per workgroup (A/B reference)
+  if (paged && (nw == 1 || nw == 3) && prm.tiles_per_seq == 1 && prm.G <= 16 && prm.BS % 16 == 0)
+    return launch_decode<D>(prm, nseq, nw == 3 ? 32 : 64, stream);
+  if (nw == 3) nw = 1;
   if (nw == 2) nw = 1;
   if (paged) {
     return nw == 1 ? launch<D, 1, true>(prm, nseq, stream) : launch<D, 4, true>(prm, nseq, stream);
@@ -523,7 +530,7 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
                                   float scale, int causal, int num_splits, int split_len,
                                   float* part_o, float* part_ml, int nw, hipStream_t stream) {
   if (nseq <= 0) return 0;
-  if (Hq % Hkv != 0 || BS <= 0 || (nw != 1 && nw != 2 && nw != 4)) return (int)hipErrorInvalidValue;
+  if (Hq % Hkv != 0 || BS <= 0 || nw < 1 || nw > 4) return (int)hipErrorInvalidValue;
   if (num_splits > 1 && (max_q_len != 1 || !part_o || !part_ml || split_len % KT != 0))
     return (int)hipErrorInvalidValue;
   AttnParams prm{};

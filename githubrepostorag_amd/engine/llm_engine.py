@@ -53,10 +53,8 @@ class EngineConfig:
 
 
 def _split_len_for(batch: int) -> int:
-    # decode split-KV plan (microbench: B64 ctx1152 split512 42us < split256 45us;
-    # small batches need more splits to fill the CUs)
-    if batch >= 32:
-        return 8 * KV_TILE
+    # decode split-KV plan (microbench, 32-key LDS-DMA tiles: B64 ctx1152 split256
+    # 36.7 us < split512 38.0 us; small batches need more splits to fill the CUs)
     if batch >= 8:
         return 4 * KV_TILE
     return 2 * KV_TILE

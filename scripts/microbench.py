@@ -74,7 +74,12 @@ def attn_decode_bench(B, ctx, split_len):
                           slot_mapping=torch.zeros(B, dtype=torch.int32, device=dev), max_q_len=1, num_seqs=B,
                           num_tokens=B, is_decode=True, num_splits=ns, split_len=split_len,
                           part_o=torch.empty(ns * B * Hq * D, device=dev), part_ml=torch.empty(ns * B * Hq * 2, device=dev))
-    r = rounds({f"paged_decode_split{split_len}": lambda: A.paged_attention(q, kc, vc, meta, 0.088)})
+    import copy
+
+    m32 = copy.copy(meta)
+    m32.extra = {"decode_nw": 3}
+    r = rounds({f"paged_decode_split{split_len}": lambda: A.paged_attention(q, kc, vc, meta, 0.088),
+                f"paged_decode_tk32_split{split_len}": lambda: A.paged_attention(q, kc, vc, m32, 0.088)})
     gb = B * ctx * Hkv * D * 2 * 2 / 1e9
     for k in r:
         r[k]["TB_s"] = round(gb / (r[k]["min_us"] * 1e-6) / 1e3, 2)

@@ -152,9 +152,11 @@ def test_paged_decode(dev, nsplit_len):
         m.num_splits, m.split_len = ns, sl
         m.part_o = torch.empty(ns * 5 * Hq * D, dtype=torch.float32, device=dev)
         m.part_ml = torch.empty(ns * 5 * Hq * 2, dtype=torch.float32, device=dev)
-    out = A.paged_attention(q.to(dev), kc.to(dev), vc.to(dev), m, scale)
     ref = A.paged_attention_ref(q, kc, vc, meta, scale).reshape(q.shape[0], -1)
-    close(out, ref, 2e-2)
+    for code in (1, 3, 2):  # 64-key LDS-DMA tiles, 32-key tiles, generic kernel
+        m.extra = {"decode_nw": code}
+        out = A.paged_attention(q.to(dev), kc.to(dev), vc.to(dev), m, scale)
+        close(out, ref, 2e-2)
 
 
 @pytest.mark.parametrize("H,D", [(12, 32), (12, 64), (16, 64)])
