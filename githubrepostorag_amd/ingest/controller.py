@@ -23,6 +23,7 @@ import math
 import os
 import time
 import uuid
+from concurrent.futures import ThreadPoolExecutor
 from datetime import datetime, timezone
 from pathlib import Path
 
@@ -164,21 +165,44 @@ class IngestController:
                     json.dump([{"id": d.id, "text": d.text, "metadata": d.metadata} for d in docs], f)
         common = dict(namespace=namespace, repo=repo, branch=branch, collection=collection, component_kind=kind,
                       is_standalone=is_sa, dev_forced=forced)
-        with timer("code_nodes"):
-            code_nodes = self.extractors.run(self.splitter.get_nodes_from_documents(docs))
-            attach_common_metadata(code_nodes, run_id=run_id, doc_type="code", **common)
-        with timer("catalog"):
-            catalog_nodes = self.hier.catalog_nodes(repo, docs, code_nodes, collection, kind, layer)
-            attach_common_metadata(catalog_nodes, run_id=uuid.UUID(int=0), doc_type="catalog", **common)
-        with timer("file_summaries"):
-            file_nodes = self.hier.file_nodes(code_nodes, repo, namespace, branch, kind)
-            attach_common_metadata(file_nodes, run_id=run_id, doc_type="file", **common)
-        with timer("module_summaries"):
-            module_nodes = self.hier.module_nodes(file_nodes, repo, namespace, branch, kind)
-            attach_common_metadata(module_nodes, run_id=run_id, doc_type="module", **common)
-        with timer("repo_summaries"):
-            repo_nodes = self.hier.repo_nodes(docs, module_nodes, repo, namespace, branch, kind)
-            attach_common_metadata(repo_nodes, run_id=run_id, doc_type="repo", **common)
+        # Stage DAG (the reference ran these 6 stages strictly in sequence,
+        # ingest_controller.py:249-389): the chunk extractors + catalog branch
+        # and the file -> module -> repo roll-up branch only share the split
+        # chunks, and each level's extractor passes run beside the next level's
+        # summary wave, so the engine sees a few large batches instead of many
+        # small serial ones.  Stage timers overlap accordingly.
+        with timer("split"):
+            split_nodes = self.splitter.get_nodes_from_documents(docs)
+        pool = ThreadPoolExecutor(max_workers=4)
+        try:
+            def code_branch():
+                with timer("code_nodes"):
+                    nodes = self.extractors.run(split_nodes)
+                with timer("catalog"):
+                    cat = self.hier.catalog_nodes(repo, docs, nodes, collection, kind, layer)
+                return nodes, cat
+
+            f_code = pool.submit(code_branch)
+            with timer("file_summaries"):
+                file_nodes = self.hier.file_summary_nodes(split_nodes, repo, namespace, branch, kind)
+            f_file_ext = pool.submit(self.hier.extract.run, file_nodes)
+            with timer("module_summaries"):
+                module_nodes = self.hier.module_summary_nodes(file_nodes, repo, namespace, branch, kind)
+            f_mod_ext = pool.submit(self.hier.extract.run, module_nodes)
+            with timer("repo_summaries"):
+                repo_nodes = self.hier.extract.run(
+                    self.hier.repo_summary_nodes(docs, module_nodes, repo, namespace, branch, kind))
+            with timer("extract_wait"):
+                code_nodes, catalog_nodes = f_code.result()
+                f_file_ext.result()
+                f_mod_ext.result()
+        finally:
+            pool.shutdown(wait=True)
+        attach_common_metadata(code_nodes, run_id=run_id, doc_type="code", **common)
+        attach_common_metadata(catalog_nodes, run_id=uuid.UUID(int=0), doc_type="catalog", **common)
+        attach_common_metadata(file_nodes, run_id=run_id, doc_type="file", **common)
+        attach_common_metadata(module_nodes, run_id=run_id, doc_type="module", **common)
+        attach_common_metadata(repo_nodes, run_id=run_id, doc_type="repo", **common)
         with timer("vector_write"):
             written = self.writer.write_nodes_per_scope(catalog_nodes=catalog_nodes, repo_nodes=repo_nodes,
                                                         module_nodes=module_nodes, file_nodes=file_nodes,

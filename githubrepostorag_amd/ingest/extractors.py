@@ -101,13 +101,23 @@ class ExtractorPipeline:
         self.enabled = enabled
 
     def run(self, nodes: list[Node]) -> list[Node]:
+        """The three extractors are independent reads of the same nodes (each
+        writes its own metadata key), so their waves are submitted together:
+        one engine batch instead of three back-to-back ones (the reference ran
+        them sequentially, code_pipeline_service.py:23-51)."""
         if not self.enabled or not nodes:
             return nodes
-        for name, fn in (("summary", lambda: extract_summaries(nodes, self.wave, self.summary_tokens)),
-                         ("title", lambda: extract_titles(nodes, self.wave, self.title_nodes, self.title_tokens)),
-                         ("keywords", lambda: extract_keywords(nodes, self.wave, 10, self.keyword_tokens))):
+        jobs = (("summary", lambda: extract_summaries(nodes, self.wave, self.summary_tokens)),
+                ("title", lambda: extract_titles(nodes, self.wave, self.title_nodes, self.title_tokens)),
+                ("keywords", lambda: extract_keywords(nodes, self.wave, 10, self.keyword_tokens)))
+
+        def guarded(item):
+            name, fn = item
             try:
                 fn()
             except Exception:
                 log.exception("%s extraction failed", name)
+
+        with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+            list(ex.map(guarded, jobs))
         return nodes

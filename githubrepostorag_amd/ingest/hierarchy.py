@@ -34,6 +34,22 @@ class HierarchyBuilder:
         return self.extract.run(self.splitter.get_nodes_from_documents(docs))
 
     def file_nodes(self, code_nodes: list[Node], repo: str, namespace: str, branch: str, kind: str) -> list[Node]:
+        return self.extract.run(self.file_summary_nodes(code_nodes, repo, namespace, branch, kind))
+
+    def module_nodes(self, file_nodes: list[Node], repo: str, namespace: str, branch: str, kind: str,
+                     depth: int = 1, max_files: int = 40) -> list[Node]:
+        return self.extract.run(self.module_summary_nodes(file_nodes, repo, namespace, branch, kind, depth, max_files))
+
+    def repo_nodes(self, docs: list[Document], module_nodes: list[Node], repo: str, namespace: str, branch: str,
+                   kind: str, readme_limit: int = 3, module_limit: int = 10) -> list[Node]:
+        return self.extract.run(self.repo_summary_nodes(docs, module_nodes, repo, namespace, branch, kind,
+                                                        readme_limit, module_limit))
+
+    # The *_summary_nodes steps produce a level's split nodes WITHOUT the
+    # extractor passes: the next level reads only the summary text, so the
+    # controller runs a level's extractors concurrently with the next level.
+    def file_summary_nodes(self, code_nodes: list[Node], repo: str, namespace: str, branch: str,
+                           kind: str) -> list[Node]:
         files = [(fp, ns) for fp, ns in group_nodes_by_file(code_nodes).items() if fp]
         concat = ["\n\n".join(n.get_content() for n in ns)[:25000] for _, ns in files]
         texts = self.wave.map([prompts.file_summary(fp) + "\n\n" + c for (fp, _), c in zip(files, concat)],
@@ -44,10 +60,10 @@ class HierarchyBuilder:
             docs.append(Document(t, {"namespace": namespace, "repo": repo, "branch": branch, "file_path": fp,
                                      "module": top_directory(fp, 1), "component_kind": kind, "doc_type": "file",
                                      "rollup_of": [n.id for n in ns], "rollup_count": len(ns)}))
-        return self._catalog_pipeline(docs)
+        return self.splitter.get_nodes_from_documents(docs)
 
-    def module_nodes(self, file_nodes: list[Node], repo: str, namespace: str, branch: str, kind: str,
-                     depth: int = 1, max_files: int = 40) -> list[Node]:
+    def module_summary_nodes(self, file_nodes: list[Node], repo: str, namespace: str, branch: str, kind: str,
+                             depth: int = 1, max_files: int = 40) -> list[Node]:
         summaries, ids = {}, {}
         for n in file_nodes:
             fp = (n.metadata.get("file_path") or "").strip()
@@ -63,10 +79,10 @@ class HierarchyBuilder:
                           "doc_type": "module", "rollup_of": [ids[f] for f in fs[:max_files] if f in ids],
                           "constituent_files": fs[:max_files]})
                 for (m, fs), t in zip(mods, texts)]
-        return self._catalog_pipeline(docs)
+        return self.splitter.get_nodes_from_documents(docs)
 
-    def repo_nodes(self, docs: list[Document], module_nodes: list[Node], repo: str, namespace: str, branch: str,
-                   kind: str, readme_limit: int = 3, module_limit: int = 10) -> list[Node]:
+    def repo_summary_nodes(self, docs: list[Document], module_nodes: list[Node], repo: str, namespace: str,
+                           branch: str, kind: str, readme_limit: int = 3, module_limit: int = 10) -> list[Node]:
         readmes = [d.text for d in docs if d.metadata.get("file_path", "").lower().endswith("readme.md")][:readme_limit]
         mods = module_nodes[:module_limit]
         seeds = "\n\n".join(readmes + [m.get_content() for m in mods])[:25000]
@@ -75,7 +91,7 @@ class HierarchyBuilder:
                        {"namespace": namespace, "repo": repo, "branch": branch, "component_kind": kind,
                         "doc_type": "repo", "rollup_of": [m.id for m in mods],
                         "constituent_modules": [m.metadata.get("module", "") for m in mods if m.metadata.get("module")]})
-        return self._catalog_pipeline([doc])
+        return self.splitter.get_nodes_from_documents([doc])
 
     # ---- catalog (catalog_builder.make_catalog_document) ------------------
     def catalog_nodes(self, repo: str, docs: list[Document], code_nodes: list[Node], collection: str, kind: str,

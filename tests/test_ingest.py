@@ -158,8 +158,14 @@ def test_controller_end_to_end(tmp_path, embedder):
     assert res["documents"] > 0 and res["nodes_written"] > 0
     per = res["nodes_per_scope"]
     assert per["catalog"] >= 1 and per["repo"] >= 1 and per["module"] >= 1 and per["file"] >= 1
-    assert set(res["stage_seconds"]) == {"preprocess", "code_nodes", "catalog", "file_summaries",
-                                         "module_summaries", "repo_summaries", "vector_write", "audit_and_clean"}
+    # the reference's eight stages (+ split / extract_wait of the concurrent stage DAG)
+    assert set(res["stage_seconds"]) == {"preprocess", "split", "code_nodes", "catalog", "file_summaries",
+                                         "module_summaries", "repo_summaries", "extract_wait", "vector_write",
+                                         "audit_and_clean"}
+    # extractor passes of every level ran (file/module/repo/catalog nodes carry keywords too)
+    for scope in ("file", "module", "repo", "catalog"):
+        hs = store.table(scope).search(embedder.embed_queries(["widgets"]), 1, {"namespace": "ns"})[0]
+        assert hs and hs[0].metadata.get("repo") == "demo"
     c = store.counts()
     assert c["embeddings"] == per["chunk"] and c["embeddings_catalog"] == per["catalog"]
     # chunk metadata carries extractor outputs that survive the allow-list
