@@ -16,11 +16,60 @@ A/B in scripts/bench_gemm.py:
 """
 from __future__ import annotations
 
+import bisect
+import json
 import os
+from pathlib import Path
 
 import torch
 
 from ._lib import call, lib, ptr
+
+TUNING_DIR = Path(__file__).resolve().parents[1] / "tuning"
+_TUNED = {"done": False, "table": None}
+
+
+def enable_tuned_gemms() -> bool:
+    """Load the measured library-GEMM solutions (PyTorch TunableOp results,
+    A/B-filtered by scripts/ab_tuned_gemms.py: only solutions that beat
+    hipBLASLt's default heuristic by >= 3 % on cold weights) READ-ONLY —
+    tuning never runs inside a timed or graph-captured region — and the
+    measured decode dispatch table (scripts/gemm_dispatch_table.py).
+    GRAG_TUNED_GEMMS=0 disables both."""
+    if _TUNED["done"]:
+        return _TUNED["table"] is not None
+    _TUNED["done"] = True
+    if os.environ.get("GRAG_TUNED_GEMMS", "1") == "0" or not torch.cuda.is_available():
+        return False
+    csv = TUNING_DIR / "tunableop_gfx950.csv"
+    try:
+        if csv.exists():
+            torch.cuda.tunable.enable(True)
+            torch.cuda.tunable.tuning_enable(False)
+            torch.cuda.tunable.record_untuned_enable(False)
+            torch.cuda.tunable.read_file(str(csv))
+    except Exception:  # validator mismatch (other ROCm/hipBLASLt build): library defaults
+        torch.cuda.tunable.enable(False)
+    js = TUNING_DIR / "gemm_dispatch_gfx950.json"
+    if js.exists():
+        raw = json.loads(js.read_text())["table"]
+        _TUNED["table"] = {tuple(map(int, k.split(","))): ([m for m, _ in v], [b for _, b in v])
+                           for k, v in raw.items()}
+    return _TUNED["table"] is not None
+
+
+def measured_choice(M: int, N: int, K: int) -> str | None:
+    """Fastest measured kernel for this decode shape ('library', 'skinny',
+    'stream'), looked up at the smallest measured bucket >= M."""
+    t = _TUNED["table"]
+    if not t:
+        return None
+    row = t.get((N, K))
+    if row is None:
+        return None
+    ms, best = row
+    i = bisect.bisect_left(ms, M)
+    return best[i] if i < len(ms) else None
 
 SKINNY_MAX_M = int(os.environ.get("GRAG_SKINNY_MAX_M", "64"))
 _SKINNY_ON = os.environ.get("GRAG_SKINNY", "1") != "0"
@@ -152,10 +201,20 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> t
             y = torch.nn.functional.linear(x.float(), w.float(), None if b is None else b.float())
             return y.to(x.dtype)
         return torch.nn.functional.linear(x, w, b)
+    if not _TUNED["done"]:
+        enable_tuned_gemms()
     if (_SKINNY_ON and x.dim() == 2 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and x.stride(1) == 1 and w.stride(1) == 1):
         M, K = x.shape
         N = w.shape[0]
+        choice = measured_choice(M, N, K)
+        if choice == "library":
+            return torch.nn.functional.linear(x, w, b)
+        if choice == "skinny" and K % 64 == 0:
+            return gemm_skinny(x, w, b)
+        if (choice == "stream" and K % 16 == 0 and N % 4 == 0
+                and (not torch.cuda.is_current_stream_capturing() or _WS.ready(x.device, M, N, K))):
+            return gemm_stream(x, w, b)
         if K % 64 == 0 and use_skinny(M, N, K):
             return gemm_skinny(x, w, b)
         if (K % 16 == 0 and N % 4 == 0 and use_stream(M, N, K)
