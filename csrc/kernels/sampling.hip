@@ -1,33 +1,42 @@
-// Fused token sampler: one 1024-thread workgroup per row.
+// Fused token sampler, multi-workgroup form.
 //
 //   x_i = logit_i, repetition penalty on tokens already seen (prompt + output,
 //         HF/vLLM rule: x>0 ? x/pen : x*pen), then x_i /= temperature
 //   greedy (temperature <= 0): argmax
-//   else: exact top-k and top-p (nucleus) thresholds by 4-round radix select
-//         over the order-preserving uint32 image of x (8 bits per round, LDS
-//         histograms of counts or of probability mass, bin search by one
-//         wave-level suffix scan), then Gumbel-max sampling over the kept
-//         tokens: argmax(x_i + G_i), G_i = -log(-log u_i) from a counter-based
-//         hash (seed, per-slot step counter, token).
-// Every pass is vectorised 8 tokens per lane (one 16-B bf16 load, one seen-
-// bitmap word per 8 tokens); the first pass computes max and the softmax
-// normaliser together (online rescaling), so a top-p draw is 6 streaming
-// passes over the row (L2/MALL-resident: 300 KB per row at V=152064).
-// The sampled token's bit is set in the slot's seen bitmap and the slot's RNG
-// counter advances on device, so the whole sampler is hipGraph-capturable.
+//   else: top-k (by count) then top-p (nucleus, by probability mass inside
+//         the top-k set) thresholds by radix select, then Gumbel-max sampling
+//         over the kept tokens: argmax(x_i + G_i), G_i = -log(-log u_i) from a
+//         counter-based hash (seed, per-slot step counter, slot, token).
+//
+// Every row is split into S segments and every pass runs on B x S
+// workgroups (~8K tokens each), so the whole chip works on the batch; the
+// previous one-workgroup-per-row kernel kept only B CUs busy and took
+// ~300 us at B = 64 over Qwen's 152K vocabulary.  Fixed launch chain, so the
+// sampler is captured in the decode hipGraph:
+//   max     per-segment max / argmax of the adjusted logits
+//   round r (r = 0..7): every workgroup folds the S partial histograms of
+//           round r-1 into the row's radix state (all workgroups of a row
+//           compute the same thing; segment 0 publishes it for the next
+//           launch), then histograms its own segment for round r.  Rounds 0-3
+//           select the top-k threshold (counts), rounds 4-7 the top-p
+//           threshold (mass exp(x - M) restricted to the top-k set, whose total
+//           is the renormaliser).  Inactive rounds (top_k = 0, top_p = 1) only
+//           forward the state.
+//   gumbel  final threshold, per-segment Gumbel argmax over the kept tokens
+//   final   per-row combine, seen-bitmap update, RNG counter advance.
+// Radix keys are the fixed-point image of (M - x) (qkey): the first digit is
+// floor(8 (M - x)), so a row's relevant logits spread over many bins (the raw
+// float bits put a whole row into one bin of the first round, serialising the
+// LDS histogram atomics).
 #include "common.h"
 
 using namespace grag;
 
 namespace {
 
-constexpr int kThreads = 1024;
-constexpr int kWaves = kThreads / 64;
-
-__device__ __forceinline__ uint32_t fkey(float x) {
-  const uint32_t b = __float_as_uint(x);
-  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-}
+constexpr int kT = 256;   // threads per workgroup
+constexpr int kNB = 256;  // bins per radix round
+constexpr int kRounds = 8;
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -36,97 +45,139 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-struct Ctl {
-  float inv_temp, pen;
-  bool greedy;
-  const uint32_t* seen;
+// Complemented fixed point (27 fractional bits) of d = M - x clamped to
+// [0, 32]: larger key = more probable.  Resolution 2^-27 logit units is finer
+// than the fp32 ulp of the logits; tokens with d > 32 (p < 1e-13 of the top
+// token) share key 0.
+__device__ __forceinline__ uint32_t qkey(float x, float M) {
+  const float d = fminf(fmaxf(M - x, 0.f), 32.f) * 134217728.f;  // 2^27
+  return d >= 4294967295.f ? 0u : ~(uint32_t)d;
+}
+
+struct Params {
+  const void* logits;
+  int ld, B, V, S, seglen;
+  const float* temperature;
+  const float* top_p;
+  const int32_t* top_k;
+  const float* penalty;
+  uint32_t* seen;
+  int seen_words;
+  int64_t* rng_counter;
+  uint64_t seed;
+  const int32_t* slots;
+  int32_t* out_tok;
+  // workspace
+  float* seg_max;    // [B][S]
+  int32_t* seg_arg;  // [B][S]
+  float* gval;       // [B][S]
+  int32_t* gidx;     // [B][S]
+  float* hist;       // [2][B][S][kNB]
+  uint32_t* state;   // [2][B][4]: prefix, pmask, thr_k, need (float bits)
 };
 
-// Load 8 adjusted logits starting at i (i % 8 == 0, i + 8 <= V).
-template <typename T>
-__device__ __forceinline__ void load8(const T* row, int i, const Ctl& c, float* x) {
-  if constexpr (sizeof(T) == 4) {
-    const float4 a = *reinterpret_cast<const float4*>(row + i);
-    const float4 b = *reinterpret_cast<const float4*>(row + i + 4);
-    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-  } else {
-    unpack8(*reinterpret_cast<const bf16x8_t*>(row + i), x);
-  }
-  if (c.pen != 1.f && c.seen) {
-    const uint32_t w = c.seen[i >> 5] >> (i & 31);
-    if (w & 0xFFu) {
+struct Row {
+  int sl;
+  float inv_temp, pen, top_p;
+  int top_k;
+  bool greedy;
+  uint32_t* seen;
+};
+
+__device__ __forceinline__ Row row_params(const Params& p, int row) {
+  Row r;
+  r.sl = p.slots ? p.slots[row] : row;
+  const float temp = p.temperature ? p.temperature[r.sl] : 1.f;
+  r.greedy = !(temp > 0.f);
+  r.inv_temp = r.greedy ? 1.f : 1.f / temp;
+  r.pen = p.penalty ? p.penalty[r.sl] : 1.f;
+  r.top_p = p.top_p ? p.top_p[r.sl] : 1.f;
+  r.top_k = p.top_k ? p.top_k[r.sl] : 0;
+  r.seen = p.seen ? p.seen + (size_t)r.sl * p.seen_words : nullptr;
+  return r;
+}
+
+// Apply fn(index, adjusted value) to every logit of [lo, hi): 8 per lane per
+// step from one 16-B (bf16) or two 16-B (fp32) loads + one seen-bitmap word.
+template <typename T, typename F>
+__device__ __forceinline__ void for_seg(const T* row, int lo, int hi, const Row& c, F&& fn) {
+  const int hi8 = lo + ((hi - lo) & ~7);
+  const bool pen = c.pen != 1.f && c.seen;
+  for (int i = lo + threadIdx.x * 8; i < hi8; i += kT * 8) {
+    float x[8];
+    if constexpr (sizeof(T) == 4) {
+      const float4 a = *reinterpret_cast<const float4*>(row + i);
+      const float4 b = *reinterpret_cast<const float4*>(row + i + 4);
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    } else {
+      unpack8(*reinterpret_cast<const bf16x8_t*>(row + i), x);
+    }
+    const uint32_t w = pen ? (c.seen[i >> 5] >> (i & 31)) & 0xFFu : 0u;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if ((w >> j) & 1u) x[j] = x[j] > 0.f ? x[j] / c.pen : x[j] * c.pen;
+    for (int j = 0; j < 8; ++j) {
+      float v = x[j];
+      if ((w >> j) & 1u) v = v > 0.f ? v / c.pen : v * c.pen;
+      fn(i + j, c.greedy ? v : v * c.inv_temp);
     }
   }
-  if (!c.greedy) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] *= c.inv_temp;
+  for (int i = hi8 + threadIdx.x; i < hi; i += kT) {
+    float v = (float)row[i];
+    if (pen && ((c.seen[i >> 5] >> (i & 31)) & 1u)) v = v > 0.f ? v / c.pen : v * c.pen;
+    fn(i, c.greedy ? v : v * c.inv_temp);
   }
 }
 
-template <typename T>
-__device__ __forceinline__ float load1(const T* row, int i, const Ctl& c) {
-  float x = (float)row[i];
-  if (c.pen != 1.f && c.seen && ((c.seen[i >> 5] >> (i & 31)) & 1u)) x = x > 0.f ? x / c.pen : x * c.pen;
-  return c.greedy ? x : x * c.inv_temp;
-}
-
-// Apply fn(index, value) to every adjusted logit of the row.
-template <typename T, typename F>
-__device__ __forceinline__ void for_each(const T* row, int V, const Ctl& c, F&& fn) {
-  const int V8 = V & ~7;
-  for (int i = threadIdx.x * 8; i < V8; i += kThreads * 8) {
-    float x[8];
-    load8(row, i, c, x);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fn(i + j, x[j]);
+// (value, index) max, ties to the lower index
+__device__ __forceinline__ void better(float& v, int& i, float ov, int oi) {
+  if (ov > v || (ov == v && oi < i)) {
+    v = ov;
+    i = oi;
   }
-  for (int i = V8 + threadIdx.x; i < V; i += kThreads) fn(i, load1(row, i, c));
 }
 
-// block argmax of (value, index) — ties break to the lower index
-__device__ __forceinline__ void block_argmax(float& v, int& idx, float* rv, int* ri) {
+__device__ __forceinline__ void block_argmax(float& v, int& idx, float* sv, int* si) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(v, o, 64);
-    const int oi = __shfl_xor(idx, o, 64);
-    if (ov > v || (ov == v && oi < idx)) {
-      v = ov;
-      idx = oi;
-    }
-  }
+  for (int o = 32; o > 0; o >>= 1) better(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
   __syncthreads();
   if (lane == 0) {
-    rv[wid] = v;
-    ri[wid] = idx;
+    sv[wid] = v;
+    si[wid] = idx;
   }
   __syncthreads();
-  v = rv[0];
-  idx = ri[0];
+  v = sv[0];
+  idx = si[0];
 #pragma unroll
-  for (int w = 1; w < kWaves; ++w)
-    if (rv[w] > v || (rv[w] == v && ri[w] < idx)) {
-      v = rv[w];
-      idx = ri[w];
-    }
+  for (int w = 1; w < kT / 64; ++w) better(v, idx, sv[w], si[w]);
 }
 
-// Wave 0 finds the highest bin b whose inclusive suffix sum (bins b..255)
-// reaches `need`; writes b and the sum of bins strictly above b.
+// row max from the S partial maxima (every thread gets it)
+__device__ __forceinline__ float row_max(const Params& p, int row, float* sv) {
+  float m = -INFINITY;
+  for (int s = threadIdx.x; s < p.S; s += kT) m = fmaxf(m, p.seg_max[row * p.S + s]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sv[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = sv[0];
+#pragma unroll
+  for (int w = 1; w < kT / 64; ++w) m = fmaxf(m, sv[w]);
+  return m;
+}
+
+// Wave 0: highest bin b whose inclusive suffix sum (bins b..255) reaches
+// `need`; writes b and the sum strictly above b.
 __device__ __forceinline__ void find_bin(const float* hist, float need, uint32_t* out_b, float* out_above) {
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
-  // lane owns bins 255-4*lane .. 252-4*lane (descending)
   float h[4], own = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     h[j] = hist[255 - 4 * lane - j];
     own += h[j];
   }
-  float incl = own;  // inclusive prefix over lanes (descending bin order)
+  float incl = own;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const float t = __shfl_up(incl, o, 64);
@@ -135,7 +186,7 @@ __device__ __forceinline__ void find_bin(const float* hist, float need, uint32_t
   const float excl = incl - own;
   const bool mine = excl < need && incl >= need;
   const unsigned long long ball = __ballot(mine);
-  int owner = ball ? __ffsll((long long)ball) - 1 : 63;
+  const int owner = ball ? __ffsll((long long)ball) - 1 : 63;
   if (lane == owner) {
     float acc = excl;
     int b = 255 - 4 * lane;
@@ -154,122 +205,180 @@ __device__ __forceinline__ void find_bin(const float* hist, float need, uint32_t
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(kThreads) void sample_kernel(
-    const T* __restrict__ logits, int ld, int V, const float* __restrict__ temperature,
-    const float* __restrict__ top_p, const int32_t* __restrict__ top_k,
-    const float* __restrict__ penalty, uint32_t* __restrict__ seen, int seen_words,
-    int64_t* __restrict__ rng_counter, uint64_t seed, const int32_t* __restrict__ slots,
-    int32_t* __restrict__ out_tok) {
-  __shared__ float red[kWaves];
-  __shared__ int redi[kWaves];
-  __shared__ float hist[256];
-  __shared__ uint32_t sh_b;
-  __shared__ float sh_above;
-  const int row = blockIdx.x;
-  // per-sequence state lives in persistent slots; `slots` maps batch row -> slot
-  const int sl = slots ? slots[row] : row;
-  const T* lr = logits + (size_t)row * ld;
-  const float temp = temperature ? temperature[sl] : 1.f;
-  const float tp = top_p ? top_p[sl] : 1.f;
-  const int tk = top_k ? top_k[sl] : 0;
-  Ctl c;
-  c.greedy = !(temp > 0.f);
-  c.inv_temp = c.greedy ? 1.f : 1.f / temp;
-  c.pen = penalty ? penalty[sl] : 1.f;
-  c.seen = seen ? seen + (size_t)sl * seen_words : nullptr;
+struct RState {
+  uint32_t prefix, pmask, thr_k;
+  float need;
+};
 
-  // pass 1: argmax + online softmax normaliser
-  float mx = -INFINITY, z = 0.f;
+__device__ __forceinline__ bool round_active(int r, const Row& c, int V) {
+  return r < 4 ? (c.top_k > 0 && c.top_k < V) : (c.top_p < 1.f);
+}
+__device__ __forceinline__ int round_shift(int r) { return 24 - 8 * (r & 3); }
+
+// State after round r_prev (r_prev = -1: initial state).
+__device__ __forceinline__ RState load_state(const Params& p, int row, int r_prev, const Row& c) {
+  RState st;
+  if (r_prev < 0) {
+    st.prefix = 0u;
+    st.pmask = 0u;
+    st.thr_k = 0u;
+    st.need = (float)c.top_k;
+    return st;
+  }
+  const uint32_t* s = p.state + ((size_t)(r_prev & 1) * p.B + row) * 4;
+  st.prefix = s[0];
+  st.pmask = s[1];
+  st.thr_k = s[2];
+  st.need = __uint_as_float(s[3]);
+  return st;
+}
+
+// Fold round r's S partial histograms into the row state (-> state after
+// round r).  Every workgroup of the row does this identically.
+__device__ void fold_round(const Params& p, int row, int r, const Row& c, RState& st, float* lds_hist,
+                           uint32_t* sh_b, float* sh_f) {
+  if (round_active(r, c, p.V)) {
+    const float* src = p.hist + ((size_t)(r & 1) * p.B + row) * p.S * kNB;
+    for (int b = threadIdx.x; b < kNB; b += kT) {
+      float s = 0.f;
+      for (int g = 0; g < p.S; ++g) s += src[g * kNB + b];
+      lds_hist[b] = s;
+    }
+    __syncthreads();
+    if (r == 4) {  // first top-p round: its histogram holds the whole kept mass
+      float tot = 0.f;
+      for (int b = threadIdx.x; b < kNB; b += kT) tot += lds_hist[b];
+      tot = wave_sum(tot);
+      if ((threadIdx.x & 63) == 0) sh_f[1 + (threadIdx.x >> 6)] = tot;
+      __syncthreads();
+      tot = 0.f;
+#pragma unroll
+      for (int w = 0; w < kT / 64; ++w) tot += sh_f[1 + w];
+      st.need = c.top_p * tot;
+    }
+    find_bin(lds_hist, st.need, sh_b, sh_f);
+    __syncthreads();
+    st.need -= sh_f[0];
+    st.prefix |= sh_b[0] << round_shift(r);
+    st.pmask |= 255u << round_shift(r);
+    __syncthreads();
+  }
+  if (r == 3) {  // top-k threshold complete (0 = keep all); top-p starts fresh inside it
+    st.thr_k = round_active(3, c, p.V) ? st.prefix : 0u;
+    st.prefix = 0u;
+    st.pmask = 0u;
+  }
+}
+
+// ---------------------------------------------------------------- kernels
+template <typename T>
+__global__ __launch_bounds__(kT) void samp_max_kernel(Params p) {
+  __shared__ float sv[kT / 64];
+  __shared__ int si[kT / 64];
+  const int row = blockIdx.x, seg = blockIdx.y;
+  const Row c = row_params(p, row);
+  const T* lr = (const T*)p.logits + (size_t)row * p.ld;
+  const int lo = seg * p.seglen, hi = min(p.V, lo + p.seglen);
+  float m = -INFINITY;
   int mi = 0x7fffffff;
-  for_each(lr, V, c, [&](int i, float x) {
-    if (x > mx) {
-      z = z * __expf(mx - x) + 1.f;
-      mx = x;
-      mi = i;
-    } else if (x > -INFINITY) {
-      z += __expf(x - mx);
+  for_seg(lr, lo, hi, c, [&](int i, float x) { better(m, mi, x, i); });
+  block_argmax(m, mi, sv, si);
+  if (threadIdx.x == 0) {
+    p.seg_max[row * p.S + seg] = m;
+    p.seg_arg[row * p.S + seg] = mi;
+  }
+}
+
+// Round r: fold round r-1 (segment 0 publishes the state), histogram round r.
+template <typename T>
+__global__ __launch_bounds__(kT) void samp_round_kernel(Params p, int r) {
+  __shared__ float hist[kNB];
+  __shared__ float sv[kT / 64];
+  __shared__ uint32_t sh_b[1];
+  __shared__ float sh_f[1 + kT / 64];
+  const int row = blockIdx.x, seg = blockIdx.y;
+  const Row c = row_params(p, row);
+  if (c.greedy) return;
+  const float M = row_max(p, row, sv);
+  RState st = load_state(p, row, r - 2, c);
+  if (r >= 1) {
+    fold_round(p, row, r - 1, c, st, hist, sh_b, sh_f);
+    if (seg == 0 && threadIdx.x == 0) {
+      uint32_t* s = p.state + ((size_t)((r - 1) & 1) * p.B + row) * 4;
+      s[0] = st.prefix;
+      s[1] = st.pmask;
+      s[2] = st.thr_k;
+      s[3] = __float_as_uint(st.need);
+    }
+  }
+  if (!round_active(r, c, p.V)) return;
+  __syncthreads();
+  for (int b = threadIdx.x; b < kNB; b += kT) hist[b] = 0.f;
+  __syncthreads();
+  const T* lr = (const T*)p.logits + (size_t)row * p.ld;
+  const int lo = seg * p.seglen, hi = min(p.V, lo + p.seglen);
+  const int shift = round_shift(r);
+  const bool mass = r >= 4;
+  const uint32_t prefix = st.prefix, pmask = st.pmask, thr_k = st.thr_k;
+  for_seg(lr, lo, hi, c, [&](int, float x) {
+    const uint32_t k = qkey(x, M);
+    if (k >= thr_k && (k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], mass ? __expf(x - M) : 1.f);
+  });
+  __syncthreads();
+  float* dst = p.hist + (((size_t)(r & 1) * p.B + row) * p.S + seg) * kNB;
+  for (int b = threadIdx.x; b < kNB; b += kT) dst[b] = hist[b];
+}
+
+template <typename T>
+__global__ __launch_bounds__(kT) void samp_gumbel_kernel(Params p) {
+  __shared__ float hist[kNB];
+  __shared__ float sv[kT / 64];
+  __shared__ int si[kT / 64];
+  __shared__ uint32_t sh_b[1];
+  __shared__ float sh_f[1 + kT / 64];
+  const int row = blockIdx.x, seg = blockIdx.y;
+  const Row c = row_params(p, row);
+  if (c.greedy) return;
+  const float M = row_max(p, row, sv);
+  RState st = load_state(p, row, kRounds - 2, c);
+  fold_round(p, row, kRounds - 1, c, st, hist, sh_b, sh_f);
+  const uint32_t thr = round_active(kRounds - 1, c, p.V) ? st.prefix : st.thr_k;
+  const uint64_t ctr = p.rng_counter ? (uint64_t)p.rng_counter[c.sl] : 0ull;
+  const uint64_t base = mix64(p.seed ^ mix64(ctr * 0x100000001B3ull + (uint64_t)c.sl));
+  const T* lr = (const T*)p.logits + (size_t)row * p.ld;
+  const int lo = seg * p.seglen, hi = min(p.V, lo + p.seglen);
+  float best = -INFINITY;
+  int bidx = 0x7fffffff;
+  for_seg(lr, lo, hi, c, [&](int i, float x) {
+    if (qkey(x, M) >= thr) {
+      const uint64_t h = mix64(base + (uint64_t)i);
+      const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+      better(best, bidx, x - __logf(-__logf(u)), i);
     }
   });
-  // combine (max, z) across the block
-  float bm = mx;
-  int bi = mi;
-  block_argmax(bm, bi, red, redi);
-  z = mx == -INFINITY ? 0.f : z * __expf(mx - bm);
-  z = block_sum(z, red);
-  mx = bm;
-  int token = bi;
-
-  if (!c.greedy && mx != -INFINITY) {
-    uint32_t thr = 0u;  // keep keys >= thr
-    if (tk > 0 && tk < V) {  // top-k by count
-      uint32_t prefix = 0u, pmask = 0u;
-      float need = (float)tk;
-      for (int shift = 24; shift >= 0; shift -= 8) {
-        for (int b = threadIdx.x; b < 256; b += kThreads) hist[b] = 0.f;
-        __syncthreads();
-        for_each(lr, V, c, [&](int, float x) {
-          const uint32_t kk = fkey(x);
-          if ((kk & pmask) == prefix) atomicAdd(&hist[(kk >> shift) & 255u], 1.f);
-        });
-        __syncthreads();
-        find_bin(hist, need, &sh_b, &sh_above);
-        __syncthreads();
-        need -= sh_above;
-        prefix |= sh_b << shift;
-        pmask |= 255u << shift;
-      }
-      thr = prefix;
-      // normaliser restricted to the top-k set
-      float zk = 0.f;
-      for_each(lr, V, c, [&](int, float x) {
-        if (fkey(x) >= thr) zk += __expf(x - mx);
-      });
-      z = block_sum(zk, red);
-    }
-    if (tp < 1.f) {  // top-p by probability mass within the kept set
-      uint32_t prefix = 0u, pmask = 0u;
-      float need = tp * z;
-      for (int shift = 24; shift >= 0; shift -= 8) {
-        for (int b = threadIdx.x; b < 256; b += kThreads) hist[b] = 0.f;
-        __syncthreads();
-        for_each(lr, V, c, [&](int, float x) {
-          const uint32_t kk = fkey(x);
-          if (kk >= thr && (kk & pmask) == prefix) atomicAdd(&hist[(kk >> shift) & 255u], __expf(x - mx));
-        });
-        __syncthreads();
-        find_bin(hist, need, &sh_b, &sh_above);
-        __syncthreads();
-        need -= sh_above;
-        prefix |= sh_b << shift;
-        pmask |= 255u << shift;
-      }
-      thr = prefix > thr ? prefix : thr;
-    }
-    // Gumbel-max over kept tokens
-    const uint64_t ctr = rng_counter ? (uint64_t)rng_counter[sl] : 0ull;
-    const uint64_t base = mix64(seed ^ mix64(ctr * 0x100000001B3ull + (uint64_t)sl));
-    float best = -INFINITY;
-    int bidx = 0x7fffffff;
-    for_each(lr, V, c, [&](int i, float x) {
-      if (fkey(x) >= thr) {
-        const uint64_t h = mix64(base + (uint64_t)i);
-        const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
-        const float y = x - __logf(-__logf(u));
-        if (y > best) {
-          best = y;
-          bidx = i;
-        }
-      }
-    });
-    block_argmax(best, bidx, red, redi);
-    if (bidx != 0x7fffffff) token = bidx;
-  }
+  block_argmax(best, bidx, sv, si);
   if (threadIdx.x == 0) {
-    if (token < 0 || token >= V) token = 0;
-    out_tok[row] = token;
-    if (c.seen) atomicOr(seen + (size_t)sl * seen_words + (token >> 5), 1u << (token & 31));
-    if (rng_counter) rng_counter[sl] += 1;
+    p.gval[row * p.S + seg] = best;
+    p.gidx[row * p.S + seg] = bidx;
+  }
+}
+
+__global__ __launch_bounds__(64) void samp_final_kernel(Params p) {
+  const int row = blockIdx.x;
+  const Row c = row_params(p, row);
+  float v = -INFINITY;
+  int idx = 0x7fffffff;
+  const float* vals = c.greedy ? p.seg_max : p.gval;
+  const int32_t* ids = c.greedy ? p.seg_arg : p.gidx;
+  for (int s = threadIdx.x; s < p.S; s += 64) better(v, idx, vals[row * p.S + s], ids[row * p.S + s]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) better(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
+  if (threadIdx.x == 0) {
+    int token = idx;
+    if (token < 0 || token >= p.V) token = 0;
+    p.out_tok[row] = token;
+    if (c.seen) atomicOr(c.seen + (token >> 5), 1u << (token & 31));
+    if (p.rng_counter) p.rng_counter[c.sl] += 1;
   }
 }
 
@@ -283,23 +392,62 @@ __global__ void mark_seen_kernel(const int32_t* __restrict__ tokens, const int32
   atomicOr(seen + (size_t)rows[i] * seen_words + (t >> 5), 1u << (t & 31));
 }
 
+template <typename T>
+int launch_all(const Params& p, hipStream_t stream) {
+  const dim3 grid(p.B, p.S);
+  samp_max_kernel<T><<<grid, kT, 0, stream>>>(p);
+  for (int r = 0; r < kRounds; ++r) samp_round_kernel<T><<<grid, kT, 0, stream>>>(p, r);
+  samp_gumbel_kernel<T><<<grid, kT, 0, stream>>>(p);
+  samp_final_kernel<<<p.B, 64, 0, stream>>>(p);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
+// Segments per row (~8K tokens per workgroup) and the workspace (floats) a
+// B-row call needs.
+GRAG_API int grag_sample_segments(int V) {
+  const int S = (V + 8191) / 8192;
+  return S < 1 ? 1 : (S > 64 ? 64 : S);
+}
+GRAG_API long grag_sample_ws_floats(int B, int V) {
+  const long S = grag_sample_segments(V);
+  return (long)B * S * (4 + 2 * kNB) + 2L * B * 4 + 64;
+}
+
 // dtype: 0 = fp32 logits, 1 = bf16 logits.  ld must be a multiple of 8.
-GRAG_API int grag_sample(const void* logits, int dtype, int ld, int B, int V,
-                         const float* temperature, const float* top_p, const int32_t* top_k,
-                         const float* penalty, uint32_t* seen, int seen_words,
-                         int64_t* rng_counter, uint64_t seed, const int32_t* slots,
-                         int32_t* out_tok, hipStream_t stream) {
+// ws: >= grag_sample_ws_floats(B, V) floats of device scratch.
+GRAG_API int grag_sample(const void* logits, int dtype, int ld, int B, int V, const float* temperature,
+                         const float* top_p, const int32_t* top_k, const float* penalty, uint32_t* seen,
+                         int seen_words, int64_t* rng_counter, uint64_t seed, const int32_t* slots, int32_t* out_tok,
+                         float* ws, hipStream_t stream) {
   if (B <= 0) return 0;
-  if (ld % 8 != 0) return (int)hipErrorInvalidValue;
-  if (dtype == 0)
-    sample_kernel<float><<<B, kThreads, 0, stream>>>((const float*)logits, ld, V, temperature, top_p, top_k,
-                                                     penalty, seen, seen_words, rng_counter, seed, slots, out_tok);
-  else
-    sample_kernel<bf16><<<B, kThreads, 0, stream>>>((const bf16*)logits, ld, V, temperature, top_p, top_k,
-                                                    penalty, seen, seen_words, rng_counter, seed, slots, out_tok);
-  return (int)hipGetLastError();
+  if (ld % 8 != 0 || ws == nullptr) return (int)hipErrorInvalidValue;
+  Params p{};
+  p.logits = logits;
+  p.ld = ld;
+  p.B = B;
+  p.V = V;
+  p.S = grag_sample_segments(V);
+  p.seglen = ((V + p.S - 1) / p.S + 7) & ~7;
+  p.temperature = temperature;
+  p.top_p = top_p;
+  p.top_k = top_k;
+  p.penalty = penalty;
+  p.seen = seen;
+  p.seen_words = seen_words;
+  p.rng_counter = rng_counter;
+  p.seed = seed;
+  p.slots = slots;
+  p.out_tok = out_tok;
+  const size_t BS = (size_t)B * p.S;
+  p.seg_max = ws;
+  p.seg_arg = reinterpret_cast<int32_t*>(ws + BS);
+  p.gval = ws + 2 * BS;
+  p.gidx = reinterpret_cast<int32_t*>(ws + 3 * BS);
+  p.hist = ws + 4 * BS;
+  p.state = reinterpret_cast<uint32_t*>(ws + 4 * BS + 2 * BS * kNB);
+  return dtype == 0 ? launch_all<float>(p, stream) : launch_all<bf16>(p, stream);
 }
 
 GRAG_API int grag_mark_seen(const int32_t* tokens, const int32_t* rows, int n, uint32_t* seen,

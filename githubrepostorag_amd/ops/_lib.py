@@ -40,7 +40,9 @@ _SIGS = {
     "grag_score_topk_flat": [P, I64, I64, I64, I, P, I, I, I, I, P, P, P, I, P, P, P, I, P, P, P, P, P],
     "grag_score_topk_work": [P, I, P, I, I, I, I, P, P, I, P, P, P, I, P, P, P, I, P, P, P, P, P],
     "grag_topk_num_waves": [],
-    "grag_sample": [P, I, I, I, I, P, P, P, P, P, I, P, U64, P, P, P],
+    "grag_sample": [P, I, I, I, I, P, P, P, P, P, I, P, U64, P, P, P, P],
+    "grag_sample_segments": [I],
+    "grag_sample_ws_floats": [I, I],
     "grag_mark_seen": [P, P, I, P, I, I, P],
     "grag_gemm_skinny": [P, P, P, P, I, I, I, I, I, I, I, P],
     "grag_gemm_stream": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
@@ -74,7 +76,7 @@ def lib():
             if fn is None:
                 continue
             fn.argtypes = args
-            fn.restype = ctypes.c_int
+            fn.restype = ctypes.c_long if name.endswith("_ws_floats") else ctypes.c_int
         _lib = handle
         return _lib
 

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import torch
 
-from ._lib import call, ptr
+from ._lib import call, lib, ptr
 
 
 class SamplerState:
@@ -23,6 +23,18 @@ class SamplerState:
         self.penalty = torch.ones(max_slots, dtype=torch.float32, device=device)
         self.seen = torch.zeros(max_slots, self.words, dtype=torch.int32, device=device)
         self.rng = torch.zeros(max_slots, dtype=torch.int64, device=device)
+        self._ws = None  # device scratch of the multi-workgroup sampler (sized on first use)
+
+    def workspace(self, rows: int) -> torch.Tensor:
+        """Scratch for a ``rows``-row call of grag_sample; sized for the
+        largest batch seen so far (>= 256 rows: every decode graph bucket) and
+        only grown outside hipGraph capture."""
+        need = int(lib().grag_sample_ws_floats(max(rows, 256), self.vocab))
+        if self._ws is None or self._ws.numel() < need:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("sampler workspace must be sized before hipGraph capture")
+            self._ws = torch.empty(need, dtype=torch.float32, device=self.device)
+        return self._ws
 
     def reset_slot(self, slot: int, temperature: float, top_p: float, top_k: int, penalty: float,
                    prompt_ids, seed: int | None = None) -> None:
@@ -146,5 +158,5 @@ def sample(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, out: 
     dtype = 0 if logits.dtype == torch.float32 else 1
     call("grag_sample", ptr(logits), dtype, logits.stride(0), B, state.vocab, ptr(state.temperature),
          ptr(state.top_p), ptr(state.top_k), ptr(state.penalty), ptr(state.seen), state.words, ptr(state.rng),
-         state.seed, ptr(slots), ptr(out))
+         state.seed, ptr(slots), ptr(out), ptr(state.workspace(B)))
     return out

@@ -113,7 +113,12 @@ def sampler_bench(B):
         st.reset_slot(i, 0.4, 0.8, 0, 1.2, list(range(0, 2000, 7)))
     logits = torch.randn(B, V, device=dev, dtype=torch.bfloat16) * 3
     slots = torch.arange(B, device=dev, dtype=torch.int32)
-    return rounds({"sampler_top_p": lambda: S.sample(logits, st, slots)})
+    out = torch.empty(B, dtype=torch.int32, device=dev)
+    S.sample(logits, st, slots, out=out)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        S.sample(logits, st, slots, out=out)
+    return rounds({"sampler_top_p": lambda: S.sample(logits, st, slots), "sampler_top_p_graph": g.replay})
 
 
 if __name__ == "__main__":
