@@ -24,10 +24,13 @@
 //           forward the state.
 //   gumbel  final threshold, per-segment Gumbel argmax over the kept tokens
 //   final   per-row combine, seen-bitmap update, RNG counter advance.
-// Radix keys are the fixed-point image of (M - x) (qkey): the first digit is
-// floor(8 (M - x)), so a row's relevant logits spread over many bins (the raw
-// float bits put a whole row into one bin of the first round, serialising the
-// LDS histogram atomics).
+// Radix keys are the fixed-point image of (M - x) (qkey), so a row's relevant
+// logits spread over the bins (the raw float bits put a whole row into one bin
+// of the first round).  The first digit (4 bits, every token of the row takes
+// part) is histogrammed in registers + a wave butterfly; the three 8-bit
+// digits after it see only the tokens of the selected bin (LDS atomics).
+// Measured (scripts/microbench.py, B=64, V=152064, top-p, in a hipGraph):
+// one-workgroup-per-row kernel 298 us -> this chain ~60-110 us.
 #include "common.h"
 
 using namespace grag;
@@ -37,6 +40,7 @@ namespace {
 constexpr int kT = 256;   // threads per workgroup
 constexpr int kNB = 256;  // bins per radix round
 constexpr int kRounds = 8;
+constexpr int kMaxS = 32;  // max segments per row
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -213,19 +217,25 @@ struct RState {
 __device__ __forceinline__ bool round_active(int r, const Row& c, int V) {
   return r < 4 ? (c.top_k > 0 && c.top_k < V) : (c.top_p < 1.f);
 }
-__device__ __forceinline__ int round_shift(int r) { return 24 - 8 * (r & 3); }
+// Digit plan of a 4-round radix select: a 4-bit first digit (16 bins: every
+// token of the row takes part, so it is histogrammed in registers, not with
+// LDS atomics), then three 8-bit digits (only tokens inside the selected bin
+// take part) -> 28 key bits (2^-23 logit units).
+__device__ __forceinline__ int round_shift(int r) { return (r & 3) == 0 ? 28 : 28 - 8 * (r & 3); }
+__device__ __forceinline__ uint32_t round_mask(int r) { return (r & 3) == 0 ? 15u : 255u; }
 
-// State after round r_prev (r_prev = -1: initial state).
-__device__ __forceinline__ RState load_state(const Params& p, int row, int r_prev, const Row& c) {
+// Row state published by launch j (state after the round launch j-1 ran);
+// j < 0: the initial state.
+__device__ __forceinline__ RState load_state(const Params& p, int row, int j, const Row& c) {
   RState st;
-  if (r_prev < 0) {
+  if (j < 0) {
     st.prefix = 0u;
     st.pmask = 0u;
     st.thr_k = 0u;
     st.need = (float)c.top_k;
     return st;
   }
-  const uint32_t* s = p.state + ((size_t)(r_prev & 1) * p.B + row) * 4;
+  const uint32_t* s = p.state + ((size_t)(j & 1) * p.B + row) * 4;
   st.prefix = s[0];
   st.pmask = s[1];
   st.thr_k = s[2];
@@ -233,15 +243,22 @@ __device__ __forceinline__ RState load_state(const Params& p, int row, int r_pre
   return st;
 }
 
-// Fold round r's S partial histograms into the row state (-> state after
+// Fold round r (histogrammed by launch j) into the row state (-> state after
 // round r).  Every workgroup of the row does this identically.
-__device__ void fold_round(const Params& p, int row, int r, const Row& c, RState& st, float* lds_hist,
+__device__ void fold_round(const Params& p, int row, int r, int j, const Row& c, RState& st, float* lds_hist,
                            uint32_t* sh_b, float* sh_f) {
+  if (r < 0) return;
   if (round_active(r, c, p.V)) {
-    const float* src = p.hist + ((size_t)(r & 1) * p.B + row) * p.S * kNB;
+    const float* src = p.hist + ((size_t)(j & 1) * p.B + row) * p.S * kNB;
     for (int b = threadIdx.x; b < kNB; b += kT) {
+      // all kMaxS partial loads issued back to back (clamped index, masked
+      // add: no per-load branch), summed in a fixed order -> deterministic
+      float v[kMaxS];
+#pragma unroll
+      for (int g = 0; g < kMaxS; ++g) v[g] = src[min(g, p.S - 1) * kNB + b];
       float s = 0.f;
-      for (int g = 0; g < p.S; ++g) s += src[g * kNB + b];
+#pragma unroll
+      for (int g = 0; g < kMaxS; ++g) s += g < p.S ? v[g] : 0.f;
       lds_hist[b] = s;
     }
     __syncthreads();
@@ -260,7 +277,7 @@ __device__ void fold_round(const Params& p, int row, int r, const Row& c, RState
     __syncthreads();
     st.need -= sh_f[0];
     st.prefix |= sh_b[0] << round_shift(r);
-    st.pmask |= 255u << round_shift(r);
+    st.pmask |= round_mask(r) << round_shift(r);
     __syncthreads();
   }
   if (r == 3) {  // top-k threshold complete (0 = keep all); top-p starts fresh inside it
@@ -289,9 +306,10 @@ __global__ __launch_bounds__(kT) void samp_max_kernel(Params p) {
   }
 }
 
-// Round r: fold round r-1 (segment 0 publishes the state), histogram round r.
+// Launch j runs round r: fold the previous launch's round r_prev (segment 0
+// publishes the resulting state), then histogram round r over its segment.
 template <typename T>
-__global__ __launch_bounds__(kT) void samp_round_kernel(Params p, int r) {
+__global__ __launch_bounds__(kT) void samp_round_kernel(Params p, int r, int r_prev, int j) {
   __shared__ float hist[kNB];
   __shared__ float sv[kT / 64];
   __shared__ uint32_t sh_b[1];
@@ -300,11 +318,11 @@ __global__ __launch_bounds__(kT) void samp_round_kernel(Params p, int r) {
   const Row c = row_params(p, row);
   if (c.greedy) return;
   const float M = row_max(p, row, sv);
-  RState st = load_state(p, row, r - 2, c);
-  if (r >= 1) {
-    fold_round(p, row, r - 1, c, st, hist, sh_b, sh_f);
+  RState st = load_state(p, row, j - 1 >= 1 ? j - 1 : -1, c);
+  if (r_prev >= 0) {
+    fold_round(p, row, r_prev, j - 1, c, st, hist, sh_b, sh_f);
     if (seg == 0 && threadIdx.x == 0) {
-      uint32_t* s = p.state + ((size_t)((r - 1) & 1) * p.B + row) * 4;
+      uint32_t* s = p.state + ((size_t)(j & 1) * p.B + row) * 4;
       s[0] = st.prefix;
       s[1] = st.pmask;
       s[2] = st.thr_k;
@@ -320,17 +338,54 @@ __global__ __launch_bounds__(kT) void samp_round_kernel(Params p, int r) {
   const int shift = round_shift(r);
   const bool mass = r >= 4;
   const uint32_t prefix = st.prefix, pmask = st.pmask, thr_k = st.thr_k;
-  for_seg(lr, lo, hi, c, [&](int, float x) {
-    const uint32_t k = qkey(x, M);
-    if (k >= thr_k && (k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], mass ? __expf(x - M) : 1.f);
-  });
+  if ((r & 3) == 0) {
+    // dense first digit: 16 register bins per lane (static indices, masked
+    // adds), a wave butterfly, then one LDS add per bin per wave
+    float acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    for_seg(lr, lo, hi, c, [&](int, float x) {
+      const uint32_t k = qkey(x, M);
+      const float w = k >= thr_k ? (mass ? __expf(x - M) : 1.f) : 0.f;
+      const uint32_t b = k >> 28;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] += b == (uint32_t)q ? w : 0.f;
+    });
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = wave_sum(acc[q]);
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) atomicAdd(&hist[q], acc[q]);
+    }
+  } else {
+    // sparse digits: only tokens inside the selected bin; run-length
+    // pre-aggregation of consecutive tokens falling into the same bin
+    uint32_t cb = 0xFFFFFFFFu;
+    float cv = 0.f;
+    for_seg(lr, lo, hi, c, [&](int, float x) {
+      const uint32_t k = qkey(x, M);
+      if (k >= thr_k && (k & pmask) == prefix) {
+        const uint32_t b = (k >> shift) & 255u;
+        const float w = mass ? __expf(x - M) : 1.f;
+        if (b == cb) {
+          cv += w;
+        } else {
+          if (cb != 0xFFFFFFFFu) atomicAdd(&hist[cb], cv);
+          cb = b;
+          cv = w;
+        }
+      }
+    });
+    if (cb != 0xFFFFFFFFu) atomicAdd(&hist[cb], cv);
+  }
   __syncthreads();
-  float* dst = p.hist + (((size_t)(r & 1) * p.B + row) * p.S + seg) * kNB;
+  float* dst = p.hist + (((size_t)(j & 1) * p.B + row) * p.S + seg) * kNB;
   for (int b = threadIdx.x; b < kNB; b += kT) dst[b] = hist[b];
 }
 
+// After J round launches (the last ran round r_last, -1 if none).
 template <typename T>
-__global__ __launch_bounds__(kT) void samp_gumbel_kernel(Params p) {
+__global__ __launch_bounds__(kT) void samp_gumbel_kernel(Params p, int r_last, int J) {
   __shared__ float hist[kNB];
   __shared__ float sv[kT / 64];
   __shared__ int si[kT / 64];
@@ -340,9 +395,9 @@ __global__ __launch_bounds__(kT) void samp_gumbel_kernel(Params p) {
   const Row c = row_params(p, row);
   if (c.greedy) return;
   const float M = row_max(p, row, sv);
-  RState st = load_state(p, row, kRounds - 2, c);
-  fold_round(p, row, kRounds - 1, c, st, hist, sh_b, sh_f);
-  const uint32_t thr = round_active(kRounds - 1, c, p.V) ? st.prefix : st.thr_k;
+  RState st = load_state(p, row, J - 1 >= 1 ? J - 1 : -1, c);
+  fold_round(p, row, r_last, J - 1, c, st, hist, sh_b, sh_f);
+  const uint32_t thr = (r_last >= 4 && round_active(r_last, c, p.V)) ? st.prefix : st.thr_k;
   const uint64_t ctr = p.rng_counter ? (uint64_t)p.rng_counter[c.sl] : 0ull;
   const uint64_t base = mix64(p.seed ^ mix64(ctr * 0x100000001B3ull + (uint64_t)c.sl));
   const T* lr = (const T*)p.logits + (size_t)row * p.ld;
@@ -392,12 +447,21 @@ __global__ void mark_seen_kernel(const int32_t* __restrict__ tokens, const int32
   atomicOr(seen + (size_t)rows[i] * seen_words + (t >> 5), 1u << (t & 31));
 }
 
+// rounds: bit 0 = top-k rounds (0-3) needed by some row, bit 1 = top-p rounds
+// (4-7); the caller knows which sampling features the batch uses, so unused
+// rounds are not launched at all.
 template <typename T>
-int launch_all(const Params& p, hipStream_t stream) {
+int launch_all(const Params& p, int rounds, hipStream_t stream) {
   const dim3 grid(p.B, p.S);
   samp_max_kernel<T><<<grid, kT, 0, stream>>>(p);
-  for (int r = 0; r < kRounds; ++r) samp_round_kernel<T><<<grid, kT, 0, stream>>>(p, r);
-  samp_gumbel_kernel<T><<<grid, kT, 0, stream>>>(p);
+  int r_prev = -1, j = 0;
+  for (int r = 0; r < kRounds; ++r) {
+    if (!((rounds >> (r / 4)) & 1)) continue;
+    samp_round_kernel<T><<<grid, kT, 0, stream>>>(p, r, r_prev, j);
+    r_prev = r;
+    ++j;
+  }
+  samp_gumbel_kernel<T><<<grid, kT, 0, stream>>>(p, r_prev, j);
   samp_final_kernel<<<p.B, 64, 0, stream>>>(p);
   return (int)hipGetLastError();
 }
@@ -408,7 +472,7 @@ int launch_all(const Params& p, hipStream_t stream) {
 // B-row call needs.
 GRAG_API int grag_sample_segments(int V) {
   const int S = (V + 8191) / 8192;
-  return S < 1 ? 1 : (S > 64 ? 64 : S);
+  return S < 1 ? 1 : (S > kMaxS ? kMaxS : S);
 }
 GRAG_API long grag_sample_ws_floats(int B, int V) {
   const long S = grag_sample_segments(V);
@@ -416,11 +480,12 @@ GRAG_API long grag_sample_ws_floats(int B, int V) {
 }
 
 // dtype: 0 = fp32 logits, 1 = bf16 logits.  ld must be a multiple of 8.
-// ws: >= grag_sample_ws_floats(B, V) floats of device scratch.
+// ws: >= grag_sample_ws_floats(B, V) floats of device scratch.  rounds: bit 0
+// if any row may use top-k, bit 1 if any row may use top-p < 1.
 GRAG_API int grag_sample(const void* logits, int dtype, int ld, int B, int V, const float* temperature,
                          const float* top_p, const int32_t* top_k, const float* penalty, uint32_t* seen,
                          int seen_words, int64_t* rng_counter, uint64_t seed, const int32_t* slots, int32_t* out_tok,
-                         float* ws, hipStream_t stream) {
+                         float* ws, int rounds, hipStream_t stream) {
   if (B <= 0) return 0;
   if (ld % 8 != 0 || ws == nullptr) return (int)hipErrorInvalidValue;
   Params p{};
@@ -447,7 +512,7 @@ GRAG_API int grag_sample(const void* logits, int dtype, int ld, int B, int V, co
   p.gidx = reinterpret_cast<int32_t*>(ws + 3 * BS);
   p.hist = ws + 4 * BS;
   p.state = reinterpret_cast<uint32_t*>(ws + 4 * BS + 2 * BS * kNB);
-  return dtype == 0 ? launch_all<float>(p, stream) : launch_all<bf16>(p, stream);
+  return dtype == 0 ? launch_all<float>(p, rounds, stream) : launch_all<bf16>(p, rounds, stream);
 }
 
 GRAG_API int grag_mark_seen(const int32_t* tokens, const int32_t* rows, int n, uint32_t* seen,

@@ -347,7 +347,7 @@ class LLMEngine:
             B = next(b for b in self.cfg.graph_batch_sizes if b >= n)
             split_len = _split_len_for(B)
             nsplit = min(_pow2_at_least(-(-max_ctx // split_len)), -(-self.cfg.max_model_len // split_len))
-            g = self._graphs.get((B, nsplit, split_len, K))
+            g = self._graphs.get((B, nsplit, split_len, K, self.sampler.rounds))
             if g is None:
                 g = self._capture(B, nsplit, split_len, K)
             packed = self._decode_inputs(seqs, B, width, K)
@@ -419,7 +419,8 @@ class LLMEngine:
         self.sampler.rng.copy_(rng_save)
         self.sampler.seen[self.scratch_slot].copy_(seen_save)
         g = _DecodeGraph(graph, out, B, nsplit, split_len, K)
-        self._graphs[(B, nsplit, split_len, K)] = g
+        # the sampler's launch chain depends on which sampling features live slots use
+        self._graphs[(B, nsplit, split_len, K, self.sampler.rounds)] = g
         self.stats["graph_captures"] += 1
         return g
 
@@ -429,7 +430,7 @@ class LLMEngine:
         for B in batch_sizes or self.cfg.graph_batch_sizes:
             split_len = _split_len_for(B)
             nsplit = _pow2_at_least(-(-max_ctx // split_len))
-            if (B, nsplit, split_len, 1) not in self._graphs:
+            if (B, nsplit, split_len, 1, self.sampler.rounds) not in self._graphs:
                 self._capture(B, nsplit, split_len, 1)
 
     # ------------------------------------------------------------------ outputs

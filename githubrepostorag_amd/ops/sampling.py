@@ -24,6 +24,14 @@ class SamplerState:
         self.seen = torch.zeros(max_slots, self.words, dtype=torch.int32, device=device)
         self.rng = torch.zeros(max_slots, dtype=torch.int64, device=device)
         self._ws = None  # device scratch of the multi-workgroup sampler (sized on first use)
+        # host mirror of which slots use top-k / top-p: the kernel chain only
+        # launches the radix rounds some slot needs (decode graphs are keyed on it)
+        self._uses_topk = [False] * max_slots
+        self._uses_topp = [False] * max_slots
+
+    @property
+    def rounds(self) -> int:
+        return (1 if any(self._uses_topk) else 0) | (2 if any(self._uses_topp) else 0)
 
     def workspace(self, rows: int) -> torch.Tensor:
         """Scratch for a ``rows``-row call of grag_sample; sized for the
@@ -43,6 +51,9 @@ class SamplerState:
         self.top_k[slot] = int(top_k)
         self.penalty[slot] = float(penalty)
         self.rng[slot] = int(seed) if seed is not None else 0
+        sampled = temperature > 0
+        self._uses_topk[slot] = sampled and 0 < int(top_k) < self.vocab
+        self._uses_topp[slot] = sampled and float(top_p) < 1.0
         self.seen[slot].zero_()
         if penalty != 1.0 and len(prompt_ids):
             toks = torch.as_tensor(list(prompt_ids), dtype=torch.int32, device=self.device)
@@ -158,5 +169,5 @@ def sample(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, out: 
     dtype = 0 if logits.dtype == torch.float32 else 1
     call("grag_sample", ptr(logits), dtype, logits.stride(0), B, state.vocab, ptr(state.temperature),
          ptr(state.top_p), ptr(state.top_k), ptr(state.penalty), ptr(state.seen), state.words, ptr(state.rng),
-         state.seed, ptr(slots), ptr(out), ptr(state.workspace(B)))
+         state.seed, ptr(slots), ptr(out), ptr(state.workspace(B)), state.rounds)
     return out

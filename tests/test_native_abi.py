@@ -1,5 +1,6 @@
 """The ctypes signatures must match the C ABI of the kernel library (parsed
 from the sources) — a mismatch would pass garbage pointers to a kernel."""
+import ctypes
 import re
 from pathlib import Path
 
@@ -14,17 +15,39 @@ def _c_decls(pattern_files, prefix):
     for f in pattern_files:
         src = f.read_text()
         for m in re.finditer(prefix + r"\s+\w+\s*\*?\s*(grag_\w+)\s*\(([^)]*)\)\s*\{", src):
-            params = [p for p in m.group(2).replace("\n", " ").split(",") if p.strip()]
-            decls[m.group(1)] = len(params)
+            params = [p.strip() for p in m.group(2).replace("\n", " ").split(",") if p.strip()]
+            decls[m.group(1)] = params
     return decls
 
 
-def test_kernel_abi_counts():
+def _ctype_of(param: str):
+    """ctypes type a C parameter declaration must be bound with."""
+    t = param.rsplit(" ", 1)[0] if " " in param else param
+    if "*" in param or "hipStream_t" in t:
+        return ctypes.c_void_p
+    if "uint64_t" in t:
+        return ctypes.c_uint64
+    if "int64_t" in t or re.search(r"\blong\b", t):
+        return ctypes.c_int64
+    if "float" in t:
+        return ctypes.c_float
+    return ctypes.c_int
+
+
+def test_kernel_abi_counts_and_types():
+    """Width/kind of every argument, not just the count: a 64-bit handle bound
+    as c_int is silently truncated (a hipStream_t that only breaks inside a
+    hipGraph capture, where the handle is a real pointer)."""
     decls = _c_decls(sorted((ROOT / "csrc" / "kernels").glob("*.hip")), r"GRAG_API")
     assert decls, "no exported kernels found"
-    for name, nargs in decls.items():
+    for name, params in decls.items():
         assert name in KSIGS, f"{name} missing from ops/_lib.py _SIGS"
-        assert len(KSIGS[name]) == nargs, f"{name}: ctypes {len(KSIGS[name])} vs C {nargs}"
+        assert len(KSIGS[name]) == len(params), f"{name}: ctypes {len(KSIGS[name])} vs C {len(params)}"
+        for i, (ct, cp) in enumerate(zip(KSIGS[name], params)):
+            want = _ctype_of(cp)
+            same = ct is want or (want is ctypes.c_int64 and ct is ctypes.c_long) or (
+                want is ctypes.c_uint64 and ct is ctypes.c_ulong)
+            assert same, f"{name} arg {i} ({cp!r}): ctypes {ct} vs C {want}"
 
 
 def test_runtime_abi_counts():
