@@ -15,15 +15,25 @@ One timed step = one batch of B RAG queries per GPU, end to end:
   blocks (reference synthesize(), agent_graph.py:448-476) -> Qwen2-7B
   prefill + decode of gen_len tokens with the reference worker's sampling
   (temperature 0.4, top_p 0.8, repetition_penalty 1.2; qwen_llm.py:107-113).
+The server runs at saturation: `--inflight` D batches are in flight at once,
+staggered by gen_len/D tokens (a fill phase before the warmup sets this up),
+so one step = submit a new batch of B queries, then run the engine until the
+OLDEST in-flight batch has completed all gen_len tokens; exactly B queries
+complete per step and every timed step does the same work (one batch's
+retrieval + prefill, gen_len/D decode tokens for each of the D batches).  The
+engine prefills new arrivals first, then decodes all D*B live sequences in one
+batch (decode is weight-bandwidth bound, so D*B rows cost little more than B).
+--inflight 1 is the closed-batch mode (submit B, finish B).
 Scaling is weak (B queries per GPU fixed).  `value` = total queries/s over
 all ranks (B * N / max-over-ranks step time).  p50 TTFT = submission -> first
-generated token per query.  The ingest phase (split -> LLM summary+keywords ->
+generated token per query (over the queries completed in the timed steps).  The ingest phase (split -> LLM summary+keywords ->
 embed -> index upsert over a synthetic repo) runs after the timed steps and is
 reported separately as ingest_docs_per_s.
 """
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
 import statistics
@@ -43,6 +53,7 @@ def parse():
     ap.add_argument("--nlist", type=int, default=4096)
     ap.add_argument("--nprobe", type=int, default=32)
     ap.add_argument("--batch", type=int, default=64, help="queries per GPU per step")
+    ap.add_argument("--inflight", type=int, default=2, help="staggered batches in flight (1 = closed batch)")
     ap.add_argument("--prompt-len", type=int, default=1024)
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--top-k", type=int, default=10)
@@ -97,7 +108,8 @@ def main():
     log(f"index shard ready: {n_local} rows ({args.index_kind}) in {time.perf_counter() - t0:.1f}s")
 
     max_len = args.prompt_len + args.gen_len + 64
-    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max(args.batch, 8), max_num_batched_tokens=16384,
+    D = max(1, min(args.inflight, args.gen_len))
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max(args.batch * D, 8), max_num_batched_tokens=16384,
                                              max_model_len=max_len, use_cuda_graph=not args.no_graph,
                                              seed=rank))
     sp = SamplingParams(max_tokens=args.gen_len, temperature=0.4, top_p=0.8, repetition_penalty=1.2,
@@ -109,8 +121,10 @@ def main():
     qcounter = [rank * 1_000_000]
     phase = {"embed": 0.0, "search": 0.0, "prompt": 0.0, "generate": 0.0}
 
-    def run_step():
-        """One batch of B RAG queries on this rank; returns per-query TTFTs (s)."""
+    inflight = collections.deque()  # (request ids, submission time), oldest first
+
+    def submit():
+        """Retrieve + build prompts for a new batch of B RAG queries and hand them to the engine."""
         B = args.batch
         t_sub = time.perf_counter()
         qs = [synthetic.question(qcounter[0] + i) for i in range(B)]
@@ -131,20 +145,34 @@ def main():
                 else pid[-args.prompt_len:]
             prompts.append(pid)
         t_p = time.perf_counter()
-        rids = [eng.add_request(p, sp) for p in prompts]
-        while eng.has_unfinished():
+        inflight.append(([eng.add_request(p, sp) for p in prompts], t_sub))
+        for k, v in (("embed", t_e - t_sub), ("search", t_s - t_e), ("prompt", t_p - t_s)):
+            phase[k] += v
+
+    def run_until(rids, ntok):
+        t0 = time.perf_counter()
+        while any(len(eng.get(r).output_ids) < ntok and eng.get(r).finish_reason is None for r in rids):
             eng.step()
+        phase["generate"] += time.perf_counter() - t0
+
+    def run_step():
+        """Submit one batch, complete the oldest; returns the completed queries' TTFTs (s)."""
+        submit()
+        rids, t_sub = inflight.popleft()
+        run_until(rids, args.gen_len)
         ttft = []
         for r in rids:
             s = eng.pop(r)
             ttft.append(s.first_token_time - t_sub)
             assert len(s.output_ids) == args.gen_len, (len(s.output_ids), s.finish_reason)
-        t_g = time.perf_counter()
-        for k, v in (("embed", t_e - t_sub), ("search", t_s - t_e), ("prompt", t_p - t_s), ("generate", t_g - t_p)):
-            phase[k] += v
         return ttft
 
-    log("warmup")
+    # pipeline fill: D-1 batches staggered by gen_len / D tokens
+    for _ in range(D - 1):
+        submit()
+        run_until(inflight[-1][0], args.gen_len // D)
+
+    log(f"warmup ({D} batches in flight)")
     for _ in range(args.warmup):
         run_step()
     comm.barrier()
@@ -172,6 +200,11 @@ def main():
     p50 = statistics.median([x for r in ttfts_all for x in r]) * 1000.0
     ms_step = elapsed / args.steps * 1000.0
 
+    while inflight:  # drain the pipeline (untimed)
+        rids, _ = inflight.popleft()
+        run_until(rids, args.gen_len)
+        for r in rids:
+            eng.pop(r)
     log(f"serving: {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms, {ms_step:.1f} ms/step")
     eng_stats = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()}
     nstep = args.steps + args.warmup
@@ -217,6 +250,8 @@ def main():
                 "model": f"{args.model} TP=1 + {args.encoder}, {args.index_size}-vec {args.index_kind} index "
                          f"(nlist={args.nlist}, nprobe={args.nprobe}) sharded dp{world}",
                 "global_batch": args.batch * world,
+                "inflight_batches": D,
+                "concurrent_seqs": args.batch * D * world,
                 "seq_len": args.prompt_len,
                 "gen_len": args.gen_len,
                 "top_k": args.top_k,

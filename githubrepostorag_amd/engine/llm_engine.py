@@ -32,6 +32,7 @@ from ..ops.attention import KV_TILE, AttnMetadata
 from ..ops.sampling import SamplerState, sample
 from .scheduler import KVCacheManager, Scheduler
 from .sequence import Completion, SamplingParams, Sequence, SeqStatus
+from .tokenizer import IncrementalDetokenizer
 
 log = logging.getLogger(__name__)
 
@@ -270,29 +271,37 @@ class LLMEngine:
 
     def _decode_inputs(self, seqs, B: int, width: int, K: int = 1) -> np.ndarray:
         """Packed int32 control buffer for a K-step decode window:
-        ids[B] | pos[K,B] | slot[K,B] | ctx[K,B] | sampler slots[B] | q_start[B+1] | block table[B,width]."""
+        ids[B] | pos[K,B] | slot[K,B] | ctx[K,B] | sampler slots[B] | q_start[B+1] | block table[B,width].
+        Rows >= len(seqs) are padding (scratch slot, slot mapping -1)."""
         n = len(seqs)
         bs = self.cfg.block_size
-        ids = np.zeros(B, dtype=np.int32)
-        pos = np.zeros((K, B), dtype=np.int32)
-        slot = np.full((K, B), -1, dtype=np.int32)
-        ctx = np.ones((K, B), dtype=np.int32)
-        sl = np.full(B, self.scratch_slot, dtype=np.int32)
-        bt = np.zeros((B, width), dtype=np.int32)
-        steps = np.arange(K, dtype=np.int64)
-        for i, s in enumerate(seqs):
-            L = s.total_len
-            ids[i] = self._last_id(s)
-            blocks = np.asarray(s.blocks[:width], dtype=np.int64)
-            p = L - 1 + steps
-            pos[:, i] = p
-            slot[:, i] = blocks[p // bs] * bs + p % bs
-            ctx[:, i] = L + steps
-            sl[i] = s.slot
-            bt[i, : len(blocks)] = blocks
-        qs = np.arange(B + 1, dtype=np.int32)
-        del n
-        return np.concatenate([ids, pos.ravel(), slot.ravel(), ctx.ravel(), sl, qs, bt.ravel()])
+        buf = np.empty(B * (3 * K + 3) + 1 + B * width, dtype=np.int32)
+        o = 0
+        ids = buf[o:o + B]; o += B
+        pos = buf[o:o + K * B].reshape(K, B); o += K * B
+        slot = buf[o:o + K * B].reshape(K, B); o += K * B
+        ctx = buf[o:o + K * B].reshape(K, B); o += K * B
+        sl = buf[o:o + B]; o += B
+        buf[o:o + B + 1] = np.arange(B + 1, dtype=np.int32); o += B + 1
+        bt = buf[o:].reshape(B, width)
+        bt.fill(0)
+        ids[n:] = 0
+        pos[:, n:] = 0
+        slot[:, n:] = -1
+        ctx[:, n:] = 1
+        sl[n:] = self.scratch_slot
+        if n:
+            for i, s in enumerate(seqs):
+                b = s.blocks
+                bt[i, :len(b)] = b if len(b) <= width else b[:width]
+            ids[:n] = [self._last_id(s) for s in seqs]
+            sl[:n] = [s.slot for s in seqs]
+            L = np.fromiter((s.total_len for s in seqs), dtype=np.int64, count=n)
+            p = L[None, :] - 1 + np.arange(K, dtype=np.int64)[:, None]  # [K, n]
+            pos[:, :n] = p
+            ctx[:, :n] = p + 1
+            slot[:, :n] = bt[np.arange(n)[None, :], p // bs].astype(np.int64) * bs + p % bs
+        return buf
 
     def _views(self, buf: torch.Tensor, B: int, width: int, K: int = 1):
         o = 0
@@ -448,10 +457,14 @@ class LLMEngine:
             reason = "length"
         elif s.total_len >= self.cfg.max_model_len:
             reason = "length"
+        if s.detok is None:
+            s.detok = IncrementalDetokenizer(self.tok)
         delta = ""
         if reason != "stop" or tok not in self._eos:
-            delta = self.tok.decode([tok])
-            s.text += delta
+            delta = s.detok.push(tok)
+        if reason is not None:
+            delta += s.detok.flush()
+        s.text += delta
         if p.stop and reason is None:
             for st in p.stop:
                 idx = s.text.find(st, max(0, len(s.text) - len(delta) - len(st)))

@@ -52,6 +52,7 @@ class Sequence:
     text: str = ""
     cancelled: bool = False
     num_preemptions: int = 0
+    detok: object = None  # tokenizer.IncrementalDetokenizer, created on the first output token
 
     @property
     def all_ids(self) -> list[int]:

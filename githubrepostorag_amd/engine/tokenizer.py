@@ -12,6 +12,7 @@
 """
 from __future__ import annotations
 
+import codecs
 import ctypes
 import os
 import threading
@@ -85,6 +86,15 @@ class ByteBPETokenizer:
         self.model_vocab_size = model_vocab_size
         self.eos_token_ids = {self.special[IM_END], self.special[ENDOFTEXT]}
         self.pad_token_id = self.special[ENDOFTEXT]
+        # id -> bytes table for the streaming detokenizer: bytes, merge products, specials
+        table = [b""] * max(model_vocab_size, max(self.special.values()) + 1)
+        for i in range(256):
+            table[i] = bytes([i])
+        for k, (a, b) in enumerate(self.merges()):
+            table[256 + k] = table[a] + table[b]
+        for tok, tid in self.special.items():
+            table[tid] = tok.encode()
+        self._table = table
 
     def __del__(self):
         try:
@@ -112,17 +122,24 @@ class ByteBPETokenizer:
             rt().grag_bpe_encode(self._h, b, len(b), out.ctypes.data, n)
         return out[:n].tolist()
 
-    def decode(self, ids) -> str:
+    def decode_bytes(self, ids) -> bytes:
         arr = np.asarray(list(ids), dtype=np.int32)
         if arr.size == 0:
-            return ""
+            return b""
         cap = 16 * arr.size + 64
         buf = ctypes.create_string_buffer(cap)
         n = rt().grag_bpe_decode(self._h, arr.ctypes.data, arr.size, buf, cap)
         if n > cap:
             buf = ctypes.create_string_buffer(n)
             rt().grag_bpe_decode(self._h, arr.ctypes.data, arr.size, buf, n)
-        return buf.raw[:n].decode("utf-8", errors="replace")
+        return buf.raw[:n]
+
+    def decode(self, ids) -> str:
+        return self.decode_bytes(ids).decode("utf-8", errors="replace")
+
+    def token_bytes(self, tid: int) -> bytes:
+        """Raw bytes of one token (table lookup: the streaming detokenizer's per-token path)."""
+        return self._table[tid] if 0 <= tid < len(self._table) else b""
 
     def apply_chat_template(self, messages: list[dict], add_generation_prompt: bool = True,
                             enable_thinking: bool | None = None) -> str:
@@ -139,6 +156,7 @@ class HFTokenizer:
                         if self._tok.token_to_id(t) is not None}
         self.eos_token_ids = set(self.special.values())
         self.pad_token_id = self.special.get(ENDOFTEXT, 0)
+        self._tok_bytes: dict[int, bytes] = {}
 
     def encode(self, text: str) -> list[int]:
         return self._tok.encode(text, add_special_tokens=False).ids
@@ -146,8 +164,59 @@ class HFTokenizer:
     def decode(self, ids) -> str:
         return self._tok.decode(list(ids), skip_special_tokens=True)
 
+    def token_bytes(self, tid: int) -> bytes:
+        b = self._tok_bytes.get(tid)
+        if b is None:
+            piece = self._tok.id_to_token(tid)
+            if piece is None or tid in self.eos_token_ids or piece in self.special:
+                b = b""
+            elif all(ch in _BYTE_DECODER for ch in piece):  # byte-level BPE piece (GPT-2 byte->unicode map)
+                b = bytes(_BYTE_DECODER[ch] for ch in piece)
+            else:
+                b = self._tok.decode([tid], skip_special_tokens=True).encode("utf-8")
+            self._tok_bytes[tid] = b
+        return b
+
     def apply_chat_template(self, messages, add_generation_prompt=True, enable_thinking=None) -> str:
         return chatml(messages, add_generation_prompt, enable_thinking)
+
+
+def _bytes_to_unicode() -> dict[int, str]:
+    """GPT-2 / Qwen byte-level BPE alphabet: every byte maps to a printable code point."""
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("\xa1"), ord("\xac") + 1)) + \
+        list(range(ord("\xae"), ord("\xff") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return dict(zip(bs, map(chr, cs)))
+
+
+_BYTE_DECODER = {c: b for b, c in _bytes_to_unicode().items()}
+
+
+class IncrementalDetokenizer:
+    """Per-sequence streaming detokenizer: token bytes go through an incremental
+    UTF-8 decoder, so a character split across tokens is emitted once complete
+    (decoding each token on its own would emit replacement characters)."""
+
+    __slots__ = ("tok", "_dec")
+
+    def __init__(self, tok):
+        self.tok = tok
+        self._dec = codecs.getincrementaldecoder("utf-8")(errors="replace")
+
+    def push(self, tid: int) -> str:
+        tb = getattr(self.tok, "token_bytes", None)
+        if tb is None:
+            return self.tok.decode([tid])
+        return self._dec.decode(tb(tid))
+
+    def flush(self) -> str:
+        return self._dec.decode(b"", final=True)
 
 
 def chatml(messages: list[dict], add_generation_prompt: bool = True, enable_thinking: bool | None = None) -> str:

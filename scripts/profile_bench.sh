@@ -9,8 +9,9 @@ cd /tmp
 timeout -k 10 ${PROF_TIMEOUT:-900} rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py ${BENCH_ARGS:---steps 1 --warmup 1 --no-ingest} > $R/gpurun_out/prof_$TAG/bench_stdout.log 2>&1
 rc=$?
 echo "rc=$rc"
+# the per-dispatch trace is large; keep only the summaries
+find $R/gpurun_out/prof_$TAG -name "*kernel_trace.csv" -delete
 tail -5 $R/gpurun_out/prof_$TAG/bench_stdout.log
-find $R/gpurun_out/prof_$TAG -name "*kernel_stats.csv" | head -3
 f=$(find $R/gpurun_out/prof_$TAG -name "*kernel_stats.csv" | head -1)
-[ -n "$f" ] && head -40 "$f" | cut -c1-220
+[ -n "$f" ] && python3 $R/scripts/summarize_prof.py "$f" 40
 exit $rc

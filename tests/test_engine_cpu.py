@@ -9,7 +9,8 @@ import torch
 from githubrepostorag_amd.engine.llm_engine import EngineConfig, LLMEngine
 from githubrepostorag_amd.engine.scheduler import KVCacheManager
 from githubrepostorag_amd.engine.sequence import SamplingParams, Sequence
-from githubrepostorag_amd.engine.tokenizer import IM_END, IM_START, ByteBPETokenizer, WordPieceTokenizer, chatml
+from githubrepostorag_amd.engine.tokenizer import (IM_END, IM_START, ByteBPETokenizer, IncrementalDetokenizer,
+                                                   WordPieceTokenizer, chatml)
 from githubrepostorag_amd.models.configs import decoder_config
 from githubrepostorag_amd.models.qwen2 import Qwen2Model
 
@@ -135,6 +136,18 @@ def test_byte_bpe_roundtrip_and_chatml(tok):
     assert msg.startswith(IM_START + "system\nbe brief" + IM_END) and msg.endswith(IM_START + "assistant\n")
     ids = tok.encode(msg)
     assert max(ids) < 512
+
+
+def test_streaming_detokenizer_multibyte(tok):
+    """Per-token deltas concatenate to the full decode even when a UTF-8 character
+    spans tokens; the id->bytes table matches the native decoder."""
+    text = "naïve café ✓ 日本語 — déjà vu; def f(): return 'ö'"
+    ids = tok.encode(text)
+    d = IncrementalDetokenizer(tok)
+    deltas = [d.push(i) for i in ids] + [d.flush()]
+    assert "".join(deltas) == text and all("\ufffd" not in x for x in deltas)
+    for i in list(range(0, 600)) + [tok.special[IM_END]]:
+        assert tok.token_bytes(i) == tok.decode_bytes([i])
 
 
 def test_wordpiece_basic():
