@@ -23,6 +23,7 @@ import threading
 from dataclasses import dataclass, field
 from typing import Any, Callable, Optional
 
+from ..utils.tracing import NULL_TRACE
 from . import prompts
 
 log = logging.getLogger(__name__)
@@ -101,6 +102,7 @@ class RunContext:
     cancel_check: Optional[Callable[[], bool]] = None
     on_answer_token: Optional[Callable[[str], None]] = None
     turns: list = field(default_factory=list)
+    trace: Any = NULL_TRACE  # utils.tracing.Trace: per-stage / per-LLM-call spans
 
     def notify(self, payload: dict) -> None:
         if self.progress_cb:
@@ -125,15 +127,22 @@ class GraphAgent:
         self.embed_fn = embed_fn
 
     # ------------------------------------------------------------------ helpers
-    def _complete(self, prompt: str, ctx: RunContext, **kw) -> str:
+    def _complete(self, prompt: str, ctx: RunContext, purpose: str = "llm", **kw) -> str:
         ctx.check()
         if ctx.cancel_check is not None:
             kw["cancel_check"] = ctx.cancel_check
-        return self.llm.complete(prompt, **kw).text
+        with ctx.trace.span("llm", purpose=purpose) as sp:
+            r = self.llm.complete(prompt, **kw)
+            for k in ("ttft_s", "tokens", "error"):
+                v = getattr(r, k, None)
+                if v is not None:
+                    sp[k] = round(v, 4) if isinstance(v, float) else v
+        return r.text
 
     def _expand(self, question: str, info: dict, ctx: RunContext) -> list[str]:
         try:
-            resp = self._complete(prompts.expand_query(question, info.get("repo"), info.get("scope")), ctx).strip()
+            resp = self._complete(prompts.expand_query(question, info.get("repo"), info.get("scope")), ctx,
+                                  "expand").strip()
             s, e = resp.find("["), resp.rfind("]") + 1
             if s >= 0 and e > s:
                 qs = json.loads(resp[s:e])
@@ -154,8 +163,12 @@ class GraphAgent:
             fb += ["application settings", "environment configuration", "setup parameters"]
         return fb[:3] if fb else [question]
 
-    def _search(self, scope: str, q: str, filters: dict) -> list:
-        return self.retrievers[scope].invoke(q, filter=filters) or []
+    def _search(self, scope: str, q: str, filters: dict, ctx: RunContext | None = None) -> list:
+        tr = ctx.trace if ctx is not None else NULL_TRACE
+        with tr.span("search", scope=scope) as sp:
+            docs = self.retrievers[scope].invoke(q, filter=filters) or []
+            sp["hits"] = len(docs)
+        return docs
 
     # ------------------------------------------------------------------ nodes
     def plan_scope(self, st: dict, ctx: RunContext) -> dict:
@@ -167,7 +180,7 @@ class GraphAgent:
         if rh:
             filters["repo"] = rh
         try:
-            data = _json_object(self._complete(prompts.plan_scope(q), ctx).strip())
+            data = _json_object(self._complete(prompts.plan_scope(q), ctx, "plan").strip())
             scope = data.get("scope") or ("code" if looks_codey(q) else "project")
             _merge_filters(filters, data.get("filters"))
         except Cancelled:
@@ -192,7 +205,7 @@ class GraphAgent:
         scope, q = st["scope"], st["query"]
         filters = st.get("filters") or {}
         attempt = st.get("attempt", 0)
-        docs = self._search(scope, q, filters)
+        docs = self._search(scope, q, filters, ctx)
         n0 = len(docs)
         if len(docs) < 3 or attempt > 0:
             expanded = self._expand(q, {"repo": filters.get("repo"), "scope": scope}, ctx)
@@ -202,7 +215,7 @@ class GraphAgent:
                 if len(all_docs) >= self.router_top_k:
                     break
                 try:
-                    for d in self._search(scope, eq, filters):
+                    for d in self._search(scope, eq, filters, ctx):
                         if len(all_docs) >= self.router_top_k:
                             break
                         h = hash(_content(d))
@@ -238,7 +251,7 @@ class GraphAgent:
                          for it in inv):
             quality = "semantically_relevant"
         try:
-            data = _json_object(self._complete(prompts.judge(q, quality, inv), ctx).strip())
+            data = _json_object(self._complete(prompts.judge(q, quality, inv), ctx, "judge").strip())
         except Cancelled:
             raise
         except Exception as e:
@@ -282,7 +295,7 @@ class GraphAgent:
         if attempt == 1:
             ctx_s = " ".join(filters[k] for k in ("repo", "module") if k in filters)
             try:
-                sharp = self._complete(prompts.rewrite(base, ctx_s), ctx).strip().strip("\"'").strip()
+                sharp = self._complete(prompts.rewrite(base, ctx_s), ctx, "rewrite").strip().strip("\"'").strip()
                 if not sharp or len(sharp) < 10:
                     raise ValueError("rewrite too short")
             except Cancelled:
@@ -314,10 +327,11 @@ class GraphAgent:
         dbg_issue = None
         try:
             kw = {"on_token": ctx.on_answer_token} if ctx.on_answer_token else {}
-            text = self._complete(prompts.synthesize(system, q, blocks), ctx, **kw)
+            text = self._complete(prompts.synthesize(system, q, blocks), ctx, "synthesize", **kw)
             if has_content and len(docs) >= 3 and any(p in text.lower() for p in _CONSERVATIVE):
                 try:
-                    retry = self._complete(prompts.synthesize(prompts.SYNTH_RETRY, q, blocks), ctx)
+                    retry = self._complete(prompts.synthesize(prompts.SYNTH_RETRY, q, blocks), ctx,
+                                           "synthesize_retry")
                     if not any(p in retry.lower() for p in _CONSERVATIVE[:3]):
                         text = retry
                 except Cancelled:
@@ -340,20 +354,27 @@ class GraphAgent:
 
     # ------------------------------------------------------------------ run
     def run(self, question: str, *, namespace: str | None = None, progress_cb=None, cancel_check=None,
-            force_level: str | None = None, on_answer_token=None) -> dict:
-        ctx = RunContext(progress_cb, cancel_check, on_answer_token)
+            force_level: str | None = None, on_answer_token=None, trace=None) -> dict:
+        ctx = RunContext(progress_cb, cancel_check, on_answer_token, trace=trace or NULL_TRACE)
+        tr = ctx.trace
         st: dict = {"query": question, "force_level": force_level}
         ns = namespace or self.namespace
         if ns:
             st["filters"] = {"namespace": ns}
-        st = self.plan_scope(st, ctx)
+        with tr.span("plan"):
+            st = self.plan_scope(st, ctx)
         while True:
-            st = self.retrieve(st, ctx)
-            st = self.judge(st, ctx)
-            st = self.rewrite_or_end(st, ctx)
+            attempt = st.get("attempt", 0)
+            with tr.span("retrieve", attempt=attempt, scope=st.get("scope")):
+                st = self.retrieve(st, ctx)
+            with tr.span("judge", attempt=attempt):
+                st = self.judge(st, ctx)
+            with tr.span("rewrite", attempt=attempt):
+                st = self.rewrite_or_end(st, ctx)
             if not st.get("needs_more"):
                 break
-        st = self.synthesize(st, ctx)
+        with tr.span("synthesize"):
+            st = self.synthesize(st, ctx)
         debug = dict(st.get("debug") or {})
         debug["turns"] = ctx.turns
         return {"answer": st.get("answer", ""), "sources": st.get("sources", []), "debug": debug,

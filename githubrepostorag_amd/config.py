@@ -88,6 +88,7 @@ class Settings:
     nprobe: int = field(default_factory=lambda: _int("NPROBE", 16))
     worker_max_jobs: int = field(default_factory=lambda: _int("WORKER_MAX_JOBS", 10))
     job_timeout_s: int = field(default_factory=lambda: _int("JOB_TIMEOUT", 300))
+    engine_watchdog_s: int = field(default_factory=lambda: _int("ENGINE_WATCHDOG_S", 120))
     keep_result_s: int = field(default_factory=lambda: _int("KEEP_RESULT", 3600))
     event_bus: str = field(default_factory=lambda: _env("EVENT_BUS", "memory"))  # memory | redis
     llm_timeout_s: float = field(default_factory=lambda: _float("LLM_TIMEOUT", 60.0))

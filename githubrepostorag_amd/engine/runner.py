@@ -6,6 +6,14 @@ own threads; one loop thread owns the GPU engine and steps it whenever work
 is queued, so all of them share continuous batches.  ``generate`` blocks the
 caller (agent threads), ``submit`` returns a handle with a per-token
 callback (SSE token streaming) and supports cancellation.
+
+Failure handling (SURVEY §5.3 "engine watchdog"): an exception inside a step
+fails every in-flight request and the loop keeps serving; a step that runs
+longer than ``watchdog_s`` (a hung kernel, a wedged collective) is detected by
+a separate watchdog thread, which marks the engine unhealthy (/health -> 503,
+``grag_engine_healthy`` 0) and fails the waiting requests at once instead of
+letting every client hang until its own timeout.  If the step eventually
+returns, the engine is marked healthy again.
 """
 from __future__ import annotations
 
@@ -43,17 +51,27 @@ class GenerationHandle:
 
 
 class EngineRunner:
-    def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005):
+    def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005, watchdog_s: float = 120.0,
+                 on_health=None):
         self.engine = engine
         self.idle_sleep = idle_sleep
+        self.watchdog_s = watchdog_s
+        self._on_health = on_health  # callable(bool), e.g. a Prometheus gauge setter
         self._cv = threading.Condition()
         self._stop = False
         self._handles: dict[str, GenerationHandle] = {}
         self._pending: list[tuple] = []
-        self._thread = threading.Thread(target=self._loop, name="grag-engine", daemon=True)
-        self._thread.start()
         self.last_error: BaseException | None = None
         self.healthy = True
+        self.hung = False
+        self.num_faults = 0
+        self._step_t0: float | None = None
+        self._thread = threading.Thread(target=self._loop, name="grag-engine", daemon=True)
+        self._thread.start()
+        self._wd = None
+        if watchdog_s and watchdog_s > 0:
+            self._wd = threading.Thread(target=self._watchdog, name="grag-engine-watchdog", daemon=True)
+            self._wd.start()
 
     # ------------------------------------------------------------------ API
     def submit(self, prompt, params: SamplingParams | None = None, on_token=None) -> GenerationHandle:
@@ -81,6 +99,8 @@ class EngineRunner:
             self._stop = True
             self._cv.notify()
         self._thread.join(timeout=10)
+        if self._wd is not None:
+            self._wd.join(timeout=2)
 
     def stats(self) -> dict:
         sch = self.engine.sched
@@ -118,15 +138,52 @@ class EngineRunner:
                     if h is not None:
                         h.error = e
                         h.done.set()
+            self._step_t0 = time.monotonic()
             try:
                 self.engine.step()
-                self.healthy = True
+                self._step_t0 = None
+                if self.hung:
+                    log.warning("engine step returned after the watchdog fired; marking healthy again")
+                    self.hung = False
+                    self.engine.sched.reap_cancelled()
+                self._set_health(True)
             except Exception as e:  # engine fault: fail every in-flight request, keep serving
+                self._step_t0 = None
                 log.exception("engine step failed")
                 self.last_error = e
-                self.healthy = False
+                self.num_faults += 1
+                self._set_health(False)
                 self._fail_all(e)
                 time.sleep(0.05)
+
+    def _set_health(self, ok: bool) -> None:
+        if ok != self.healthy and self._on_health is not None:
+            try:
+                self._on_health(ok)
+            except Exception:
+                pass
+        self.healthy = ok
+
+    def _watchdog(self) -> None:
+        period = min(1.0, self.watchdog_s / 4)
+        while not self._stop:
+            time.sleep(period)
+            t0 = self._step_t0
+            if t0 is None or self.hung or time.monotonic() - t0 < self.watchdog_s:
+                continue
+            err = TimeoutError(f"engine step exceeded the {self.watchdog_s:.0f}s watchdog")
+            log.error("%s; failing in-flight requests", err)
+            self.hung = True
+            self.last_error = err
+            self.num_faults += 1
+            self._set_health(False)
+            # only flag + release waiters here: the stuck loop thread still owns the engine
+            with self._cv:
+                handles, self._handles = self._handles, {}
+            for rid, h in handles.items():
+                self.engine.abort(rid)
+                h.error = err
+                h.done.set()
 
     def _fail_all(self, err: BaseException) -> None:
         with self._cv:

@@ -51,8 +51,17 @@ INDEX_SEARCH_SECONDS = Histogram("grag_index_search_seconds", "Vector search lat
 INDEX_ROWS = Gauge("grag_index_rows", "Rows per scope table", ["table"], registry=REGISTRY)
 EMBED_TEXTS = Counter("grag_embed_texts_total", "Texts embedded", registry=REGISTRY)
 INGEST_DOCS = Counter("grag_ingest_documents_total", "Source files fully ingested", registry=REGISTRY)
+SPAN_SECONDS = Histogram("grag_span_seconds", "Per-stage span durations of RAG jobs (utils.tracing)", ["span"],
+                         buckets=(0.001, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10, 30),
+                         registry=REGISTRY)
+ENGINE_HEALTHY = Gauge("grag_engine_healthy", "1 when the engine loop is stepping normally, 0 after a fault/hang",
+                       registry=REGISTRY)
 GPU_MEM_USED = Gauge("grag_gpu_memory_used_bytes", "HBM bytes allocated by this process", ["device"],
                      registry=REGISTRY)
+
+
+def observe_span(name: str, seconds: float) -> None:
+    SPAN_SECONDS.labels(span=name).observe(seconds)
 
 
 def render() -> bytes:

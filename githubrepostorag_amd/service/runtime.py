@@ -62,7 +62,11 @@ class RAGRuntime:
                                 kv_cache_gb=s.kv_cache_gb or None, use_cuda_graph=s.cuda_graphs,
                                 enable_prefix_caching=s.prefix_caching, seed=s.seed)
             self.engine = LLMEngine(model, self.tokenizer, ecfg)
-            self.runner = EngineRunner(self.engine)
+            from . import metrics as M
+
+            M.ENGINE_HEALTHY.set(1)
+            self.runner = EngineRunner(self.engine, watchdog_s=s.engine_watchdog_s,
+                                       on_health=lambda ok: M.ENGINE_HEALTHY.set(1 if ok else 0))
             llm = MeteredLLM(EngineLLM(self.runner, self.tokenizer, max_tokens=s.qwen_max_output,
                                        timeout_s=s.job_timeout_s, retries=s.llm_retries))
             ingest_llm = EngineLLM(self.runner, self.tokenizer, max_tokens=2048, mode="ingest",

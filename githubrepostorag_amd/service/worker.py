@@ -22,6 +22,7 @@ import uuid
 
 from ..agent.graph_agent import Cancelled
 from . import metrics as M
+from ..utils.tracing import Trace
 from .events import CancelFlags, EventLog
 
 log = logging.getLogger(__name__)
@@ -108,6 +109,7 @@ class RAGWorker:
 
     async def run_rag_job(self, ctx, job_id: str, req: dict) -> dict | None:
         t_job = time.perf_counter()
+        queue_wait = max(0.0, time.time() - float((self.queue.results.get(job_id) or {}).get("enqueued", time.time())))
         query = (req.get("query") or "").strip()
         forced = req.get("force_level")
         s = self.runtime.settings
@@ -133,11 +135,14 @@ class RAGWorker:
 
             loop = asyncio.get_running_loop()
             t_rag = time.perf_counter()
+            trace = Trace(job_id, observer=M.observe_span)
+            trace.add("queue_wait", queue_wait)
             result = await loop.run_in_executor(
                 self.executor,
                 lambda: agent.run(query, namespace=namespace, progress_cb=progress,
                                   cancel_check=lambda: self.flags.is_cancelled_sync(job_id),
-                                  force_level=forced, on_answer_token=on_token if self.stream_tokens else None))
+                                  force_level=forced, on_answer_token=on_token if self.stream_tokens else None,
+                                  trace=trace))
             M.WORKER_RETRIEVAL_DURATION.observe(time.perf_counter() - t_rag)
             sources = result.get("sources") or []
             debug = result.get("debug") or {}
@@ -146,7 +151,9 @@ class RAGWorker:
                                                          "turns": debug.get("turns", []),
                                                          "final_ctx_blocks": debug.get("final_ctx_blocks", 0)})
             await self.events.emit(job_id, "timing", {"job_s": round(time.perf_counter() - t_job, 4),
-                                                      "agent_s": round(time.perf_counter() - t_rag, 4)})
+                                                      "agent_s": round(time.perf_counter() - t_rag, 4),
+                                                      "trace_id": trace.trace_id, "totals_ms": trace.totals(),
+                                                      "spans": trace.to_list()})
             await self.events.emit(job_id, "final", {"answer": result.get("answer", ""), "sources": sources or None})
             M.WORKER_JOBS_TOTAL.labels(status="success").inc()
             return {"answer": result.get("answer", ""), "n_sources": len(sources)}

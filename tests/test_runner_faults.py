@@ -1,0 +1,94 @@
+"""Fault injection for the engine loop: a step that raises fails
+the in-flight requests and the loop keeps serving; a step that hangs past the
+watchdog marks the engine unhealthy and releases every waiter at once; the
+engine is healthy again once a step completes."""
+import threading
+import time
+
+import pytest
+
+from githubrepostorag_amd.engine.runner import EngineRunner
+from githubrepostorag_amd.engine.sequence import Completion
+
+
+class _Sched:
+    def __init__(self):
+        self.running, self.waiting = [], []
+
+    def reap_cancelled(self):
+        return []
+
+
+class FakeEngine:
+    """Minimal engine: each request finishes after one step with a fixed text;
+    ``mode`` injects faults into the next step."""
+
+    on_gpu = False
+
+    def __init__(self):
+        self.sched = _Sched()
+        self.reqs = {}
+        self.mode = "ok"
+        self.release = threading.Event()
+        self.stats = {}
+
+    def add_request(self, prompt, params, req_id, on_token):
+        self.reqs[req_id] = on_token
+
+    def has_unfinished(self):
+        return bool(self.reqs)
+
+    def abort(self, rid):
+        pass
+
+    def pop(self, rid):
+        return None
+
+    def completion(self, seq):
+        return Completion(seq.req_id, "done", [1], "length", 1, 0.0, 0.0)
+
+    def step(self):
+        if self.mode == "raise":
+            self.mode = "ok"
+            self.reqs.clear()
+            raise RuntimeError("injected kernel fault")
+        if self.mode == "hang":
+            self.release.wait(10)
+            self.mode = "ok"
+        reqs, self.reqs = self.reqs, {}
+        for rid, cb in reqs.items():
+            seq = type("S", (), {"req_id": rid})()
+            cb(seq, "done", True)
+
+
+def test_step_exception_fails_requests_then_recovers():
+    eng = FakeEngine()
+    eng.mode = "raise"
+    r = EngineRunner(eng, watchdog_s=0)
+    try:
+        with pytest.raises(RuntimeError, match="injected"):
+            r.generate("p", timeout=5)
+        assert not r.healthy and r.num_faults == 1
+        assert r.generate("p", timeout=5).text == "done"
+        assert r.healthy
+    finally:
+        r.shutdown()
+
+
+def test_watchdog_releases_waiters_on_hung_step():
+    eng = FakeEngine()
+    eng.mode = "hang"
+    health = []
+    r = EngineRunner(eng, watchdog_s=0.4, on_health=health.append)
+    try:
+        t0 = time.monotonic()
+        with pytest.raises(TimeoutError, match="watchdog"):
+            r.generate("p", timeout=8)
+        assert time.monotonic() - t0 < 4  # released by the watchdog, not the client timeout
+        assert r.hung and not r.healthy and health == [False]
+        eng.release.set()  # the stuck step finally returns
+        assert r.generate("p", timeout=5).text == "done"
+        assert r.healthy and not r.hung and health == [False, True]
+    finally:
+        eng.release.set()
+        r.shutdown()

@@ -73,6 +73,14 @@ def test_job_lifecycle_and_event_order(embedder):
         for k in ("turn", "token", "retrieval", "timing"):
             assert k in kinds, kinds
         assert kinds.index("retrieval") < kinds.index("final")
+        timing = next(d for k, d in evs if k == "timing")
+        names = [sp["name"] for sp in timing["spans"]]
+        for n in ("queue_wait", "plan", "retrieve", "search", "judge", "synthesize", "llm"):
+            assert n in names, names
+        llm_purposes = {sp.get("purpose") for sp in timing["spans"] if sp["name"] == "llm"}
+        assert {"plan", "judge", "synthesize"} <= llm_purposes
+        assert timing["totals_ms"]["synthesize"] >= 0 and timing["trace_id"] == job_id
+        assert b"grag_span_seconds_bucket" in client.get("/metrics").content
         final = evs[-1][1]
         assert final["answer"] == "Widgets are handled in [1]."
         assert final["sources"] and final["sources"][0]["metadata"]["repo"] == "r"
