@@ -1,4 +1,4 @@
-// Weight-streaming split-K GEMM for decode-batch shapes (SURVEY §2.7 N1c/N1h/
+// Weight-streaming stream-K GEMM for decode-batch shapes (SURVEY §2.7 N1c/N1h/
 // N1i/N1j/N1k and N2b/N2d at small M):
 //
 //   C[M, N] = A[M, K] · W[N, K]^T (+ bias[N])          bf16 in, fp32 acc
@@ -9,7 +9,10 @@
 //
 // Structure (cdna guide §5 "Projection GEMM at M = 256": x through LDS in full
 // 128-B lines filled by LDS-DMA; "glds vs register staging"):
-//   * one workgroup = 4 waves = BN output columns x 16*MT rows x one K slice;
+//   * one workgroup = 4 waves = BN output columns x 16*MT rows; every
+//     workgroup walks an equal share of the flattened (tile, k-step) space
+//     (stream-K: G = number of resident workgroups, so every CU streams the
+//     same number of weight bytes whatever N / BN is);
 //   * every 64-k step, the W tile (BN rows x 128 B) and the A tile (16*MT rows
 //     x 128 B) arrive by global_load_lds_dwordx4 — one wave instruction moves
 //     8 whole 128-B lines, so HBM sees only full-line requests — into an
@@ -20,14 +23,16 @@
 //     across the barrier (a __syncthreads() would drain them);
 //   * wave w owns columns [w*BN/4, (w+1)*BN/4) and all 16*MT rows, so A is read
 //     from LDS by all four waves but fetched from L2 once per workgroup;
-//   * split-K over S workgroups restores parallelism for narrow N (o_proj,
-//     down_proj: N = 3584) — combined IN-LAUNCH (§5 item 2): each slice writes
-//     an fp32 slab, drains, one lane releases (agent fence) and takes a relaxed
-//     agent-scope ticket; the slice that draws S-1 acquires and sums all S
-//     slabs + bias -> bf16.  The ticket word is reset by that last arriver; the
-//     counter array is zero-initialised at allocation (graph replays need no
-//     memset).  Slices of a tile get consecutive logical ids after the XCD
-//     remap, so the reducer mostly reads same-XCD slabs (speed only).
+//   * a tile whose k range lies wholly inside one workgroup's share is written
+//     directly (bias + bf16); a tile split across workgroups is combined
+//     IN-LAUNCH (§5 item 2): each part writes an fp32 slab slot, drains, one
+//     lane releases (agent fence) and takes a relaxed agent-scope ticket; the
+//     part that draws the last ticket acquires, sums the slots + bias -> bf16
+//     and resets the ticket word (the counter array is zero-initialised at
+//     allocation, so graph replays need no memset).
+// Measured: the library GEMMs (TunableOp-selected hipBLASLt) win at M >= 16-32
+// on most Qwen2-7B shapes; ops/linear.py picks per shape from a table timed
+// inside hipGraphs (tuning/gemm_dispatch_gfx950.json).
 #include "common.h"
 
 #include <algorithm>
