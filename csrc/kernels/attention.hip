@@ -259,6 +259,224 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// Paged prefill, 8-wave variant (nw code 5): more query rows per K/V tile and
+// K/V streamed by LDS-DMA into a 2-stage ring.
+//
+// The 4-wave kernel above stages 64 GQA rows per 32 KiB K/V tile through
+// registers, so every tile costs a full global->LDS round trip per 64 rows
+// and the load latency sits in front of the MFMAs.  Here a workgroup is 8
+// waves x RPW row groups of 16 = 256 rows (36 positions x 7 heads at GQA 7):
+//   * K and V tiles arrive by global_load_lds_dwordx4 (1 KiB per wave
+//     instruction, lane-linear LDS destination, XOR swizzle applied to the
+//     per-lane SOURCE chunk — rule 21), tile t+1 issued right after the
+//     barrier that opens tile t, so its flight overlaps tile t's MFMAs;
+//   * one barrier per tile: s_waitcnt vmcnt(0) (own pieces of tile t landed)
+//     then the barrier (everyone's pieces landed AND everyone finished tile
+//     t-1, whose stage the next issue overwrites);
+//   * every K fragment (ds_read_b128) and V^T fragment (ds_read_b64_tr_b16) a
+//     wave reads feeds RPW MFMAs (one per row group), halving LDS reads per
+//     FLOP against the 4-wave kernel;
+//   * the workgroup's block-table window sits in LDS, so no dependent global
+//     load precedes the DMA of a tile;
+//   * causal: a row group skips the tiles wholly above its diagonal (wave-
+//     uniform test), and the heaviest (latest) q tiles are dispatched first.
+// The math (swapped QK^T, exp2 online softmax, P^T straight from the S^T
+// accumulators) is the 4-wave kernel's.
+template <int D, int RPW>
+__global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
+  constexpr int NW = 8;
+  constexpr int RB = 2 * D;            // bytes per K/V row
+  constexpr int CPR = D / 8;           // 16-B chunks per row
+  constexpr int NC = D / 32;
+  constexpr int ND = D / 16;
+  constexpr int TILE = KT * RB;        // bytes per K (or V) tile
+  constexpr int NP = TILE / 1024;      // LDS-DMA pieces per tile per tensor
+  constexpr int PPW = NP / NW;         // pieces per wave per tensor
+  constexpr int RPP = 1024 / RB;       // rows per piece
+  constexpr int ROWS = 16 * RPW * NW;  // GQA rows per workgroup
+  constexpr int MAXB = 1024;           // block-table window in LDS (16 K keys at BS 16)
+  static_assert(PPW >= 1 && PPW * NW == NP, "piece split");
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + MAXB * 4];
+  int* bt_lds = reinterpret_cast<int*>(smem + 2 * 2 * TILE);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h4 = lane >> 4, li = lane & 15;
+  const int tiles = p.tiles_per_seq;
+  const int seq = blockIdx.x / tiles;
+  const int tile = tiles - 1 - (int)(blockIdx.x % tiles);
+  const int kvh = blockIdx.y;
+  const int q0 = p.q_start[seq], qlen = p.q_start[seq + 1] - q0;
+  const int ctx = p.ctx_len[seq];
+  const int G = p.G;
+  const int nrows = qlen * G;
+  const int row_base = tile * ROWS;
+  if (row_base >= nrows) return;
+  const int last_row = min(row_base + ROWS, nrows) - 1;
+  const int kv_hi = p.causal ? min(ctx, ctx - qlen + last_row / G + 1) : ctx;
+
+  const int nb = (kv_hi + p.BS - 1) / p.BS;
+  const bool bt_fast = nb <= MAXB;
+  const int32_t* bt = p.block_tables + (size_t)seq * p.bt_stride;
+  if (bt_fast)
+    for (int i = threadIdx.x; i < nb; i += 64 * NW) bt_lds[i] = bt[i];
+
+  bf16x8_t qf[RPW][NC];
+  int key_lim[RPW];  // this lane's row limit
+  bool valid[RPW];
+  int pq[RPW], gq[RPW];
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const int grow = row_base + (wave * RPW + j) * 16;
+    const int my_row = grow + li;
+    valid[j] = my_row < nrows;
+    pq[j] = valid[j] ? my_row / G : 0;
+    gq[j] = valid[j] ? my_row % G : 0;
+    key_lim[j] = p.causal ? ctx - qlen + pq[j] + 1 : ctx;
+    const bf16* qp = p.q + (size_t)(q0 + pq[j]) * p.q_stride + (size_t)(kvh * G + gq[j]) * D + 8 * h4;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (valid[j]) qf[j][c] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * c);
+      else qf[j][c] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  __syncthreads();  // block-table window visible
+  // smallest key limit over the wave's rows (its first row), wave-uniform:
+  // tiles ending below it need no mask
+  const int wrow0 = row_base + __builtin_amdgcn_readfirstlane(wave) * RPW * 16;
+  const int wave_lim_min = min(kv_hi, p.causal ? ctx - qlen + min(wrow0, nrows - 1) / G + 1 : ctx);
+
+  const int lrow = lane / CPR, lch = lane % CPR;
+  auto issue = [&](int kt0, int stage) {
+    char* kdst = smem + stage * 2 * TILE;
+    char* vdst = kdst + TILE;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int piece = wave * PPW + i;
+      const int row = piece * RPP + lrow;
+      const int key = min(kt0 + row, kv_hi - 1);
+      const int bi = key / p.BS;
+      const int blk = bt_fast ? bt_lds[bi] : bt[bi];
+      const size_t off = (((size_t)blk * p.Hkv + kvh) * p.BS + (key % p.BS)) * D;
+      glds16(p.k + off + ((lch ^ kswz<D>(row)) << 3), kdst + piece * 1024);
+      glds16(p.v + off + ((lch ^ vswz<D>(row)) << 3), vdst + piece * 1024);
+    }
+  };
+
+  float m[RPW], lsum[RPW];
+  f32x4_t o[RPW][ND];
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    m[j] = -INFINITY;
+    lsum[j] = 0.f;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) o[j][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  const int ntiles = (kv_hi + KT - 1) / KT;
+  issue(0, 0);
+  for (int t = 0; t < ntiles; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < ntiles) issue((t + 1) * KT, (t + 1) & 1);
+    const int kt0 = t * KT;
+    const char* k_lds = smem + (t & 1) * 2 * TILE;
+    const char* v_lds = k_lds + TILE;
+
+    // S^T = K Q^T: every K fragment read once, used by all RPW row groups
+    f32x4_t s[RPW][4];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int row = 16 * tt + li;
+      bf16x8_t a[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        a[c] = *reinterpret_cast<const bf16x8_t*>(k_lds + row * RB + (((4 * c + h4) ^ kswz<D>(row)) << 4));
+#pragma unroll
+      for (int j = 0; j < RPW; ++j) {
+        s[j][tt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < NC; ++c) s[j][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], qf[j][c], s[j][tt], 0, 0, 0);
+      }
+    }
+    // masking is needed only on tiles that reach the wave's diagonal / the context end
+    const bool need_mask = kt0 + KT > wave_lim_min;
+    bf16x8_t bp[RPW][2];
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = s[j][tt][r] * p.scale_log2;
+          if (need_mask) {
+            const int key = kt0 + 16 * tt + 4 * h4 + r;
+            x = (key >= key_lim[j] || key >= kv_hi) ? -INFINITY : x;
+          }
+          s[j][tt][r] = x;
+          tmax = __builtin_fmaxf(tmax, x);
+        }
+      tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float m_new = __builtin_fmaxf(m[j], tmax);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = __builtin_amdgcn_exp2f(m[j] - m_use);
+      m[j] = m_new;
+      lsum[j] *= alpha;
+#pragma unroll
+      for (int n = 0; n < ND; ++n) o[j][n] *= alpha;
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p0 = __builtin_amdgcn_exp2f(s[j][2 * cc][r] - m_use);
+          const float p1 = __builtin_amdgcn_exp2f(s[j][2 * cc + 1][r] - m_use);
+          lsum[j] += p0 + p1;
+          bp[j][cc][r] = f2bits(p0);
+          bp[j][cc][4 + r] = f2bits(p1);
+        }
+    }
+    // O^T += V^T P^T: every V^T fragment read once, used by all RPW row groups
+    const int tq = li >> 2, tp = li & 3;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int r0 = 32 * cc + 4 * h4 + tq;
+      const int r1 = r0 + 16;
+      bf16x8_t a[ND];
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+        const int unit = 4 * n + tp;
+        const int b0 = r0 * RB + ((unit ^ (vswz<D>(r0) << 1)) << 3);
+        const int b1 = r1 * RB + ((unit ^ (vswz<D>(r1) << 1)) << 3);
+        const bf16x4_t a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(v_lds + b0));
+        const bf16x4_t a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(v_lds + b1));
+        a[n] = bf16x8_t{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      }
+#pragma unroll
+      for (int n = 0; n < ND; ++n)
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) o[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[n], bp[j][cc], o[j][n], 0, 0, 0);
+    }
+  }
+
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    float l = lsum[j];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (!valid[j]) continue;
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16* op = p.out + (size_t)(q0 + pq[j]) * p.out_stride + (size_t)(kvh * G + gq[j]) * D;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+      bf16x4_t w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = f2bits(o[j][n][r] * inv);
+      *reinterpret_cast<bf16x4_t*>(op + 16 * n + 4 * h4) = w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Decode (q_len == 1) specialisation: one wave per (sequence, kv head, split).
 // The GQA group's G <= 16 query heads are the 16 MFMA columns.  K/V tiles are
 // fetched by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave instruction,
@@ -501,12 +719,25 @@ int launch_decode(const AttnParams& prm, int nseq, int tk, hipStream_t stream) {
 }
 
 template <int D>
+int launch_prefill(const AttnParams& prm, int nseq, hipStream_t stream) {
+  dim3 grid(nseq * prm.tiles_per_seq, prm.Hkv, 1);
+  attn_prefill_kernel<D, 2><<<grid, 512, 0, stream>>>(prm);
+  return (int)hipGetLastError();
+}
+
+template <int D>
 int dispatch_nw(const AttnParams& prm, int nseq, int nw, bool paged, hipStream_t stream) {
   // nw == 1 / 3 with q_len == 1: LDS-DMA pipelined decode kernel with 64- / 32-key
   // tiles (32-key tiles halve the LDS ring so more single-wave workgroups share a
   // CU); nw == 2: the generic kernel with one wave per workgroup (A/B reference)
   if (paged && (nw == 1 || nw == 3) && prm.tiles_per_seq == 1 && prm.G <= 16 && prm.BS % 16 == 0)
     return launch_decode<D>(prm, nseq, nw == 3 ? 32 : 64, stream);
+  if (nw == 5) {
+    if constexpr (D == 128 || D == 64) {
+      if (paged && prm.num_splits == 1) return launch_prefill<D>(prm, nseq, stream);
+    }
+    return (int)hipErrorInvalidValue;
+  }
   if (nw == 3) nw = 1;
   if (nw == 2) nw = 1;
   if (paged) {
@@ -530,7 +761,8 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
                                   float scale, int causal, int num_splits, int split_len,
                                   float* part_o, float* part_ml, int nw, hipStream_t stream) {
   if (nseq <= 0) return 0;
-  if (Hq % Hkv != 0 || BS <= 0 || nw < 1 || nw > 4) return (int)hipErrorInvalidValue;
+  if (Hq % Hkv != 0 || BS <= 0 || nw < 1 || nw > 5) return (int)hipErrorInvalidValue;
+  if (nw == 5 && num_splits > 1) return (int)hipErrorInvalidValue;
   if (num_splits > 1 && (max_q_len != 1 || !part_o || !part_ml || split_len % KT != 0))
     return (int)hipErrorInvalidValue;
   AttnParams prm{};
@@ -551,8 +783,8 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
   prm.G = Hq / Hkv;
   prm.BS = BS;
   prm.bt_stride = bt_stride;
-  const int nwr = nw == 2 ? 1 : nw;
-  prm.tiles_per_seq = (max_q_len * prm.G + 16 * nwr - 1) / (16 * nwr);
+  const int rows_per_wg = nw == 5 ? 256 : 16 * (nw == 2 ? 1 : nw);  // nw 5: 8 waves x 2 row groups
+  prm.tiles_per_seq = (max_q_len * prm.G + rows_per_wg - 1) / rows_per_wg;
   if (nw == 1 && max_q_len != 1) return (int)hipErrorInvalidValue;
   prm.num_splits = num_splits < 1 ? 1 : num_splits;
   prm.split_len = prm.num_splits > 1 ? split_len : (1 << 30);

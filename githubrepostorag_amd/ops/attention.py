@@ -14,6 +14,9 @@ KV_TILE = 64  # keys per kernel tile; split lengths must be multiples of this
 # half the LDS ring -> more single-wave workgroups per CU)
 # (scripts/microbench.py, B=64 ctx=1152: 64-key 42.3 us -> 32-key 36.7 us)
 DECODE_NW = {64: 1, 32: 3}[int(os.environ.get("GRAG_DECODE_TK", "32"))]
+# prefill kernel: 8-wave LDS-DMA variant (nw code 5, head_dim 64/128) or the
+# 4-wave register-staged kernel (nw code 4); GRAG_PREFILL_ATTN=v1 selects the latter
+PREFILL_NW = 4 if os.environ.get("GRAG_PREFILL_ATTN", "v2") == "v1" else 5
 
 
 @dataclass
@@ -93,7 +96,12 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     if out is None:
         out = torch.empty(T, Hq * D, dtype=q.dtype, device=q.device)
     nsplit = meta.num_splits if meta.is_decode else 1
-    nw = meta.extra.get("decode_nw", DECODE_NW) if meta.is_decode else 4
+    if meta.is_decode:
+        nw = meta.extra.get("decode_nw", DECODE_NW)
+    else:
+        nw = meta.extra.get("prefill_nw", PREFILL_NW)
+        if nw == 5 and D not in (64, 128):
+            nw = 4
     call("grag_paged_attention", ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(out), out.stride(0),
          ptr(meta.block_tables), meta.block_tables.stride(0), ptr(meta.q_start), ptr(meta.ctx_len),
          meta.num_seqs, T, meta.max_q_len, Hq, Hkv, D, BS, float(scale), 1 if causal else 0, nsplit,

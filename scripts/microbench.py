@@ -98,7 +98,11 @@ def attn_prefill_bench(nseq, L):
                           ctx_len=torch.full((nseq,), L, device=dev, dtype=torch.int32), block_tables=bt,
                           slot_mapping=torch.zeros(nseq * L, dtype=torch.int32, device=dev), max_q_len=L,
                           num_seqs=nseq, num_tokens=nseq * L)
-    r = rounds({"paged_prefill": lambda: A.paged_attention(q, kc, vc, meta, 0.088)}, n=3, iters=10)
+    def run(code):
+        meta.extra = {"prefill_nw": code}
+        return A.paged_attention(q, kc, vc, meta, 0.088)
+
+    r = rounds({"prefill_4wave": lambda: run(4), "prefill_8wave_dma": lambda: run(5)}, n=3, iters=10)
     fl = nseq * Hq * L * L / 2 * D * 4 / 1e12
     for k in r:
         r[k]["TFLOPs"] = round(fl / (r[k]["min_us"] * 1e-6), 1)
@@ -134,6 +138,9 @@ if __name__ == "__main__":
             res[f"decode_B64_ctx1152_split{sl}"] = attn_decode_bench(64, 1152, sl)
         res["decode_B1_ctx4096_split64"] = attn_decode_bench(1, 4096, 64)
         res["prefill_16x1024"] = attn_prefill_bench(16, 1024)
+    if args.what == "prefill":
+        res["prefill_16x1024"] = attn_prefill_bench(16, 1024)
+        res["prefill_4x4096"] = attn_prefill_bench(4, 4096)
     if args.what in ("all", "sampler"):
         res["sampler_B64"] = sampler_bench(64)
     print(json.dumps(res, indent=1))

@@ -133,9 +133,27 @@ def test_paged_prefill(dev, Hq, Hkv, D):
     lens_ctx = [37, 200, 70, 64]  # seq 1 and 2 have cached prefixes (chunked prefill)
     q, kc, vc, meta = _paged_setup(dev, lens_q, lens_ctx, Hq, Hkv, D)
     scale = 1 / math.sqrt(D)
-    out = A.paged_attention(q.to(dev), kc.to(dev), vc.to(dev), _to(meta, dev), scale)
     ref = A.paged_attention_ref(q, kc, vc, meta, scale).reshape(q.shape[0], -1)
-    close(out, ref, 2e-2)
+    for code in (4, 5):  # 4-wave register-staged kernel, 8-wave LDS-DMA kernel
+        m = _to(meta, dev)
+        m.extra = {"prefill_nw": code}
+        out = A.paged_attention(q.to(dev), kc.to(dev), vc.to(dev), m, scale)
+        close(out, ref, 2e-2)
+
+
+def test_paged_prefill_long_context(dev):
+    """Chunked prefill deep into a long context (many K/V tiles, a block-table
+    window wider than one tile, 256-row workgroups cut by the GQA packing)."""
+    Hq, Hkv, D = 28, 4, 128
+    lens_q = [300, 5, 513]
+    lens_ctx = [2100, 1030, 513]
+    q, kc, vc, meta = _paged_setup(dev, lens_q, lens_ctx, Hq, Hkv, D, seed=7)
+    scale = 1 / math.sqrt(D)
+    ref = A.paged_attention_ref(q, kc, vc, meta, scale).reshape(q.shape[0], -1)
+    for code in (4, 5):
+        m = _to(meta, dev)
+        m.extra = {"prefill_nw": code}
+        close(A.paged_attention(q.to(dev), kc.to(dev), vc.to(dev), m, scale), ref, 2e-2)
 
 
 @pytest.mark.parametrize("nsplit_len", [(1, 0), (4, 64), (8, 128)])
