@@ -15,15 +15,19 @@ One timed step = one batch of B RAG queries per GPU, end to end:
   blocks (reference synthesize(), agent_graph.py:448-476) -> Qwen2-7B
   prefill + decode of gen_len tokens with the reference worker's sampling
   (temperature 0.4, top_p 0.8, repetition_penalty 1.2; qwen_llm.py:107-113).
-The server runs at saturation: `--inflight` D batches are in flight at once,
-staggered by gen_len/D tokens (a fill phase before the warmup sets this up),
-so one step = submit a new batch of B queries, then run the engine until the
-OLDEST in-flight batch has completed all gen_len tokens; exactly B queries
-complete per step and every timed step does the same work (one batch's
-retrieval + prefill, gen_len/D decode tokens for each of the D batches).  The
-engine prefills new arrivals first, then decodes all D*B live sequences in one
-batch (decode is weight-bandwidth bound, so D*B rows cost little more than B).
---inflight 1 is the closed-batch mode (submit B, finish B).
+The server runs at saturation with a continuous arrival stream (closed loop,
+the engine stepping on its own thread as in the service): queries
+arrive in groups of u = B/A (`--arrival-groups` A), and U = D*A groups are in
+flight at once (`--inflight` D batches' worth), staggered by gen_len/U
+generated tokens (a fill phase before the warmup sets this up).  One step =
+A times {a group of u queries arrives (embed + search + prompt) and is handed
+to the engine; the engine runs until the OLDEST in-flight group has all
+gen_len tokens}.  Exactly B queries complete per step and every timed step
+does the same work (B queries' retrieval + prefill, gen_len/U decode tokens
+per in-flight group per sub-step).  The engine prefills new arrivals first
+(chunked prefill), then decodes all live sequences in one batch (decode is
+weight-bandwidth bound, so D*B rows cost little more than B).
+--inflight 1 --arrival-groups 1 is the closed-batch mode (submit B, finish B).
 Scaling is weak (B queries per GPU fixed).  `value` = total queries/s over
 all ranks (B * N / max-over-ranks step time).  p50 TTFT = submission -> first
 generated token per query (over the queries completed in the timed steps).  The ingest phase (split -> LLM summary+keywords ->
@@ -53,11 +57,12 @@ def parse():
     ap.add_argument("--nlist", type=int, default=4096)
     ap.add_argument("--nprobe", type=int, default=32)
     ap.add_argument("--batch", type=int, default=64, help="queries per GPU per step")
-    ap.add_argument("--inflight", type=int, default=2, help="staggered batches in flight (1 = closed batch)")
+    ap.add_argument("--inflight", type=int, default=2, help="batches' worth of queries in flight (1 = closed batch)")
+    ap.add_argument("--arrival-groups", type=int, default=8, help="queries of a step arrive in this many groups")
     ap.add_argument("--prompt-len", type=int, default=1024)
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--top-k", type=int, default=10)
-    ap.add_argument("--ingest-files", type=int, default=48)
+    ap.add_argument("--ingest-files", type=int, default=192, help="source files in the synthetic repo to ingest")
     ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--out", default=None)
@@ -109,6 +114,12 @@ def main():
 
     max_len = args.prompt_len + args.gen_len + 64
     D = max(1, min(args.inflight, args.gen_len))
+    A = max(1, min(args.arrival_groups, args.batch, max(1, args.gen_len // D)))
+    while args.batch % A:
+        A -= 1
+    U = D * A  # groups in flight
+    u = args.batch // A  # queries per group
+    stagger = max(1, args.gen_len // U)
     eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max(args.batch * D, 8), max_num_batched_tokens=16384,
                                              max_model_len=max_len, use_cuda_graph=not args.no_graph,
                                              seed=rank))
@@ -121,11 +132,17 @@ def main():
     qcounter = [rank * 1_000_000]
     phase = {"embed": 0.0, "search": 0.0, "prompt": 0.0, "generate": 0.0}
 
-    inflight = collections.deque()  # (request ids, submission time), oldest first
+    # The engine runs on its own thread (engine/runner.py, the serving
+    # architecture): retrieval + prompt building of a new group overlaps the
+    # engine's decode of the groups already in flight.
+    from githubrepostorag_amd.engine.runner import EngineRunner
+
+    runner = EngineRunner(eng, watchdog_s=0)
+    inflight = collections.deque()  # groups, oldest first: (handles, submission time)
 
     def submit():
-        """Retrieve + build prompts for a new batch of B RAG queries and hand them to the engine."""
-        B = args.batch
+        """Retrieve + build prompts for a new group of u RAG queries and hand them to the engine."""
+        B = u
         t_sub = time.perf_counter()
         qs = [synthetic.question(qcounter[0] + i) for i in range(B)]
         qcounter[0] += B
@@ -145,34 +162,37 @@ def main():
                 else pid[-args.prompt_len:]
             prompts.append(pid)
         t_p = time.perf_counter()
-        inflight.append(([eng.add_request(p, sp) for p in prompts], t_sub))
+        inflight.append(([runner.submit(p, sp) for p in prompts], t_sub))
         for k, v in (("embed", t_e - t_sub), ("search", t_s - t_e), ("prompt", t_p - t_s)):
             phase[k] += v
 
-    def run_until(rids, ntok):
-        t0 = time.perf_counter()
-        while any(len(eng.get(r).output_ids) < ntok and eng.get(r).finish_reason is None for r in rids):
-            eng.step()
-        phase["generate"] += time.perf_counter() - t0
+    def wait_tokens(handles, ntok):
+        """Block until every request of the group has >= ntok tokens (or finished)."""
+        while True:
+            if all(h.done.is_set() or len(getattr(eng.get(h.req_id), "output_ids", ())) >= ntok for h in handles):
+                return
+            time.sleep(0.0005)
 
     def run_step():
-        """Submit one batch, complete the oldest; returns the completed queries' TTFTs (s)."""
-        submit()
-        rids, t_sub = inflight.popleft()
-        run_until(rids, args.gen_len)
+        """A groups arrive, the A oldest complete; returns the completed queries' TTFTs (s)."""
         ttft = []
-        for r in rids:
-            s = eng.pop(r)
-            ttft.append(s.first_token_time - t_sub)
-            assert len(s.output_ids) == args.gen_len, (len(s.output_ids), s.finish_reason)
+        for _ in range(A):
+            submit()
+            handles, t_sub = inflight.popleft()
+            t0 = time.perf_counter()
+            for h in handles:
+                c = h.wait(600)
+                assert len(c.token_ids) == args.gen_len, (len(c.token_ids), c.finish_reason)
+                ttft.append(c.first_token_at - t_sub)
+            phase["generate"] += time.perf_counter() - t0
         return ttft
 
-    # pipeline fill: D-1 batches staggered by gen_len / D tokens
-    for _ in range(D - 1):
+    # pipeline fill: U-1 groups staggered by gen_len / U tokens
+    for _ in range(U - 1):
         submit()
-        run_until(inflight[-1][0], args.gen_len // D)
+        wait_tokens(inflight[-1][0], stagger)
 
-    log(f"warmup ({D} batches in flight)")
+    log(f"warmup ({U} groups of {u} queries in flight)")
     for _ in range(args.warmup):
         run_step()
     comm.barrier()
@@ -201,10 +221,9 @@ def main():
     ms_step = elapsed / args.steps * 1000.0
 
     while inflight:  # drain the pipeline (untimed)
-        rids, _ = inflight.popleft()
-        run_until(rids, args.gen_len)
-        for r in rids:
-            eng.pop(r)
+        for h in inflight.popleft()[0]:
+            h.wait(600)
+    runner.shutdown()
     log(f"serving: {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms, {ms_step:.1f} ms/step")
     eng_stats = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()}
     nstep = args.steps + args.warmup
@@ -251,6 +270,7 @@ def main():
                          f"(nlist={args.nlist}, nprobe={args.nprobe}) sharded dp{world}",
                 "global_batch": args.batch * world,
                 "inflight_batches": D,
+                "arrival_groups": A,
                 "concurrent_seqs": args.batch * D * world,
                 "seq_len": args.prompt_len,
                 "gen_len": args.gen_len,

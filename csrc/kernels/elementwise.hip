@@ -93,20 +93,30 @@ __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
 }
 
 // out[t, i] = silu(gu[t, i]) * gu[t, I + i]
+// grid (ceil(I/8 / 256), ceil(T / kSiluRows)): a thread owns one 16-B column
+// vector and walks kSiluRows token rows (unrolled, so 8 row loads are in
+// flight per thread); 32-bit indexing only (the grid-stride form spent most of
+// its issue slots on 64-bit div/mod).
+constexpr int kSiluRows = 8;
 __global__ __launch_bounds__(kThreads) void silu_mul_kernel(const bf16* __restrict__ gu,
                                                             bf16* __restrict__ out, int T, int I) {
   const int nvec = I >> 3;
-  const size_t total = (size_t)T * nvec;
-  for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
-       i += (size_t)gridDim.x * kThreads) {
-    const int t = (int)(i / nvec), v = (int)(i % nvec);
-    const bf16* r = gu + (size_t)t * 2 * I;
+  const int v = blockIdx.x * kThreads + threadIdx.x;
+  if (v >= nvec) return;
+  const int t0 = blockIdx.y * kSiluRows;
+  const int t1 = min(T, t0 + kSiluRows);
+  const bf16x8_t* src = reinterpret_cast<const bf16x8_t*>(gu) + (size_t)t0 * 2 * nvec + v;
+  bf16x8_t* dst = reinterpret_cast<bf16x8_t*>(out) + (size_t)t0 * nvec + v;
+#pragma unroll 4
+  for (int t = t0; t < t1; ++t) {
     float g[8], u[8], o[8];
-    unpack8(reinterpret_cast<const bf16x8_t*>(r)[v], g);
-    unpack8(reinterpret_cast<const bf16x8_t*>(r + I)[v], u);
+    unpack8(src[0], g);
+    unpack8(src[nvec], u);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = silu(g[j]) * u[j];
-    reinterpret_cast<bf16x8_t*>(out + (size_t)t * I)[v] = pack8(o);
+    for (int j = 0; j < 8; ++j) o[j] = g[j] * __builtin_amdgcn_rcpf(1.f + __expf(-g[j])) * u[j];
+    dst[0] = pack8(o);
+    src += 2 * nvec;
+    dst += nvec;
   }
 }
 
@@ -227,8 +237,8 @@ GRAG_API int grag_qkv_rope_kvstore(const void* qkv, int ld, const void* bias,
 GRAG_API int grag_silu_mul(const void* gu, void* out, int T, int I, hipStream_t stream) {
   if (T <= 0) return 0;
   if (I % 8 != 0) return (int)hipErrorInvalidValue;
-  silu_mul_kernel<<<grid_for((size_t)T * I / 8), kThreads, 0, stream>>>((const bf16*)gu,
-                                                                         (bf16*)out, T, I);
+  dim3 grid((I / 8 + kThreads - 1) / kThreads, (T + kSiluRows - 1) / kSiluRows);
+  silu_mul_kernel<<<grid, kThreads, 0, stream>>>((const bf16*)gu, (bf16*)out, T, I);
   return (int)hipGetLastError();
 }
 

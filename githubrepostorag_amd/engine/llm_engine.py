@@ -169,7 +169,7 @@ class LLMEngine:
     def completion(self, seq: Sequence) -> Completion:
         return Completion(seq.req_id, seq.text, list(seq.output_ids), seq.finish_reason, len(seq.prompt_ids),
                           seq.ttft, None if seq.finish_time is None else seq.finish_time - seq.arrival,
-                          seq.cached_prefix)
+                          seq.cached_prefix, seq.first_token_time)
 
     # ------------------------------------------------------------------ step
     @torch.inference_mode()
@@ -422,7 +422,9 @@ class LLMEngine:
                 self._decode_forward(v, B, nsplit, split_len, out, K)
         torch.cuda.current_stream().wait_stream(s)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, pool=self._graph_pool):
+        # thread_local: API / retrieval threads keep launching (and syncing) on
+        # their own streams while the engine thread captures
+        with torch.cuda.graph(graph, pool=self._graph_pool, capture_error_mode="thread_local"):
             self._decode_forward(v, B, nsplit, split_len, out, K)
         torch.cuda.synchronize()
         self.sampler.rng.copy_(rng_save)

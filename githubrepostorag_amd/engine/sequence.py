@@ -82,3 +82,4 @@ class Completion:
     ttft_s: float | None
     latency_s: float | None
     cached_tokens: int = 0
+    first_token_at: float | None = None  # time.perf_counter() stamp of the first generated token

@@ -109,6 +109,25 @@ def attn_prefill_bench(nseq, L):
     return r
 
 
+def elementwise_bench():
+    """Prefill-size elementwise kernels: GB/s of silu_mul and fused add+RMSNorm."""
+    from githubrepostorag_amd.ops import elementwise as E
+    from githubrepostorag_amd.ops.norm import rmsnorm
+
+    dev = torch.device("cuda")
+    T, I, H = 14336, 18944, 3584
+    gu = torch.randn(T, 2 * I, device=dev, dtype=torch.bfloat16)
+    x = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
+    res = torch.randn(T, H, device=dev, dtype=torch.bfloat16)
+    w = torch.ones(H, device=dev, dtype=torch.bfloat16)
+    r = rounds({"silu_mul": lambda: E.silu_mul(gu), "add_rmsnorm": lambda: rmsnorm(x, w, 1e-6, residual=res)},
+               n=3, iters=10)
+    nbytes = {"silu_mul": T * I * 2 * 3, "add_rmsnorm": T * H * 2 * 4}
+    for k in r:
+        r[k]["GB_s"] = round(nbytes[k] / (r[k]["min_us"] * 1e-6) / 1e9, 1)
+    return r
+
+
 def sampler_bench(B):
     dev = torch.device("cuda")
     V = 152064
@@ -141,6 +160,8 @@ if __name__ == "__main__":
     if args.what == "prefill":
         res["prefill_16x1024"] = attn_prefill_bench(16, 1024)
         res["prefill_4x4096"] = attn_prefill_bench(4, 4096)
+    if args.what in ("all", "elementwise"):
+        res["elementwise_T14336"] = elementwise_bench()
     if args.what in ("all", "sampler"):
         res["sampler_B64"] = sampler_bench(64)
     print(json.dumps(res, indent=1))
