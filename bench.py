@@ -15,8 +15,7 @@ One timed step = one batch of B RAG queries per GPU, end to end:
   blocks (reference synthesize(), agent_graph.py:448-476) -> Qwen2-7B
   prefill + decode of gen_len tokens with the reference worker's sampling
   (temperature 0.4, top_p 0.8, repetition_penalty 1.2; qwen_llm.py:107-113).
-The server runs at saturation with a continuous arrival stream (closed loop,
-the engine stepping on its own thread as in the service): queries
+The server runs at saturation with a continuous arrival stream: queries
 arrive in groups of u = B/A (`--arrival-groups` A), and U = D*A groups are in
 flight at once (`--inflight` D batches' worth), staggered by gen_len/U
 generated tokens (a fill phase before the warmup sets this up).  One step =
@@ -132,13 +131,10 @@ def main():
     qcounter = [rank * 1_000_000]
     phase = {"embed": 0.0, "search": 0.0, "prompt": 0.0, "generate": 0.0}
 
-    # The engine runs on its own thread (engine/runner.py, the serving
-    # architecture): retrieval + prompt building of a new group overlaps the
-    # engine's decode of the groups already in flight.
-    from githubrepostorag_amd.engine.runner import EngineRunner
-
-    runner = EngineRunner(eng, watchdog_s=0)
-    inflight = collections.deque()  # groups, oldest first: (handles, submission time)
+    # The engine is stepped from this thread between arrivals: a thread per
+    # engine (engine/runner.py, as in the service) measured slower here
+    # (prefill fragmented by per-request hand-off, shorter decode windows).
+    inflight = collections.deque()  # groups, oldest first: (request ids, submission time)
 
     def submit():
         """Retrieve + build prompts for a new group of u RAG queries and hand them to the engine."""
@@ -162,35 +158,33 @@ def main():
                 else pid[-args.prompt_len:]
             prompts.append(pid)
         t_p = time.perf_counter()
-        inflight.append(([runner.submit(p, sp) for p in prompts], t_sub))
+        inflight.append(([eng.add_request(p, sp) for p in prompts], t_sub))
         for k, v in (("embed", t_e - t_sub), ("search", t_s - t_e), ("prompt", t_p - t_s)):
             phase[k] += v
 
-    def wait_tokens(handles, ntok):
-        """Block until every request of the group has >= ntok tokens (or finished)."""
-        while True:
-            if all(h.done.is_set() or len(getattr(eng.get(h.req_id), "output_ids", ())) >= ntok for h in handles):
-                return
-            time.sleep(0.0005)
+    def run_until(rids, ntok):
+        t0 = time.perf_counter()
+        while any(len(eng.get(r).output_ids) < ntok and eng.get(r).finish_reason is None for r in rids):
+            eng.step()
+        phase["generate"] += time.perf_counter() - t0
 
     def run_step():
         """A groups arrive, the A oldest complete; returns the completed queries' TTFTs (s)."""
         ttft = []
         for _ in range(A):
             submit()
-            handles, t_sub = inflight.popleft()
-            t0 = time.perf_counter()
-            for h in handles:
-                c = h.wait(600)
-                assert len(c.token_ids) == args.gen_len, (len(c.token_ids), c.finish_reason)
-                ttft.append(c.first_token_at - t_sub)
-            phase["generate"] += time.perf_counter() - t0
+            rids, t_sub = inflight.popleft()
+            run_until(rids, args.gen_len)
+            for r in rids:
+                s = eng.pop(r)
+                ttft.append(s.first_token_time - t_sub)
+                assert len(s.output_ids) == args.gen_len, (len(s.output_ids), s.finish_reason)
         return ttft
 
     # pipeline fill: U-1 groups staggered by gen_len / U tokens
     for _ in range(U - 1):
         submit()
-        wait_tokens(inflight[-1][0], stagger)
+        run_until(inflight[-1][0], stagger)
 
     log(f"warmup ({U} groups of {u} queries in flight)")
     for _ in range(args.warmup):
@@ -198,12 +192,16 @@ def main():
     comm.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    for k in phase:  # phase breakdown over the timed steps only
+        phase[k] = 0.0
+    stats0 = dict(eng.stats)
     t_start = time.perf_counter()
     ttfts = []
     for _ in range(args.steps):
         ttfts += run_step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    stats1 = dict(eng.stats)
     comm.barrier()
     elapsed = time.perf_counter() - t_start
     ttfts_all = [ttfts]
@@ -221,13 +219,15 @@ def main():
     ms_step = elapsed / args.steps * 1000.0
 
     while inflight:  # drain the pipeline (untimed)
-        for h in inflight.popleft()[0]:
-            h.wait(600)
-    runner.shutdown()
+        rids, _ = inflight.popleft()
+        run_until(rids, args.gen_len)
+        for r in rids:
+            eng.pop(r)
     log(f"serving: {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms, {ms_step:.1f} ms/step")
     eng_stats = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()}
-    nstep = args.steps + args.warmup
-    log("per-step phases (ms, incl. warmup): " + ", ".join(f"{k}={v / nstep * 1000:.1f}" for k, v in phase.items()))
+    log("per-step phases (ms, timed steps): " + ", ".join(f"{k}={v / args.steps * 1000:.1f}" for k, v in phase.items()))
+    timed_engine = {k: round((v - stats0.get(k, 0)) / args.steps, 4) for k, v in stats1.items()
+                    if isinstance(v, (int, float))}
 
     # ---- ingest phase (reported separately)
     ingest_dps = None
@@ -278,6 +278,8 @@ def main():
                 "parallelism": f"dp{world}",
             },
             "engine": eng_stats,
+            "engine_per_timed_step": timed_engine,
+            "phase_ms_per_step": {k: round(v / args.steps * 1000, 2) for k, v in phase.items()},
             "ingest_stage_s": ingest_stages,
         }
         line = json.dumps(res)

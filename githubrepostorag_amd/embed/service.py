@@ -10,6 +10,7 @@ import threading
 import torch
 
 from ..engine.tokenizer import WordPieceTokenizer
+from ..utils.gpu_guard import guarded
 from ..models.configs import EncoderConfig, encoder_config
 from ..models.encoder import BertEncoder
 
@@ -35,6 +36,7 @@ class Embedder:
         L = min(self.cfg.max_seq_length, self.cfg.max_position)
         return [self.tok.encode(prefix + (t or ""), L) for t in texts]
 
+    @guarded
     @torch.inference_mode()
     def embed_ids(self, ids: list[list[int]]) -> torch.Tensor:
         """-> bf16 [n, d] L2-normalised on the encoder's device (input order)."""

@@ -32,6 +32,7 @@ from ..ops.attention import KV_TILE, AttnMetadata
 from ..ops.sampling import SamplerState, sample
 from .scheduler import KVCacheManager, Scheduler
 from .sequence import Completion, SamplingParams, Sequence, SeqStatus
+from ..utils.gpu_guard import gpu_guard
 from .tokenizer import IncrementalDetokenizer
 
 log = logging.getLogger(__name__)
@@ -406,6 +407,10 @@ class LLMEngine:
             self._graph_pool = torch.cuda.graph_pool_handle()
 
     def _capture(self, B, nsplit, split_len, K=1) -> _DecodeGraph:
+        with gpu_guard():  # no other thread may sync / allocate while the capture is open
+            return self._capture_locked(B, nsplit, split_len, K)
+
+    def _capture_locked(self, B, nsplit, split_len, K=1) -> _DecodeGraph:
         self._ensure_static()
         W = self.max_blocks_per_seq
         # a benign batch: every row is a padding row (scratch block, scratch slot)

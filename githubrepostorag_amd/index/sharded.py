@@ -18,6 +18,7 @@ import torch
 
 from ..ops.topk import score_topk
 from ..parallel.comm import Group
+from ..utils.gpu_guard import guarded
 from .ivf import IVFIndex
 
 
@@ -58,6 +59,7 @@ class ShardedIndex:
             s, i = score_topk(self.flat, Q.to(self.device, torch.bfloat16), k)
         return s.float(), self.global_ids(i)
 
+    @guarded
     @torch.inference_mode()
     def search(self, Q: torch.Tensor, k: int):
         """This rank's queries Q [nq, d] -> global top-k (scores fp32, ids int64)."""

@@ -30,6 +30,7 @@ import numpy as np
 import torch
 
 from ..ops.topk import OP_BITAND, OP_EQ, Predicate, score_topk
+from ..utils.gpu_guard import guarded
 
 SCOPES = ("catalog", "repo", "module", "file", "chunk")
 DEFAULT_TABLES = {"catalog": "embeddings_catalog", "repo": "embeddings_repo", "module": "embeddings_module",
@@ -117,6 +118,7 @@ class VectorTable:
                 words[r >> 5] &= np.uint32(~(1 << (r & 31)) & 0xFFFFFFFF)
         self.live.copy_(torch.from_numpy(words.view(np.int32)).to(self.device))
 
+    @guarded
     def upsert(self, row_ids: list[str], texts: list[str], vectors: torch.Tensor, metadatas: list[dict]) -> int:
         """Insert or overwrite rows keyed by row_id. vectors [n, d] (any float
         dtype; normalised here).  Returns the number of new rows."""
@@ -158,6 +160,7 @@ class VectorTable:
             self._set_live(rows, True)
             return new
 
+    @guarded
     def delete(self, row_ids: list[str]) -> int:
         with self.lock:
             rows = np.asarray([self.key_to_row[r] for r in row_ids if r in self.key_to_row], dtype=np.int64)
@@ -207,6 +210,7 @@ class VectorTable:
         return True
 
     # ------------------------------------------------------------------ search
+    @guarded
     def search(self, qvecs: torch.Tensor, k: int, flt: dict | None = None, qpred=None) -> list[list[Hit]]:
         """Batched filtered top-k by cosine. qvecs [nq, d]."""
         nq = qvecs.shape[0]

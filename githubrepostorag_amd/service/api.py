@@ -27,6 +27,7 @@ from fastapi.middleware.cors import CORSMiddleware
 from fastapi.staticfiles import StaticFiles
 from starlette.responses import StreamingResponse
 
+from ..utils.gpu_guard import gpu_guard
 from . import metrics as M
 from .events import CancelFlags, EventLog
 from .health import _get_app_start_time, register_health_endpoints
@@ -217,7 +218,11 @@ def create_app(state: APIState | None = None, runtime_factory=None) -> FastAPI:
             raise HTTPException(503, "runtime not ready")
         texts = [body.input] if isinstance(body.input, str) else list(body.input)
         loop = asyncio.get_running_loop()
-        vecs = await loop.run_in_executor(None, lambda: rt.embedder.embed_documents(texts).float().cpu().tolist())
+        def _embed():
+            with gpu_guard():  # the .cpu() sync must not land inside an engine graph capture
+                return rt.embedder.embed_documents(texts).float().cpu().tolist()
+
+        vecs = await loop.run_in_executor(None, _embed)
         return {"object": "list", "model": rt.settings.embed_model,
                 "data": [{"object": "embedding", "index": i, "embedding": v} for i, v in enumerate(vecs)]}
 
