@@ -17,6 +17,13 @@ __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); 
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
 }
+// GPT-2 "gelu_new": 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3))),
+// tanh(u) = 1 - 2 / (1 + exp(2u)) (saturates correctly at +-inf)
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u));
+  return 0.5f * x * (1.f + t);
+}
 
 // One block per token.  Work units (16 B each):
 //   [0, (Hq+Hkv)*D/16)           rotary units: 8 pairs (i..i+7, i+D/2..i+D/2+7)
@@ -34,7 +41,9 @@ __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
   const bf16* row = qkv + (size_t)t * ld;
   const int pos = positions[t];
   const int slot = slot_mapping ? slot_mapping[t] : -1;
-  const float* cs = cos_sin + (size_t)pos * D;
+  // cos_sin == nullptr: no rotary (absolute-position decoders, GPT-2) — the
+  // kernel is then the fused bias add + q split + paged K/V store
+  const float* cs = cos_sin ? cos_sin + (size_t)pos * D : nullptr;
   const int blk = slot >= 0 ? slot / BS : 0;
   const int off = slot >= 0 ? slot % BS : 0;
   for (int u = threadIdx.x; u < n_rot + n_v; u += kThreads) {
@@ -57,11 +66,19 @@ __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
         }
       }
       float o1[8], o2[8];
+      if (cs) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float c = cs[i0 + j], s = cs[half + i0 + j];
-        o1[j] = x1[j] * c - x2[j] * s;
-        o2[j] = x2[j] * c + x1[j] * s;
+        for (int j = 0; j < 8; ++j) {
+          const float c = cs[i0 + j], s = cs[half + i0 + j];
+          o1[j] = x1[j] * c - x2[j] * s;
+          o2[j] = x2[j] * c + x1[j] * s;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          o1[j] = x1[j];
+          o2[j] = x2[j];
+        }
       }
       if (head < Hq) {
         bf16* qo = q_out + ((size_t)t * Hq + head) * D + i0;
@@ -120,7 +137,7 @@ __global__ __launch_bounds__(kThreads) void silu_mul_kernel(const bf16* __restri
   }
 }
 
-// y = act(x + b); act 0 = identity, 1 = gelu(erf), 2 = silu.  In place allowed.
+// y = act(x + b); act 0 = identity, 1 = gelu(erf), 2 = silu, 3 = gelu(tanh).  In place allowed.
 __global__ __launch_bounds__(kThreads) void bias_act_kernel(const bf16* __restrict__ x,
                                                             const bf16* __restrict__ b,
                                                             bf16* __restrict__ y, int T, int N,
@@ -143,6 +160,9 @@ __global__ __launch_bounds__(kThreads) void bias_act_kernel(const bf16* __restri
     } else if (act == 2) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) a[j] = silu(a[j]);
+    } else if (act == 3) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = gelu_tanh(a[j]);
     }
     reinterpret_cast<bf16x8_t*>(y)[i] = pack8(a);
   }

@@ -70,18 +70,21 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_kernel(
   }
 }
 
-// y = LN(x [+ bias] [+ residual]) * gamma + beta
-template <int VPT>
+// y = LN(x [+ bias] [+ residual]) * gamma + beta.
+// WRITEBACK (pre-LN decoders, GPT-2): the bf16-rounded sum x + bias + residual
+// is stored back into `residual` (the residual stream) before it is
+// normalised, so a pre-LN block boundary is one pass over the row:
+// residual += h + b ; y = LN(residual).
+template <int VPT, bool WRITEBACK>
 __global__ __launch_bounds__(kThreads) void layernorm_kernel(
-    const bf16* __restrict__ x, const bf16* __restrict__ bias, const bf16* __restrict__ residual,
+    const bf16* __restrict__ x, const bf16* __restrict__ bias, bf16* __restrict__ residual,
     const bf16* __restrict__ gamma, const bf16* __restrict__ beta, bf16* __restrict__ out, int H,
     float eps) {
   __shared__ float red[kThreads / 64];
   const int row = blockIdx.x;
   const int nvec = H >> 3;
   const bf16x8_t* xr = reinterpret_cast<const bf16x8_t*>(x + (size_t)row * H);
-  const bf16x8_t* rr =
-      residual ? reinterpret_cast<const bf16x8_t*>(residual + (size_t)row * H) : nullptr;
+  bf16x8_t* rr = residual ? reinterpret_cast<bf16x8_t*>(residual + (size_t)row * H) : nullptr;
   const bf16x8_t* br = bias ? reinterpret_cast<const bf16x8_t*>(bias) : nullptr;
   float v[VPT][8];
   float s = 0.f;
@@ -103,6 +106,11 @@ __global__ __launch_bounds__(kThreads) void layernorm_kernel(
         unpack8(rr[idx], b);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[i][j] += b[j];
+        if (WRITEBACK) {  // the stream is bf16: normalise the rounded sum
+          const bf16x8_t sum = pack8(v[i]);
+          rr[idx] = sum;
+          unpack8(sum, v[i]);
+        }
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[i][j];
@@ -243,22 +251,38 @@ GRAG_API int grag_rmsnorm(const void* x, void* residual, const void* w, void* ou
   return (int)hipGetLastError();
 }
 
-GRAG_API int grag_layernorm(const void* x, const void* bias, const void* residual,
-                            const void* gamma, const void* beta, void* out, int T, int H,
-                            float eps, hipStream_t stream) {
+template <bool WB>
+static int launch_layernorm(const void* x, const void* bias, void* residual, const void* gamma,
+                            const void* beta, void* out, int T, int H, float eps,
+                            hipStream_t stream) {
   if (T <= 0) return 0;
   if (H % 8 != 0 || H > 8 * 8 * kThreads) return (int)hipErrorInvalidValue;
   auto args = [&](auto kern) {
-    kern<<<T, kThreads, 0, stream>>>((const bf16*)x, (const bf16*)bias, (const bf16*)residual,
+    kern<<<T, kThreads, 0, stream>>>((const bf16*)x, (const bf16*)bias, (bf16*)residual,
                                      (const bf16*)gamma, (const bf16*)beta, (bf16*)out, H, eps);
   };
   switch (vpt_for(H)) {
-    case 1: args(layernorm_kernel<1>); break;
-    case 2: args(layernorm_kernel<2>); break;
-    case 4: args(layernorm_kernel<4>); break;
-    default: args(layernorm_kernel<8>); break;
+    case 1: args(layernorm_kernel<1, WB>); break;
+    case 2: args(layernorm_kernel<2, WB>); break;
+    case 4: args(layernorm_kernel<4, WB>); break;
+    default: args(layernorm_kernel<8, WB>); break;
   }
   return (int)hipGetLastError();
+}
+
+GRAG_API int grag_layernorm(const void* x, const void* bias, const void* residual,
+                            const void* gamma, const void* beta, void* out, int T, int H,
+                            float eps, hipStream_t stream) {
+  return launch_layernorm<false>(x, bias, const_cast<void*>(residual), gamma, beta, out, T, H, eps,
+                                 stream);
+}
+
+// Pre-LN block boundary: residual += x (+ bias), out = LN(residual).
+GRAG_API int grag_add_layernorm(const void* x, const void* bias, void* residual,
+                                const void* gamma, const void* beta, void* out, int T, int H,
+                                float eps, hipStream_t stream) {
+  if (residual == nullptr) return (int)hipErrorInvalidValue;
+  return launch_layernorm<true>(x, bias, residual, gamma, beta, out, T, H, eps, stream);
 }
 
 GRAG_API int grag_bert_embed_ln(const int32_t* ids, const int32_t* pos_ids,

@@ -229,14 +229,28 @@ def chatml(messages: list[dict], add_generation_prompt: bool = True, enable_thin
     return "".join(parts)
 
 
-def load_tokenizer(model_dir: str | None, model_vocab_size: int):
+def plain_template(messages: list[dict], add_generation_prompt: bool = True, enable_thinking: bool | None = None) -> str:
+    """Prompt layout for base LMs without chat special tokens (GPT-2):
+    ``Role: content`` turns separated by blank lines, ending in ``Assistant:``."""
+    parts = [f"{m['role'].capitalize()}: {m['content']}\n\n" for m in messages]
+    if add_generation_prompt:
+        parts.append("Assistant:")
+    return "".join(parts)
+
+
+def load_tokenizer(model_dir: str | None, model_vocab_size: int, arch: str = "qwen2"):
     if model_dir and (Path(model_dir) / "tokenizer.json").exists():
-        return HFTokenizer(model_dir)
-    cache = os.environ.get("GRAG_BPE_MERGES")
-    if cache and Path(cache).exists():
-        pairs = [tuple(map(int, ln.split())) for ln in Path(cache).read_text().splitlines() if ln.strip()]
-        return ByteBPETokenizer(model_vocab_size, merges=pairs)
-    return ByteBPETokenizer(model_vocab_size)
+        tok = HFTokenizer(model_dir)
+    else:
+        cache = os.environ.get("GRAG_BPE_MERGES")
+        if cache and Path(cache).exists():
+            pairs = [tuple(map(int, ln.split())) for ln in Path(cache).read_text().splitlines() if ln.strip()]
+            tok = ByteBPETokenizer(model_vocab_size, merges=pairs)
+        else:
+            tok = ByteBPETokenizer(model_vocab_size)
+    if arch == "gpt2":  # base LM: no ChatML tokens; <|endoftext|> ends generation
+        tok.apply_chat_template = plain_template
+    return tok
 
 
 class WordPieceTokenizer:

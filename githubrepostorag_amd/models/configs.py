@@ -30,12 +30,19 @@ class DecoderConfig:
     def to_dict(self):
         return asdict(self)
 
+    @property
+    def norm_eps(self) -> float:
+        return self.rms_norm_eps
+
     def param_count(self) -> int:
         H, I, L = self.hidden_size, self.intermediate_size, self.num_layers
         q = self.num_heads * self.head_dim
         kv = self.num_kv_heads * self.head_dim
-        per_layer = H * (q + 2 * kv) + (q + 2 * kv) + q * H + 3 * H * I + 2 * H
         emb = self.vocab_size * H * (1 if self.tie_word_embeddings else 2)
+        if self.arch == "gpt2":  # LN(w,b) x2, qkv+bias, o+bias, fc+bias, proj+bias; learned positions
+            per_layer = 4 * H + H * 3 * q + 3 * q + q * H + H + 2 * H * I + I + H
+            return L * per_layer + emb + self.max_position * H + 2 * H
+        per_layer = H * (q + 2 * kv) + (q + 2 * kv) + q * H + 3 * H * I + 2 * H
         return L * per_layer + emb + H
 
 
@@ -75,6 +82,15 @@ DECODERS = {
     # tiny configs for tests / CPU plumbing
     "qwen2-tiny": DecoderConfig("qwen2-tiny", 512, 256, 512, 2, 4, 2, 64, max_position=4096),
     "qwen2-small": DecoderConfig("qwen2-small", 4096, 512, 1408, 4, 8, 2, 64, max_position=8192),
+    # GPT-2 family (BASELINE config 1: "GPT-2-small greedy answer"): pre-LN,
+    # learned absolute positions, GELU(tanh) MLP, MHA, tied LM head
+    "gpt2": DecoderConfig("gpt2", 50257, 768, 3072, 12, 12, 12, 64, 1e-5, 0.0, 1024, True, True, "gpt2"),
+    "gpt2-medium": DecoderConfig("gpt2-medium", 50257, 1024, 4096, 24, 16, 16, 64, 1e-5, 0.0, 1024, True, True,
+                                 "gpt2"),
+    "gpt2-large": DecoderConfig("gpt2-large", 50257, 1280, 5120, 36, 20, 20, 64, 1e-5, 0.0, 1024, True, True,
+                                "gpt2"),
+    "gpt2-xl": DecoderConfig("gpt2-xl", 50257, 1600, 6400, 48, 25, 25, 64, 1e-5, 0.0, 1024, True, True, "gpt2"),
+    "gpt2-tiny": DecoderConfig("gpt2-tiny", 512, 256, 1024, 2, 4, 4, 64, 1e-5, 0.0, 512, True, True, "gpt2"),
 }
 
 ENCODERS = {
@@ -103,6 +119,9 @@ ALIASES = {
     "qwen/qwen2-7b-instruct": "qwen2-7b",
     "qwen/qwen2-1.5b": "qwen2-1.5b",
     "qwen/qwen2-72b": "qwen2-72b",
+    "openai-community/gpt2": "gpt2",
+    "openai-community/gpt2-medium": "gpt2-medium",
+    "gpt2-small": "gpt2",
     "sentence-transformers/all-minilm-l6-v2": "all-minilm-l6-v2",
     "intfloat/e5-small-v2": "e5-small-v2",
     "baai/bge-base-en-v1.5": "bge-base-en-v1.5",

@@ -29,6 +29,7 @@ F = ctypes.c_float
 _SIGS = {
     "grag_rmsnorm": [P, P, P, P, I, I, F, P],
     "grag_layernorm": [P, P, P, P, P, P, I, I, F, P],
+    "grag_add_layernorm": [P, P, P, P, P, P, I, I, F, P],
     "grag_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, P],
     "grag_embed_gather": [P, P, P, I, I, P],
     "grag_qkv_rope_kvstore": [P, I, P, P, P, P, P, P, P, I, I, I, I, I, P],

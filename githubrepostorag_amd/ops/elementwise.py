@@ -8,7 +8,7 @@ import torch
 
 from ._lib import call, ptr
 
-ACT_NONE, ACT_GELU, ACT_SILU = 0, 1, 2
+ACT_NONE, ACT_GELU, ACT_SILU, ACT_GELU_TANH = 0, 1, 2, 3
 
 
 def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
@@ -27,14 +27,15 @@ def qkv_rope_kvstore_ref(qkv, bias, positions, cos_sin, slot_mapping, k_cache, v
     q = x[:, : Hq * D].view(T, Hq, D)
     k = x[:, Hq * D : (Hq + Hkv) * D].view(T, Hkv, D)
     v = x[:, (Hq + Hkv) * D : (Hq + 2 * Hkv) * D].view(T, Hkv, D)
-    cs = cos_sin[positions.long()]
-    cos, sin = cs[:, : D // 2].unsqueeze(1), cs[:, D // 2 :].unsqueeze(1)
+    if cos_sin is not None:  # None: no rotary (GPT-2 absolute positions)
+        cs = cos_sin[positions.long()]
+        cos, sin = cs[:, : D // 2].unsqueeze(1), cs[:, D // 2 :].unsqueeze(1)
 
-    def rot(t):
-        a, b = t[..., : D // 2], t[..., D // 2 :]
-        return torch.cat([a * cos - b * sin, b * cos + a * sin], dim=-1)
+        def rot(t):
+            a, b = t[..., : D // 2], t[..., D // 2 :]
+            return torch.cat([a * cos - b * sin, b * cos + a * sin], dim=-1)
 
-    q, k = rot(q), rot(k)
+        q, k = rot(q), rot(k)
     if slot_mapping is not None and k_cache is not None:
         BS = k_cache.shape[2]
         sm = slot_mapping.long()
@@ -46,8 +47,9 @@ def qkv_rope_kvstore_ref(qkv, bias, positions, cos_sin, slot_mapping, k_cache, v
 
 
 def qkv_rope_kvstore(qkv, bias, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D):
-    """Split packed QKV [T, (Hq+2Hkv)*D], add bias, apply NeoX RoPE to q/k,
-    return q [T, Hq, D] and scatter k/v into the paged caches [blocks, Hkv, BS, D]."""
+    """Split packed QKV [T, (Hq+2Hkv)*D], add bias, apply NeoX RoPE to q/k
+    (skipped when ``cos_sin`` is None), return q [T, Hq, D] and scatter k/v
+    into the paged caches [blocks, Hkv, BS, D]."""
     if not qkv.is_cuda:
         return qkv_rope_kvstore_ref(qkv, bias, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
     T = qkv.shape[0]
@@ -77,6 +79,8 @@ def bias_act(x: torch.Tensor, b: torch.Tensor | None, act: int, inplace: bool = 
             v = torch.nn.functional.gelu(v)
         elif act == ACT_SILU:
             v = torch.nn.functional.silu(v)
+        elif act == ACT_GELU_TANH:
+            v = torch.nn.functional.gelu(v, approximate="tanh")
         return v.to(x.dtype)
     x = x.contiguous()
     N = x.shape[-1]

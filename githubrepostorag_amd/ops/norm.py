@@ -55,6 +55,30 @@ def layernorm(x, gamma, beta, eps, bias=None, residual=None):
     return out
 
 
+def add_layernorm_ref(x, gamma, beta, eps, residual, bias=None):
+    v = x.float() + residual.float()
+    if bias is not None:
+        v = v + bias.float()
+    s = v.to(residual.dtype)
+    residual.copy_(s)
+    return torch.nn.functional.layer_norm(s.float(), (v.shape[-1],), gamma.float(), beta.float(),
+                                          eps).to(x.dtype)
+
+
+def add_layernorm(x, gamma, beta, eps, residual, bias=None):
+    """Pre-LN block boundary (GPT-2): ``residual += x [+ bias]`` in place, then
+    return LN(residual) * gamma + beta — one pass over the row."""
+    if not _on_gpu(x):
+        return add_layernorm_ref(x, gamma, beta, eps, residual, bias)
+    x = x.contiguous()
+    H = x.shape[-1]
+    T = x.numel() // H
+    out = torch.empty_like(x)
+    call("grag_add_layernorm", ptr(x), ptr(bias), ptr(residual), ptr(gamma), ptr(beta), ptr(out), T, H,
+         float(eps))
+    return out
+
+
 def bert_embed_ln_ref(ids, pos_ids, type_ids, word, pos, typ, gamma, beta, eps):
     v = word[ids.long()].float() + pos[pos_ids.long()].float()
     v = v + (typ[type_ids.long()].float() if type_ids is not None else typ[0].float())

@@ -20,7 +20,7 @@ from ..engine.tokenizer import WordPieceTokenizer, load_tokenizer
 from ..index.store import VectorStore
 from ..models.configs import decoder_config, encoder_config
 from ..models.encoder import BertEncoder
-from ..models.qwen2 import Qwen2Model
+from ..models import build_decoder
 from ..models.weights import load_state_dict
 from ..retrieval.graph import RetrieverFactory
 
@@ -55,8 +55,8 @@ class RAGRuntime:
         if llm is None and build_engine:
             dcfg = decoder_config(s.qwen_model)
             sd = load_state_dict(s.model_dir) if s.model_dir else None
-            model = Qwen2Model(dcfg, device=self.device, dtype=dtype, seed=s.seed + 1, state_dict=sd)
-            self.tokenizer = load_tokenizer(s.model_dir, dcfg.vocab_size)
+            model = build_decoder(dcfg, device=self.device, dtype=dtype, seed=s.seed + 1, state_dict=sd)
+            self.tokenizer = load_tokenizer(s.model_dir, dcfg.vocab_size, dcfg.arch)
             ecfg = EngineConfig(max_num_seqs=s.max_num_seqs, max_num_batched_tokens=s.max_num_batched_tokens,
                                 max_model_len=s.max_model_len, block_size=s.kv_block,
                                 kv_cache_gb=s.kv_cache_gb or None, use_cuda_graph=s.cuda_graphs,
