@@ -10,7 +10,7 @@ import threading
 import torch
 
 from ..engine.tokenizer import WordPieceTokenizer
-from ..utils.gpu_guard import guarded
+from ..utils.gpu_guard import guarded, side_stream
 from ..models.configs import EncoderConfig, encoder_config
 from ..models.encoder import BertEncoder
 
@@ -45,7 +45,7 @@ class Embedder:
         if n == 0:
             return out
         order = sorted(range(n), key=lambda i: len(ids[i]))
-        with self.lock:
+        with self.lock, side_stream(self.encoder.device):
             i = 0
             while i < n:
                 j, tok = i, 0

@@ -64,6 +64,17 @@ docker build -t rag-worker . && kubectl apply -f deployment.yaml
 """ * 4
 
 
+_LETTERS = b"etaoinshrdlucmfwypvbgkqjxz"
+
+
+def _synthetic_piece(i: int) -> bytes:
+    out = bytearray(b" ")
+    for _ in range(2 + i % 4):
+        out.append(_LETTERS[i % 26])
+        i //= 26
+    return bytes(out)
+
+
 class ByteBPETokenizer:
     def __init__(self, model_vocab_size: int, num_merges: int = 2000, corpus: str | None = None,
                  merges: list[tuple[int, int]] | None = None):
@@ -90,8 +101,15 @@ class ByteBPETokenizer:
         table = [b""] * max(model_vocab_size, max(self.special.values()) + 1)
         for i in range(256):
             table[i] = bytes([i])
-        for k, (a, b) in enumerate(self.merges()):
+        merges = self.merges()
+        for k, (a, b) in enumerate(merges):
             table[256 + k] = table[a] + table[b]
+        self._known = 256 + len(merges)
+        # ids the offline vocabulary does not cover (a random-init model with
+        # the real 152K vocab samples them all the time) still decode to text,
+        # as they would with the real tokenizer: a deterministic short word
+        for i in range(self._known, len(table)):
+            table[i] = _synthetic_piece(i)
         for tok, tid in self.special.items():
             table[tid] = tok.encode()
         self._table = table
@@ -126,6 +144,8 @@ class ByteBPETokenizer:
         arr = np.asarray(list(ids), dtype=np.int32)
         if arr.size == 0:
             return b""
+        if int(arr.max()) >= self._known:  # specials / ids outside the trained vocabulary
+            return b"".join(self.token_bytes(int(t)) for t in arr)
         cap = 16 * arr.size + 64
         buf = ctypes.create_string_buffer(cap)
         n = rt().grag_bpe_decode(self._h, arr.ctypes.data, arr.size, buf, cap)

@@ -30,7 +30,7 @@ import numpy as np
 import torch
 
 from ..ops.topk import OP_BITAND, OP_EQ, Predicate, score_topk
-from ..utils.gpu_guard import guarded
+from ..utils.gpu_guard import guarded, side_stream
 
 SCOPES = ("catalog", "repo", "module", "file", "chunk")
 DEFAULT_TABLES = {"catalog": "embeddings_catalog", "repo": "embeddings_repo", "module": "embeddings_module",
@@ -117,6 +117,8 @@ class VectorTable:
             else:
                 words[r >> 5] &= np.uint32(~(1 << (r & 31)) & 0xFFFFFFFF)
         self.live.copy_(torch.from_numpy(words.view(np.int32)).to(self.device))
+        if self.device.type == "cuda":  # searches read the table from other (side) streams
+            torch.cuda.current_stream(self.device).synchronize()
 
     @guarded
     def upsert(self, row_ids: list[str], texts: list[str], vectors: torch.Tensor, metadatas: list[dict]) -> int:
@@ -214,7 +216,7 @@ class VectorTable:
     def search(self, qvecs: torch.Tensor, k: int, flt: dict | None = None, qpred=None) -> list[list[Hit]]:
         """Batched filtered top-k by cosine. qvecs [nq, d]."""
         nq = qvecs.shape[0]
-        with self.lock:
+        with self.lock, side_stream(self.device, wait_caller=qvecs.is_cuda):
             if self.n == 0:
                 return [[] for _ in range(nq)]
             pc = self.predicates(flt)

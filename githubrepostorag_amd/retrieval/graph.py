@@ -24,6 +24,7 @@ from dataclasses import dataclass, field
 import torch
 
 from ..index.store import FILTER_FIELDS, Hit, VectorTable
+from ..utils.gpu_guard import side_stream
 
 
 @dataclass
@@ -58,6 +59,11 @@ class GraphRetriever:
         return Document(h.text, md, h.row_id, h.score)
 
     def invoke(self, query: str, filter: dict | None = None, qvec: torch.Tensor | None = None) -> list[Document]:
+        # the embed + every traversal hop share one side stream (utils/gpu_guard.py)
+        with side_stream(self.table.device, wait_caller=qvec is not None):
+            return self._invoke(query, filter, qvec)
+
+    def _invoke(self, query: str, filter: dict | None, qvec: torch.Tensor | None) -> list[Document]:
         t0 = time.perf_counter()
         tab = self.table
         if qvec is None:
