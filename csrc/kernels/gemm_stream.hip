@@ -3,7 +3,8 @@
 //
 //   C[M, N] = A[M, K] · W[N, K]^T (+ bias[N])          bf16 in, fp32 acc
 //
-// Regime: M = decode batch (17..64 per row tile).  W (e.g. Qwen2-7B down_proj,
+// Regime: M = decode batch (17..128 per row tile: MT = 2, 4 or 8 sixteen-row
+// MFMA tiles, so a batch of up to 128 rows streams the weights exactly once).  W (e.g. Qwen2-7B down_proj,
 // 136 MB) is read once from HBM per step; A (M x K) is re-read from L2 by every
 // column tile, so the A:W L2 traffic ratio is M / BN.
 //
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(const bf16* __restrict
   constexpr int GA = MT / 2;      // A glds per wave per stage
   constexpr int GPS = GW + GA;
   constexpr int TILE = AROWS * BN;
-  static_assert(MT == 2 || MT == 4, "MT");
+  static_assert(MT == 2 || MT == 4 || MT == 8, "MT");
   static_assert(BN == 64 || BN == 128 || BN == 256, "BN");
   __shared__ __attribute__((aligned(16))) char smem[NST * STAGE + 16];
   unsigned* flag = reinterpret_cast<unsigned*>(smem + NST * STAGE);
@@ -282,7 +283,7 @@ int launch(const bf16* A, int lda, const bf16* W, int ldw, const bf16* bias, bf1
 // a 4x128 workgroup holds 96 KB of LDS ring); pmax = max workgroups sharing a
 // tile (slab slots per tile).
 GRAG_API int grag_gemm_stream_plan(int M, int N, int K, int ncu, int* out5) {
-  const int mt = M <= 32 ? 2 : 4;
+  const int mt = M <= 32 ? 2 : (M <= 64 ? 4 : 8);
   const int bn = 256;
   const int ntm = (M + mt * 16 - 1) / (mt * 16);
   const long ks = (K + 63) / 64;
@@ -327,8 +328,14 @@ GRAG_API int grag_gemm_stream(const void* A, const void* W, const void* bias, vo
     if (bn == 128) GO(2, 128, 7);
     GO(2, 256, 4);
   }
-  if (bn == 64) GO(4, 64, 4);
-  if (bn == 128) GO(4, 128, 6);
-  GO(4, 256, 3);
+  if (mt <= 4) {
+    if (bn == 64) GO(4, 64, 4);
+    if (bn == 128) GO(4, 128, 6);
+    GO(4, 256, 3);
+  }
+  // 128-row tiles (decode batches 65..128): 24 / 32 / 48 KB per ring stage
+  if (bn == 64) GO(8, 64, 6);
+  if (bn == 128) GO(8, 128, 4);
+  GO(8, 256, 3);
 #undef GO
 }

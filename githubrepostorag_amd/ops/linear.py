@@ -141,7 +141,7 @@ def stream_plan(M: int, N: int, K: int, mt: int | None = None, bn: int | None = 
     key = (M, N, K, mt, bn, grid)
     p = _PLAN_CACHE.get(key)
     if p is None:
-        mt = mt or (2 if M <= 32 else 4)
+        mt = mt or (2 if M <= 32 else (4 if M <= 64 else 8))
         bn = bn or 128
         ntm = -(-M // (16 * mt))
         ks = -(-K // 64)
