@@ -56,14 +56,16 @@ def parse():
     ap.add_argument("--nlist", type=int, default=4096)
     ap.add_argument("--nprobe", type=int, default=32)
     ap.add_argument("--batch", type=int, default=64, help="queries per GPU per step")
-    ap.add_argument("--inflight", type=int, default=2, help="batches' worth of queries in flight (1 = closed batch)")
-    ap.add_argument("--arrival-groups", type=int, default=8, help="queries of a step arrive in this many groups")
+    ap.add_argument("--inflight", type=int, default=3, help="batches' worth of queries in flight (1 = closed batch)")
+    ap.add_argument("--arrival-groups", type=int, default=16, help="queries of a step arrive in this many groups")
     ap.add_argument("--prompt-len", type=int, default=1024)
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--top-k", type=int, default=10)
     ap.add_argument("--ingest-files", type=int, default=192, help="source files in the synthetic repo to ingest")
     ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--prefetch", type=int, default=1,
+                    help="1: the next group's retrieval overlaps engine steps on a helper thread")
     ap.add_argument("--out", default=None)
     return ap.parse_args()
 
@@ -136,17 +138,23 @@ def main():
     # (prefill fragmented by per-request hand-off, shorter decode windows).
     inflight = collections.deque()  # groups, oldest first: (request ids, submission time)
 
-    def submit():
-        """Retrieve + build prompts for a new group of u RAG queries and hand them to the engine."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from githubrepostorag_amd.utils.gpu_guard import side_stream
+
+    def prepare():
+        """Retrieve + build prompts for the next group of u RAG queries (the
+        group's arrival time is when its retrieval starts)."""
         B = u
-        t_sub = time.perf_counter()
-        qs = [synthetic.question(qcounter[0] + i) for i in range(B)]
-        qcounter[0] += B
-        qv = emb.embed_queries(qs)
-        t_e = time.perf_counter()
-        scores, ids = index.search(qv, args.top_k)
-        ids = ids.cpu().tolist()
-        t_s = time.perf_counter()
+        with side_stream(dev):  # off the engine's stream: the .cpu() waits only for the search
+            t_sub = time.perf_counter()
+            qs = [synthetic.question(qcounter[0] + i) for i in range(B)]
+            qcounter[0] += B
+            qv = emb.embed_queries(qs)
+            t_e = time.perf_counter()
+            scores, ids = index.search(qv, args.top_k)
+            ids = ids.cpu().tolist()
+            t_s = time.perf_counter()
         prompts = []
         for q, row in zip(qs, ids):
             blocks = [f"[{j + 1}] repo=synthetic module=m{d % 97} file=f{d}.py\n{synthetic.chunk_text(d)}"
@@ -158,23 +166,50 @@ def main():
                 else pid[-args.prompt_len:]
             prompts.append(pid)
         t_p = time.perf_counter()
+        return prompts, t_sub, (("embed", t_e - t_sub), ("search", t_s - t_e), ("prompt", t_p - t_s))
+
+    # --prefetch: a new group's retrieval (embed + search + prompt) runs on a
+    # helper thread (side stream) while this thread keeps stepping the engine;
+    # the group is admitted at the first engine step after its prompts are
+    # ready, as a continuous-batching server admits arrivals.  Only one thread
+    # issues collectives at a time: every arrival is admitted (its future
+    # joined) before the sub-step ends, so barriers never overlap a search.
+    pool = ThreadPoolExecutor(1, thread_name_prefix="prefetch") if args.prefetch else None
+
+    def admit(nxt):
+        prompts, t_sub, ph = nxt
         inflight.append(([eng.add_request(p, sp) for p in prompts], t_sub))
-        for k, v in (("embed", t_e - t_sub), ("search", t_s - t_e), ("prompt", t_p - t_s)):
+        for k, v in ph:
             phase[k] += v
 
-    def run_until(rids, ntok):
+    def submit():
+        """A new group of u RAG queries arrives; retrieve + prompt it, hand it to the engine."""
+        admit(prepare())
+
+    def run_until(rids, ntok, arrival=None):
+        """Step the engine until every request in ``rids`` has ``ntok`` tokens,
+        admitting the ``arrival`` future's group as soon as it is ready."""
         t0 = time.perf_counter()
         while any(len(eng.get(r).output_ids) < ntok and eng.get(r).finish_reason is None for r in rids):
             eng.step()
+            if arrival is not None and arrival.done():
+                admit(arrival.result())
+                arrival = None
+        if arrival is not None:
+            admit(arrival.result())
         phase["generate"] += time.perf_counter() - t0
 
     def run_step():
         """A groups arrive, the A oldest complete; returns the completed queries' TTFTs (s)."""
         ttft = []
         for _ in range(A):
-            submit()
+            arrival = None
+            if pool is not None and inflight:
+                arrival = pool.submit(prepare)
+            else:
+                submit()
             rids, t_sub = inflight.popleft()
-            run_until(rids, args.gen_len)
+            run_until(rids, args.gen_len, arrival)
             for r in rids:
                 s = eng.pop(r)
                 ttft.append(s.first_token_time - t_sub)
@@ -186,6 +221,16 @@ def main():
         submit()
         run_until(inflight[-1][0], stagger)
 
+    # capture the decode graphs of the steady state now (batch buckets the
+    # live count can reach x every decode window), not inside a timed step
+    if dev.type == "cuda" and not args.no_graph:
+        buckets = eng.cfg.graph_batch_sizes
+        lo = next((b for b in buckets if b >= (U - 1) * u), buckets[-1])
+        hi = next((b for b in buckets if b >= (U + 1) * u), buckets[-1])
+        t0 = time.perf_counter()
+        ncap = eng.warmup_graphs([b for b in buckets if lo <= b <= hi], args.prompt_len + args.gen_len,
+                                 windows=(1, 2, 4, 8))
+        log(f"captured {ncap} decode graphs in {time.perf_counter() - t0:.1f}s")
     log(f"warmup ({U} groups of {u} queries in flight)")
     for _ in range(args.warmup):
         run_step()
@@ -204,6 +249,7 @@ def main():
     stats1 = dict(eng.stats)
     comm.barrier()
     elapsed = time.perf_counter() - t_start
+    phase_timed = dict(phase)
     ttfts_all = [ttfts]
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -225,7 +271,10 @@ def main():
             eng.pop(r)
     log(f"serving: {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms, {ms_step:.1f} ms/step")
     eng_stats = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()}
-    log("per-step phases (ms, timed steps): " + ", ".join(f"{k}={v / args.steps * 1000:.1f}" for k, v in phase.items()))
+    if pool is not None:
+        pool.shutdown(wait=True)
+    log("per-step phases (ms, timed steps): " + ", ".join(f"{k}={v / args.steps * 1000:.1f}"
+                                                           for k, v in phase_timed.items()))
     timed_engine = {k: round((v - stats0.get(k, 0)) / args.steps, 4) for k, v in stats1.items()
                     if isinstance(v, (int, float))}
 
@@ -279,7 +328,8 @@ def main():
             },
             "engine": eng_stats,
             "engine_per_timed_step": timed_engine,
-            "phase_ms_per_step": {k: round(v / args.steps * 1000, 2) for k, v in phase.items()},
+            "phase_ms_per_step": {k: round(v / args.steps * 1000, 2) for k, v in phase_timed.items()},
+            "retrieval_prefetch": bool(args.prefetch),
             "ingest_stage_s": ingest_stages,
         }
         line = json.dumps(res)

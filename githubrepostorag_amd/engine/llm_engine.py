@@ -440,14 +440,27 @@ class LLMEngine:
         self.stats["graph_captures"] += 1
         return g
 
-    def warmup_graphs(self, batch_sizes=None, max_ctx: int = 2048) -> None:
+    @torch.inference_mode()
+    def warmup_graphs(self, batch_sizes=None, max_ctx: int = 2048, windows=(1,)) -> int:
+        """Capture the decode graphs a workload will replay ahead of time
+        (batch buckets x decode windows K, split plan of ``max_ctx``) so no
+        capture lands inside a latency-sensitive step.  Keyed on the
+        sampler's current launch chain: call it once requests with the
+        serving sampling parameters have been admitted.  Returns the number
+        of graphs captured."""
         if not (self.on_gpu and self.cfg.use_cuda_graph and self.model.tp.trivial):
-            return
+            return 0
+        n = 0
         for B in batch_sizes or self.cfg.graph_batch_sizes:
             split_len = _split_len_for(B)
-            nsplit = _pow2_at_least(-(-max_ctx // split_len))
-            if (B, nsplit, split_len, 1, self.sampler.rounds) not in self._graphs:
-                self._capture(B, nsplit, split_len, 1)
+            nsplit = min(_pow2_at_least(-(-max_ctx // split_len)), -(-self.cfg.max_model_len // split_len))
+            for K in windows:
+                if K > max(1, self.cfg.decode_window):
+                    continue
+                if (B, nsplit, split_len, K, self.sampler.rounds) not in self._graphs:
+                    self._capture(B, nsplit, split_len, K)
+                    n += 1
+        return n
 
     # ------------------------------------------------------------------ outputs
     def _append(self, s: Sequence, tok: int, now: float) -> bool:
