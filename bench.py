@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--ingest-files", type=int, default=192, help="source files in the synthetic repo to ingest")
     ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--switch-interval", type=float, default=0.0,
+                    help="Python GIL switch interval (s): the engine thread re-takes the GIL quickly after a GPU wait")
     ap.add_argument("--prefetch", type=int, default=1,
                     help="1: the next group's retrieval overlaps engine steps on a helper thread")
     ap.add_argument("--out", default=None)
@@ -72,6 +74,8 @@ def parse():
 
 def main():
     args = parse()
+    if args.switch_interval > 0:
+        sys.setswitchinterval(args.switch_interval)
     import torch
 
     from githubrepostorag_amd.parallel import comm
@@ -130,6 +134,14 @@ def main():
                   "Cite blocks as [1], [2]. If the specific information needed is not in the context, "
                   "say so clearly and suggest looking in specific repos/modules that might contain the answer.")
 
+    # row texts: the index's body_blob column (the reference stores chunk text
+    # next to the vector, vector_write_service.py:166-198) — a pool generated
+    # once here, so the timed loop does a lookup, not synthetic text generation
+    text_pool = [synthetic.chunk_text(i) for i in range(4096)]
+
+    def row_text(d: int) -> str:
+        return text_pool[d % len(text_pool)]
+
     qcounter = [rank * 1_000_000]
     phase = {"embed": 0.0, "search": 0.0, "prompt": 0.0, "generate": 0.0}
 
@@ -157,7 +169,7 @@ def main():
             t_s = time.perf_counter()
         prompts = []
         for q, row in zip(qs, ids):
-            blocks = [f"[{j + 1}] repo=synthetic module=m{d % 97} file=f{d}.py\n{synthetic.chunk_text(d)}"
+            blocks = [f"[{j + 1}] repo=synthetic module=m{d % 97} file=f{d}.py\n{row_text(d)}"
                       for j, d in enumerate([x for x in row if x >= 0][:5])]
             text = tok.apply_chat_template([{"role": "user", "content": f"{sys_prompt}\n\nQuestion: {q}\n\n"
                                              "Context:\n" + "\n\n".join(blocks) + "\n\nAnswer:"}])
@@ -177,8 +189,10 @@ def main():
     pool = ThreadPoolExecutor(1, thread_name_prefix="prefetch") if args.prefetch else None
 
     def admit(nxt):
+        t0 = time.perf_counter()
         prompts, t_sub, ph = nxt
         inflight.append(([eng.add_request(p, sp) for p in prompts], t_sub))
+        phase["admit"] = phase.get("admit", 0.0) + time.perf_counter() - t0
         for k, v in ph:
             phase[k] += v
 
@@ -241,6 +255,7 @@ def main():
         phase[k] = 0.0
     stats0 = dict(eng.stats)
     t_start = time.perf_counter()
+    phase["admit"] = 0.0
     ttfts = []
     for _ in range(args.steps):
         ttfts += run_step()
@@ -329,6 +344,9 @@ def main():
             "engine": eng_stats,
             "engine_per_timed_step": timed_engine,
             "phase_ms_per_step": {k: round(v / args.steps * 1000, 2) for k, v in phase_timed.items()},
+            "main_thread_ms_per_step": {"engine_step": round(timed_engine.get("step_s", 0) * 1000, 2),
+                                        "engine_prefill": round(timed_engine.get("prefill_s", 0) * 1000, 2),
+                                        "engine_decode": round(timed_engine.get("decode_s", 0) * 1000, 2)},
             "retrieval_prefetch": bool(args.prefetch),
             "ingest_stage_s": ingest_stages,
         }

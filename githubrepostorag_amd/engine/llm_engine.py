@@ -101,7 +101,8 @@ class LLMEngine:
         self._graph_pool = None
         self._static = None
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0, "steps": 0,
-                      "graph_replays": 0, "graph_captures": 0, "decode_steps": 0, "decode_wait_s": 0.0}
+                      "graph_replays": 0, "graph_captures": 0, "decode_steps": 0, "decode_wait_s": 0.0,
+                      "step_s": 0.0}
         self._eos = set(getattr(tokenizer, "eos_token_ids", set()))
         self._lock = threading.RLock()
         max_split = -(-cfg.max_model_len // KV_TILE)
@@ -173,9 +174,16 @@ class LLMEngine:
                           seq.cached_prefix, seq.first_token_time)
 
     # ------------------------------------------------------------------ step
-    @torch.inference_mode()
     def step(self) -> list[Sequence]:
         """Run one scheduler step; returns sequences that finished in it."""
+        t0 = time.perf_counter()
+        try:
+            return self._step()
+        finally:
+            self.stats["step_s"] += time.perf_counter() - t0
+
+    @torch.inference_mode()
+    def _step(self) -> list[Sequence]:
         finished = self.sched.reap_cancelled()
         for s in finished:
             self._notify(s, None, True)

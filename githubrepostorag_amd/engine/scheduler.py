@@ -219,15 +219,21 @@ class Scheduler:
                 return "prefill", items
             # decode every running sequence (one new token each)
             out = []
+            preempted = False
+            bs = self.kv.block_size
             for seq in list(self.running):
-                if seq not in self.running or seq.is_prefill:
+                if seq.status != SeqStatus.RUNNING or seq.is_prefill:  # preempted earlier in this loop
                     continue
-                while not self.kv.ensure(seq, seq.total_len):
-                    if not self._preempt_one(seq):
-                        break
-                if seq in self.running and len(seq.blocks) * self.kv.block_size >= seq.total_len:
-                    out.append((seq, seq.total_len - 1, seq.total_len))
-            out = [it for it in out if it[0] in self.running]  # drop anything preempted meanwhile
+                L = seq.total_len
+                if len(seq.blocks) * bs < L:
+                    while not self.kv.ensure(seq, L):
+                        if not self._preempt_one(seq):
+                            break
+                        preempted = True
+                if seq.status == SeqStatus.RUNNING and len(seq.blocks) * bs >= L:
+                    out.append((seq, L - 1, L))
+            if preempted:  # drop anything preempted meanwhile
+                out = [it for it in out if it[0].status == SeqStatus.RUNNING]
             if out:
                 return "decode", out
             return None, []

@@ -32,8 +32,8 @@ class SeqStatus(enum.Enum):
     FINISHED = 2
 
 
-@dataclass
-class Sequence:
+@dataclass(eq=False)  # identity semantics: the scheduler's list membership tests must not
+class Sequence:      # compare every field (that cost ~150 ms per step at 192 live sequences)
     req_id: str
     prompt_ids: list[int]
     params: SamplingParams

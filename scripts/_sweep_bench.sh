@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export PYTHONUNBUFFERED=1
 for cfg in ${CFGS:-2x8 3x8 4x8 3x16 4x16}; do
   set -- ${cfg/x/ }
-  timeout -k 10 300 python bench.py --no-ingest --steps 3 --inflight $1 --arrival-groups $2 > gpurun_out/bS_$1_$2.log 2>&1 || { tail -20 gpurun_out/bS_$1_$2.log; exit 1; }
+  timeout -k 10 300 python bench.py --no-ingest --steps 3 --inflight $1 --arrival-groups $2 ${EXTRA} > gpurun_out/bS_$1_$2.log 2>&1 || { tail -20 gpurun_out/bS_$1_$2.log; exit 1; }
   python - gpurun_out/bS_$1_$2.log <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); e = d["engine_per_timed_step"]
