@@ -50,7 +50,13 @@ def cmd_serve(args) -> int:
 
     s = _settings(args)
     logging.basicConfig(level=s.log_level, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
-    app = create_app(runtime_factory=lambda: _runtime(args))
+    def factory():
+        rt = _runtime(args)
+        n = rt.warmup()  # decode graphs captured before the first request, not inside one
+        logging.getLogger(__name__).info("captured %d decode graphs", n)
+        return rt
+
+    app = create_app(runtime_factory=factory)
     uvicorn.run(app, host=args.host, port=args.port, log_level=s.log_level.lower())
     return 0
 

@@ -94,6 +94,8 @@ class Settings:
     llm_timeout_s: float = field(default_factory=lambda: _float("LLM_TIMEOUT", 60.0))
     llm_retries: int = field(default_factory=lambda: _int("LLM_RETRIES", 1))
     stream_tokens: bool = field(default_factory=lambda: _bool("STREAM_TOKENS", True))
+    # coalesce concurrent jobs' query embeddings into one encoder pass (0 disables)
+    embed_batch_window_ms: float = field(default_factory=lambda: _float("EMBED_BATCH_WINDOW_MS", 1.0))
     seed: int = field(default_factory=lambda: _int("SEED", 0))
 
     def table_names(self) -> dict:

@@ -64,7 +64,102 @@ class Embedder:
         return self.embed_ids(self.tokenize(texts))
 
     def embed_queries(self, texts: list[str]) -> torch.Tensor:
-        return self.embed_ids(self.tokenize(texts, self.cfg.query_prefix))
+        ids = self.tokenize(texts, self.cfg.query_prefix)
+        b = self._batcher
+        if b is not None:
+            return b.submit(ids)
+        return self.embed_ids(ids)
 
     def embed_query(self, text: str) -> torch.Tensor:
         return self.embed_queries([text])[0]
+
+    _batcher = None
+
+    def enable_batching(self, window_s: float = 0.001, max_texts: int = 256) -> None:
+        """Coalesce concurrent query embeddings (the service's job threads each
+        embed one query per retriever hop) into one varlen encoder pass:
+        64 concurrent jobs cost one launch sequence instead of 64."""
+        if self._batcher is None:
+            self._batcher = _QueryBatcher(self, window_s, max_texts)
+
+    def close(self) -> None:
+        if self._batcher is not None:
+            self._batcher.stop()
+            self._batcher = None
+
+
+class _QueryBatcher:
+    """One worker thread gathers query-embedding requests for ``window_s``
+    after the first arrives (or until ``max_texts``), runs them as a single
+    ``embed_ids`` call on its own side stream, synchronises that stream and
+    hands every caller its rows (complete in memory, so any stream may read
+    them)."""
+
+    def __init__(self, emb: Embedder, window_s: float, max_texts: int):
+        import queue
+
+        self.emb, self.window, self.max_texts = emb, window_s, max_texts
+        self.q: "queue.Queue" = queue.Queue()
+        self.batches = 0
+        self.texts = 0
+        self._stop = False
+        self._t = threading.Thread(target=self._loop, name="embed-batcher", daemon=True)
+        self._t.start()
+
+    def submit(self, ids: list[list[int]]) -> torch.Tensor:
+        from concurrent.futures import Future
+
+        f: Future = Future()
+        self.q.put((ids, f))
+        out = f.result()
+        if out.is_cuda:  # the rows live in the batcher stream's pool: keep them until this stream is done
+            out.record_stream(torch.cuda.current_stream(out.device))
+        return out
+
+    def stop(self) -> None:
+        self._stop = True
+        self.q.put(None)
+        self._t.join(timeout=5)
+
+    def _loop(self) -> None:
+        import queue
+        import time
+
+        if self.emb.encoder.device.type == "cuda":
+            torch.cuda.set_device(self.emb.encoder.device)
+        while not self._stop:
+            first = self.q.get()
+            if first is None:
+                break
+            items = [first]
+            n = len(first[0])
+            t_end = time.perf_counter() + self.window
+            while n < self.max_texts:
+                left = t_end - time.perf_counter()
+                if left <= 0:
+                    break
+                try:
+                    it = self.q.get(timeout=left)
+                except queue.Empty:
+                    break
+                if it is None:
+                    self._stop = True
+                    break
+                items.append(it)
+                n += len(it[0])
+            try:
+                flat = [x for ids, _ in items for x in ids]
+                with side_stream(self.emb.encoder.device):
+                    out = self.emb.embed_ids(flat)
+                    if out.is_cuda:
+                        torch.cuda.current_stream(out.device).synchronize()
+                self.batches += 1
+                self.texts += len(flat)
+                o = 0
+                for ids, f in items:
+                    f.set_result(out[o:o + len(ids)])
+                    o += len(ids)
+            except BaseException as e:  # fail the callers, keep serving
+                for _, f in items:
+                    if not f.done():
+                        f.set_exception(e)

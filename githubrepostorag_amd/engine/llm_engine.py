@@ -430,9 +430,8 @@ class LLMEngine:
         seen_save = self.sampler.seen[self.scratch_slot].clone()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                self._decode_forward(v, B, nsplit, split_len, out, K)
+        with torch.cuda.stream(s):  # one warm-up step of this shape (every window step has the same shapes)
+            self._decode_forward(v, B, nsplit, split_len, out, 1)
         torch.cuda.current_stream().wait_stream(s)
         graph = torch.cuda.CUDAGraph()
         # thread_local: API / retrieval threads keep launching (and syncing) on

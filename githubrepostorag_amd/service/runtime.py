@@ -42,6 +42,8 @@ class RAGRuntime:
             enc = BertEncoder(ecfg, device=self.device, dtype=dtype, seed=s.seed + 2, state_dict=sd)
             embedder = Embedder(enc, WordPieceTokenizer(ecfg.vocab_size, vocab))
         self.embedder = embedder
+        if s.embed_batch_window_ms > 0 and hasattr(embedder, "enable_batching"):
+            embedder.enable_batching(s.embed_batch_window_ms / 1000.0)
         # store
         if store is None:
             if s.index_dir and (Path(s.index_dir) / "manifest.json").exists():
@@ -75,6 +77,26 @@ class RAGRuntime:
         self.llm = llm
         self.ingest_llm = ingest_llm or llm
 
+    def warmup(self, contexts=(1024, 2048, 4096), windows=(1, 2, 4, 8)) -> int:
+        """Capture the decode graphs a serving mix needs at startup (batch
+        buckets up to MAX_NUM_SEQS x decode windows x split plans of the
+        given context lengths), as vLLM does, so no capture stalls a live
+        request.  The engine thread must be idle (call before serving)."""
+        eng = self.engine
+        if eng is None or not eng.on_gpu:
+            return 0
+        from ..engine.sequence import SamplingParams
+
+        # admit one request with the worker's sampling knobs first: graphs are keyed on the sampler chain
+        eng.generate([[1, 2, 3, 4]], SamplingParams(max_tokens=2, temperature=0.4, top_p=0.8,
+                                                     repetition_penalty=1.2, ignore_eos=True))
+        buckets = [b for b in eng.cfg.graph_batch_sizes if b <= max(1, eng.cfg.max_num_seqs)]
+        n = 0
+        for ctx in contexts:
+            if ctx <= eng.cfg.max_model_len:
+                n += eng.warmup_graphs(buckets, ctx, windows)
+        return n
+
     def agent(self) -> GraphAgent:
         """A fresh agent per job (cheap: it only holds references)."""
         s = self.settings
@@ -96,3 +118,5 @@ class RAGRuntime:
     def close(self) -> None:
         if self.runner is not None:
             self.runner.shutdown()
+        if hasattr(self.embedder, "close"):
+            self.embedder.close()

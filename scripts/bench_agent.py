@@ -43,8 +43,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="qwen2-7b")
     ap.add_argument("--encoder", default="bge-large-en-v1.5")
-    ap.add_argument("--concurrency", type=int, default=64, help="jobs in flight (worker max_jobs)")
-    ap.add_argument("--jobs", type=int, default=128, help="timed jobs")
+    ap.add_argument("--concurrency", type=int, default=128, help="jobs in flight (worker max_jobs)")
+    ap.add_argument("--jobs", type=int, default=256, help="timed jobs")
     ap.add_argument("--warmup-jobs", type=int, default=16)
     ap.add_argument("--gen-len", type=int, default=64, help="token cap of every LLM call")
     ap.add_argument("--ingest-files", type=int, default=64)
@@ -87,6 +87,9 @@ def main():
     t0 = time.perf_counter()
     rt = RAGRuntime(s, device=str(dev))
     log(f"runtime ready in {time.perf_counter() - t0:.1f}s (decoder {args.model}, encoder {args.encoder})")
+    t0 = time.perf_counter()
+    ncap = rt.warmup()
+    log(f"captured {ncap} decode graphs in {time.perf_counter() - t0:.1f}s")
 
     # ---- populate the five scope tables through the real ingest pipeline
     t0 = time.perf_counter()

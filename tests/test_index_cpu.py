@@ -89,3 +89,33 @@ def test_ivf_recall_cpu():
 
     assert recall(16) >= 0.99  # probing every list is exact search (up to bf16 score ties)
     assert recall(6) >= 0.8
+
+
+def test_query_embedding_batcher_coalesces_threads():
+    """Concurrent embed_queries calls (one per agent job thread) are served
+    by one encoder pass and return exactly the rows a direct call gives."""
+    import threading
+
+    from githubrepostorag_amd.embed.service import Embedder
+
+    emb = Embedder.from_name("encoder-tiny", device="cpu", seed=3)
+    qs = [f"how does retry policy {i} handle timeouts" for i in range(24)]
+    ref = emb.embed_queries(qs)
+    emb.enable_batching(window_s=0.05)
+    out = [None] * len(qs)
+    barrier = threading.Barrier(len(qs))
+
+    def run(i):
+        barrier.wait()
+        out[i] = emb.embed_queries([qs[i]])[0]
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(len(qs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    b = emb._batcher
+    assert b.texts == len(qs) and b.batches < len(qs)
+    for i in range(len(qs)):
+        assert torch.allclose(out[i].float(), ref[i].float(), atol=2e-2)
+    emb.close()
