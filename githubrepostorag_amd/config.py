@@ -83,6 +83,7 @@ class Settings:
     kv_cache_gb: float = field(default_factory=lambda: _float("KV_CACHE_GB", 0.0))
     cuda_graphs: bool = field(default_factory=lambda: _bool("CUDA_GRAPHS", True))
     prefix_caching: bool = field(default_factory=lambda: _bool("PREFIX_CACHING", True))
+    mixed_batches: bool = field(default_factory=lambda: _bool("MIXED_BATCHES", False))
     index_kind: str = field(default_factory=lambda: _env("INDEX_KIND", "flat"))
     nlist: int = field(default_factory=lambda: _int("NLIST", 1024))
     nprobe: int = field(default_factory=lambda: _int("NPROBE", 16))

@@ -51,6 +51,10 @@ class EngineConfig:
     use_cuda_graph: bool = True
     graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
     decode_window: int = 8  # max decode steps per graph replay (power of two)
+    # decode tokens ride along in prefill steps (one weight pass for both).  Off by
+    # default: measured on the headline bench the odd GEMM M (4096 + live rows)
+    # misses the tuned library solutions and costs more than the saved decode steps
+    mixed_batches: bool = False
     seed: int = 0
 
 
@@ -92,7 +96,8 @@ class LLMEngine:
         nblocks = cfg.num_blocks or self._plan_blocks()
         self.kv = KVCacheManager(nblocks, bs, cfg.enable_prefix_caching)
         self.kv_caches = model.allocate_kv_cache(nblocks, bs)
-        self.sched = Scheduler(self.kv, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
+        self.sched = Scheduler(self.kv, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len,
+                               mixed_batches=cfg.mixed_batches)
         self.scratch_slot = cfg.max_num_seqs
         self.sampler = SamplerState(cfg.max_num_seqs + 1, model.cfg.vocab_size, self.device, seed=cfg.seed)
         self.max_blocks_per_seq = -(-cfg.max_model_len // bs)
@@ -102,7 +107,7 @@ class LLMEngine:
         self._static = None
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0, "steps": 0,
                       "graph_replays": 0, "graph_captures": 0, "decode_steps": 0, "decode_wait_s": 0.0,
-                      "step_s": 0.0}
+                      "step_s": 0.0, "mixed_steps": 0}
         self._eos = set(getattr(tokenizer, "eos_token_ids", set()))
         self._lock = threading.RLock()
         max_split = -(-cfg.max_model_len // KV_TILE)
@@ -174,16 +179,17 @@ class LLMEngine:
                           seq.cached_prefix, seq.first_token_time)
 
     # ------------------------------------------------------------------ step
-    def step(self) -> list[Sequence]:
-        """Run one scheduler step; returns sequences that finished in it."""
+    def step(self, max_window: int | None = None) -> list[Sequence]:
+        """Run one scheduler step; returns sequences that finished in it.
+        ``max_window`` caps the decode window (tokens per sequence this step)."""
         t0 = time.perf_counter()
         try:
-            return self._step()
+            return self._step(max_window)
         finally:
             self.stats["step_s"] += time.perf_counter() - t0
 
     @torch.inference_mode()
-    def _step(self) -> list[Sequence]:
+    def _step(self, max_window: int | None = None) -> list[Sequence]:
         finished = self.sched.reap_cancelled()
         for s in finished:
             self._notify(s, None, True)
@@ -198,10 +204,10 @@ class LLMEngine:
         if not items:
             return finished
         self.stats["steps"] += 1
-        if kind == "prefill":
+        if kind in ("prefill", "mixed"):
             finished += self._run_prefill(items)
         else:
-            finished += self._run_decode([s for s, _, _ in items])
+            finished += self._run_decode([s for s, _, _ in items], max_window)
         return finished
 
     # ------------------------------------------------------------------ helpers
@@ -250,13 +256,30 @@ class LLMEngine:
         d_bt = dev[o:o + n * width].view(n, width)
         meta = AttnMetadata(q_start=d_qs, ctx_len=d_ctx, block_tables=d_bt, slot_mapping=d_slot,
                             max_q_len=max(b - a for _, a, b in items), num_seqs=n, num_tokens=T)
+        # mixed step: trailing one-token decode rows (scheduler.schedule); on the
+        # GPU their attention runs on the split-KV decode kernel
+        n_pref = next((i for i, (s, a, b) in enumerate(items) if b - a == 1 and s.output_ids and a == s.total_len - 1),
+                      n)
+        n_dec = n - n_pref
+        if n_dec and n_pref and self.on_gpu:
+            Tp = q_start[n_pref]
+            split_len = _split_len_for(n_dec)
+            nsplit = max(1, -(-max(ctx[n_pref:]) // split_len))
+            hq, dh = self.model.hq, self.model.head_dim
+            meta.extra["decode_rows"] = (Tp, AttnMetadata(
+                q_start=d_qs[n_pref:] - Tp, ctx_len=d_ctx[n_pref:], block_tables=d_bt[n_pref:],
+                slot_mapping=d_slot[Tp:], max_q_len=1, num_seqs=n_dec, num_tokens=n_dec, is_decode=True,
+                num_splits=nsplit, split_len=split_len, part_o=self._part_o[: nsplit * n_dec * hq * dh],
+                part_ml=self._part_ml[: nsplit * n_dec * hq * 2]))
+            meta.num_seqs, meta.num_tokens = n_pref, Tp
+            meta.max_q_len = max(b - a for _, a, b in items[:n_pref])
         hidden = self.model.forward(d_ids, d_pos, meta, self.kv_caches)
-        # sample for sequences whose prompt is now complete and have no pending token
+        # sample for sequences whose prompt is now complete (first token) and for decode rows (next token)
         samp_rows, samp_seqs = [], []
         for i, (s, a, b) in enumerate(items):
             s.num_computed = b
             self.kv.register_full_blocks(s)
-            if b == s.total_len and not s.output_ids:
+            if b == s.total_len:
                 samp_rows.append(q_start[i + 1] - 1)
                 samp_seqs.append(s)
         finished = []
@@ -269,7 +292,10 @@ class LLMEngine:
             for s, t in zip(samp_seqs, toks):
                 if self._append(s, int(t), now):
                     finished.append(s)
-        self.stats["prefill_tokens"] += T
+        self.stats["prefill_tokens"] += T - n_dec
+        if n_dec:
+            self.stats["decode_tokens"] += n_dec
+            self.stats["mixed_steps"] += 1
         self.stats["prefill_s"] += time.perf_counter() - t0
         return finished
 
@@ -338,10 +364,10 @@ class LLMEngine:
             sample(logits, self.sampler, v["slots"], out=out_tokens[j])
         return out_tokens
 
-    def _window(self, seqs) -> int:
+    def _window(self, seqs, cap: int | None = None) -> int:
         """Largest power-of-two window <= decode_window that no sequence's
         max_tokens / max_model_len cuts short and whose KV blocks fit."""
-        K = max(1, self.cfg.decode_window)
+        K = max(1, self.cfg.decode_window if cap is None else min(cap, self.cfg.decode_window))
         for s in seqs:
             K = min(K, s.params.max_tokens - len(s.output_ids), self.cfg.max_model_len - s.total_len)
         K = max(1, K)
@@ -353,12 +379,12 @@ class LLMEngine:
                     return 1
         return K
 
-    def _run_decode(self, seqs) -> list[Sequence]:
+    def _run_decode(self, seqs, max_window: int | None = None) -> list[Sequence]:
         t0 = time.perf_counter()
         n = len(seqs)
         use_graph = (self.on_gpu and self.cfg.use_cuda_graph and self.model.tp.trivial
                      and n <= max(self.cfg.graph_batch_sizes))
-        K = self._window(seqs) if use_graph else 1
+        K = self._window(seqs, max_window) if use_graph else 1
         max_ctx = max(s.total_len for s in seqs) + K - 1
         if use_graph:
             width = self.max_blocks_per_seq

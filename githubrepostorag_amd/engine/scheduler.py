@@ -9,7 +9,15 @@ Policy (what vLLM gave the reference at ``--max-num-seqs 4``, generalised):
   instead of recomputed — the agent's repeated instructions and the ingest
   extractor prompts share long prefixes;
 * when decode runs out of blocks the youngest running sequence is preempted
-  (blocks freed, recomputed later).
+  (blocks freed, recomputed later);
+* waiting requests carry a priority (SamplingParams.priority): critical-path
+  requests (ingest roll-up summaries, interactive agent calls) are admitted
+  ahead of bulk extractor waves, FCFS within a priority;
+* prefix-aware admission: a waiting prompt whose first SIG_BLOCKS blocks are
+  identical to a prompt being prefilled in this very step is deferred by one
+  step, so it reuses those blocks from the prefix cache instead of computing
+  them again (waves submit the summary / title / keyword prompts of one chunk
+  together; without this every copy of the shared chunk would be prefilled).
 """
 from __future__ import annotations
 
@@ -109,8 +117,10 @@ class KVCacheManager:
 
 
 class Scheduler:
-    def __init__(self, kv: KVCacheManager, max_num_seqs: int, max_num_batched_tokens: int, max_model_len: int):
+    def __init__(self, kv: KVCacheManager, max_num_seqs: int, max_num_batched_tokens: int, max_model_len: int,
+                 mixed_batches: bool = True):
         self.kv = kv
+        self.mixed_batches = mixed_batches
         self.max_num_seqs = max_num_seqs
         self.max_num_batched_tokens = max_num_batched_tokens
         self.max_model_len = max_model_len
@@ -120,9 +130,36 @@ class Scheduler:
         self.lock = threading.Lock()
         self.num_preemptions = 0
 
+    # 16 blocks = 256 tokens: a shared system prompt of a few dozen tokens is not worth a
+    # step of extra latency; a shared chunk of hundreds of tokens is
+    SIG_BLOCKS = 16
+
     def add(self, seq: Sequence) -> None:
         with self.lock:
-            self.waiting.append(seq)
+            pr = seq.params.priority
+            if pr <= 0 or not self.waiting or self.waiting[-1].params.priority >= pr:
+                self.waiting.append(seq)
+                return
+            # insert after the last waiting request of priority >= pr
+            i = len(self.waiting)
+            while i > 0 and self.waiting[i - 1].params.priority < pr:
+                i -= 1
+            self.waiting.insert(i, seq)
+
+    def _sig(self, seq: Sequence) -> int:
+        """Chained hash of the first SIG_BLOCKS full prompt blocks (0 = shorter)."""
+        if seq.prefix_sig is None:
+            bs = self.kv.block_size
+            n = self.SIG_BLOCKS * bs
+            if not self.kv.prefix_caching or len(seq.prompt_ids) <= n:
+                seq.prefix_sig = 0
+            else:
+                toks = np.asarray(seq.prompt_ids[:n], dtype=np.int32)
+                h = 0
+                for b in range(self.SIG_BLOCKS):
+                    h = int(rt().grag_hash_block(h, toks[b * bs:].ctypes.data, bs))
+                seq.prefix_sig = h
+        return seq.prefix_sig
 
     def has_work(self) -> bool:
         return bool(self.waiting or self.running)
@@ -177,7 +214,8 @@ class Scheduler:
         return True
 
     def schedule(self):
-        """Returns ("prefill", [(seq, start, end)]) or ("decode", [(seq, pos, pos+1)]) or (None, [])."""
+        """Returns ("prefill", [(seq, start, end)]), ("mixed", prefill items then
+        one-token decode items), ("decode", [(seq, pos, pos+1)]) or (None, [])."""
         with self.lock:
             budget = self.max_num_batched_tokens
             items = []
@@ -192,6 +230,11 @@ class Scheduler:
                         items.append((seq, seq.num_computed, seq.num_computed + n))
                         budget -= n
             admitted = []
+            pending: set[int] = set()  # prefix signatures being computed in this step
+            for seq, a, _ in items:
+                if a < self.SIG_BLOCKS * self.kv.block_size and self._sig(seq):
+                    pending.add(seq.prefix_sig)
+            deferred = []
             while self.waiting and budget > 0 and self.free_slots and len(self.running) < self.max_num_seqs:
                 seq = self.waiting[0]
                 if seq.total_len >= self.max_model_len:
@@ -200,7 +243,12 @@ class Scheduler:
                     self._finish(seq)
                     admitted.append(("rejected", seq))
                     continue
-                if not seq.blocks:
+                fresh = not seq.blocks
+                if fresh and self._sig(seq) and seq.prefix_sig in pending:
+                    # the same first blocks are being prefilled right now: take them from the cache next step
+                    deferred.append(self.waiting.popleft())
+                    continue
+                if fresh:
                     self.kv.match_prefix(seq)
                 tgt = self.prefill_target(seq)
                 n = min(tgt - seq.num_computed, budget)
@@ -213,9 +261,26 @@ class Scheduler:
                 admitted.append(("admitted", seq))
                 items.append((seq, seq.num_computed, seq.num_computed + n))
                 budget -= n
+                if seq.num_computed < self.SIG_BLOCKS * self.kv.block_size and seq.prefix_sig:
+                    pending.add(seq.prefix_sig)
+            self.waiting.extendleft(reversed(deferred))
             self.last_admitted = [s for tag, s in admitted if tag == "admitted"]
             self.last_rejected = [s for tag, s in admitted if tag == "rejected"]
             if items:
+                if self.mixed_batches:
+                    # piggyback one decode token of every decode-ready sequence on
+                    # this prefill step: the weights are streamed once for both
+                    # (a separate decode step would stream all of them again)
+                    n_pref = len(items)
+                    taken = {id(it[0]) for it in items}
+                    for seq in self.running:
+                        if id(seq) in taken or seq.is_prefill or not seq.output_ids:
+                            continue
+                        L = seq.total_len
+                        if self.kv.ensure(seq, L):
+                            items.append((seq, L - 1, L))
+                    if len(items) > n_pref:
+                        return "mixed", items
                 return "prefill", items
             # decode every running sequence (one new token each)
             out = []

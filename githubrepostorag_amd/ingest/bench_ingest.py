@@ -26,7 +26,7 @@ from .controller import IngestController
 from .readers import Document
 
 
-def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs: int = 128,
+def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs: int = 256,
                      max_model_len: int = 8192, use_graph: bool = True, summary_tokens: int = 128) -> tuple[int, float, dict]:
     """Returns (documents ingested, seconds, per-stage seconds)."""
     dev = next(model.parameters()).device if hasattr(model, "parameters") else torch.device("cpu")

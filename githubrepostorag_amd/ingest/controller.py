@@ -30,13 +30,14 @@ from pathlib import Path
 from ..config import settings as get_settings
 from ..service import metrics as M
 from .extractors import ExtractorPipeline
-from .hierarchy import HierarchyBuilder
+from .hierarchy import ROLLUP_PRIORITY, HierarchyBuilder
 from .preprocess import infer_component_kind, prepare_repo_documents
 from .readers import GithubReader, LocalDirReader, SyntheticRepoReader, fetch_repositories
 from .splitters import DynamicCodeSplitter
 from .writer import VectorWriter
 
 log = logging.getLogger(__name__)
+CATALOG_HEAD = 16  # chunks extracted first: the catalog uses the first 10 summaries (> 20 chars)
 
 DOC_TYPE_TO_SCOPE = {"catalog": "catalog", "repo": "repo", "module": "module", "file": "file"}
 
@@ -173,14 +174,21 @@ class IngestController:
         # small serial ones.  Stage timers overlap accordingly.
         with timer("split"):
             split_nodes = self.splitter.get_nodes_from_documents(docs)
-        pool = ThreadPoolExecutor(max_workers=4)
+        pool = ThreadPoolExecutor(max_workers=5)
         try:
             def code_branch():
+                # the catalog reads the first <= 10 code-chunk summaries
+                # (catalog_builder.py:140-194): extract those first, at roll-up
+                # priority, and build the catalog while the bulk extractor
+                # waves over the remaining chunks run
+                head, rest = split_nodes[:CATALOG_HEAD], split_nodes[CATALOG_HEAD:]
                 with timer("code_nodes"):
-                    nodes = self.extractors.run(split_nodes)
-                with timer("catalog"):
-                    cat = self.hier.catalog_nodes(repo, docs, nodes, collection, kind, layer)
-                return nodes, cat
+                    self.extractors.run(head, priority=ROLLUP_PRIORITY)
+                    f_rest = pool.submit(self.extractors.run, rest)
+                    with timer("catalog"):
+                        cat = self.hier.catalog_nodes(repo, docs, split_nodes, collection, kind, layer)
+                    f_rest.result()
+                return split_nodes, cat
 
             f_code = pool.submit(code_branch)
             with timer("file_summaries"):
@@ -191,7 +199,8 @@ class IngestController:
             f_mod_ext = pool.submit(self.hier.extract.run, module_nodes)
             with timer("repo_summaries"):
                 repo_nodes = self.hier.extract.run(
-                    self.hier.repo_summary_nodes(docs, module_nodes, repo, namespace, branch, kind))
+                    self.hier.repo_summary_nodes(docs, module_nodes, repo, namespace, branch, kind),
+                    priority=ROLLUP_PRIORITY)
             with timer("extract_wait"):
                 code_nodes, catalog_nodes = f_code.result()
                 f_file_ext.result()

@@ -52,21 +52,21 @@ def _shared_prefix(context: str) -> str:
     return f"Here is the content of the section:\n{context}\n\n"
 
 
-def extract_summaries(nodes: list[Node], wave: LLMWave, max_tokens: int = 256) -> None:
-    outs = wave.map([prompts.summary_extract(n.get_content()) for n in nodes], max_tokens=max_tokens)
+def extract_summaries(nodes: list[Node], wave: LLMWave, max_tokens: int = 256, **kw) -> None:
+    outs = wave.map([prompts.summary_extract(n.get_content()) for n in nodes], max_tokens=max_tokens, **kw)
     for n, o in zip(nodes, outs):
         n.metadata["section_summary"] = o
 
 
-def extract_keywords(nodes: list[Node], wave: LLMWave, n_keywords: int = 10, max_tokens: int = 64) -> None:
+def extract_keywords(nodes: list[Node], wave: LLMWave, n_keywords: int = 10, max_tokens: int = 64, **kw) -> None:
     ps = [_shared_prefix(n.get_content()) + f"Give {n_keywords} unique keywords for this document. "
           "Format as comma separated. Keywords: " for n in nodes]
-    outs = wave.map(ps, max_tokens=max_tokens)
+    outs = wave.map(ps, max_tokens=max_tokens, **kw)
     for n, o in zip(nodes, outs):
         n.metadata["excerpt_keywords"] = o
 
 
-def extract_titles(nodes: list[Node], wave: LLMWave, nodes_per_doc: int = 5, max_tokens: int = 32) -> None:
+def extract_titles(nodes: list[Node], wave: LLMWave, nodes_per_doc: int = 5, max_tokens: int = 32, **kw) -> None:
     by_doc = defaultdict(list)
     for n in nodes:
         by_doc[n.metadata.get("source_doc_id") or n.metadata.get("file_path") or ""].append(n)
@@ -77,12 +77,12 @@ def extract_titles(nodes: list[Node], wave: LLMWave, nodes_per_doc: int = 5, max
             cand_prompts.append(_shared_prefix(n.get_content()) + "Give a title that summarizes all of the unique "
                                 "entities, titles or themes found in the context. Title: ")
             owners.append(key)
-    cands = wave.map(cand_prompts, max_tokens=max_tokens)
+    cands = wave.map(cand_prompts, max_tokens=max_tokens, **kw)
     per_doc = defaultdict(list)
     for k, c in zip(owners, cands):
         per_doc[k].append(c)
     keys = [k for k, _ in docs]
-    combined = wave.map([prompts.title_combine(per_doc[k]) for k in keys], max_tokens=max_tokens)
+    combined = wave.map([prompts.title_combine(per_doc[k]) for k in keys], max_tokens=max_tokens, **kw)
     for (k, ns), t in zip(docs, combined):
         for n in ns:
             n.metadata["document_title"] = t
@@ -100,16 +100,18 @@ class ExtractorPipeline:
         self.title_tokens = title_tokens
         self.enabled = enabled
 
-    def run(self, nodes: list[Node]) -> list[Node]:
+    def run(self, nodes: list[Node], priority: int = 0) -> list[Node]:
         """The three extractors are independent reads of the same nodes (each
         writes its own metadata key), so their waves are submitted together:
         one engine batch instead of three back-to-back ones (the reference ran
-        them sequentially, code_pipeline_service.py:23-51)."""
+        them sequentially, code_pipeline_service.py:23-51).  ``priority``:
+        engine admission priority of the waves (critical-path passes)."""
         if not self.enabled or not nodes:
             return nodes
-        jobs = (("summary", lambda: extract_summaries(nodes, self.wave, self.summary_tokens)),
-                ("title", lambda: extract_titles(nodes, self.wave, self.title_nodes, self.title_tokens)),
-                ("keywords", lambda: extract_keywords(nodes, self.wave, 10, self.keyword_tokens)))
+        kw = {"priority": priority} if priority else {}
+        jobs = (("summary", lambda: extract_summaries(nodes, self.wave, self.summary_tokens, **kw)),
+                ("title", lambda: extract_titles(nodes, self.wave, self.title_nodes, self.title_tokens, **kw)),
+                ("keywords", lambda: extract_keywords(nodes, self.wave, 10, self.keyword_tokens, **kw)))
 
         def guarded(item):
             name, fn = item

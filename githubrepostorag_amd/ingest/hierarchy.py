@@ -21,6 +21,9 @@ from .readers import Document, Node
 from .splitters import SentenceSplitter
 
 log = logging.getLogger(__name__)
+# the file -> module -> repo chain is the ingest critical path: its waves are
+# admitted ahead of the bulk extractor waves running beside them
+ROLLUP_PRIORITY = 1
 
 
 class HierarchyBuilder:
@@ -53,7 +56,7 @@ class HierarchyBuilder:
         files = [(fp, ns) for fp, ns in group_nodes_by_file(code_nodes).items() if fp]
         concat = ["\n\n".join(n.get_content() for n in ns)[:25000] for _, ns in files]
         texts = self.wave.map([prompts.file_summary(fp) + "\n\n" + c for (fp, _), c in zip(files, concat)],
-                              max_tokens=self.summary_tokens)
+                              max_tokens=self.summary_tokens, priority=ROLLUP_PRIORITY)
         docs = []
         for (fp, ns), t in zip(files, texts):
             t = t or f"{fp} summary unavailable."
@@ -73,7 +76,7 @@ class HierarchyBuilder:
         mods = [(m, fs) for m, fs in group_files_by_module(list(summaries), depth).items() if m]
         joined = ["\n\n".join(summaries[f] for f in fs[:max_files])[:25000] for _, fs in mods]
         texts = self.wave.map([prompts.module_summary(m, repo) + "\n\n" + j for (m, _), j in zip(mods, joined)],
-                              max_tokens=self.summary_tokens)
+                              max_tokens=self.summary_tokens, priority=ROLLUP_PRIORITY)
         docs = [Document(t or f"{m} module summary unavailable.",
                          {"namespace": namespace, "repo": repo, "branch": branch, "module": m, "component_kind": kind,
                           "doc_type": "module", "rollup_of": [ids[f] for f in fs[:max_files] if f in ids],
@@ -86,7 +89,8 @@ class HierarchyBuilder:
         readmes = [d.text for d in docs if d.metadata.get("file_path", "").lower().endswith("readme.md")][:readme_limit]
         mods = module_nodes[:module_limit]
         seeds = "\n\n".join(readmes + [m.get_content() for m in mods])[:25000]
-        text = self.wave.map([prompts.repo_overview(repo) + "\n\n" + seeds], max_tokens=self.summary_tokens)[0]
+        text = self.wave.map([prompts.repo_overview(repo) + "\n\n" + seeds], max_tokens=self.summary_tokens,
+                             priority=ROLLUP_PRIORITY)[0]
         doc = Document(text or f"{repo}: overview unavailable.",
                        {"namespace": namespace, "repo": repo, "branch": branch, "component_kind": kind,
                         "doc_type": "repo", "rollup_of": [m.id for m in mods],

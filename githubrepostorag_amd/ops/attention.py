@@ -91,6 +91,17 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     """q [T, Hq, D] (token-major) -> out [T, Hq*D]."""
     if not q.is_cuda:
         return paged_attention_ref(q, k_cache, v_cache, meta, scale, causal).reshape(q.shape[0], -1)
+    dec = meta.extra.get("decode_rows")
+    if dec is not None:  # mixed step: prefill rows [0, Tp) + one-token decode rows [Tp, T)
+        Tp, dmeta = dec
+        if out is None:
+            out = torch.empty(q.shape[0], q.shape[1] * q.shape[2], dtype=q.dtype, device=q.device)
+        pmeta = AttnMetadata(q_start=meta.q_start, ctx_len=meta.ctx_len, block_tables=meta.block_tables,
+                             slot_mapping=meta.slot_mapping, max_q_len=meta.max_q_len, num_seqs=meta.num_seqs,
+                             num_tokens=Tp)
+        paged_attention(q[:Tp], k_cache, v_cache, pmeta, scale, causal, out=out[:Tp])
+        paged_attention(q[Tp:], k_cache, v_cache, dmeta, scale, causal, out=out[Tp:])
+        return out
     T, Hq, D = q.shape
     Hkv, BS = k_cache.shape[1], k_cache.shape[2]
     if out is None:

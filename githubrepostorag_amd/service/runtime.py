@@ -62,7 +62,7 @@ class RAGRuntime:
             ecfg = EngineConfig(max_num_seqs=s.max_num_seqs, max_num_batched_tokens=s.max_num_batched_tokens,
                                 max_model_len=s.max_model_len, block_size=s.kv_block,
                                 kv_cache_gb=s.kv_cache_gb or None, use_cuda_graph=s.cuda_graphs,
-                                enable_prefix_caching=s.prefix_caching, seed=s.seed)
+                                enable_prefix_caching=s.prefix_caching, mixed_batches=s.mixed_batches, seed=s.seed)
             self.engine = LLMEngine(model, self.tokenizer, ecfg)
             from . import metrics as M
 

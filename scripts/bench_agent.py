@@ -83,7 +83,8 @@ def main():
     s = Settings(qwen_model=args.model, embed_model=args.encoder, qwen_max_output=args.gen_len,
                  max_num_seqs=max(8, 2 * args.concurrency), max_model_len=8192, worker_max_jobs=args.concurrency,
                  max_rag_attempts=args.max_iters, default_namespace="default", job_timeout_s=1800,
-                 engine_watchdog_s=600, llm_retries=0, seed=rank, data_dir=None)
+                 engine_watchdog_s=600, llm_retries=0, seed=rank, data_dir=None,
+                 mixed_batches=bool(int(os.environ.get("MIXED_BATCHES", "0"))))
     t0 = time.perf_counter()
     rt = RAGRuntime(s, device=str(dev))
     log(f"runtime ready in {time.perf_counter() - t0:.1f}s (decoder {args.model}, encoder {args.encoder})")

@@ -157,3 +157,52 @@ def test_wordpiece_basic():
     assert all(0 <= i < 2048 for i in ids)
     assert wp.encode("hello world", 64) == wp.encode("HELLO world", 64)  # lowercasing
     assert np.asarray(wp.encode("x " * 500, 32)).shape == (32,)
+
+
+def test_prefix_aware_admission_defers_duplicates(model, tok):
+    """Prompts submitted together that share their first blocks: the first is
+    prefilled, the others are deferred one step and hit the prefix cache —
+    outputs identical to an engine without prefix caching."""
+    base = [(7 * i) % 480 + 10 for i in range(300)]  # 300 shared tokens > SIG_BLOCKS * 16
+    prompts = [base + [1], base + [2], base + [3]]
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_model_len=512, num_blocks=256,
+                                             use_cuda_graph=False))
+    outs = eng.generate(prompts, GREEDY)
+    assert sum(o.cached_tokens >= 256 for o in outs) == 2
+    _, ref = _gen(model, tok, prompts=prompts, enable_prefix_caching=False)
+    assert [o.token_ids for o in outs] == [o.token_ids for o in ref]
+
+
+def test_priority_admission_order(model, tok):
+    """A high-priority request jumps the waiting queue (FCFS within a priority)."""
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=1, max_model_len=512, num_blocks=256,
+                                             use_cuda_graph=False))
+    lo = SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True)
+    hi = SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True, priority=1)
+    ids = [eng.add_request([5, 6, 7], lo)]
+    eng.step()  # the first request is running; the next ones queue behind it
+    ids += [eng.add_request([8, 9], lo), eng.add_request([3, 4], hi), eng.add_request([1, 2], hi)]
+    while eng.has_unfinished():
+        eng.step()
+    order = sorted(ids, key=lambda r: eng.get(r).first_token_time)
+    assert order == [ids[0], ids[2], ids[3], ids[1]]
+
+
+def test_mixed_prefill_decode_steps_identical(model, tok):
+    """Decode tokens riding along in prefill steps (one weight pass for both)
+    give the same greedy outputs as separate prefill / decode steps."""
+    def run(mixed):
+        eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_model_len=512, num_blocks=256,
+                                                 max_num_batched_tokens=24, use_cuda_graph=False,
+                                                 mixed_batches=mixed))
+        ids = [eng.add_request(PROMPTS[0], GREEDY)]
+        for p in PROMPTS[1:]:  # later arrivals prefill (in 24-token chunks) while the first decodes
+            eng.step()
+            ids.append(eng.add_request(p, GREEDY))
+        while eng.has_unfinished():
+            eng.step()
+        return [eng.get(r).output_ids for r in ids], eng.stats["mixed_steps"]
+
+    a, n_mixed = run(True)
+    b, n_sep = run(False)
+    assert a == b and n_mixed > 0 and n_sep == 0
