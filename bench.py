@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--nprobe", type=int, default=32)
     ap.add_argument("--batch", type=int, default=64, help="queries per GPU per step")
     ap.add_argument("--inflight", type=int, default=3, help="batches' worth of queries in flight (1 = closed batch)")
-    ap.add_argument("--arrival-groups", type=int, default=16, help="queries of a step arrive in this many groups")
+    ap.add_argument("--arrival-groups", type=int, default=8, help="queries of a step arrive in this many groups")
     ap.add_argument("--prompt-len", type=int, default=1024)
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--top-k", type=int, default=10)

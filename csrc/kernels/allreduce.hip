@@ -1,0 +1,161 @@
+// One-shot all-reduce over IPC-mapped peer buffers (the TP
+// all-reduce of Qwen2 o_proj / down_proj at decode is latency-bound — 7 KB per
+// sequence row — so instead of a ring (one xGMI link per direction, 2(W-1)
+// dependent hops) every rank reads all W-1 peers' copies directly, which
+// drives all 7 xGMI links of an MI355X at once and costs one signal round).
+//
+// Per rank, one uncached (fine-grained, system-coherent) region, exported with
+// hipIpcGetMemHandle and opened by every peer:
+//     [ flags: kMaxBlocks x kMaxRanks uint32 | pad | data: 2 slots x slot_bytes ]
+// Block b of every rank owns the same element range R_b, so no grid-wide
+// barrier is needed:
+//   1. read+bump this block's private epoch counter e (regular device memory;
+//      identical on all ranks because every call launches the same grid);
+//   2. copy x[R_b] into my data slot (e & 1), fence (system scope);
+//   3. signal: store e into peer p's flags[b][rank] for every peer (release);
+//   4. wait until my flags[b][p] >= e for every peer (acquire; bounded spin —
+//      on timeout set *err and return, so a lost peer can never hang the GPU);
+//   5. out[R_b] = sum_r slot_r[R_b] in rank order (fp32 accumulate), so every
+//      rank produces bit-identical results.
+// Double buffering by epoch parity makes step 2 of call k+2 safe: a peer only
+// signals call k+1 after its kernel k (which read slot k & 1) has finished.
+// The peer pointers are a by-value kernel argument, so the launch is
+// hipGraph-capturable; in-place (out == x) is allowed.
+#include "common.h"
+
+#include <cstring>
+
+using namespace grag;
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 256;
+constexpr int kThreads = 512;
+
+struct Peers {
+  const bf16* data[kMaxRanks];
+  unsigned* flags[kMaxRanks];
+};
+
+__device__ __forceinline__ void st_release_sys(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned ld_acquire_sys(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int W>
+__global__ __launch_bounds__(kThreads) void ar_oneshot_kernel(Peers peers, int rank, const bf16* __restrict__ x,
+                                                              bf16* out, long n8, long slot_elems,
+                                                              unsigned* __restrict__ epochs, unsigned* err,
+                                                              long spin_max) {
+  __shared__ unsigned s_epoch;
+  __shared__ int s_fail;
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) {
+    s_epoch = epochs[b] + 1u;
+    epochs[b] = s_epoch;
+    s_fail = 0;
+  }
+  __syncthreads();
+  const unsigned ep = s_epoch;
+  const long off = (long)(ep & 1u) * slot_elems;
+  // block b's range of 16-B vectors
+  const long per = (n8 + gridDim.x - 1) / gridDim.x;
+  const long v0 = (long)b * per, v1 = min(n8, v0 + per);
+  bf16x8_t* mine = reinterpret_cast<bf16x8_t*>(const_cast<bf16*>(peers.data[rank]) + off);
+  const bf16x8_t* xv = reinterpret_cast<const bf16x8_t*>(x);
+  for (long i = v0 + threadIdx.x; i < v1; i += kThreads) mine[i] = xv[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < W && threadIdx.x != rank)
+    st_release_sys(&peers.flags[threadIdx.x][b * kMaxRanks + rank], ep);
+  if (threadIdx.x < W && threadIdx.x != rank) {
+    const unsigned* f = &peers.flags[rank][b * kMaxRanks + threadIdx.x];
+    long it = 0;
+    while (ld_acquire_sys(f) < ep) {
+      if (++it > spin_max) {
+        atomicOr(err, 1u);
+        s_fail = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  if (s_fail) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: peers' slot data, not stale L1 lines
+  bf16x8_t* ov = reinterpret_cast<bf16x8_t*>(out);
+  for (long i = v0 + threadIdx.x; i < v1; i += kThreads) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+      float v[8];
+      unpack8(reinterpret_cast<const bf16x8_t*>(peers.data[r] + off)[i], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    ov[i] = pack8(acc);
+  }
+}
+
+}  // namespace
+
+// Region layout helpers (host): data offset (bytes) and total size for a slot size.
+GRAG_API long grag_ar_data_offset() { return (long)kMaxBlocks * kMaxRanks * sizeof(unsigned) + 256; }
+GRAG_API long grag_ar_region_bytes(long slot_bytes) { return grag_ar_data_offset() + 2 * slot_bytes; }
+
+// Allocate a zeroed uncached (fine-grained) region that peers can map.
+GRAG_API int grag_ar_alloc(long bytes, void** ptr) {
+  hipError_t e = hipExtMallocWithFlags(ptr, (size_t)bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipMemset(*ptr, 0, (size_t)bytes);
+}
+GRAG_API int grag_ar_free(void* ptr) { return (int)hipFree(ptr); }
+
+GRAG_API int grag_ar_get_handle(void* ptr, void* handle_out /* 64 bytes */) {
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, ptr);
+  if (e == hipSuccess) std::memcpy(handle_out, &h, sizeof(h));
+  return (int)e;
+}
+GRAG_API int grag_ar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+GRAG_API int grag_ar_open_handle(const void* handle /* 64 bytes */, void** ptr) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+GRAG_API int grag_ar_close_handle(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+// regions: host array of W region base pointers (own + opened peers), rank order.
+// n: elements (bf16, multiple of 8, <= slot_bytes / 2); grid: fixed per communicator (<= kMaxBlocks).
+GRAG_API int grag_ar_oneshot(void* const* regions, int W, int rank, const void* x, void* out, long n,
+                             long slot_bytes, void* epochs, void* err, int grid, long spin_max,
+                             hipStream_t stream) {
+  if (W < 1 || W > kMaxRanks || rank < 0 || rank >= W || grid < 1 || grid > kMaxBlocks) return (int)hipErrorInvalidValue;
+  if (n % 8 != 0 || n * 2 > slot_bytes) return (int)hipErrorInvalidValue;
+  Peers p{};
+  const long doff = grag_ar_data_offset();
+  for (int r = 0; r < W; ++r) {
+    p.flags[r] = reinterpret_cast<unsigned*>(regions[r]);
+    p.data[r] = reinterpret_cast<const bf16*>(reinterpret_cast<char*>(regions[r]) + doff);
+  }
+  const long n8 = n / 8, slot_elems = slot_bytes / 2;
+  auto go = [&](auto kern) {
+    kern<<<grid, kThreads, 0, stream>>>(p, rank, (const bf16*)x, (bf16*)out, n8, slot_elems, (unsigned*)epochs,
+                                        (unsigned*)err, spin_max);
+  };
+  switch (W) {
+    case 1: go(ar_oneshot_kernel<1>); break;
+    case 2: go(ar_oneshot_kernel<2>); break;
+    case 3: go(ar_oneshot_kernel<3>); break;
+    case 4: go(ar_oneshot_kernel<4>); break;
+    case 5: go(ar_oneshot_kernel<5>); break;
+    case 6: go(ar_oneshot_kernel<6>); break;
+    case 7: go(ar_oneshot_kernel<7>); break;
+    default: go(ar_oneshot_kernel<8>); break;
+  }
+  return (int)hipGetLastError();
+}

@@ -8,7 +8,8 @@ engine, encoder, index, job workers and API together:
 
   serve    FastAPI app (jobs + SSE, /health, /metrics, /static UI, OpenAI /v1)
            with the in-process job workers; the runtime (models, index) is
-           built once at startup on this process's GPU.
+           built once at startup on this process's GPU.  With TP=N under
+           torchrun the engine is sharded over N GPUs and TP rank 0 serves.
   ingest   ingest repositories (github | local dir | synthetic) into the
            index and optionally snapshot it to INDEX_DIR.
   ask      one RAG query through the agent, printing events as they arrive.
@@ -56,6 +57,21 @@ def cmd_serve(args) -> int:
         logging.getLogger(__name__).info("captured %d decode graphs", n)
         return rt
 
+    if s.tp > 1:
+        # TP serving under torchrun: every rank builds its shard of the engine
+        # now (collective), followers mirror the leader's engine loop, only
+        # TP rank 0 of each group runs the API (port + DP index).
+        from .service.api import APIState
+
+        rt = factory()
+        if not rt.tp_leader:
+            rt.runner.join()
+            return 0
+        port = args.port + (rt.dp_group.rank if rt.dp_group is not None else 0)
+        app = create_app(APIState(runtime=rt))
+        uvicorn.run(app, host=args.host, port=port, log_level=s.log_level.lower())
+        rt.close()
+        return 0
     app = create_app(runtime_factory=factory)
     uvicorn.run(app, host=args.host, port=args.port, log_level=s.log_level.lower())
     return 0

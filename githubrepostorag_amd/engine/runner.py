@@ -7,6 +7,15 @@ is queued, so all of them share continuous batches.  ``generate`` blocks the
 caller (agent threads), ``submit`` returns a handle with a per-token
 callback (SSE token streaming) and supports cancellation.
 
+Tensor parallelism (replicated scheduling): every rank of a TP group runs the
+same engine.  The leader (TP rank 0) owns the request queue; at the top of
+every loop iteration it broadcasts the iteration's new requests (token ids +
+sampling params), aborts and the stop flag over the TP group, and every rank
+applies them and steps.  The scheduler is deterministic given the same
+request stream, so all ranks form the same batches and meet in the same
+collectives; followers only drop their outputs.  ``follow()`` is the
+followers' loop (no API server on those ranks).
+
 Failure handling (SURVEY §5.3 "engine watchdog"): an exception inside a step
 fails every in-flight request and the loop keeps serving; a step that runs
 longer than ``watchdog_s`` (a hung kernel, a wedged collective) is detected by
@@ -52,8 +61,11 @@ class GenerationHandle:
 
 class EngineRunner:
     def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005, watchdog_s: float = 120.0,
-                 on_health=None):
+                 on_health=None, tp=None, start: bool = True):
         self.engine = engine
+        self.tp = tp if tp is not None and not tp.trivial else None
+        self.leader = self.tp is None or self.tp.rank == 0
+        self._aborts: list[str] = []
         self.idle_sleep = idle_sleep
         self.watchdog_s = watchdog_s
         self._on_health = on_health  # callable(bool), e.g. a Prometheus gauge setter
@@ -66,10 +78,12 @@ class EngineRunner:
         self.hung = False
         self.num_faults = 0
         self._step_t0: float | None = None
-        self._thread = threading.Thread(target=self._loop, name="grag-engine", daemon=True)
-        self._thread.start()
+        self._thread = threading.Thread(target=self._loop if self.leader else self.follow, name="grag-engine",
+                                        daemon=True)
+        if start:
+            self._thread.start()
         self._wd = None
-        if watchdog_s and watchdog_s > 0:
+        if watchdog_s and watchdog_s > 0 and self.leader:
             self._wd = threading.Thread(target=self._watchdog, name="grag-engine-watchdog", daemon=True)
             self._wd.start()
 
@@ -90,8 +104,11 @@ class EngineRunner:
         return self.submit(prompt, params, on_token).wait(timeout)
 
     def abort(self, req_id: str) -> None:
-        self.engine.abort(req_id)
         with self._cv:
+            if self.tp is not None:  # applied on every rank at the same iteration
+                self._aborts.append(req_id)
+            else:
+                self.engine.abort(req_id)
             self._cv.notify()
 
     def shutdown(self) -> None:
@@ -120,16 +137,64 @@ class EngineRunner:
                     h.done.set()
         return cb
 
+    # ------------------------------------------------------------------ TP
+    def _bcast(self, msg):
+        import torch.distributed as dist
+
+        obj = [msg]
+        dist.broadcast_object_list(obj, src=self.tp.ranks[0], group=self.tp.pg)
+        return obj[0]
+
+    def follow(self) -> None:
+        """Follower loop of a TP rank: mirror the leader's request stream and
+        step in lockstep until the leader stops."""
+        if self.engine.on_gpu:
+            torch.cuda.set_device(self.engine.device)
+
+        def drop(seq, delta, finished):
+            if finished:
+                self.engine.pop(seq.req_id)
+
+        while True:
+            msg = self._bcast(None)
+            for rid, ids, params in msg["add"]:
+                try:
+                    self.engine.add_request(ids, params, req_id=rid, on_token=drop)
+                except Exception:  # the leader failed the same request
+                    pass
+            for rid in msg["abort"]:
+                self.engine.abort(rid)
+            if msg["stop"]:
+                break
+            if self.engine.has_unfinished():
+                self.engine.step()
+
+    def join(self, timeout: float | None = None) -> None:
+        self._thread.join(timeout)
+
     def _loop(self):
         if self.engine.on_gpu:
             torch.cuda.set_device(self.engine.device)
         while True:
             with self._cv:
-                while not self._stop and not self._pending and not self.engine.has_unfinished():
+                while not self._stop and not self._pending and not self._aborts and not self.engine.has_unfinished():
                     self._cv.wait(timeout=1.0)
-                if self._stop:
-                    break
+                    if self.tp is not None:
+                        break  # idle heartbeat: followers block in the broadcast meanwhile
+                stop = self._stop
                 pending, self._pending = self._pending, []
+                aborts, self._aborts = self._aborts, []
+            if self.tp is not None:
+                adds = []
+                for rid, prompt, params, cb in pending:
+                    ids = self.engine.tok.encode(prompt) if isinstance(prompt, str) else list(prompt)
+                    adds.append((rid, ids, params or SamplingParams()))
+                self._bcast({"add": adds, "abort": aborts, "stop": stop})
+                pending = [(rid, ids, p, cb) for (rid, ids, p), (_, _, _, cb) in zip(adds, pending)]
+            if stop:
+                break
+            if self.tp is not None and not pending and not self.engine.has_unfinished():
+                continue
             for rid, prompt, params, cb in pending:
                 try:
                     self.engine.add_request(prompt, params, req_id=rid, on_token=self._on_token_wrapper(cb))
@@ -138,6 +203,9 @@ class EngineRunner:
                     if h is not None:
                         h.error = e
                         h.done.set()
+            if self.tp is not None:  # after the adds, as the followers do
+                for rid in aborts:
+                    self.engine.abort(rid)
             self._step_t0 = time.monotonic()
             try:
                 self.engine.step()
@@ -181,15 +249,24 @@ class EngineRunner:
             with self._cv:
                 handles, self._handles = self._handles, {}
             for rid, h in handles.items():
-                self.engine.abort(rid)
+                self._abort_mirrored(rid)
                 h.error = err
                 h.done.set()
+
+    def _abort_mirrored(self, rid: str) -> None:
+        """Abort that every TP rank applies at the same iteration (queued for the
+        next broadcast); a plain abort without TP."""
+        if self.tp is not None:
+            with self._cv:
+                self._aborts.append(rid)
+        else:
+            self.engine.abort(rid)
 
     def _fail_all(self, err: BaseException) -> None:
         with self._cv:
             handles, self._handles = self._handles, {}
         for rid, h in handles.items():
-            self.engine.abort(rid)
+            self._abort_mirrored(rid)
             h.error = err
             h.done.set()
         try:  # drop the aborted sequences from the scheduler

@@ -96,8 +96,15 @@ class Group:
     def trivial(self) -> bool:
         return self.size == 1
 
+    custom_ar = None  # parallel.custom_ar.IpcAllReduce: one-shot xGMI all-reduce for small messages
+
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        """C1: small bf16 messages (decode [B, hidden]) take the one-shot IPC
+        all-reduce when attached; everything else goes to RCCL / gloo."""
         if not self.trivial:
+            ar = self.custom_ar
+            if ar is not None and ar.fits(t):
+                return ar.all_reduce(t)
             dist.all_reduce(t, group=self.pg)
         return t
 

@@ -31,6 +31,19 @@ class RAGRuntime:
     def __init__(self, settings: Settings | None = None, device: str | None = None, llm=None, ingest_llm=None,
                  embedder: Embedder | None = None, store: VectorStore | None = None, build_engine: bool = True):
         self.settings = s = settings or get_settings()
+        # TP serving (TP=N under torchrun): one process per GPU, the engine's
+        # weights sharded over the TP group, replicated scheduling
+        # (engine/runner.py); TP rank 0 of each group serves the API.
+        self.tp_group = self.dp_group = None
+        if s.tp > 1 and build_engine and llm is None:
+            from ..parallel import comm
+            from ..parallel.custom_ar import enable_for_group
+
+            info = comm.init_distributed()
+            if device is None and torch.cuda.is_available():
+                device = f"cuda:{info.local_rank}"
+            self.tp_group, self.dp_group = comm.make_tp_dp_groups(s.tp)
+            enable_for_group(self.tp_group, device or s.resolved_device())
         self.device = torch.device(device or s.resolved_device())
         self.started = time.time()
         dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
@@ -57,7 +70,8 @@ class RAGRuntime:
         if llm is None and build_engine:
             dcfg = decoder_config(s.qwen_model)
             sd = load_state_dict(s.model_dir) if s.model_dir else None
-            model = build_decoder(dcfg, device=self.device, dtype=dtype, seed=s.seed + 1, state_dict=sd)
+            model = build_decoder(dcfg, device=self.device, dtype=dtype, seed=s.seed + 1, state_dict=sd,
+                                  tp=self.tp_group)
             self.tokenizer = load_tokenizer(s.model_dir, dcfg.vocab_size, dcfg.arch)
             ecfg = EngineConfig(max_num_seqs=s.max_num_seqs, max_num_batched_tokens=s.max_num_batched_tokens,
                                 max_model_len=s.max_model_len, block_size=s.kv_block,
@@ -68,7 +82,8 @@ class RAGRuntime:
 
             M.ENGINE_HEALTHY.set(1)
             self.runner = EngineRunner(self.engine, watchdog_s=s.engine_watchdog_s,
-                                       on_health=lambda ok: M.ENGINE_HEALTHY.set(1 if ok else 0))
+                                       on_health=lambda ok: M.ENGINE_HEALTHY.set(1 if ok else 0),
+                                       tp=self.tp_group)
             llm = MeteredLLM(EngineLLM(self.runner, self.tokenizer, max_tokens=s.qwen_max_output,
                                        timeout_s=s.job_timeout_s, retries=s.llm_retries))
             ingest_llm = EngineLLM(self.runner, self.tokenizer, max_tokens=2048, mode="ingest",
@@ -77,14 +92,19 @@ class RAGRuntime:
         self.llm = llm
         self.ingest_llm = ingest_llm or llm
 
+    @property
+    def tp_leader(self) -> bool:
+        """True on the rank that owns the request queue (always without TP)."""
+        return self.runner is None or self.runner.leader
+
     def warmup(self, contexts=(1024, 2048, 4096), windows=(1, 2, 4, 8)) -> int:
         """Capture the decode graphs a serving mix needs at startup (batch
         buckets up to MAX_NUM_SEQS x decode windows x split plans of the
         given context lengths), as vLLM does, so no capture stalls a live
         request.  The engine thread must be idle (call before serving)."""
         eng = self.engine
-        if eng is None or not eng.on_gpu:
-            return 0
+        if eng is None or not eng.on_gpu or (self.tp_group is not None and not self.tp_group.trivial):
+            return 0  # TP: the engine threads already step in lockstep; graphs capture on first use
         from ..engine.sequence import SamplingParams
 
         # admit one request with the worker's sampling knobs first: graphs are keyed on the sampler chain
@@ -105,6 +125,9 @@ class RAGRuntime:
 
     def health(self) -> dict:
         out = {"device": str(self.device), "tables": self.store.counts()}
+        if self.tp_group is not None and not self.tp_group.trivial:
+            out["tp"] = {"size": self.tp_group.size, "rank": self.tp_group.rank,
+                         "custom_allreduce": self.tp_group.custom_ar is not None}
         if self.runner is not None:
             out["engine"] = {"healthy": self.runner.healthy, **{k: v for k, v in self.runner.stats().items()
                                                                  if isinstance(v, (int, float))}}

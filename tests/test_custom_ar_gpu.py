@@ -1,0 +1,114 @@
+"""One-shot xGMI all-reduce (csrc/kernels/allreduce.hip, parallel/custom_ar.py).
+
+The gpurun box has ONE GPU, so the protocol is exercised two ways:
+* simulated ranks: W communicators over W regions in one process, each
+  rank's launch on its own stream so the W kernels run concurrently and
+  signal each other through the flag words (epochs, double buffering,
+  in-place and out-of-place, repeated calls); checked against an fp32 sum
+  and for bit-identical results on every rank;
+* IPC plumbing: two processes on the same device export / open each
+  other's uncached regions with hipIpcGetMemHandle / hipIpcOpenMemHandle
+  (handles exchanged over gloo) and read each other's data.
+The bounded spin makes a lost peer a test failure (err flag), never a hang.
+"""
+import ctypes
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+# W = 2: simulated ranks need their kernels co-resident, i.e. each stream on its
+# own hardware queue; the box runs GPU_MAX_HW_QUEUES=4 per process and measured
+# 3 streams already sharing one (the 3rd rank then serialised behind another
+# and, by design, timed out with the err flag instead of hanging).  Real ranks
+# are separate processes on separate GPUs.
+@pytest.mark.parametrize("W", [2])
+def test_oneshot_simulated_ranks(dev, W):
+    from githubrepostorag_amd.parallel.custom_ar import IpcAllReduce
+
+    comms = IpcAllReduce.simulated(W, dev, slot_bytes=1 << 20, grid=32)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(W)]
+    g = torch.Generator(device="cpu").manual_seed(W)
+    try:
+        for it, n in enumerate([8, 4096, 3584 * 7, 3584 * 64, 8 * 1000] * 4):  # epochs cycle both slots
+            xs = [(torch.randn(n, generator=g) * (r + 1)).to(torch.bfloat16).to(dev) for r in range(W)]
+            ref = sum(x.float() for x in xs)
+            inplace = it % 2 == 0
+            outs = [x.clone() if inplace else torch.empty_like(x) for x in xs]
+            torch.cuda.synchronize()
+            for r in range(W):
+                with torch.cuda.stream(streams[r]):
+                    comms[r].all_reduce(outs[r] if inplace else xs[r], out=None if inplace else outs[r],
+                                        stream=streams[r])
+            torch.cuda.synchronize()
+            for r in range(W):
+                assert not comms[r].failed(), f"rank {r} timed out waiting for peers"
+                assert torch.allclose(outs[r].float(), ref, atol=0.05 * W, rtol=1e-2)
+                assert torch.equal(outs[r], outs[0])  # every rank sums in the same order
+    finally:
+        for c in comms:
+            c.close()
+
+
+def _hip():
+    return ctypes.CDLL("libamdhip64.so")
+
+
+def _ipc_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from githubrepostorag_amd.ops._lib import check
+    from githubrepostorag_amd.parallel.custom_ar import _alloc, _fn
+
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        nbytes = 1 << 16
+        base = _alloc(nbytes)
+        mine = torch.full((nbytes // 4,), float(rank + 7), device="cuda")
+        hip = _hip()
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        assert hip.hipMemcpy(base, mine.data_ptr(), nbytes, 3) == 0
+        hs = int(_fn("grag_ar_handle_size")())
+        buf = ctypes.create_string_buffer(hs)
+        check(_fn("grag_ar_get_handle")(base, buf), "get_handle")
+        handles = [None] * world
+        dist.all_gather_object(handles, bytes(buf.raw))
+        peer = 1 - rank
+        p = ctypes.c_void_p()
+        check(_fn("grag_ar_open_handle")(ctypes.create_string_buffer(handles[peer], hs), ctypes.byref(p)), "open")
+        got = torch.empty(nbytes // 4, device="cuda")
+        assert hip.hipMemcpy(got.data_ptr(), p.value, nbytes, 3) == 0
+        ok = bool(torch.all(got == float(peer + 7)).item())
+        dist.barrier()
+        _fn("grag_ar_close_handle")(p.value)
+        dist.barrier()
+        _fn("grag_ar_free")(base)
+        dist.destroy_process_group()
+        q.put((rank, ok, ""))
+    except Exception as e:  # report, never hang the parent
+        q.put((rank, False, repr(e)))
+
+
+def test_ipc_regions_two_processes():
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ipc_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=90) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+    assert all(ok for _, ok, _ in res), res

@@ -5,7 +5,11 @@ import re
 from pathlib import Path
 
 from githubrepostorag_amd.ops._lib import _SIGS as KSIGS
+from githubrepostorag_amd.parallel.custom_ar import _SIGS as _AR_SIGS
 from githubrepostorag_amd.utils.runtime import _SIGS as RSIGS
+
+# the one-shot all-reduce binds its entry points itself (argtypes, restype)
+KSIGS = {**KSIGS, **{k: v[0] for k, v in _AR_SIGS.items()}}
 
 ROOT = Path(__file__).resolve().parents[1]
 

@@ -124,3 +124,59 @@ def test_sharded_index_matches_flat():
         # the merged ids are a true top-k up to bf16 score ties
         assert torch.allclose(exact.gather(1, got), ref.values, atol=2e-2)
         assert torch.allclose(torch.tensor(s), ref.values, atol=2e-2)
+
+
+def _tp_runner_worker(rank, world, cfg_name):
+    """TP=2 serving: the leader's runner takes requests and broadcasts them;
+    the follower mirrors the stream and steps in lockstep (replicated
+    scheduling), meeting the leader in every TP collective."""
+    from githubrepostorag_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from githubrepostorag_amd.engine.runner import EngineRunner
+    from githubrepostorag_amd.engine.sequence import SamplingParams
+    from githubrepostorag_amd.engine.tokenizer import ByteBPETokenizer
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import Qwen2Model
+    from githubrepostorag_amd.parallel.comm import make_tp_dp_groups
+
+    cfg = decoder_config(cfg_name)
+    tp, _ = make_tp_dp_groups(world)
+    model = Qwen2Model(cfg, device="cpu", dtype=torch.float32, tp=tp, state_dict=_hf_state_dict(cfg))
+    eng = LLMEngine(model, ByteBPETokenizer(cfg.vocab_size),
+                    EngineConfig(max_num_seqs=4, max_model_len=256, num_blocks=64, use_cuda_graph=False))
+    runner = EngineRunner(eng, tp=tp, watchdog_s=0)
+    if rank != 0:
+        runner.join(120)
+        return None
+    import threading
+
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    prompts = [[5, 17, 99, 3, 250], [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]]
+    out = [None, None]
+
+    def ask(i):  # concurrent clients, like agent job threads
+        out[i] = runner.generate(prompts[i], sp, timeout=60).token_ids
+
+    th = [threading.Thread(target=ask, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    h = runner.submit([9, 9, 9, 9], SamplingParams(max_tokens=200, temperature=0.0, ignore_eos=True))
+    h.cancel()  # aborts are mirrored at the same iteration on every rank
+    try:
+        h.wait(30)
+    except Exception:
+        pass
+    runner.shutdown()
+    return out
+
+
+def test_tp_runner_replicated_scheduling():
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import Qwen2Model
+
+    cfg = decoder_config("qwen2-tiny")
+    ref = _generate(Qwen2Model(cfg, device="cpu", dtype=torch.float32, state_dict=_hf_state_dict(cfg)),
+                    [[5, 17, 99, 3, 250], [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]])
+    res = run_ranks(_tp_runner_worker, 2, "qwen2-tiny")
+    assert res[0] == ref and res[1] is None
