@@ -8,7 +8,12 @@ from pathlib import Path
 import torch
 
 
-def load_state_dict(path: str | Path | None) -> dict | None:
+def load_state_dict(path: str | Path | None, device=None) -> dict | None:
+    """All tensors of a safetensors checkpoint (file, directory or sharded
+    index).  AutoAWQ W4A16 checkpoints (the reference's deployed
+    Qwen2.5-Coder-7B-Instruct-AWQ, helm/values.yaml:67) are dequantised to
+    bf16 HF-layout ``.weight`` tensors — on ``device`` with the HIP kernel
+    when it is a GPU (ops/quant.py)."""
     if not path:
         return None
     from safetensors.torch import load_file
@@ -24,6 +29,10 @@ def load_state_dict(path: str | Path | None) -> dict | None:
     sd: dict = {}
     for f in files:
         sd.update(load_file(str(f)))
+    if any(k.endswith(".qweight") for k in sd):
+        from ..ops.quant import dequantize_awq_state_dict
+
+        sd = dequantize_awq_state_dict(sd, device=device)
     return sd
 
 

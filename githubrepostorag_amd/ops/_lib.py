@@ -48,6 +48,7 @@ _SIGS = {
     "grag_gemm_skinny": [P, P, P, P, I, I, I, I, I, I, I, P],
     "grag_gemm_stream": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "grag_gemm_stream_plan": [I, I, I, I, P],
+    "grag_awq_dequant": [P, P, P, P, I, I, I, P],
 }
 
 

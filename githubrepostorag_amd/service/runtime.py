@@ -69,7 +69,7 @@ class RAGRuntime:
         self.engine = self.runner = None
         if llm is None and build_engine:
             dcfg = decoder_config(s.qwen_model)
-            sd = load_state_dict(s.model_dir) if s.model_dir else None
+            sd = load_state_dict(s.model_dir, device=self.device) if s.model_dir else None
             model = build_decoder(dcfg, device=self.device, dtype=dtype, seed=s.seed + 1, state_dict=sd,
                                   tp=self.tp_group)
             self.tokenizer = load_tokenizer(s.model_dir, dcfg.vocab_size, dcfg.arch)
