@@ -82,3 +82,29 @@ def test_multistep_window_sampling_and_stop(setup):
                          stop_token_ids=[stop_at])
     c = mk(True).generate(_prompts(tok), sp2)
     assert c[2].token_ids == a[2].token_ids[: first + 1] and c[2].finish_reason == "stop"
+
+
+def test_long_context_chunked_prefill_and_split_kv_decode(dev):
+    """prompts past the reference's --max-model-len (11712) up to
+    32K run on one GPU through chunked prefill (4096-token chunks attending to
+    the paged context) and split-KV decode; the generated tokens must match a
+    one-token recompute of the full prefix in a single unchunked prefill."""
+    cfg = decoder_config("qwen2-small", max_position=32768)
+    model = Qwen2Model(cfg, device=dev, seed=5)
+    tok = ByteBPETokenizer(cfg.vocab_size)
+    g = torch.Generator().manual_seed(11)
+    prompts = [torch.randint(10, 4000, (n,), generator=g).tolist() for n in (12000, 30000)]
+    sp = SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True)
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_num_batched_tokens=4096, max_model_len=32768,
+                                             num_blocks=4096))
+    outs = eng.generate(prompts, sp)
+    assert all(len(o.token_ids) == 4 for o in outs)
+    ref = LLMEngine(model, tok, EngineConfig(max_num_seqs=1, max_num_batched_tokens=32768, max_model_len=32768,
+                                             num_blocks=2304, enable_prefix_caching=False, use_cuda_graph=False))
+    agree = total = 0
+    for p, o in zip(prompts, outs):
+        for j in range(len(o.token_ids)):
+            r = ref.generate([p + o.token_ids[:j]], SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))
+            agree += int(r[0].token_ids[0] == o.token_ids[j])
+            total += 1
+    assert agree / total >= 0.75, (agree, total)
