@@ -194,6 +194,35 @@ def use_stream(M: int, N: int, K: int) -> bool:
     return M <= 32 and N >= 65536
 
 
+_SPLITK_ON = os.environ.get("GRAG_SPLITK", "1") != "0"
+SPLITK_S = 8
+
+
+def use_splitk(M: int, N: int, K: int) -> bool:
+    """Deep-K projections (down_proj: K = 18944 = 5.3 N) at large decode
+    batches: hipBLASLt has only N/tile x M/tile output tiles (~56 workgroups
+    for 256 CUs) and no split-K solution in the tuned table.  Cold-weight
+    hipGraph timings (scripts/bench_splitk.py, profiles/splitk_decode_gemm.jsonl),
+    down_proj N=3584: M=160 105.7 -> 62.7 us, 192 75.9 -> 66.3, 224 117.4 -> 70.0,
+    256 77.0 -> 56.7; at M <= 128 and for o/qkv/gate_up the library wins."""
+    return _SPLITK_ON and M > 128 and K >= 4 * N and K % (SPLITK_S * 64) == 0
+
+
+def gemm_splitk(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+    """Split-K over the library: S strided-batched GEMMs of K/S slices (one
+    hipBLASLt launch, S x more workgroups) with fp32 output, reduced in fp32
+    — no weight copy (the slices are strided views of ``w``)."""
+    M, K = x.shape
+    N = w.shape[0]
+    S = SPLITK_S
+    xs = x.view(M, S, K // S).transpose(0, 1)
+    ws = w.view(N, S, K // S).transpose(0, 1).transpose(1, 2)
+    y = torch.bmm(xs, ws, out_dtype=torch.float32).sum(0)
+    if b is not None:
+        y += b.float()
+    return y.to(x.dtype)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
     """y = x @ w.T (+ b); w is [out, in] (K-contiguous, TN GEMM)."""
     if not x.is_cuda:
@@ -207,6 +236,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> t
             and x.stride(1) == 1 and w.stride(1) == 1):
         M, K = x.shape
         N = w.shape[0]
+        if use_splitk(M, N, K):
+            return gemm_splitk(x, w, b)
         choice = measured_choice(M, N, K)
         if choice == "library":
             return torch.nn.functional.linear(x, w, b)

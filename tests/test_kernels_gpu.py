@@ -319,3 +319,19 @@ def test_sampler_matches_reference_stream(dev):
             b = S.sample_ref(logits, st_c, slots)
             agree += int((a == b).sum())
     assert agree >= 3 * B - 2, agree
+
+
+@pytest.mark.parametrize("M", [160, 192, 256])
+def test_linear_splitk_down_proj(dev, M):
+    """Deep-K decode GEMMs at large batches dispatch to the split-K library
+    path (fp32 partials reduced in fp32); numerics vs the fp32 reference."""
+    from githubrepostorag_amd.ops.linear import gemm_splitk, linear, use_splitk
+
+    N, K = 3584, 18944
+    assert use_splitk(M, N, K) and not use_splitk(128, N, K) and not use_splitk(M, 37888, 3584)
+    x = rnd(M, K, dev=dev, scale=0.5)
+    w = rnd(N, K, dev=dev, scale=0.05, seed=1)
+    b = rnd(N, dev=dev, seed=2)
+    ref = x.float().cpu() @ w.float().cpu().T
+    close(linear(x, w), ref, 3e-2, 2e-2)
+    close(gemm_splitk(x, w, b), ref + b.float().cpu(), 3e-2, 2e-2)
