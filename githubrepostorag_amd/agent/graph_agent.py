@@ -176,13 +176,15 @@ class GraphAgent:
         filters = dict(st.get("filters") or {})
         if self.namespace:
             filters.setdefault("namespace", self.namespace)
-        rh = extract_repo_hint(q)
+        rh = st.get("repo") or extract_repo_hint(q)
         if rh:
             filters["repo"] = rh
         try:
             data = _json_object(self._complete(prompts.plan_scope(q), ctx, "plan").strip())
             scope = data.get("scope") or ("code" if looks_codey(q) else "project")
             _merge_filters(filters, data.get("filters"))
+            if st.get("repo"):  # an explicit repo_name pins the filter
+                filters["repo"] = st["repo"]
         except Cancelled:
             raise
         except Exception as e:
@@ -204,6 +206,8 @@ class GraphAgent:
         ctx.check()
         scope, q = st["scope"], st["query"]
         filters = st.get("filters") or {}
+        if st.get("repo") and filters.get("repo") != st["repo"]:  # judge suggestions cannot unpin it
+            filters = {**filters, "repo": st["repo"]}
         attempt = st.get("attempt", 0)
         docs = self._search(scope, q, filters, ctx)
         n0 = len(docs)
@@ -229,6 +233,8 @@ class GraphAgent:
                 ctx.notify({"stage": "retrieve_expanded", "original_hits": n0, "expanded_hits": len(docs),
                             "expanded_queries": expanded})
         docs = sorted(docs, key=lambda d: score_of(d) or 0.0, reverse=True)
+        if st.get("top_k"):
+            docs = docs[: int(st["top_k"])]
         ctx.turns.append({"stage": "retrieve", "scope": scope, "filters": dict(filters), "hits": len(docs),
                           "original_hits": n0, "attempt": attempt})
         ctx.notify({"stage": "retrieve", "scope": scope, "filters": dict(filters), "hits": len(docs)})
@@ -354,10 +360,15 @@ class GraphAgent:
 
     # ------------------------------------------------------------------ run
     def run(self, question: str, *, namespace: str | None = None, progress_cb=None, cancel_check=None,
-            force_level: str | None = None, on_answer_token=None, trace=None) -> dict:
+            force_level: str | None = None, on_answer_token=None, trace=None, repo: str | None = None,
+            top_k: int | None = None) -> dict:
+        """``repo`` / ``top_k`` are the API's ``QueryRequest.repo_name`` /
+        ``top_k``, which the reference accepts but never reads
+        (rag_shared/models.py:6-14): here ``repo`` pins the repo
+        filter of every retrieval and ``top_k`` caps the retrieved documents."""
         ctx = RunContext(progress_cb, cancel_check, on_answer_token, trace=trace or NULL_TRACE)
         tr = ctx.trace
-        st: dict = {"query": question, "force_level": force_level}
+        st: dict = {"query": question, "force_level": force_level, "repo": repo, "top_k": top_k}
         ns = namespace or self.namespace
         if ns:
             st["filters"] = {"namespace": ns}

@@ -31,7 +31,7 @@ from ..config import settings as get_settings
 from ..service import metrics as M
 from .extractors import ExtractorPipeline
 from .hierarchy import ROLLUP_PRIORITY, HierarchyBuilder
-from .preprocess import infer_component_kind, prepare_repo_documents
+from .preprocess import infer_component_kind, prepare_repo_documents, top_directory
 from .readers import GithubReader, LocalDirReader, SyntheticRepoReader, fetch_repositories
 from .splitters import DynamicCodeSplitter
 from .writer import VectorWriter
@@ -88,6 +88,10 @@ def attach_common_metadata(nodes, *, namespace, repo, branch, collection, compon
                   is_standalone=is_standalone, dev_forced_standalone=dev_forced, ingest_run_id=str(run_id))
         md.setdefault("doc_type", doc_type)
         md.setdefault("path", md.get("file_path"))
+        if md.get("file_path") and "module" not in md:
+            # chunks get their module too (the reference never sets it, so its
+            # module edge/filter is empty at code scope: SURVEY §2.11-10)
+            md["module"] = top_directory(md["file_path"], 1)
         md["scope"] = DOC_TYPE_TO_SCOPE.get(doc_type, "chunk")
 
 

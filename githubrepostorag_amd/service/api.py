@@ -95,7 +95,10 @@ def create_app(state: APIState | None = None, runtime_factory=None) -> FastAPI:
         if state.queue is None:
             raise HTTPException(503, "worker queue not ready")
         job_id = uuid.uuid4().hex
-        await state.queue.enqueue_job("run_rag_job", job_id, req.model_dump())
+        body = req.model_dump()
+        if "top_k" not in req.model_fields_set:
+            body["top_k"] = None  # only an explicit top_k caps the retrieved documents
+        await state.queue.enqueue_job("run_rag_job", job_id, body)
         return {"job_id": job_id}
 
     @app.get("/rag/jobs/{job_id}/events")

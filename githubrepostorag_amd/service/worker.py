@@ -142,7 +142,8 @@ class RAGWorker:
                 lambda: agent.run(query, namespace=namespace, progress_cb=progress,
                                   cancel_check=lambda: self.flags.is_cancelled_sync(job_id),
                                   force_level=forced, on_answer_token=on_token if self.stream_tokens else None,
-                                  trace=trace))
+                                  trace=trace, repo=req.get("repo_name") or None,
+                                  top_k=req.get("top_k") or None))
             M.WORKER_RETRIEVAL_DURATION.observe(time.perf_counter() - t_rag)
             sources = result.get("sources") or []
             debug = result.get("debug") or {}

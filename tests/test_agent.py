@@ -71,6 +71,23 @@ def test_force_level_and_repo_hint():
     assert extract_repo_hint("look at repo:billing-api please") in ("billing-api", None)
 
 
+def test_repo_name_pins_filter_and_top_k_caps_docs():
+    """QueryRequest.repo_name / top_k (accepted but ignored by the reference)
+    pin the repo filter against the planner's and judge's suggestions and cap
+    the retrieved documents."""
+    plan = json.dumps({"scope": "code", "filters": {"repo": "other-repo"}})
+    judges = iter([json.dumps({"coverage": 0.1, "needs_more": True, "suggest_filters": {"repo": "x"}}),
+                   json.dumps({"coverage": 0.9, "needs_more": False})])
+    rs = _retrievers(n=6)
+
+    def reply(p):
+        return next(judges) if p.startswith("Judge if") else _router(plan=plan)(p)
+
+    out = GraphAgent(ScriptedLLM(reply), rs).run("where is the retry loop?", repo="payments", top_k=2)
+    assert rs["code"].calls and all(f["repo"] == "payments" for _, f in rs["code"].calls)
+    assert len(out["sources"]) == 2
+
+
 def test_judge_stage_down_and_rewrite_loop():
     judges = iter([json.dumps({"coverage": 0.1, "needs_more": True, "stage_down": "file"}),
                    json.dumps({"coverage": 0.9, "needs_more": False})])

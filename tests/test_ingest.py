@@ -222,3 +222,16 @@ def test_synthetic_reader_deterministic():
     b = SyntheticRepoReader(5).load_data("same")
     assert [d.text for d in a] == [d.text for d in b]
     assert torch.tensor(0).item() == 0
+
+
+def test_chunk_nodes_get_module_metadata():
+    """the reference never stamps ``module`` on chunk nodes,
+    leaving its module edge/filter empty at code scope."""
+    from githubrepostorag_amd.ingest.controller import attach_common_metadata
+    from githubrepostorag_amd.ingest.readers import Node
+
+    n = Node(text="def f(): pass", metadata={"file_path": "billing/api/handlers.py"})
+    attach_common_metadata([n], namespace="default", repo="r", branch="main", collection="misc",
+                           component_kind="service", is_standalone=False, run_id="0", dev_forced=False,
+                           doc_type="chunk")
+    assert n.metadata["module"] == "billing" and n.metadata["scope"] == "chunk"
