@@ -116,12 +116,12 @@ __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
 // its issue slots on 64-bit div/mod).
 constexpr int kSiluRows = 8;
 __global__ __launch_bounds__(kThreads) void silu_mul_kernel(const bf16* __restrict__ gu,
-                                                            bf16* __restrict__ out, int T, int I) {
+                                                            bf16* __restrict__ out, int T, int I, int rows) {
   const int nvec = I >> 3;
   const int v = blockIdx.x * kThreads + threadIdx.x;
   if (v >= nvec) return;
-  const int t0 = blockIdx.y * kSiluRows;
-  const int t1 = min(T, t0 + kSiluRows);
+  const int t0 = blockIdx.y * rows;
+  const int t1 = min(T, t0 + rows);
   const bf16x8_t* src = reinterpret_cast<const bf16x8_t*>(gu) + (size_t)t0 * 2 * nvec + v;
   bf16x8_t* dst = reinterpret_cast<bf16x8_t*>(out) + (size_t)t0 * nvec + v;
 #pragma unroll 4
@@ -257,8 +257,11 @@ GRAG_API int grag_qkv_rope_kvstore(const void* qkv, int ld, const void* bias,
 GRAG_API int grag_silu_mul(const void* gu, void* out, int T, int I, hipStream_t stream) {
   if (T <= 0) return 0;
   if (I % 8 != 0) return (int)hipErrorInvalidValue;
-  dim3 grid((I / 8 + kThreads - 1) / kThreads, (T + kSiluRows - 1) / kSiluRows);
-  silu_mul_kernel<<<grid, kThreads, 0, stream>>>((const bf16*)gu, (bf16*)out, T, I);
+  // decode-sized T: one row per thread so the grid still fills 256 CUs
+  // (T = 192, I = 18944: 240 blocks with 8 rows, 1920 with 1)
+  const int rows = T >= 2048 ? kSiluRows : 1;
+  dim3 grid((I / 8 + kThreads - 1) / kThreads, (T + rows - 1) / rows);
+  silu_mul_kernel<<<grid, kThreads, 0, stream>>>((const bf16*)gu, (bf16*)out, T, I, rows);
   return (int)hipGetLastError();
 }
 

@@ -85,6 +85,9 @@ def test_qkv_rope_kvstore(dev):
 def test_silu_mul_bias_act(dev):
     gu = rnd(17, 2 * 1024, dev=dev)
     close(E.silu_mul(gu), E.silu_mul(gu.cpu()), 2e-2)
+    for T in (192, 2051):  # one row per thread (decode) / 8 rows per thread with a ragged tail (prefill)
+        gu = rnd(T, 2 * 18944, dev=dev, seed=T)
+        close(E.silu_mul(gu), E.silu_mul(gu.cpu()), 2e-2)
     x, b = rnd(17, 1536, dev=dev), rnd(1536, dev=dev, seed=1)
     close(E.bias_act(x, b, E.ACT_GELU), E.bias_act(x.cpu(), b.cpu(), E.ACT_GELU), 2e-2)
 
