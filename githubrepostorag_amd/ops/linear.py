@@ -205,7 +205,9 @@ def use_splitk(M: int, N: int, K: int) -> bool:
     hipGraph timings (scripts/bench_splitk.py, profiles/splitk_decode_gemm.jsonl),
     down_proj N=3584: M=160 105.7 -> 62.7 us, 192 75.9 -> 66.3, 224 117.4 -> 70.0,
     256 77.0 -> 56.7; at M <= 128 and for o/qkv/gate_up the library wins."""
-    return _SPLITK_ON and M > 128 and K >= 4 * N and K % (SPLITK_S * 64) == 0
+    # decode batch range only, and only the measured shape family (Qwen down_proj,
+    # K >= 8192): encoder FFN2 / GPT-2 MLPs at prefill-sized M stay on the library
+    return _SPLITK_ON and 128 < M <= 256 and K >= 8192 and K >= 4 * N and K % (SPLITK_S * 64) == 0
 
 
 def gemm_splitk(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:

@@ -332,6 +332,7 @@ def test_linear_splitk_down_proj(dev, M):
 
     N, K = 3584, 18944
     assert use_splitk(M, N, K) and not use_splitk(128, N, K) and not use_splitk(M, 37888, 3584)
+    assert not use_splitk(1024, N, K) and not use_splitk(M, 1024, 4096)  # prefill M, encoder FFN2
     x = rnd(M, K, dev=dev, scale=0.5)
     w = rnd(N, K, dev=dev, scale=0.05, seed=1)
     b = rnd(N, dev=dev, seed=2)

@@ -1,0 +1,14 @@
+"""Decode-GEMM dispatch rules of ops/linear.py (CPU: predicates only; the
+numerics of every path are in tests/test_kernels_gpu.py)."""
+from githubrepostorag_amd.ops.linear import use_splitk
+
+
+def test_splitk_only_for_decode_sized_deep_k_down_proj():
+    assert use_splitk(192, 3584, 18944) and use_splitk(256, 3584, 18944)  # Qwen2-7B down_proj
+    assert use_splitk(160, 2048, 11008 // 512 * 512)
+    assert not use_splitk(128, 3584, 18944)  # the tuned library wins at M <= 128
+    assert not use_splitk(1024, 3584, 18944)  # prefill-sized M
+    assert not use_splitk(192, 1024, 4096)  # bge-large FFN2
+    assert not use_splitk(192, 768, 3072)  # GPT-2 MLP
+    assert not use_splitk(192, 37888, 3584)  # gate_up (wide N)
+    assert not use_splitk(192, 1536, 8960)  # K not a multiple of 8 x 64

@@ -112,3 +112,4 @@ def test_awq_dequant_kernel_matches_fp32_reference(K, N, G):
     torch.cuda.synchronize()
     assert out.shape == (N, K) and out.dtype == torch.bfloat16
     torch.testing.assert_close(out.float().cpu(), ref, atol=1e-6, rtol=8e-3)
+
