@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="qwen2-7b")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree of the decoder (BASELINE config 4: qwen2-72b --tp 8); "
+                         "TP peers serve the same queries in lockstep, DP = world / tp")
     ap.add_argument("--encoder", default="bge-large-en-v1.5")
     ap.add_argument("--index-size", type=int, default=10_000_000)
     ap.add_argument("--index-kind", default="ivf", choices=["ivf", "flat"])
@@ -87,6 +90,26 @@ def main():
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     dev = torch.device("cuda", info.local_rank) if torch.cuda.is_available() else torch.device("cpu")
     group = comm.world_group()
+    tp = max(1, args.tp)
+    tp_group = dp_group = None
+    dp_rank, dp_size = rank, world
+    if tp > 1:
+        # TP groups of consecutive ranks; every rank of a group runs the same
+        # arrivals (seeded by its DP rank) and steps its shard of the engine in
+        # lockstep (deterministic scheduler + identical sampling seeds).  The
+        # retrieval runs synchronously (no helper thread) so the world-group
+        # search collectives never interleave with the TP all-reduces.
+        from githubrepostorag_amd.parallel.custom_ar import enable_for_group
+
+        tp_group, dp_group = comm.make_tp_dp_groups(tp)
+        if dev.type == "cuda":
+            enable_for_group(tp_group, dev)
+        dp_rank, dp_size = rank // tp, world // tp
+        args.prefetch = 0
+        if not args.no_ingest:
+            args.no_ingest = True  # the ingest engine's runner threads are not TP-replicated here
+            if rank == 0:
+                print("[bench] --tp > 1: ingest phase skipped", file=sys.stderr)
 
     from githubrepostorag_amd.embed.service import Embedder
     from githubrepostorag_amd.engine.llm_engine import EngineConfig, LLMEngine
@@ -103,7 +126,7 @@ def main():
 
     t_setup = time.perf_counter()
     dcfg = decoder_config(args.model)
-    model = Qwen2Model(dcfg, device=dev, seed=1)
+    model = Qwen2Model(dcfg, device=dev, seed=1, tp=tp_group)
     tok = load_tokenizer(None, dcfg.vocab_size)
     emb = Embedder.from_name(args.encoder, device=dev, seed=2)
     log(f"models ready {time.perf_counter() - t_setup:.1f}s  decoder={model.param_bytes() / 1e9:.1f} GB")
@@ -127,7 +150,7 @@ def main():
     u = args.batch // A  # queries per group
     eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max(args.batch * D, 8), max_num_batched_tokens=16384,
                                              max_model_len=max_len, use_cuda_graph=not args.no_graph,
-                                             seed=rank))
+                                             seed=dp_rank))
     sp = SamplingParams(max_tokens=args.gen_len, temperature=0.4, top_p=0.8, repetition_penalty=1.2,
                         ignore_eos=True)
     sys_prompt = ("You are a senior developer assistant. Answer using the provided context blocks. "
@@ -142,7 +165,7 @@ def main():
     def row_text(d: int) -> str:
         return text_pool[d % len(text_pool)]
 
-    qcounter = [rank * 1_000_000]
+    qcounter = [dp_rank * 1_000_000]
     phase = {"embed": 0.0, "search": 0.0, "prompt": 0.0, "generate": 0.0}
 
     # The engine is stepped from this thread between arrivals: a thread per
@@ -288,7 +311,7 @@ def main():
         tt = torch.tensor(ttfts, dtype=torch.float64, device=dev)
         ttfts_all = group.all_gather(tt).cpu().tolist()
     elapsed = float(t.item())
-    total_q = args.batch * args.steps * world
+    total_q = args.batch * args.steps * dp_size
     qps = total_q / elapsed
     p50 = statistics.median([x for r in ttfts_all for x in r]) * 1000.0
     ms_step = elapsed / args.steps * 1000.0
@@ -344,16 +367,16 @@ def main():
             "p50_ttft_ms": round(p50, 2),
             "ingest_docs_per_s": None if ingest_dps is None else round(ingest_dps, 3),
             "config": {
-                "model": f"{args.model} TP=1 + {args.encoder}, {args.index_size}-vec {args.index_kind} index "
+                "model": f"{args.model} TP={tp} + {args.encoder}, {args.index_size}-vec {args.index_kind} index "
                          f"(nlist={args.nlist}, nprobe={args.nprobe}) sharded dp{world}",
-                "global_batch": args.batch * world,
+                "global_batch": args.batch * dp_size,
                 "inflight_batches": D,
                 "arrival_groups": A,
-                "concurrent_seqs": args.batch * D * world,
+                "concurrent_seqs": args.batch * D * dp_size,
                 "seq_len": args.prompt_len,
                 "gen_len": args.gen_len,
                 "top_k": args.top_k,
-                "parallelism": f"dp{world}",
+                "parallelism": f"tp{tp}dp{dp_size}" if tp > 1 else f"dp{world}",
             },
             "engine": eng_stats,
             "engine_per_timed_step": timed_engine,

@@ -38,3 +38,14 @@ def test_bench_two_ranks_gloo():
                env)
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 6 and res["config"]["parallelism"] == "dp2"
     assert res["value"] > 0
+
+
+def test_bench_tensor_parallel_two_ranks_gloo():
+    """--tp 2 on two ranks: one TP group serving one DP replica's queries in
+    lockstep (a desync would hang or fail the run), index sharded over both."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    res = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2",
+                "--tp", "2", *TINY], env)
+    assert res["config"]["parallelism"] == "tp2dp1" and res["config"]["global_batch"] == 3
+    assert res["value"] > 0 and res["ingest_docs_per_s"] is None and "TP=2" in res["config"]["model"]
