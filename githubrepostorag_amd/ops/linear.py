@@ -198,25 +198,37 @@ _SPLITK_ON = os.environ.get("GRAG_SPLITK", "1") != "0"
 SPLITK_S = 8
 
 
+def splitk_parts(M: int, N: int, K: int) -> int:
+    """K-slices for the split-K library path (0 = not taken).  Deep-K
+    projections (down_proj: K = 18944 = 5.3 N) at decode batches: hipBLASLt
+    has only N/tile x M/tile output tiles (~56 workgroups for 256 CUs) and no
+    split-K solution in the tuned table.  Cold-weight hipGraph timings
+    (scripts/bench_splitk.py, profiles/splitk_decode_gemm.jsonl), down_proj
+    N=3584: 8 slices at M=160 105.7 -> 62.7 us, 192 75.9 -> 66.3, 224 117.4 ->
+    70.0, 256 77.0 -> 56.7; 2 slices at M=96 63.5 -> 52.4, M=64 46.5 -> 43.0.
+    At M=128 and for o/qkv/gate_up the library wins.  Decode batch range only,
+    and only the measured shape family (Qwen down_proj, K >= 8192): encoder
+    FFN2 / GPT-2 MLPs / prefill stay on the library."""
+    if not _SPLITK_ON or K < 8192 or K < 4 * N:
+        return 0
+    if 128 < M <= 256 and K % (8 * 64) == 0:
+        return 8
+    if 32 < M <= 96 and K % (2 * 64) == 0:
+        return 2
+    return 0
+
+
 def use_splitk(M: int, N: int, K: int) -> bool:
-    """Deep-K projections (down_proj: K = 18944 = 5.3 N) at large decode
-    batches: hipBLASLt has only N/tile x M/tile output tiles (~56 workgroups
-    for 256 CUs) and no split-K solution in the tuned table.  Cold-weight
-    hipGraph timings (scripts/bench_splitk.py, profiles/splitk_decode_gemm.jsonl),
-    down_proj N=3584: M=160 105.7 -> 62.7 us, 192 75.9 -> 66.3, 224 117.4 -> 70.0,
-    256 77.0 -> 56.7; at M <= 128 and for o/qkv/gate_up the library wins."""
-    # decode batch range only, and only the measured shape family (Qwen down_proj,
-    # K >= 8192): encoder FFN2 / GPT-2 MLPs at prefill-sized M stay on the library
-    return _SPLITK_ON and 128 < M <= 256 and K >= 8192 and K >= 4 * N and K % (SPLITK_S * 64) == 0
+    return splitk_parts(M, N, K) > 0
 
 
-def gemm_splitk(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+def gemm_splitk(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, parts: int = SPLITK_S) -> torch.Tensor:
     """Split-K over the library: S strided-batched GEMMs of K/S slices (one
     hipBLASLt launch, S x more workgroups) with fp32 output, reduced in fp32
     — no weight copy (the slices are strided views of ``w``)."""
     M, K = x.shape
     N = w.shape[0]
-    S = SPLITK_S
+    S = parts
     xs = x.view(M, S, K // S).transpose(0, 1)
     ws = w.view(N, S, K // S).transpose(0, 1).transpose(1, 2)
     y = torch.bmm(xs, ws, out_dtype=torch.float32).sum(0)
@@ -238,8 +250,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> t
             and x.stride(1) == 1 and w.stride(1) == 1):
         M, K = x.shape
         N = w.shape[0]
-        if use_splitk(M, N, K):
-            return gemm_splitk(x, w, b)
+        parts = splitk_parts(M, N, K)
+        if parts:
+            return gemm_splitk(x, w, b, parts)
         choice = measured_choice(M, N, K)
         if choice == "library":
             return torch.nn.functional.linear(x, w, b)

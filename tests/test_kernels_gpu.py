@@ -324,10 +324,11 @@ def test_sampler_matches_reference_stream(dev):
     assert agree >= 3 * B - 2, agree
 
 
-@pytest.mark.parametrize("M", [160, 192, 256])
+@pytest.mark.parametrize("M", [64, 96, 160, 192, 256])
 def test_linear_splitk_down_proj(dev, M):
-    """Deep-K decode GEMMs at large batches dispatch to the split-K library
-    path (fp32 partials reduced in fp32); numerics vs the fp32 reference."""
+    """Deep-K decode GEMMs at decode batches dispatch to the split-K library
+    path (2 or 8 K-slices, fp32 partials reduced in fp32); numerics vs the
+    fp32 reference."""
     from githubrepostorag_amd.ops.linear import gemm_splitk, linear, use_splitk
 
     N, K = 3584, 18944
@@ -339,3 +340,4 @@ def test_linear_splitk_down_proj(dev, M):
     ref = x.float().cpu() @ w.float().cpu().T
     close(linear(x, w), ref, 3e-2, 2e-2)
     close(gemm_splitk(x, w, b), ref + b.float().cpu(), 3e-2, 2e-2)
+    close(gemm_splitk(x, w, None, 2), ref, 3e-2, 2e-2)

@@ -1,6 +1,6 @@
 """Decode-GEMM dispatch rules of ops/linear.py (CPU: predicates only; the
 numerics of every path are in tests/test_kernels_gpu.py)."""
-from githubrepostorag_amd.ops.linear import use_splitk
+from githubrepostorag_amd.ops.linear import splitk_parts, use_splitk
 
 
 def test_splitk_only_for_decode_sized_deep_k_down_proj():
@@ -12,3 +12,7 @@ def test_splitk_only_for_decode_sized_deep_k_down_proj():
     assert not use_splitk(192, 768, 3072)  # GPT-2 MLP
     assert not use_splitk(192, 37888, 3584)  # gate_up (wide N)
     assert not use_splitk(192, 1536, 8960)  # K not a multiple of 8 x 64
+
+
+def test_splitk_parts_by_batch():
+    assert [splitk_parts(M, 3584, 18944) for M in (16, 48, 64, 96, 128, 192, 256, 512)] == [0, 2, 2, 2, 0, 8, 8, 0]
