@@ -97,6 +97,9 @@ class Settings:
     stream_tokens: bool = field(default_factory=lambda: _bool("STREAM_TOKENS", True))
     # coalesce concurrent jobs' query embeddings into one encoder pass (0 disables)
     embed_batch_window_ms: float = field(default_factory=lambda: _float("EMBED_BATCH_WINDOW_MS", 1.0))
+    # POST /ingest is off by default; `local` sources must resolve under INGEST_ROOT
+    http_ingest: bool = field(default_factory=lambda: _bool("HTTP_INGEST", False))
+    ingest_root: str | None = field(default_factory=lambda: os.environ.get("INGEST_ROOT"))
     seed: int = field(default_factory=lambda: _int("SEED", 0))
 
     def table_names(self) -> dict:

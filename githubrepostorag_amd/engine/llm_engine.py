@@ -131,7 +131,10 @@ class LLMEngine:
         else:
             free, _ = torch.cuda.mem_get_info(self.device)
             cap = int(free * cfg.gpu_memory_fraction // per_block)
-        return max(64, min(want, cap))
+        n = max(64, min(want, cap))
+        # replicated TP scheduling needs bit-identical admission/preemption on
+        # every rank, hence the same block pool: take the group minimum
+        return self.model.tp.min_int(n, self.device)
 
     # ------------------------------------------------------------------ API
     def add_request(self, prompt, params: SamplingParams | None = None, req_id: str | None = None,
@@ -287,7 +290,10 @@ class LLMEngine:
             rows = torch.as_tensor(samp_rows, dtype=torch.long, device=self.device)
             logits = self.model.compute_logits(hidden.index_select(0, rows))
             slot_t = self._to_dev(np.asarray([s.slot for s in samp_seqs], dtype=np.int32))
+            tp = self.model.tp
+            tp.stage_health()
             toks = sample(logits, self.sampler, slot_t).tolist()
+            tp.check_health()
             now = time.perf_counter()
             for s, t in zip(samp_seqs, toks):
                 if self._append(s, int(t), now):
@@ -399,7 +405,9 @@ class LLMEngine:
             self._static_dev[: packed.size].copy_(self._static_host[: packed.size], non_blocking=True)
             g.graph.replay()
             tw = time.perf_counter()
+            self.model.tp.stage_health()
             toks = g.out_tokens[:K, :n].cpu().numpy()
+            self.model.tp.check_health()
             self.stats["decode_wait_s"] += time.perf_counter() - tw
             self.stats["graph_replays"] += 1
         else:
@@ -408,7 +416,10 @@ class LLMEngine:
             width = max(len(s.blocks) for s in seqs)
             dev = self._to_dev(self._decode_inputs(seqs, n, width, 1))
             out = torch.empty(1, n, dtype=torch.int32, device=self.device)
-            toks = self._decode_forward(self._views(dev, n, width, 1), n, nsplit, split_len, out, 1).cpu().numpy()
+            out = self._decode_forward(self._views(dev, n, width, 1), n, nsplit, split_len, out, 1)
+            self.model.tp.stage_health()
+            toks = out.cpu().numpy()
+            self.model.tp.check_health()
         now = time.perf_counter()
         finished = []
         live = list(seqs)

@@ -166,8 +166,31 @@ class EngineRunner:
                 self.engine.abort(rid)
             if msg["stop"]:
                 break
-            if self.engine.has_unfinished():
+            if not msg.get("step", True):
+                continue
+            ok = True
+            try:
                 self.engine.step()
+            except Exception as e:
+                log.exception("TP follower step failed")
+                self.last_error = e
+                self.num_faults += 1
+                ok = False
+            # every rank learns whether the step succeeded everywhere, so all
+            # ranks fail the same requests and stay in lockstep
+            if not self.tp.agree(ok, self.engine.device):
+                self._drop_all()
+
+    def _drop_all(self) -> None:
+        """Follower side of a failed step: cancel every in-flight sequence
+        (the leader fails the same requests in _fail_all)."""
+        for rid in list(self.engine._seqs):
+            self.engine.abort(rid)
+        try:
+            for s in self.engine.sched.reap_cancelled():
+                self.engine.pop(s.req_id)
+        except Exception:
+            pass
 
     def join(self, timeout: float | None = None) -> None:
         self._thread.join(timeout)
@@ -184,16 +207,17 @@ class EngineRunner:
                 stop = self._stop
                 pending, self._pending = self._pending, []
                 aborts, self._aborts = self._aborts, []
+            will_step = bool(pending) or self.engine.has_unfinished()
             if self.tp is not None:
                 adds = []
                 for rid, prompt, params, cb in pending:
                     ids = self.engine.tok.encode(prompt) if isinstance(prompt, str) else list(prompt)
                     adds.append((rid, ids, params or SamplingParams()))
-                self._bcast({"add": adds, "abort": aborts, "stop": stop})
+                self._bcast({"add": adds, "abort": aborts, "stop": stop, "step": will_step and not stop})
                 pending = [(rid, ids, p, cb) for (rid, ids, p), (_, _, _, cb) in zip(adds, pending)]
             if stop:
                 break
-            if self.tp is not None and not pending and not self.engine.has_unfinished():
+            if self.tp is not None and not will_step:
                 continue
             for rid, prompt, params, cb in pending:
                 try:
@@ -207,21 +231,26 @@ class EngineRunner:
                 for rid in aborts:
                     self.engine.abort(rid)
             self._step_t0 = time.monotonic()
+            err = None
             try:
                 self.engine.step()
-                self._step_t0 = None
+            except Exception as e:  # engine fault: fail every in-flight request, keep serving
+                log.exception("engine step failed")
+                err = e
+            self._step_t0 = None
+            if self.tp is not None and not self.tp.agree(err is None, self.engine.device) and err is None:
+                err = RuntimeError("a TP follower rank failed this engine step")
+            if err is None:
                 if self.hung:
                     log.warning("engine step returned after the watchdog fired; marking healthy again")
                     self.hung = False
                     self.engine.sched.reap_cancelled()
                 self._set_health(True)
-            except Exception as e:  # engine fault: fail every in-flight request, keep serving
-                self._step_t0 = None
-                log.exception("engine step failed")
-                self.last_error = e
+            else:
+                self.last_error = err
                 self.num_faults += 1
                 self._set_health(False)
-                self._fail_all(e)
+                self._fail_all(err)
                 time.sleep(0.05)
 
     def _set_health(self, ok: bool) -> None:

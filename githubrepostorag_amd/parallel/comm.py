@@ -108,6 +108,42 @@ class Group:
             dist.all_reduce(t, group=self.pg)
         return t
 
+    def stage_health(self) -> None:
+        """Queue the device-side error word of the attached one-shot all-reduce
+        for readback (before the engine's per-step token sync)."""
+        ar = self.custom_ar
+        if ar is not None:
+            ar.stage_error_check()
+
+    def check_health(self) -> None:
+        """After the step's sync: raise if a one-shot all-reduce of this step
+        timed out on a peer.  The custom all-reduce is then detached for good
+        (RCCL from here on) so the failure cannot repeat with stale epochs."""
+        ar = self.custom_ar
+        if ar is None:
+            return
+        try:
+            ar.raise_if_failed()
+        except Exception:
+            self.custom_ar = None
+            raise
+
+    def agree(self, ok: bool, device=None) -> bool:
+        """All ranks learn whether every rank's step succeeded (MIN all-reduce
+        of a status word; RCCL needs it on the GPU, gloo on the host)."""
+        return bool(self.min_int(1 if ok else 0, device))
+
+    def min_int(self, v: int, device=None) -> int:
+        """Group-wide minimum of a host integer (e.g. the planned KV block count:
+        replicated scheduling needs identical pools on every TP rank)."""
+        if self.trivial:
+            return int(v)
+        dev = device if device is not None and torch.device(device).type == "cuda" and _INFO.backend == "nccl" \
+            else "cpu"
+        t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.pg)
+        return int(t.item())
+
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[...] -> [size, ...] (one collective)."""
         if self.trivial:

@@ -66,6 +66,9 @@ class IpcAllReduce:
         self._arr = (ctypes.c_void_p * self.W)(*regions)
         self.epochs = torch.zeros(grid, dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # host mirror of `err`, refreshed asynchronously once per engine step
+        # (stage_error_check) and read after the step's token sync (raise_if_failed)
+        self._host_err = torch.zeros(1, dtype=torch.int32, pin_memory=self.device.type == "cuda")
 
     # ------------------------------------------------------------------ setup
     @classmethod
@@ -130,6 +133,29 @@ class IpcAllReduce:
 
     def failed(self) -> bool:
         return bool(self.err.item())
+
+    # A spin that times out inside the kernel sets `err` and leaves `out`
+    # holding only the local partial sum, so a stalled peer must surface as an
+    # error, not as silently wrong logits.  The engine queues the err copy
+    # before its per-step token sync and checks it right after (no extra sync).
+    def stage_error_check(self, stream=None) -> None:
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(s):
+            self._host_err.copy_(self.err, non_blocking=True)
+
+    def raise_if_failed(self) -> None:
+        """Call after the stream that ran stage_error_check() was synchronised."""
+        if int(self._host_err[0]) != 0:
+            raise CommError(f"one-shot all-reduce timed out waiting for a peer (rank {self.rank} of {self.W}); "
+                            "outputs of this step are invalid")
+
+    def reset_error(self) -> None:
+        self.err.zero_()
+        self._host_err.zero_()
+
+
+class CommError(RuntimeError):
+    """A collective failed on device (peer stalled / timed out)."""
 
 
 def enable_for_group(group, device) -> IpcAllReduce | None:

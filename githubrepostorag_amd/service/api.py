@@ -230,11 +230,31 @@ def create_app(state: APIState | None = None, runtime_factory=None) -> FastAPI:
                 "data": [{"object": "embedding", "index": i, "embedding": v} for i, v in enumerate(vecs)]}
 
     # ------------------------------------------------------------------ ingest trigger
+    # The reference exposes no HTTP ingest (its ingest is a batch Job); this
+    # route is OFF unless HTTP_INGEST=1, and a `local` source is confined to
+    # INGEST_ROOT (checked after resolve(), so `..` and symlinks cannot escape).
     @app.post("/ingest")
     async def ingest(payload: dict):
+        from ..config import settings as _settings
+
+        cfg = _settings()
+        if not cfg.http_ingest:
+            raise HTTPException(403, "HTTP ingest is disabled (set HTTP_INGEST=1 to enable)")
         rt = state.runtime
         if rt is None:
             raise HTTPException(503, "runtime not ready")
+        source = payload.get("source", "synthetic")
+        if source not in ("synthetic", "github", "local"):
+            raise HTTPException(400, f"unknown ingest source {source!r}")
+        path = payload.get("path")
+        if source == "local":
+            if not cfg.ingest_root or not path:
+                raise HTTPException(403, "local ingest needs INGEST_ROOT and a path under it")
+            root = Path(cfg.ingest_root).resolve()
+            target = (root / path).resolve()
+            if target != root and root not in target.parents:
+                raise HTTPException(403, "path escapes INGEST_ROOT")
+            path = str(target)
         from ..ingest.controller import IngestController
 
         job_id = uuid.uuid4().hex
@@ -243,8 +263,7 @@ def create_app(state: APIState | None = None, runtime_factory=None) -> FastAPI:
         def run():
             ctl = IngestController(rt)
             try:
-                res = ctl.ingest_many(payload.get("components") or [], source=payload.get("source", "synthetic"),
-                                      path=payload.get("path"))
+                res = ctl.ingest_many(payload.get("components") or [], source=source, path=path)
                 state.events.emit_sync(job_id, "final", {"results": res})
             except Exception as e:
                 state.events.emit_sync(job_id, "error", {"message": str(e)})

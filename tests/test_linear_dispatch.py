@@ -16,3 +16,10 @@ def test_splitk_only_for_decode_sized_deep_k_down_proj():
 
 def test_splitk_parts_by_batch():
     assert [splitk_parts(M, 3584, 18944) for M in (16, 48, 64, 96, 128, 192, 256, 512)] == [0, 2, 2, 2, 0, 8, 8, 0]
+
+
+def test_two_slice_splitk_only_for_measured_shape():
+    # 2-slice branch was timed only on Qwen2-7B down_proj (N=3584, K=18944)
+    assert splitk_parts(64, 1536, 8960) == 0  # Qwen2-1.5B down_proj
+    assert splitk_parts(64, 2048, 11008) == 0  # Qwen2.5-3B down_proj
+    assert splitk_parts(64, 3584, 18944) == 2

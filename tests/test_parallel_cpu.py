@@ -171,6 +171,65 @@ def _tp_runner_worker(rank, world, cfg_name):
     return out
 
 
+def _tp_fault_worker(rank, world, cfg_name, faulty_rank):
+    """One rank raises after its collectives in a decode step: both ranks must
+    fail the same requests (status all-reduce) and keep serving in lockstep."""
+    from githubrepostorag_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from githubrepostorag_amd.engine.runner import EngineRunner
+    from githubrepostorag_amd.engine.sequence import SamplingParams
+    from githubrepostorag_amd.engine.tokenizer import ByteBPETokenizer
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import Qwen2Model
+    from githubrepostorag_amd.parallel.comm import make_tp_dp_groups
+
+    cfg = decoder_config(cfg_name)
+    tp, _ = make_tp_dp_groups(world)
+    model = Qwen2Model(cfg, device="cpu", dtype=torch.float32, tp=tp, state_dict=_hf_state_dict(cfg))
+    eng = LLMEngine(model, ByteBPETokenizer(cfg.vocab_size),
+                    EngineConfig(max_num_seqs=4, max_model_len=256, num_blocks=64, use_cuda_graph=False))
+    if rank == faulty_rank:
+        real = eng._run_decode
+        calls = {"n": 0}
+
+        def flaky(seqs, max_window=None):
+            out = real(seqs, max_window)  # every collective of the step has run
+            calls["n"] += 1
+            if calls["n"] == 2:
+                raise RuntimeError("injected fault")
+            return out
+
+        eng._run_decode = flaky
+    runner = EngineRunner(eng, tp=tp, watchdog_s=0)
+    if rank != 0:
+        runner.join(120)
+        return runner.num_faults
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    first = None
+    try:
+        runner.generate([5, 17, 99, 3, 250], sp, timeout=60)
+    except Exception as e:  # the injected fault fails this request on every rank
+        first = type(e).__name__
+    second = runner.generate([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12], sp, timeout=60).token_ids
+    runner.shutdown()
+    return first, second, runner.num_faults
+
+
+def test_tp_runner_fault_keeps_lockstep():
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import Qwen2Model
+
+    cfg = decoder_config("qwen2-tiny")
+    ref = _generate(Qwen2Model(cfg, device="cpu", dtype=torch.float32, state_dict=_hf_state_dict(cfg)),
+                    [[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]])
+    for faulty in (1, 0):  # follower fault, then leader fault
+        res = run_ranks(_tp_fault_worker, 2, "qwen2-tiny", faulty)
+        first, second, leader_faults = res[0]
+        assert first == "RuntimeError", res
+        assert second == ref[0]
+        assert leader_faults == 1
+        assert res[1] == (1 if faulty == 1 else 0)
+
+
 def test_tp_runner_replicated_scheduling():
     from githubrepostorag_amd.models.configs import decoder_config
     from githubrepostorag_amd.models.qwen2 import Qwen2Model

@@ -213,15 +213,48 @@ def test_v1_requires_engine(embedder):
         assert client.post("/v1/completions", json={"prompt": "hi"}).status_code == 503
 
 
-def test_ingest_endpoint(embedder):
+def test_ingest_endpoint(embedder, monkeypatch):
+    from githubrepostorag_amd.config import settings
+
+    monkeypatch.setenv("HTTP_INGEST", "1")
+    settings(reload=True)
+    try:
+        rt = _runtime(embedder)
+        state = APIState(runtime=rt)
+        with TestClient(create_app(state)) as client:
+            job = client.post("/ingest", json={"components": [{"repo": "demo", "namespace": "default"}]}).json()
+            evs = _sse(client, job["job_id"])
+            res = evs[-1][1]["results"]
+            assert res[0]["repo"] == "demo" and res[0]["nodes_written"] > 0
+            assert rt.store.counts()["embeddings_catalog"] >= 1
+    finally:
+        monkeypatch.delenv("HTTP_INGEST")
+        settings(reload=True)
+
+
+def test_ingest_endpoint_locked_down(embedder, monkeypatch, tmp_path):
+    """POST /ingest is off by default; when on, a `local` source may not leave INGEST_ROOT."""
+    from githubrepostorag_amd.config import settings
+
     rt = _runtime(embedder)
-    state = APIState(runtime=rt)
-    with TestClient(create_app(state)) as client:
-        job = client.post("/ingest", json={"components": [{"repo": "demo", "namespace": "default"}]}).json()
-        evs = _sse(client, job["job_id"])
-        res = evs[-1][1]["results"]
-        assert res[0]["repo"] == "demo" and res[0]["nodes_written"] > 0
-        assert rt.store.counts()["embeddings_catalog"] >= 1
+    try:
+        settings(reload=True)
+        with TestClient(create_app(APIState(runtime=rt))) as client:
+            assert client.post("/ingest", json={"source": "local", "path": "/etc"}).status_code == 403
+        root = tmp_path / "repos"
+        (root / "ok").mkdir(parents=True)
+        monkeypatch.setenv("HTTP_INGEST", "1")
+        monkeypatch.setenv("INGEST_ROOT", str(root))
+        settings(reload=True)
+        with TestClient(create_app(APIState(runtime=rt))) as client:
+            for bad in ("/etc", "../../etc", "ok/../../"):
+                r = client.post("/ingest", json={"source": "local", "path": bad})
+                assert r.status_code == 403, bad
+            assert client.post("/ingest", json={"source": "ftp"}).status_code == 400
+    finally:
+        monkeypatch.delenv("HTTP_INGEST", raising=False)
+        monkeypatch.delenv("INGEST_ROOT", raising=False)
+        settings(reload=True)
 
 
 def test_job_queue_timeout():
