@@ -1,0 +1,434 @@
+// Owned bf16 MFMA GEMM for the prefill / encoder / decode projections
+// (SURVEY §2.7 N1c, N1h, N1i, N1j, N1k, N2b, N2d):
+//
+//   D[M, N] = A[M, K] · W[N, K]^T        bf16 in, fp32 accumulate
+//
+// with the epilogue fused into the kernel:
+//   EPI_STORE   bf16 out = act(acc + bias)                (act: none / gelu-erf / gelu-tanh)
+//   EPI_SILU    bf16 out[M, N/2] = silu(g + bg) * (u + bu) (gate/up rows interleaved in 32-row
+//               blocks by ops/gemm.py: rows [64j, 64j+32) = gate j*32.., [64j+32, 64j+64) = up)
+//   EPI_PARTIAL fp32 split-K slab ws[split][M][N] (reduced + epilogued by splitk_reduce_kernel)
+//
+// Geometry (cdna_hip_programming.md §5 "The 256² 8-phase template", re-derived
+// for this schedule): 256x256 output tile, BK = 64, 8 waves (512 threads) as
+// 2 (M) x 4 (N); wave (wr, wc) owns rows [128 wr, +128) x cols [64 wc, +64) as
+// 2x2 quadrants of 64x32.  Each K-tile is computed in 4 phases, one quadrant
+// per phase (16 v_mfma_f32_16x16x32_bf16 each):
+//     P1 (0,0)  reads A(q0) 8x b128 + B(q0) 4x b128
+//     P2 (0,1)  reads B(q1) 4x b128            (A(q0) kept in registers)
+//     P3 (1,1)  reads A(q1) 8x b128            (B(q1) kept)
+//     P4 (1,0)  no LDS reads                    (A(q1), B(q0) kept)
+// LDS = 2 K-tile buffers x 4 slots of 16 KB (A q0, A q1, B q0, B q1), each slot
+// = the 128 rows (both wave rows / all 4 wave columns) one quadrant needs.  A
+// slot is refilled by LDS-DMA (global_load_lds_dwordx4, 2 per thread) as soon
+// as its last reader phase has passed a barrier:
+//     P1(t): A q1 of tile t+1   P2(t): A q0 of t+2   P3(t): B q0 of t+2   P4(t): B q1 of t+2
+// so every slot is in flight for 4 phases and ONE counted `s_waitcnt
+// vmcnt(8)` per phase (never 0 in the main loop) retires exactly the slot the
+// phase after next reads.  Waves 4-7 run one barrier interval behind waves 0-3
+// (stagger, MI355X_MICROARCH.md "Two waves per SIMD" item 9): on every SIMD one
+// wave is in its LDS/DMA segment while its partner runs its MFMA cluster; the
+// waits are placed one phase early for exactly that reason (a reader in the
+// leading group must not outrun a DMA the lagging group issued).
+// Rows are 128 B; chunks XOR-swizzled by (row >> 1) & 7 on the SOURCE address
+// (LDS image lane-linear, rule 21) — conflict-free for the b128 lane groups.
+// The MFMA is issued with the W fragment as operand A, so each lane ends with
+// 4 consecutive output columns of one row: 8-byte bf16 / 16-byte fp32 stores.
+#include "common.h"
+
+using namespace grag;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+namespace {
+
+constexpr int kSlot = 128 * 128;  // 128 rows x 64 bf16
+constexpr int kBuf = 4 * kSlot;   // one K-tile: A q0, A q1, B q0, B q1
+constexpr int kThreads = 512;
+
+enum { EPI_STORE = 0, EPI_SILU = 1, EPI_PARTIAL = 2 };
+enum { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_GELU_TANH = 3 };
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ float gelu_erf_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_tanh_f(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (2.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u)));
+}
+template <int ACT>
+__device__ __forceinline__ float act_f(float x) {
+  if constexpr (ACT == ACT_GELU) return gelu_erf_f(x);
+  else if constexpr (ACT == ACT_SILU) return silu_f(x);
+  else if constexpr (ACT == ACT_GELU_TANH) return gelu_tanh_f(x);
+  else return x;
+}
+
+__device__ __forceinline__ void glds16(const void* g, char* l) {
+  __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)l, 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// raw barrier: never drains the LDS-DMA in flight (a __syncthreads() would emit vmcnt(0))
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+struct Args {
+  const bf16* A;
+  const bf16* W;
+  const bf16* bias;
+  void* C;
+  int lda, ldw, ldc;
+  int M, N, K;
+  int tiles_m, tiles_n, ksplit, kt_split;  // K-tiles (of 64) per split
+};
+
+typedef f32x4_t Acc[4][2];
+typedef bf16x8_t FragA[4][2];  // [mt][k-half]
+typedef bf16x8_t FragB[2][2];  // [nt][k-half]
+
+__device__ __forceinline__ void mma_cluster(Acc& acc, const FragA& a, const FragB& b) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt][s], a[mt][s], acc[mt][nt], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <int EPI, int ACT>
+__global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
+
+  const int tid = threadIdx.x;
+  const int L = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const bool lag = w >= 4;  // waves 4-7: one barrier interval behind
+
+  // ---- tile / split of this workgroup (XCD-contiguous ids, then group-M order)
+  const int nwg = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int split = bid % p.ksplit;
+  const int t = bid / p.ksplit;
+  constexpr int GM = 8;
+  const int band = GM * p.tiles_n;
+  const int first_m = (t / band) * GM;
+  const int gsz = min(p.tiles_m - first_m, GM);
+  const int tm = first_m + (t % band) % gsz;
+  const int tn = (t % band) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int kt0 = split * p.kt_split;
+  const int nk = min(p.kt_split, (p.K >> 6) - kt0);
+
+  // ---- LDS-DMA sources: piece q = 2w + i fills slot rows [8q, 8q+8); lane -> row 8q + L/8,
+  // physical chunk L%8 = logical chunk c ^ ((row >> 1) & 7)
+  const bf16* srcA[2][2];
+  const bf16* srcB[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rs = (2 * w + i) * 8 + (L >> 3);
+    const int c = (L & 7) ^ ((rs >> 1) & 7);
+    const int koff = kt0 * 64 + c * 8;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      int gm = m0 + (rs >> 6) * 128 + q * 64 + (rs & 63);
+      gm = gm < p.M ? gm : p.M - 1;
+      srcA[q][i] = p.A + (size_t)gm * p.lda + koff;
+      int gn = n0 + (rs >> 5) * 64 + q * 32 + (rs & 31);
+      gn = gn < p.N ? gn : p.N - 1;
+      srcB[q][i] = p.W + (size_t)gn * p.ldw + koff;
+    }
+  }
+  // slot order inside a buffer: 0 A q0, 1 A q1, 2 B q0, 3 B q1
+  auto issueA = [&](int q, int kt, int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(srcA[q][i] + kt * 64, smem + buf * kBuf + q * kSlot + (2 * w + i) * 1024);
+  };
+  auto issueB = [&](int q, int kt, int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      glds16(srcB[q][i] + kt * 64, smem + buf * kBuf + (2 + q) * kSlot + (2 * w + i) * 1024);
+  };
+
+  // ---- fragment reads: row (L & 15) of a 16-row group, logical chunk 4s + L/16, swizzle (L>>1)&7
+  const int cb = (L >> 4) ^ ((L >> 1) & 7);
+  const int off0 = (L & 15) * 128 + cb * 16;
+  const int off1 = (L & 15) * 128 + (cb ^ 4) * 16;
+  auto readA = [&](FragA& a, int q, int buf) {
+    const char* base = smem + buf * kBuf + q * kSlot + wr * 64 * 128;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      a[mt][0] = *reinterpret_cast<const bf16x8_t*>(base + mt * 2048 + off0);
+      a[mt][1] = *reinterpret_cast<const bf16x8_t*>(base + mt * 2048 + off1);
+    }
+  };
+  auto readB = [&](FragB& b, int q, int buf) {
+    const char* base = smem + buf * kBuf + (2 + q) * kSlot + wc * 32 * 128;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      b[nt][0] = *reinterpret_cast<const bf16x8_t*>(base + nt * 2048 + off0);
+      b[nt][1] = *reinterpret_cast<const bf16x8_t*>(base + nt * 2048 + off1);
+    }
+  };
+
+  Acc acc00, acc01, acc11, acc10;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      acc00[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      acc01[mt][nt] = acc00[mt][nt];
+      acc11[mt][nt] = acc00[mt][nt];
+      acc10[mt][nt] = acc00[mt][nt];
+    }
+  FragA a;
+  FragB b0, b1;
+
+  // ---- prologue: tile 0 (all 4 slots) + tile 1 (A q0, B q0, B q1); tile 1's A q1 goes out in P1(0)
+  issueA(0, 0, 0);
+  issueB(0, 0, 0);
+  issueB(1, 0, 0);
+  issueA(1, 0, 0);
+  if (nk > 1) {
+    issueA(0, 1, 1);
+    issueB(0, 1, 1);
+    issueB(1, 1, 1);
+    wait_vm<6>();
+  } else {
+    wait_vm<0>();
+  }
+  bar();
+  if (lag) bar();
+
+  // one K-tile = 4 phases; STEADY: every refill issued, counted waits
+  auto ktile = [&](int kt, auto steady_c) {
+    constexpr bool STEADY = decltype(steady_c)::value;
+    const int buf = kt & 1;
+    // P1: quadrant (0,0)
+    readA(a, 0, buf);
+    readB(b0, 0, buf);
+    if (STEADY || kt + 1 < nk) issueA(1, kt + 1, buf ^ 1);
+    wait_lgkm0();
+    bar();
+    mma_cluster(acc00, a, b0);
+    if (STEADY) wait_vm<8>(); else wait_vm<0>();
+    bar();
+    // P2: quadrant (0,1)
+    readB(b1, 1, buf);
+    if (STEADY) issueA(0, kt + 2, buf);
+    wait_lgkm0();
+    bar();
+    mma_cluster(acc01, a, b1);
+    if (STEADY) wait_vm<8>(); else wait_vm<0>();
+    bar();
+    // P3: quadrant (1,1)
+    readA(a, 1, buf);
+    if (STEADY) issueB(0, kt + 2, buf);
+    wait_lgkm0();
+    bar();
+    mma_cluster(acc11, a, b1);
+    if (STEADY) wait_vm<8>(); else wait_vm<0>();
+    bar();
+    // P4: quadrant (1,0)
+    if (STEADY) issueB(1, kt + 2, buf);
+    bar();
+    mma_cluster(acc10, a, b0);
+    if (STEADY) wait_vm<8>(); else wait_vm<0>();
+    bar();
+  };
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) ktile(kt, std::integral_constant<bool, true>{});
+  for (; kt < nk; ++kt) ktile(kt, std::integral_constant<bool, false>{});
+  if (!lag) bar();
+
+  // ---- epilogue.  acc_qm_qn[mt][nt][r]: row m0 + 128 wr + 64 qm + 16 mt + (L & 15),
+  // col n0 + 64 wc + 32 qn + 16 nt + 4 (L >> 4) + r
+  const int mrow = m0 + wr * 128 + (L & 15);
+  const int ncol = n0 + wc * 64 + 4 * (L >> 4);
+  if constexpr (EPI == EPI_SILU) {
+    bf16* C = (bf16*)p.C;
+    const int ocol = (n0 + wc * 64) / 2 + 4 * (L >> 4);
+    float bg[2][4], bu[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = ncol + nt * 16 + r;
+        bg[nt][r] = (p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
+        bu[nt][r] = (p.bias && n + 32 < p.N) ? (float)p.bias[n + 32] : 0.f;
+      }
+    auto emit = [&](const Acc& g, const Acc& u, int qm) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int m = mrow + qm * 64 + mt * 16;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int oc = ocol + nt * 16;
+          if (2 * oc >= p.N) continue;
+          bf16x4_t o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = f2bits(silu_f(g[mt][nt][r] + bg[nt][r]) * (u[mt][nt][r] + bu[nt][r]));
+          *reinterpret_cast<bf16x4_t*>(C + (size_t)m * p.ldc + oc) = o;
+        }
+      }
+    };
+    emit(acc00, acc01, 0);
+    emit(acc10, acc11, 1);
+  } else {
+    float bv[2][2][4];
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = ncol + qn * 32 + nt * 16 + r;
+          bv[qn][nt][r] = (EPI == EPI_STORE && p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
+        }
+    auto emit = [&](const Acc& acc, int qm, int qn) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int m = mrow + qm * 64 + mt * 16;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int n = ncol + qn * 32 + nt * 16;
+          if (n >= p.N) continue;
+          if constexpr (EPI == EPI_PARTIAL) {
+            float* ws = (float*)p.C + ((size_t)split * p.M + m) * p.N + n;
+            *reinterpret_cast<f32x4_t*>(ws) = acc[mt][nt];
+          } else {
+            bf16x4_t o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = f2bits(act_f<ACT>(acc[mt][nt][r] + bv[qn][nt][r]));
+            *reinterpret_cast<bf16x4_t*>((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+          }
+        }
+      }
+    };
+    emit(acc00, 0, 0);
+    emit(acc01, 0, 1);
+    emit(acc11, 1, 1);
+    emit(acc10, 1, 0);
+  }
+}
+
+// Split-K combine: out = epilogue(sum_s ws[s]) — 8 output columns per thread.
+// EPI_STORE: out[M, N] = act(sum + bias); EPI_SILU: out[M, N/2] from the interleaved gate/up layout.
+template <int EPI, int ACT>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, const bf16* __restrict__ bias,
+                                                            bf16* __restrict__ C, int ldc, int M, int N, int S) {
+  const int NO = EPI == EPI_SILU ? N / 2 : N;
+  const int per_row = NO / 8;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)M * per_row) return;
+  const int m = (int)(e / per_row), o = (int)(e % per_row) * 8;
+  const size_t plane = (size_t)M * N;
+  float v[8];
+  if constexpr (EPI == EPI_SILU) {
+    const int n = (o / 32) * 64 + (o % 32);  // gate col of output o; up = n + 32
+    float g[8], u[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = u[j] = 0.f;
+    for (int s = 0; s < S; ++s) {
+      const float* r = ws + s * plane + (size_t)m * N + n;
+      const f32x4_t g0 = *reinterpret_cast<const f32x4_t*>(r), g1 = *reinterpret_cast<const f32x4_t*>(r + 4);
+      const f32x4_t u0 = *reinterpret_cast<const f32x4_t*>(r + 32), u1 = *reinterpret_cast<const f32x4_t*>(r + 36);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        g[j] += g0[j]; g[j + 4] += g1[j];
+        u[j] += u0[j]; u[j + 4] += u1[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float bg = bias ? (float)bias[n + j] : 0.f, bu = bias ? (float)bias[n + 32 + j] : 0.f;
+      v[j] = silu_f(g[j] + bg) * (u[j] + bu);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    for (int s = 0; s < S; ++s) {
+      const float* r = ws + s * plane + (size_t)m * N + o;
+      const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(r), x1 = *reinterpret_cast<const f32x4_t*>(r + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] += x0[j]; v[j + 4] += x1[j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = act_f<ACT>(v[j] + (bias ? (float)bias[o + j] : 0.f));
+  }
+  *reinterpret_cast<bf16x8_t*>(C + (size_t)m * ldc + o) = pack8(v);
+}
+
+template <int EPI, int ACT>
+int launch(const Args& a, hipStream_t stream) {
+  const int nwg = a.tiles_m * a.tiles_n * a.ksplit;
+  gemm_tile_kernel<EPI, ACT><<<nwg, kThreads, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// y = epilogue(x @ w^T).  epi: 0 store (act: 0 none, 1 gelu-erf, 3 gelu-tanh), 1 silu*mul
+// (w rows interleaved in 32-row gate/up blocks, out [M, N/2]).  ksplit > 1: partial
+// slabs into ws (ksplit * M * N fp32) + splitk_reduce_kernel applies the epilogue.
+// Requirements (checked): K % 64 == 0, every split >= 2 K-tiles, lda/ldw % 8 == 0,
+// N % 8 == 0 (silu: N % 64 == 0), ldc % 8 == 0, 16-B aligned pointers.
+GRAG_API int grag_gemm_tile(const void* A, const void* W, const void* bias, void* C, int lda, int ldw, int ldc,
+                            int M, int N, int K, int epi, int act, int ksplit, void* ws, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 64 != 0 || K < 128 || lda % 8 != 0 || ldw % 8 != 0 || ldc % 8 != 0 || N % 8 != 0)
+    return (int)hipErrorInvalidValue;
+  if (epi == EPI_SILU && N % 64 != 0) return (int)hipErrorInvalidValue;
+  if (epi != EPI_STORE && epi != EPI_SILU) return (int)hipErrorInvalidValue;
+  if (act != ACT_NONE && act != ACT_GELU && act != ACT_GELU_TANH) return (int)hipErrorInvalidValue;
+  if (epi == EPI_SILU && act != ACT_NONE) return (int)hipErrorInvalidValue;
+  const int kt = K / 64;
+  if (ksplit < 1) ksplit = 1;
+  const int kts = (kt + ksplit - 1) / ksplit;
+  if (kts < 2 || (ksplit - 1) * kts >= kt) return (int)hipErrorInvalidValue;  // every split non-empty, >= 2 tiles
+  if (ksplit > 1 && (kt - (ksplit - 1) * kts) < 2) return (int)hipErrorInvalidValue;
+  if (ksplit > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
+  Args a;
+  a.A = (const bf16*)A;
+  a.W = (const bf16*)W;
+  a.bias = (const bf16*)bias;
+  a.C = ksplit > 1 ? ws : C;
+  a.lda = lda; a.ldw = ldw; a.ldc = ldc;
+  a.M = M; a.N = N; a.K = K;
+  a.tiles_m = (M + 255) / 256;
+  a.tiles_n = (N + 255) / 256;
+  a.ksplit = ksplit;
+  a.kt_split = kts;
+  if ((long)a.tiles_m * a.tiles_n * ksplit >= (1L << 31)) return (int)hipErrorInvalidValue;
+  int err;
+  if (ksplit > 1) {
+    err = launch<EPI_PARTIAL, ACT_NONE>(a, stream);
+    if (err) return err;
+    const int NO = epi == EPI_SILU ? N / 2 : N;
+    const long n8 = (long)M * (NO / 8);
+    const int blocks = (int)((n8 + 255) / 256);
+#define RED(E, AC) splitk_reduce_kernel<E, AC><<<blocks, 256, 0, stream>>>((const float*)ws, (const bf16*)bias, (bf16*)C, ldc, M, N, ksplit)
+    if (epi == EPI_SILU) RED(EPI_SILU, ACT_NONE);
+    else if (act == ACT_GELU) RED(EPI_STORE, ACT_GELU);
+    else if (act == ACT_GELU_TANH) RED(EPI_STORE, ACT_GELU_TANH);
+    else RED(EPI_STORE, ACT_NONE);
+#undef RED
+    return (int)hipGetLastError();
+  }
+  if (epi == EPI_SILU) return launch<EPI_SILU, ACT_NONE>(a, stream);
+  if (act == ACT_GELU) return launch<EPI_STORE, ACT_GELU>(a, stream);
+  if (act == ACT_GELU_TANH) return launch<EPI_STORE, ACT_GELU_TANH>(a, stream);
+  return launch<EPI_STORE, ACT_NONE>(a, stream);
+}

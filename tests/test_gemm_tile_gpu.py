@@ -1,0 +1,106 @@
+"""Owned 256x256 MFMA GEMM (csrc/kernels/gemm_tile.hip) against an fp32
+PyTorch reference: plain / bias / GELU / SiLU*mul epilogues, ragged M and N
+tails, split-K partial slabs + combine, and hipGraph replay."""
+import pytest
+import torch
+
+from githubrepostorag_amd.ops import gemm as G
+
+pytestmark = pytest.mark.gpu
+
+
+def rnd(*shape, dev, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(dev)
+
+
+def ref(x, w, b=None):
+    y = x.float().cpu() @ w.float().cpu().T
+    return y if b is None else y + b.float().cpu()
+
+
+def check(y, r, K):
+    # bf16 output rounding + fp32 accumulation-order differences; |y| ~ sqrt(K) * scale^2
+    y = y.float().cpu()
+    tol = 2e-2 * r.abs().max().item() + 1e-2
+    err = (y - r).abs().max().item()
+    assert err <= tol, f"max err {err} > {tol}"
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 256), (300, 520, 192), (1, 264, 128),
+                                   (4096, 4608, 3584), (777, 3584, 640)])
+def test_gemm_plain(dev, M, N, K):
+    x, w = rnd(M, K, dev=dev, scale=0.5), rnd(N, K, dev=dev, seed=1, scale=0.5)
+    y = G.gemm(x, w, ksplit=1)
+    check(y, ref(x, w), K)
+
+
+def test_gemm_bias_identity_asymmetric(dev):
+    # A = I with an asymmetric B catches a transposed C write (cdna guide §3)
+    K = 256
+    x = torch.eye(K, dtype=torch.bfloat16, device=dev)
+    w = (torch.arange(K * 264, dtype=torch.float32).reshape(264, K) % 251 - 125).to(torch.bfloat16).to(dev)
+    b = rnd(264, dev=dev, seed=3)
+    y = G.gemm(x, w, b, ksplit=1)
+    assert torch.equal(y.cpu(), (w.float().T + b.float()).to(torch.bfloat16).cpu())
+
+
+@pytest.mark.parametrize("act", [G.ACT_GELU, G.ACT_GELU_TANH])
+def test_gemm_gelu(dev, act):
+    M, N, K = 333, 1024, 384
+    x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+    y = G.gemm(x, w, b, act=act, ksplit=1)
+    r = ref(x, w, b)
+    r = torch.nn.functional.gelu(r, approximate="tanh" if act == G.ACT_GELU_TANH else "none")
+    check(y, r, K)
+
+
+@pytest.mark.parametrize("M", [5, 192, 700])
+def test_gemm_silu(dev, M):
+    I, K = 512, 384
+    x = rnd(M, K, dev=dev, scale=0.5)
+    wg, wu = rnd(I, K, dev=dev, seed=1, scale=0.3), rnd(I, K, dev=dev, seed=2, scale=0.3)
+    bg, bu = rnd(I, dev=dev, seed=3), rnd(I, dev=dev, seed=4)
+    wgu = G.interleave_gate_up(wg, wu)
+    bgu = G.interleave_gate_up(bg.view(I, 1), bu.view(I, 1)).view(2 * I)
+    h = G.gemm_silu(x, wgu, bgu, ksplit=1)
+    r = torch.nn.functional.silu(ref(x, wg, bg)) * ref(x, wu, bu)
+    check(h, r, K)
+
+
+@pytest.mark.parametrize("M,N,K,S", [(192, 3584, 18944, 8), (64, 4608, 3584, 7), (200, 1024, 1024, 4)])
+def test_gemm_splitk(dev, M, N, K, S):
+    x, w, b = rnd(M, K, dev=dev, scale=0.2), rnd(N, K, dev=dev, seed=1, scale=0.2), rnd(N, dev=dev, seed=2)
+    y = G.gemm(x, w, b, ksplit=S)
+    check(y, ref(x, w, b), K)
+
+
+def test_gemm_silu_splitk(dev):
+    M, I, K = 160, 1024, 2048
+    x = rnd(M, K, dev=dev, scale=0.3)
+    wg, wu = rnd(I, K, dev=dev, seed=1, scale=0.2), rnd(I, K, dev=dev, seed=2, scale=0.2)
+    h = G.gemm_silu(x, G.interleave_gate_up(wg, wu), ksplit=6)
+    check(h, torch.nn.functional.silu(ref(x, wg)) * ref(x, wu), K)
+
+
+def test_plan_ksplit():
+    assert G.plan_ksplit(8192, 4608, 3584) == 1
+    s = G.plan_ksplit(192, 3584, 18944)
+    assert 14 * s <= 256 + 14 and s >= 8
+
+
+def test_gemm_graph_replay(dev):
+    M, N, K = 192, 2048, 1024
+    x, w = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3)
+    S = G.plan_ksplit(M, N, K)
+    G.WS.reserve(dev, S * M * N)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    G.gemm(x, w, out=out)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        G.gemm(x, w, out=out)
+    x.copy_(rnd(M, K, dev=dev, seed=7, scale=0.3))
+    g.replay()
+    torch.cuda.synchronize()
+    check(out, ref(x, w), K)
