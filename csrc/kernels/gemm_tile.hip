@@ -87,9 +87,14 @@ struct Args {
   int lda, ldw, ldc;
   int M, N, K;
   int tiles_m, tiles_n, ksplit, kt_split;  // K-tiles (of 64) per split
+  int dp_tiles;    // blockIdx < dp_tiles: one whole tile (or K-split) each
+  int sk_grid;     // blockIdx >= dp_tiles: stream-K workgroups over the remaining tiles
+  float* slab;     // split-K partial planes, or 2 x 256 KB stream-K slots per SK workgroup
+  unsigned* cnt;   // stream-K arrival tickets, one per SK tile (zero at rest)
 };
 
 typedef f32x4_t Acc[4][2];
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef bf16x8_t FragA[4][2];  // [mt][k-half]
 typedef bf16x8_t FragB[2][2];  // [nt][k-half]
 
@@ -114,50 +119,16 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 2, wc = w & 3;
   const bool lag = w >= 4;  // waves 4-7: one barrier interval behind
+  const int ks = p.K >> 6;
 
-  // ---- tile / split of this workgroup (XCD-contiguous ids, then group-M order)
-  const int nwg = gridDim.x;
-  const int bid = xcd_remap(blockIdx.x, nwg);
-  const int split = bid % p.ksplit;
-  const int t = bid / p.ksplit;
-  constexpr int GM = 8;
-  const int band = GM * p.tiles_n;
-  const int first_m = (t / band) * GM;
-  const int gsz = min(p.tiles_m - first_m, GM);
-  const int tm = first_m + (t % band) % gsz;
-  const int tn = (t % band) / gsz;
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int kt0 = split * p.kt_split;
-  const int nk = min(p.kt_split, (p.K >> 6) - kt0);
-
-  // ---- LDS-DMA sources: piece q = 2w + i fills slot rows [8q, 8q+8); lane -> row 8q + L/8,
-  // physical chunk L%8 = logical chunk c ^ ((row >> 1) & 7)
-  const bf16* srcA[2][2];
-  const bf16* srcB[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int rs = (2 * w + i) * 8 + (L >> 3);
-    const int c = (L & 7) ^ ((rs >> 1) & 7);
-    const int koff = kt0 * 64 + c * 8;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      int gm = m0 + (rs >> 6) * 128 + q * 64 + (rs & 63);
-      gm = gm < p.M ? gm : p.M - 1;
-      srcA[q][i] = p.A + (size_t)gm * p.lda + koff;
-      int gn = n0 + (rs >> 5) * 64 + q * 32 + (rs & 31);
-      gn = gn < p.N ? gn : p.N - 1;
-      srcB[q][i] = p.W + (size_t)gn * p.ldw + koff;
-    }
-  }
-  // slot order inside a buffer: 0 A q0, 1 A q1, 2 B q0, 3 B q1
-  auto issueA = [&](int q, int kt, int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(srcA[q][i] + kt * 64, smem + buf * kBuf + q * kSlot + (2 * w + i) * 1024);
-  };
-  auto issueB = [&](int q, int kt, int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      glds16(srcB[q][i] + kt * 64, smem + buf * kBuf + (2 + q) * kSlot + (2 * w + i) * 1024);
+  // group-M order over all output tiles: 8 row tiles x every column tile per band
+  auto tile_coords = [&](int t, int& m0, int& n0) {
+    constexpr int GM = 8;
+    const int band = GM * p.tiles_n;
+    const int first_m = (t / band) * GM;
+    const int gsz = min(p.tiles_m - first_m, GM);
+    m0 = (first_m + (t % band) % gsz) * 256;
+    n0 = ((t % band) / gsz) * 256;
   };
 
   // ---- fragment reads: row (L & 15) of a 16-row group, logical chunk 4s + L/16, swizzle (L>>1)&7
@@ -182,146 +153,280 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
   };
 
   Acc acc00, acc01, acc11, acc10;
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      acc00[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      acc01[mt][nt] = acc00[mt][nt];
-      acc11[mt][nt] = acc00[mt][nt];
-      acc10[mt][nt] = acc00[mt][nt];
-    }
   FragA a;
   FragB b0, b1;
 
-  // ---- prologue: tile 0 (all 4 slots) + tile 1 (A q0, B q0, B q1); tile 1's A q1 goes out in P1(0)
-  issueA(0, 0, 0);
-  issueB(0, 0, 0);
-  issueB(1, 0, 0);
-  issueA(1, 0, 0);
-  if (nk > 1) {
-    issueA(0, 1, 1);
-    issueB(0, 1, 1);
-    issueB(1, 1, 1);
-    wait_vm<6>();
-  } else {
-    wait_vm<0>();
-  }
-  bar();
-  if (lag) bar();
+  // ---- K-tiles [kb, kb + nk) of the tile at (m0, n0) into the accumulators
+  auto mainloop = [&](int m0, int n0, int kb, int nk) {
+    // LDS-DMA sources: piece q = 2w + i fills slot rows [8q, 8q+8); lane -> row 8q + L/8,
+    // physical chunk L%8 = logical chunk c ^ ((row >> 1) & 7)
+    const bf16* srcA[2][2];
+    const bf16* srcB[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rs = (2 * w + i) * 8 + (L >> 3);
+      const int c = (L & 7) ^ ((rs >> 1) & 7);
+      const int koff = kb * 64 + c * 8;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        int gm = m0 + (rs >> 6) * 128 + q * 64 + (rs & 63);
+        gm = gm < p.M ? gm : p.M - 1;
+        srcA[q][i] = p.A + (size_t)gm * p.lda + koff;
+        int gn = n0 + (rs >> 5) * 64 + q * 32 + (rs & 31);
+        gn = gn < p.N ? gn : p.N - 1;
+        srcB[q][i] = p.W + (size_t)gn * p.ldw + koff;
+      }
+    }
+    // slot order inside a buffer: 0 A q0, 1 A q1, 2 B q0, 3 B q1
+    auto issueA = [&](int q, int kt, int buf) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16(srcA[q][i] + kt * 64, smem + buf * kBuf + q * kSlot + (2 * w + i) * 1024);
+    };
+    auto issueB = [&](int q, int kt, int buf) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        glds16(srcB[q][i] + kt * 64, smem + buf * kBuf + (2 + q) * kSlot + (2 * w + i) * 1024);
+    };
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        acc00[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        acc01[mt][nt] = acc00[mt][nt];
+        acc11[mt][nt] = acc00[mt][nt];
+        acc10[mt][nt] = acc00[mt][nt];
+      }
+    // prologue: tile 0 (all 4 slots) + tile 1 (A q0, B q0, B q1); tile 1's A q1 goes out in P1(0)
+    issueA(0, 0, 0);
+    issueB(0, 0, 0);
+    issueB(1, 0, 0);
+    issueA(1, 0, 0);
+    if (nk > 1) {
+      issueA(0, 1, 1);
+      issueB(0, 1, 1);
+      issueB(1, 1, 1);
+      wait_vm<6>();
+    } else {
+      wait_vm<0>();
+    }
+    bar();
+    if (lag) bar();
 
-  // one K-tile = 4 phases; STEADY: every refill issued, counted waits
-  auto ktile = [&](int kt, auto steady_c) {
-    constexpr bool STEADY = decltype(steady_c)::value;
-    const int buf = kt & 1;
-    // P1: quadrant (0,0)
-    readA(a, 0, buf);
-    readB(b0, 0, buf);
-    if (STEADY || kt + 1 < nk) issueA(1, kt + 1, buf ^ 1);
-    wait_lgkm0();
-    bar();
-    mma_cluster(acc00, a, b0);
-    if (STEADY) wait_vm<8>(); else wait_vm<0>();
-    bar();
-    // P2: quadrant (0,1)
-    readB(b1, 1, buf);
-    if (STEADY) issueA(0, kt + 2, buf);
-    wait_lgkm0();
-    bar();
-    mma_cluster(acc01, a, b1);
-    if (STEADY) wait_vm<8>(); else wait_vm<0>();
-    bar();
-    // P3: quadrant (1,1)
-    readA(a, 1, buf);
-    if (STEADY) issueB(0, kt + 2, buf);
-    wait_lgkm0();
-    bar();
-    mma_cluster(acc11, a, b1);
-    if (STEADY) wait_vm<8>(); else wait_vm<0>();
-    bar();
-    // P4: quadrant (1,0)
-    if (STEADY) issueB(1, kt + 2, buf);
-    bar();
-    mma_cluster(acc10, a, b0);
-    if (STEADY) wait_vm<8>(); else wait_vm<0>();
-    bar();
+    // one K-tile = 4 phases; STEADY: every refill issued, counted waits
+    auto ktile = [&](int kt, auto steady_c) {
+      constexpr bool STEADY = decltype(steady_c)::value;
+      const int buf = kt & 1;
+      // P1: quadrant (0,0)
+      readA(a, 0, buf);
+      readB(b0, 0, buf);
+      if (STEADY || kt + 1 < nk) issueA(1, kt + 1, buf ^ 1);
+      wait_lgkm0();
+      bar();
+      mma_cluster(acc00, a, b0);
+      if (STEADY) wait_vm<8>(); else wait_vm<0>();
+      bar();
+      // P2: quadrant (0,1)
+      readB(b1, 1, buf);
+      if (STEADY) issueA(0, kt + 2, buf);
+      wait_lgkm0();
+      bar();
+      mma_cluster(acc01, a, b1);
+      if (STEADY) wait_vm<8>(); else wait_vm<0>();
+      bar();
+      // P3: quadrant (1,1)
+      readA(a, 1, buf);
+      if (STEADY) issueB(0, kt + 2, buf);
+      wait_lgkm0();
+      bar();
+      mma_cluster(acc11, a, b1);
+      if (STEADY) wait_vm<8>(); else wait_vm<0>();
+      bar();
+      // P4: quadrant (1,0)
+      if (STEADY) issueB(1, kt + 2, buf);
+      bar();
+      mma_cluster(acc10, a, b0);
+      if (STEADY) wait_vm<8>(); else wait_vm<0>();
+      bar();
+    };
+    int kt = 0;
+    for (; kt + 2 < nk; ++kt) ktile(kt, std::integral_constant<bool, true>{});
+    for (; kt < nk; ++kt) ktile(kt, std::integral_constant<bool, false>{});
+    if (!lag) bar();
   };
-  int kt = 0;
-  for (; kt + 2 < nk; ++kt) ktile(kt, std::integral_constant<bool, true>{});
-  for (; kt < nk; ++kt) ktile(kt, std::integral_constant<bool, false>{});
-  if (!lag) bar();
+
+  // accumulator chunks (quadrant, mt, nt) in a fixed order: the stream-K slab layout
+#define GT_CHUNKS(X)                                                                                            \
+  X(acc00, 0, 0, 0) X(acc00, 1, 0, 1) X(acc00, 2, 1, 0) X(acc00, 3, 1, 1) X(acc00, 4, 2, 0) X(acc00, 5, 2, 1)  \
+  X(acc00, 6, 3, 0) X(acc00, 7, 3, 1) X(acc01, 8, 0, 0) X(acc01, 9, 0, 1) X(acc01, 10, 1, 0) X(acc01, 11, 1, 1) \
+  X(acc01, 12, 2, 0) X(acc01, 13, 2, 1) X(acc01, 14, 3, 0) X(acc01, 15, 3, 1) X(acc11, 16, 0, 0)             \
+  X(acc11, 17, 0, 1) X(acc11, 18, 1, 0) X(acc11, 19, 1, 1) X(acc11, 20, 2, 0) X(acc11, 21, 2, 1)             \
+  X(acc11, 22, 3, 0) X(acc11, 23, 3, 1) X(acc10, 24, 0, 0) X(acc10, 25, 0, 1) X(acc10, 26, 1, 0)             \
+  X(acc10, 27, 1, 1) X(acc10, 28, 2, 0) X(acc10, 29, 2, 1) X(acc10, 30, 3, 0) X(acc10, 31, 3, 1)
 
   // ---- epilogue.  acc_qm_qn[mt][nt][r]: row m0 + 128 wr + 64 qm + 16 mt + (L & 15),
   // col n0 + 64 wc + 32 qn + 16 nt + 4 (L >> 4) + r
-  const int mrow = m0 + wr * 128 + (L & 15);
-  const int ncol = n0 + wc * 64 + 4 * (L >> 4);
-  if constexpr (EPI == EPI_SILU) {
-    bf16* C = (bf16*)p.C;
-    const int ocol = (n0 + wc * 64) / 2 + 4 * (L >> 4);
-    float bg[2][4], bu[2][4];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = ncol + nt * 16 + r;
-        bg[nt][r] = (p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
-        bu[nt][r] = (p.bias && n + 32 < p.N) ? (float)p.bias[n + 32] : 0.f;
-      }
-    auto emit = [&](const Acc& g, const Acc& u, int qm) {
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int m = mrow + qm * 64 + mt * 16;
-        if (m >= p.M) continue;
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const int oc = ocol + nt * 16;
-          if (2 * oc >= p.N) continue;
-          bf16x4_t o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = f2bits(silu_f(g[mt][nt][r] + bg[nt][r]) * (u[mt][nt][r] + bu[nt][r]));
-          *reinterpret_cast<bf16x4_t*>(C + (size_t)m * p.ldc + oc) = o;
-        }
-      }
-    };
-    emit(acc00, acc01, 0);
-    emit(acc10, acc11, 1);
-  } else {
-    float bv[2][2][4];
-#pragma unroll
-    for (int qn = 0; qn < 2; ++qn)
+  auto epilogue = [&](int m0, int n0, int split) {
+    const int mrow = m0 + wr * 128 + (L & 15);
+    const int ncol = n0 + wc * 64 + 4 * (L >> 4);
+    if constexpr (EPI == EPI_SILU) {
+      bf16* C = (bf16*)p.C;
+      const int ocol = (n0 + wc * 64) / 2 + 4 * (L >> 4);
+      float bg[2][4], bu[2][4];
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int n = ncol + qn * 32 + nt * 16 + r;
-          bv[qn][nt][r] = (EPI == EPI_STORE && p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
+          const int n = ncol + nt * 16 + r;
+          bg[nt][r] = (p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
+          bu[nt][r] = (p.bias && n + 32 < p.N) ? (float)p.bias[n + 32] : 0.f;
         }
-    auto emit = [&](const Acc& acc, int qm, int qn) {
+      auto emit = [&](const Acc& g, const Acc& u, int qm) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int m = mrow + qm * 64 + mt * 16;
-        if (m >= p.M) continue;
+        for (int mt = 0; mt < 4; ++mt) {
+          const int m = mrow + qm * 64 + mt * 16;
+          if (m >= p.M) continue;
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const int n = ncol + qn * 32 + nt * 16;
-          if (n >= p.N) continue;
-          if constexpr (EPI == EPI_PARTIAL) {
-            float* ws = (float*)p.C + ((size_t)split * p.M + m) * p.N + n;
-            *reinterpret_cast<f32x4_t*>(ws) = acc[mt][nt];
-          } else {
+          for (int nt = 0; nt < 2; ++nt) {
+            const int oc = ocol + nt * 16;
+            if (2 * oc >= p.N) continue;
             bf16x4_t o;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = f2bits(act_f<ACT>(acc[mt][nt][r] + bv[qn][nt][r]));
-            *reinterpret_cast<bf16x4_t*>((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+            for (int r = 0; r < 4; ++r) o[r] = f2bits(silu_f(g[mt][nt][r] + bg[nt][r]) * (u[mt][nt][r] + bu[nt][r]));
+            *reinterpret_cast<bf16x4_t*>(C + (size_t)m * p.ldc + oc) = o;
           }
         }
+      };
+      emit(acc00, acc01, 0);
+      emit(acc10, acc11, 1);
+    } else {
+      float bv[2][2][4];
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = ncol + qn * 32 + nt * 16 + r;
+            bv[qn][nt][r] = (EPI == EPI_STORE && p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
+          }
+      auto emit = [&](const Acc& acc, int qm, int qn) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const int m = mrow + qm * 64 + mt * 16;
+          if (m >= p.M) continue;
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const int n = ncol + qn * 32 + nt * 16;
+            if (n >= p.N) continue;
+            if constexpr (EPI == EPI_PARTIAL) {
+              float* ws = p.slab + ((size_t)split * p.M + m) * p.N + n;
+              *reinterpret_cast<f32x4_t*>(ws) = acc[mt][nt];
+            } else {
+              bf16x4_t o;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = f2bits(act_f<ACT>(acc[mt][nt][r] + bv[qn][nt][r]));
+              *reinterpret_cast<bf16x4_t*>((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+            }
+          }
+        }
+      };
+      emit(acc00, 0, 0);
+      emit(acc01, 0, 1);
+      emit(acc11, 1, 1);
+      emit(acc10, 1, 0);
+    }
+  };
+
+  // ---- work: a data-parallel workgroup runs one segment (a whole tile or one K-split of it);
+  // a stream-K workgroup runs an equal contiguous share of the remaining tiles' (tile, K-tile)
+  // iterations.  A tile split across stream-K workgroups is combined in-launch (cdna guide §5
+  // item 2): each part stores its fp32 accumulators to its own slab, drains, one lane releases
+  // (agent) and takes a relaxed agent ticket; the part that draws the last ticket acquires,
+  // sums every part in workgroup order (bitwise reproducible whichever part arrives last),
+  // resets the ticket word and runs the epilogue.
+  const bool dp = (int)blockIdx.x < p.dp_tiles;
+  const int G = p.sk_grid;
+  const int j = dp ? xcd_remap(blockIdx.x, p.dp_tiles) : xcd_remap(blockIdx.x - p.dp_tiles, G);
+  const long tot = dp ? 0 : (long)(p.tiles_m * p.tiles_n - p.dp_tiles) * ks;
+  auto it_begin = [&](int b) -> long { return (long)b * tot / G; };
+  auto owner = [&](long x) -> int { return (int)(((x + 1) * G + tot - 1) / tot) - 1; };
+  auto slot_of = [&](int b, int ts) -> int { return 2 * b + (ts == (int)(it_begin(b) / ks) ? 0 : 1); };
+  long it = dp ? 0 : it_begin(j);
+  const long it1 = dp ? 1 : it_begin(j + 1);
+  unsigned* flag = reinterpret_cast<unsigned*>(smem);
+  while (it < it1) {
+    int tile, kb, ke, split = 0;
+    if (dp) {
+      split = j % p.ksplit;
+      tile = j / p.ksplit;
+      kb = split * p.kt_split;
+      ke = min(ks, kb + p.kt_split);
+      it = 1;
+    } else {
+      const int ts = (int)(it / ks);
+      tile = p.dp_tiles + ts;
+      kb = (int)(it % ks);
+      ke = (int)min((long)ks, kb + (it1 - it));
+      it += ke - kb;
+    }
+    int m0, n0;
+    tile_coords(tile, m0, n0);
+    mainloop(m0, n0, kb, ke - kb);
+    if (!dp && !(kb == 0 && ke == ks)) {
+      const int ts = tile - p.dp_tiles;
+      const int first = owner((long)ts * ks), last = owner((long)ts * ks + ks - 1);
+      // slab stores write-through (sc1): no L2 write-back fence needed before the ticket
+      // (cdna guide §5 item 2, the sc1 form); every wave drains its stores before the barrier
+      {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            p.slab + (size_t)slot_of(j, ts) * 65536, 0, 65536 * 4, 0x00020000);
+#define GT_STORE(ACC, Q, MT, NT) \
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ACC[MT][NT]), rs, tid * 16, Q * kThreads * 16, 16);
+        GT_CHUNKS(GT_STORE)
+#undef GT_STORE
       }
-    };
-    emit(acc00, 0, 0);
-    emit(acc01, 0, 1);
-    emit(acc11, 1, 1);
-    emit(acc10, 1, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned tk = __hip_atomic_fetch_add(&p.cnt[ts], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned is_last = tk == (unsigned)(last - first) ? 1u : 0u;
+        if (is_last) {
+          __hip_atomic_store(&p.cnt[ts], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        flag[0] = is_last;
+      }
+      __syncthreads();
+      const bool is_last = flag[0] != 0u;
+      __syncthreads();  // every wave has read the flag before the next segment's DMA reuses the LDS
+      if (!is_last) continue;
+      // fixed-order sum (((s_first + s_first+1) + ...) + s_last); this part's own from registers
+      for (int c = first; c <= last; ++c) {
+        if (c == j) continue;
+        const float* src = p.slab + (size_t)slot_of(c, ts) * 65536 + tid * 4;
+        // 8 loads in flight per quadrant, then the adds (one vmcnt per quadrant, not per chunk)
+        auto fold = [&](Acc& acc, int q0) {
+          f32x4_t t[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) t[i] = *reinterpret_cast<const f32x4_t*>(src + (q0 + i) * kThreads * 4);
+          if (c < j) {  // parts before this one are summed first: fold them left of the registers
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i >> 1][i & 1] = t[i] + acc[i >> 1][i & 1];
+          } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i >> 1][i & 1] += t[i];
+          }
+        };
+        fold(acc00, 0);
+        fold(acc01, 8);
+        fold(acc11, 16);
+        fold(acc10, 24);
+      }
+    }
+    epilogue(m0, n0, split);
   }
+#undef GT_CHUNKS
 }
 
 // Split-K combine: out = epilogue(sum_s ws[s]) — 8 output columns per thread.
@@ -373,7 +478,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 template <int EPI, int ACT>
 int launch(const Args& a, hipStream_t stream) {
-  const int nwg = a.tiles_m * a.tiles_n * a.ksplit;
+  const int nwg = a.dp_tiles + a.sk_grid;
   gemm_tile_kernel<EPI, ACT><<<nwg, kThreads, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
@@ -381,12 +486,19 @@ int launch(const Args& a, hipStream_t stream) {
 }  // namespace
 
 // y = epilogue(x @ w^T).  epi: 0 store (act: 0 none, 1 gelu-erf, 3 gelu-tanh), 1 silu*mul
-// (w rows interleaved in 32-row gate/up blocks, out [M, N/2]).  ksplit > 1: partial
-// slabs into ws (ksplit * M * N fp32) + splitk_reduce_kernel applies the epilogue.
+// (w rows interleaved in 32-row gate/up blocks, out [M, N/2]).
+//   ksplit > 1: K split into ksplit parts, fp32 planes into ws (ksplit * M * N floats) and
+//               splitk_reduce_kernel applies the epilogue (decode-sized M, few tiles);
+//   ksplit == 1, sk_grid > 0: data-parallel rounds of whole tiles, then sk_grid stream-K
+//               workgroups share the last (tiles - dp) tiles, dp = (tiles / sk_grid - 1) * sk_grid
+//               (all tiles when tiles < sk_grid); ws >= 2 * sk_grid * 65536 floats, cnt >= tiles
+//               zero-initialised words (each reset by its tile's last arriver);
+//   otherwise every tile is one workgroup.
 // Requirements (checked): K % 64 == 0, every split >= 2 K-tiles, lda/ldw % 8 == 0,
 // N % 8 == 0 (silu: N % 64 == 0), ldc % 8 == 0, 16-B aligned pointers.
 GRAG_API int grag_gemm_tile(const void* A, const void* W, const void* bias, void* C, int lda, int ldw, int ldc,
-                            int M, int N, int K, int epi, int act, int ksplit, void* ws, hipStream_t stream) {
+                            int M, int N, int K, int epi, int act, int ksplit, int sk_grid, void* ws, void* cnt,
+                            hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 64 != 0 || K < 128 || lda % 8 != 0 || ldw % 8 != 0 || ldc % 8 != 0 || N % 8 != 0)
     return (int)hipErrorInvalidValue;
@@ -404,14 +516,27 @@ GRAG_API int grag_gemm_tile(const void* A, const void* W, const void* bias, void
   a.A = (const bf16*)A;
   a.W = (const bf16*)W;
   a.bias = (const bf16*)bias;
-  a.C = ksplit > 1 ? ws : C;
+  a.C = C;
+  a.slab = (float*)ws;
+  a.cnt = (unsigned*)cnt;
   a.lda = lda; a.ldw = ldw; a.ldc = ldc;
   a.M = M; a.N = N; a.K = K;
   a.tiles_m = (M + 255) / 256;
   a.tiles_n = (N + 255) / 256;
   a.ksplit = ksplit;
   a.kt_split = kts;
-  if ((long)a.tiles_m * a.tiles_n * ksplit >= (1L << 31)) return (int)hipErrorInvalidValue;
+  const long tiles = (long)a.tiles_m * a.tiles_n;
+  if (tiles * ksplit >= (1L << 30)) return (int)hipErrorInvalidValue;
+  a.dp_tiles = (int)(tiles * ksplit);
+  a.sk_grid = 0;
+  if (ksplit == 1 && sk_grid > 0 && tiles % sk_grid != 0) {
+    if (ws == nullptr || cnt == nullptr) return (int)hipErrorInvalidValue;
+    const long rounds = tiles / sk_grid;
+    a.dp_tiles = rounds >= 1 ? (int)((rounds - 1) * sk_grid) : 0;
+    a.sk_grid = sk_grid;
+    // every stream-K share must cover >= half a tile (<= 3 parts per tile, bounded fixup reads)
+    if ((tiles - a.dp_tiles) * kt < (long)sk_grid * ((kt + 1) / 2)) return (int)hipErrorInvalidValue;
+  }
   int err;
   if (ksplit > 1) {
     err = launch<EPI_PARTIAL, ACT_NONE>(a, stream);

@@ -20,6 +20,7 @@ import torch
 
 from ..ops.attention import varlen_attention
 from ..ops.elementwise import ACT_GELU, POOL_CLS, POOL_MEAN, bias_act, pool_l2norm
+from ..ops import gemm as _tile
 from ..ops.linear import linear
 from ..ops.norm import bert_embed_ln, layernorm
 from .configs import EncoderConfig
@@ -135,7 +136,10 @@ class BertEncoder:
             qkv = linear(h, L.qkv_w, L.qkv_b)
             a = varlen_attention(qkv, seq_start, seq_len, max_len, nh, cfg.head_dim, self.scale, causal=False)
             h = layernorm(linear(a, L.o_w), L.ln1_g, L.ln1_b, eps, bias=L.o_b, residual=h)
-            f = bias_act(linear(h, L.f1_w), L.f1_b, ACT_GELU, inplace=True)
+            if _tile.supported(h, L.f1_w) and _tile.capture_ok(h.device, h.shape[0], L.f1_w.shape[0], H):
+                f = _tile.gemm(h, L.f1_w, L.f1_b, act=_tile.ACT_GELU)  # bias + GELU in the GEMM epilogue
+            else:
+                f = bias_act(linear(h, L.f1_w), L.f1_b, ACT_GELU, inplace=True)
             h = layernorm(linear(f, L.f2_w), L.ln2_g, L.ln2_b, eps, bias=L.f2_b, residual=h)
         mode = POOL_CLS if cfg.pooling == "cls" else POOL_MEAN
         return pool_l2norm(h, seq_start[:-1], seq_len, mode, cfg.normalize, want_bf16=want_bf16)

@@ -7,12 +7,14 @@ Layer dataflow per step (T tokens, kernels in brackets):
   embed gather [grag_embed_gather]
   per layer:
     residual += h ; x = RMSNorm(residual)            [grag_rmsnorm, fused]
-    qkv = x W_qkv^T                                   (hipBLASLt, plain GEMM)
+    qkv = x W_qkv^T                                   [grag_gemm_tile at decode M, else library]
     q, K/V-cache <- bias + NeoX RoPE + paged store    [grag_qkv_rope_kvstore]
     a = paged flash attention (GQA-packed, MFMA)      [grag_paged_attention]
     h = a W_o^T        (+ TP all-reduce, RCCL)
     residual += h ; x = RMSNorm(residual)            [grag_rmsnorm]
-    gu = x W_gu^T ; m = SiLU(g) * u                   [grag_silu_mul]
+    m = SiLU(x W_g^T) * (x W_u^T)                     [grag_gemm_tile EPI_SILU: one GEMM, the
+                                                       SwiGLU product formed in registers; W_gu
+                                                       stored gate/up-interleaved in 32-row blocks]
     h = m W_down^T     (+ TP all-reduce, RCCL)
   final RMSNorm ; LM head on last tokens (vocab-parallel under TP) ; fused
   sampler [grag_sample].
@@ -28,6 +30,7 @@ import torch
 
 from ..ops.attention import AttnMetadata, paged_attention
 from ..ops.elementwise import qkv_rope_kvstore, rope_cos_sin, silu_mul
+from ..ops.gemm import deinterleave_gate_up, interleave_gate_up, mlp_gate_up
 from ..ops.linear import linear
 from ..ops.norm import embed_gather, rmsnorm
 from ..parallel.comm import Group
@@ -58,6 +61,8 @@ class Qwen2Model:
         self.head_dim = cfg.head_dim
         assert cfg.intermediate_size % ts == 0
         self.inter = cfg.intermediate_size // ts
+        # gate/up interleaved in 32-row blocks for the fused SwiGLU GEMM epilogue
+        self.gu_interleaved = self.inter % 32 == 0
         self.vocab_shard = -(-cfg.vocab_size // ts)
         self.vocab0 = tr * self.vocab_shard
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
@@ -136,13 +141,19 @@ class Qwen2Model:
                 L.qkv_b = None
             L.o_w = get(p + "self_attn.o_proj.weight")[:, q0:q1].contiguous()
             L.post_norm = get(p + "post_attention_layernorm.weight")
-            L.gu_w = torch.cat([get(p + "mlp.gate_proj.weight")[i0:i1], get(p + "mlp.up_proj.weight")[i0:i1]],
-                               0).contiguous()
+            wg, wu = get(p + "mlp.gate_proj.weight")[i0:i1], get(p + "mlp.up_proj.weight")[i0:i1]
+            L.gu_w = interleave_gate_up(wg, wu) if self.gu_interleaved else torch.cat([wg, wu], 0).contiguous()
             L.down_w = get(p + "mlp.down_proj.weight")[:, i0:i1].contiguous()
             self.layers.append(L)
         self.norm = get("model.norm.weight")
         head = self.embed if cfg.tie_word_embeddings or "lm_head.weight" not in sd else get("lm_head.weight")
         self.lm_head = self._pad_rows(head[self.vocab0:self.vocab0 + self.vocab_shard].contiguous())
+
+    def gate_up_weights(self, L) -> tuple[torch.Tensor, torch.Tensor]:
+        """(gate [I, H], up [I, H]) of a layer in plain HF row order."""
+        if self.gu_interleaved:
+            return deinterleave_gate_up(L.gu_w)
+        return L.gu_w[: self.inter], L.gu_w[self.inter:]
 
     def param_bytes(self) -> int:
         n = self.embed.numel() + self.norm.numel()
@@ -180,7 +191,8 @@ class Qwen2Model:
             a = paged_attention(q, kc, vc, meta, self.scale, causal=True)
             h = self.tp.all_reduce(linear(a, L.o_w))
             x = rmsnorm(h, L.post_norm, eps, residual=residual)
-            h = self.tp.all_reduce(linear(silu_mul(linear(x, L.gu_w)), L.down_w))
+            m = mlp_gate_up(x, L.gu_w) if self.gu_interleaved else silu_mul(linear(x, L.gu_w))
+            h = self.tp.all_reduce(linear(m, L.down_w))
         return rmsnorm(h, self.norm, eps, residual=residual)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:

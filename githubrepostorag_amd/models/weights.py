@@ -61,9 +61,7 @@ def qwen2_hf_state_dict(model) -> dict:
             sd[p + "self_attn.k_proj.bias"] = L.qkv_b[q:q + kv]
             sd[p + "self_attn.v_proj.bias"] = L.qkv_b[q + kv:]
         sd[p + "self_attn.o_proj.weight"] = L.o_w
-        I = model.inter
-        sd[p + "mlp.gate_proj.weight"] = L.gu_w[:I]
-        sd[p + "mlp.up_proj.weight"] = L.gu_w[I:]
+        sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"] = model.gate_up_weights(L)
         sd[p + "mlp.down_proj.weight"] = L.down_w
     if not cfg.tie_word_embeddings:
         sd["lm_head.weight"] = model.lm_head[: cfg.vocab_size]

@@ -49,7 +49,7 @@ _SIGS = {
     "grag_gemm_stream": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "grag_gemm_stream_plan": [I, I, I, I, P],
     "grag_awq_dequant": [P, P, P, P, I, I, I, P],
-    "grag_gemm_tile": [P, P, P, P, I, I, I, I, I, I, I, I, I, P, P],
+    "grag_gemm_tile": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
 }
 
 

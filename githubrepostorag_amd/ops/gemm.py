@@ -16,6 +16,7 @@ covers the chip.
 from __future__ import annotations
 
 import os
+import threading
 
 import torch
 
@@ -80,23 +81,73 @@ def plan_ksplit(M: int, N: int, K: int) -> int:
     return s
 
 
+SK_EFF = float(os.environ.get("GRAG_TILE_SK_EFF", "0.92"))
+
+
+def plan(M: int, N: int, K: int) -> tuple[int, int]:
+    """(ksplit, sk_grid) for a shape.  Few tiles (<= half the CUs): split-K.
+    Otherwise whole tiles per workgroup, unless the last round of tiles would
+    leave the chip idle enough (tiles / (rounds * CUs) < SK_EFF): then the
+    last full round plus the remainder are shared by one stream-K round.
+    Measured (profiles/gemm_tile_ab_v2.jsonl): stream-K pays only with >= 2
+    rounds ahead of it (down_proj M=16384: 1721 -> 1534 us); an all-stream-K
+    grid (one round or less) loses to whole tiles (o_proj M=4096 95 -> 149 us,
+    gate_up M=192 94 -> 102 us: the fixup slabs cost more than the idle CUs)."""
+    ks = plan_ksplit(M, N, K)
+    if ks > 1:
+        return ks, 0
+    tiles = -(-M // 256) * -(-N // 256)
+    ncu = _num_cus()
+    if tiles % ncu == 0 or tiles <= 2 * ncu:
+        return 1, 0
+    eff = tiles / (-(-tiles // ncu) * ncu)
+    return (1, ncu) if eff < SK_EFF else (1, 0)
+
+
+def _ws_floats(M: int, N: int, ksplit: int, sk: int) -> int:
+    return ksplit * M * N if ksplit > 1 else (2 * sk * 65536 if sk else 0)
+
+
 class _Workspace:
-    """Per-device fp32 split-K slab; grown only outside hipGraph capture."""
+    """fp32 split-K slabs, one per (thread, device): the engine thread and the
+    retrieval threads run GEMMs on different streams concurrently, so a shared
+    slab would race.  Grown only outside hipGraph capture (a capture reuses the
+    slab its eager warm-up step sized); outgrown slabs stay alive because
+    captured graphs may still point at them."""
 
     def __init__(self):
-        self.buf: dict = {}
+        self._tls = threading.local()
         self.retired: list = []
 
     def get(self, dev: torch.device, floats: int) -> torch.Tensor:
-        b = self.buf.get(dev.index)
+        bufs = getattr(self._tls, "bufs", None)
+        if bufs is None:
+            bufs = self._tls.bufs = {}
+        b = bufs.get(dev.index)
         if b is None or b.numel() < floats:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("gemm_tile split-K workspace must be sized before hipGraph capture")
             if b is not None:
-                self.retired.append(b)  # captured graphs may still reference it
+                self.retired.append(b)
             b = torch.empty(max(floats, 1 << 20), dtype=torch.float32, device=dev)
-            self.buf[dev.index] = b
+            bufs[dev.index] = b
         return b
+
+    def ready(self, dev: torch.device, floats: int) -> bool:
+        b = getattr(self._tls, "bufs", {}).get(dev.index)
+        return b is not None and b.numel() >= floats
+
+    def counters(self, dev: torch.device) -> torch.Tensor:
+        """Stream-K arrival tickets: zero at rest (each tile's last arriver resets its word)."""
+        cs = getattr(self._tls, "cnts", None)
+        if cs is None:
+            cs = self._tls.cnts = {}
+        c = cs.get(dev.index)
+        if c is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("gemm_tile stream-K counters must be allocated before hipGraph capture")
+            c = cs[dev.index] = torch.zeros(1 << 14, dtype=torch.int32, device=dev)
+        return c
 
     def reserve(self, dev: torch.device, floats: int) -> None:
         self.get(dev, floats)
@@ -105,17 +156,19 @@ class _Workspace:
 WS = _Workspace()
 
 
-def _launch(x, w, b, out, epi, act, ksplit):
+def _launch(x, w, b, out, epi, act, ksplit, sk):
     M, K = x.shape
     N = w.shape[0]
-    ws = WS.get(x.device, ksplit * M * N) if ksplit > 1 else None
+    fl = _ws_floats(M, N, ksplit, sk)
+    ws = WS.get(x.device, fl) if fl else None
+    cnt = WS.counters(x.device) if sk else None
     call("grag_gemm_tile", ptr(x), ptr(w), ptr(b), ptr(out), x.stride(0), w.stride(0), out.stride(0),
-         M, N, K, epi, act, ksplit, ptr(ws))
+         M, N, K, epi, act, ksplit, sk, ptr(ws), ptr(cnt))
     return out
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, act: int = ACT_NONE,
-         ksplit: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+         ksplit: int | None = None, out: torch.Tensor | None = None, sk: int | None = None) -> torch.Tensor:
     """y = act(x @ w.T + b), bf16 [M, N] on the owned MFMA kernel (fp32 CPU reference)."""
     if not x.is_cuda:
         y = torch.nn.functional.linear(x.float(), w.float(), None if b is None else b.float())
@@ -126,15 +179,14 @@ def gemm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, act: i
         return y.to(x.dtype)
     M, K = x.shape
     N = w.shape[0]
-    if ksplit is None:
-        ksplit = plan_ksplit(M, N, K)
+    ksplit, sk = plan(M, N, K) if ksplit is None else (ksplit, sk or 0)
     if out is None:
         out = torch.empty(M, N, dtype=x.dtype, device=x.device)
-    return _launch(x, w, b, out, EPI_STORE, act, ksplit)
+    return _launch(x, w, b, out, EPI_STORE, act, ksplit, sk)
 
 
 def gemm_silu(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None = None,
-              ksplit: int | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+              ksplit: int | None = None, out: torch.Tensor | None = None, sk: int | None = None) -> torch.Tensor:
     """h = silu(x @ wg.T + bg) * (x @ wu.T + bu) with ``w_gu`` interleaved (see module doc)."""
     M, K = x.shape
     N2 = w_gu.shape[0]
@@ -146,8 +198,25 @@ def gemm_silu(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None = N
         return (torch.nn.functional.silu(g) * u).to(x.dtype)
     if N2 % 64:
         raise ValueError("gemm_silu: 2I must be a multiple of 64")
-    if ksplit is None:
-        ksplit = plan_ksplit(M, N2, K)
+    ksplit, sk = plan(M, N2, K) if ksplit is None else (ksplit, sk or 0)
     if out is None:
         out = torch.empty(M, N2 // 2, dtype=x.dtype, device=x.device)
-    return _launch(x, w_gu, b_gu, out, EPI_SILU, ACT_NONE, ksplit)
+    return _launch(x, w_gu, b_gu, out, EPI_SILU, ACT_NONE, ksplit, sk)
+
+
+def capture_ok(dev: torch.device, M: int, N: int, K: int) -> bool:
+    """False only inside a hipGraph capture whose split-K slab was not sized by an eager step."""
+    ks, sk = plan(M, N, K)
+    fl = _ws_floats(M, N, ks, sk)
+    return fl == 0 or not torch.cuda.is_current_stream_capturing() or (WS.ready(dev, fl) and (
+        not sk or getattr(WS._tls, "cnts", {}).get(dev.index) is not None))
+
+
+def mlp_gate_up(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None = None) -> torch.Tensor:
+    """SwiGLU input half for an interleaved gate/up weight: the fused tile
+    kernel when it takes the shape, else library GEMM + reshape (same math)."""
+    M, K = x.shape
+    if not x.is_cuda or (supported(x, w_gu) and capture_ok(x.device, M, w_gu.shape[0], K)):
+        return gemm_silu(x, w_gu, b_gu)
+    y = torch.nn.functional.linear(x, w_gu, b_gu).view(M, -1, 2, 32)
+    return (torch.nn.functional.silu(y[:, :, 0].float()) * y[:, :, 1].float()).to(x.dtype).reshape(M, -1)

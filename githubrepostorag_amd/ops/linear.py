@@ -8,6 +8,9 @@ A/B in scripts/bench_gemm.py:
 * ``grag_gemm_stream`` (deep-K projections such as down_proj, and the LM head
   at M <= 32): stream-K over (tile, 64-k) iterations, full-line LDS-DMA ring,
   in-launch split-tile combine;
+* ``grag_gemm_tile`` (ops/gemm.py, 256x256 MFMA tiles + split-K slabs) for
+  decode batches 32 < M <= 256: 1.1-1.5x the library on every Qwen2-7B
+  projection (profiles/gemm_tile_ab_v1.jsonl);
 * larger M (prefill, encoder batches): plain GEMMs go to hipBLASLt through
   ``torch.nn.functional.linear`` — the library is used only for plain
   (epilogue-free / bias-only) GEMMs; everything fused around them
@@ -23,6 +26,7 @@ from pathlib import Path
 
 import torch
 
+from . import gemm as _tile
 from ._lib import call, lib, ptr
 
 TUNING_DIR = Path(__file__).resolve().parents[1] / "tuning"
@@ -218,6 +222,17 @@ def splitk_parts(M: int, N: int, K: int) -> int:
     return 0
 
 
+TILE_MIN_M = int(os.environ.get("GRAG_TILE_MIN_M", "33"))
+TILE_MAX_M = int(os.environ.get("GRAG_TILE_MAX_M", "256"))
+
+
+def use_tile(M: int, N: int, K: int) -> bool:
+    """Owned tile GEMM at decode batches (measured range 64..256: every
+    Qwen2-7B projection 1.1-1.5x the library); the vocab-wide LM head and
+    prefill-sized M stay on the measured paths below."""
+    return TILE_MIN_M <= M <= TILE_MAX_M and N <= 65536 and K >= 512
+
+
 def use_splitk(M: int, N: int, K: int) -> bool:
     return splitk_parts(M, N, K) > 0
 
@@ -250,6 +265,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> t
             and x.stride(1) == 1 and w.stride(1) == 1):
         M, K = x.shape
         N = w.shape[0]
+        if use_tile(M, N, K) and _tile.supported(x, w) and _tile.capture_ok(x.device, M, N, K):
+            return _tile.gemm(x, w, b)
         parts = splitk_parts(M, N, K)
         if parts:
             return gemm_splitk(x, w, b, parts)

@@ -70,8 +70,8 @@ def main():
         ncopy = max(1, min(8, (600 << 20) // wbytes + 1))
         ws = [(torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16) * 0.05 for _ in range(ncopy)]
         x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
-        S = G.plan_ksplit(M, N, K)
-        G.WS.reserve(dev, S * M * N)
+        S, SK = G.plan(M, N, K)
+        G.WS.reserve(dev, G._ws_floats(M, N, S, SK))
         it = {"i": 0}
 
         def lib_fn():
@@ -86,26 +86,34 @@ def main():
         def own_fn():
             w = ws[it["i"] % ncopy]
             it["i"] += 1
-            return G.gemm_silu(x, w, ksplit=S) if silu else G.gemm(x, w, ksplit=S)
+            return G.gemm_silu(x, w, ksplit=S, sk=SK) if silu else G.gemm(x, w, ksplit=S, sk=SK)
+
+        def own_nosk():
+            w = ws[it["i"] % ncopy]
+            it["i"] += 1
+            return G.gemm_silu(x, w, ksplit=S, sk=0) if silu else G.gemm(x, w, ksplit=S, sk=0)
 
         # correctness spot check (plain GEMM part) before timing
         if not silu:
             r = torch.nn.functional.linear(x[:64].float(), ws[0].float())
-            y = G.gemm(x, ws[0], ksplit=S)[:64].float()
+            y = G.gemm(x, ws[0], ksplit=S, sk=SK)[:64].float()
             err = ((y - r).abs().max() / (r.abs().max() + 1e-6)).item()
         else:
             err = float("nan")
         for _ in range(3):
             lib_fn(); own_fn()
         torch.cuda.synchronize()
-        tl, to = [], []
+        tl, to, tn = [], [], []
         for _ in range(args.reps):
             tl += timeit(lib_fn, 1)
             to += timeit(own_fn, 1)
+            if SK:
+                tn += timeit(own_nosk, 1)
         ml, mo = statistics.median(tl), statistics.median(to)
         flop = 2.0 * M * N * K
         byts = wbytes + M * K * 2 + M * N * 2
-        row = {"shape": name, "M": M, "N": N, "K": K, "ksplit": S, "silu_fused": silu,
+        row = {"shape": name, "M": M, "N": N, "K": K, "ksplit": S, "sk": SK, "silu_fused": silu,
+               "own_nosk_us": round(statistics.median(tn), 1) if tn else None,
                "lib_us": round(ml, 1), "own_us": round(mo, 1), "speedup": round(ml / mo, 3),
                "own_tflops": round(flop / mo / 1e6, 1), "lib_tflops": round(flop / ml / 1e6, 1),
                "own_TBps": round(byts / mo / 1e6, 2), "lib_TBps": round(byts / ml / 1e6, 2), "relerr": err}

@@ -104,3 +104,29 @@ def test_gemm_graph_replay(dev):
     g.replay()
     torch.cuda.synchronize()
     check(out, ref(x, w), K)
+
+
+@pytest.mark.parametrize("M,N,K,sk", [(512, 1536, 512, 16), (512, 1536, 512, 20), (2560, 1024, 384, 16),
+                                      (4096, 4608, 1024, 256), (192, 37888, 1024, 256)])
+def test_gemm_stream_k(dev, M, N, K, sk):
+    x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+    y = G.gemm(x, w, b, ksplit=1, sk=sk)
+    check(y, ref(x, w, b), K)
+    y2 = G.gemm(x, w, b, ksplit=1, sk=sk)
+    assert torch.equal(y, y2), "stream-K fixup must be bitwise reproducible"
+
+
+def test_gemm_silu_stream_k(dev):
+    M, I, K = 192, 4096, 1024  # 32 tiles over 48 stream-K workgroups: every tile split
+    x = rnd(M, K, dev=dev, scale=0.3)
+    wg, wu = rnd(I, K, dev=dev, seed=1, scale=0.2), rnd(I, K, dev=dev, seed=2, scale=0.2)
+    h = G.gemm_silu(x, G.interleave_gate_up(wg, wu), ksplit=1, sk=48)
+    check(h, torch.nn.functional.silu(ref(x, wg)) * ref(x, wu), K)
+
+
+def test_plan_stream_k():
+    if G._num_cus() != 256:
+        pytest.skip("plan thresholds are stated for 256 CUs")
+    assert G.plan(192, 37888, 3584) == (1, 0)     # 148 tiles: whole tiles (all-stream-K measured slower)
+    assert G.plan(16384, 4608, 3584) == (1, 256)  # 1152 tiles = 4.5 rounds
+    assert G.plan(16384, 37888, 3584) == (1, 0)   # 9472 tiles = 37 full rounds
