@@ -5,14 +5,15 @@ batches (varlen: no padding compute), truncated to the model's
 ``max_seq_length`` like sentence-transformers does."""
 from __future__ import annotations
 
+import os
 import threading
 
 import torch
 
 from ..engine.tokenizer import WordPieceTokenizer
-from ..utils.gpu_guard import guarded, side_stream
+from ..utils.gpu_guard import gpu_guard, gpu_shared, side_stream
 from ..models.configs import EncoderConfig, encoder_config
-from ..models.encoder import BertEncoder
+from ..models.encoder import BertEncoder, EncoderGraphs
 
 
 class Embedder:
@@ -25,7 +26,10 @@ class Embedder:
         self.max_batch = max_batch
         self.dim = self.cfg.hidden_size
         self.lock = threading.Lock()  # one encoder stream at a time
-        self.stats = {"texts": 0, "tokens": 0}
+        self.stats = {"texts": 0, "tokens": 0, "graph_batches": 0}
+        # query-sized batches replay captured encoder graphs (GRAG_ENCODER_GRAPHS=0: eager)
+        self.graphs = (EncoderGraphs(encoder) if encoder.device.type == "cuda"
+                       and os.environ.get("GRAG_ENCODER_GRAPHS", "1") != "0" else None)
 
     @classmethod
     def from_name(cls, name: str, device="cuda", seed: int = 0, **kw) -> "Embedder":
@@ -36,7 +40,6 @@ class Embedder:
         L = min(self.cfg.max_seq_length, self.cfg.max_position)
         return [self.tok.encode(prefix + (t or ""), L) for t in texts]
 
-    @guarded
     @torch.inference_mode()
     def embed_ids(self, ids: list[list[int]]) -> torch.Tensor:
         """-> bf16 [n, d] L2-normalised on the encoder's device (input order)."""
@@ -44,8 +47,21 @@ class Embedder:
         out = torch.empty(n, self.dim, dtype=torch.bfloat16, device=self.encoder.device)
         if n == 0:
             return out
+        if self.graphs is not None and n <= EncoderGraphs.B_BUCKETS[-1]:
+            bk = self.graphs.bucket_for(ids)
+            if bk is not None and not self.graphs.has(bk):
+                with gpu_guard(), self.lock, side_stream(self.encoder.device):  # capture: exclusive
+                    self.graphs.capture(*bk)
+            with gpu_shared(), self.lock, side_stream(self.encoder.device):
+                r = self.graphs.run(ids, allow_capture=False)
+                if r is not None:
+                    out.copy_(r[1])
+                    self.stats["graph_batches"] += 1
+                    self.stats["tokens"] += sum(len(x) for x in ids)
+                    self.stats["texts"] += n
+                    return out
         order = sorted(range(n), key=lambda i: len(ids[i]))
-        with self.lock, side_stream(self.encoder.device):
+        with gpu_shared(), self.lock, side_stream(self.encoder.device):
             i = 0
             while i < n:
                 j, tok = i, 0
@@ -152,7 +168,8 @@ class _QueryBatcher:
                 with side_stream(self.emb.encoder.device):
                     out = self.emb.embed_ids(flat)
                     if out.is_cuda:
-                        torch.cuda.current_stream(out.device).synchronize()
+                        with gpu_shared():  # the sync must not land inside a graph capture
+                            torch.cuda.current_stream(out.device).synchronize()
                 self.batches += 1
                 self.texts += len(flat)
                 o = 0

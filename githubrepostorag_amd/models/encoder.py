@@ -128,7 +128,13 @@ class BertEncoder:
         pos_ids = torch.cat([torch.arange(n, dtype=torch.int32) for n in lens]).to(dev)
         seq_start = torch.tensor(starts, dtype=torch.int32, device=dev)
         seq_len = torch.tensor(lens, dtype=torch.int32, device=dev)
-        max_len = max(lens)
+        return self.forward(ids, pos_ids, seq_start, seq_len, max(lens), want_bf16)
+
+    def forward(self, ids, pos_ids, seq_start, seq_len, max_len: int, want_bf16: bool = True):
+        """Packed token rows -> pooled, L2-normalised embeddings.  Sequence b owns rows
+        [seq_start[b], seq_start[b] + seq_len[b]); rows past that (the fixed-shape padding
+        of a captured batch) are computed but never attended to or pooled."""
+        cfg = self.cfg
         H, nh = cfg.hidden_size, cfg.num_heads
         eps = cfg.layer_norm_eps
         h = bert_embed_ln(ids, pos_ids, None, self.word, self.pos, self.typ, self.emb_g, self.emb_b, eps)
@@ -143,3 +149,99 @@ class BertEncoder:
             h = layernorm(linear(f, L.f2_w), L.ln2_g, L.ln2_b, eps, bias=L.f2_b, residual=h)
         mode = POOL_CLS if cfg.pooling == "cls" else POOL_MEAN
         return pool_l2norm(h, seq_start[:-1], seq_len, mode, cfg.normalize, want_bf16=want_bf16)
+
+
+class EncoderGraphs:
+    """hipGraph-captured encoder passes for query-sized batches (VERDICT r1 weak
+    item 4: the eager encoder is launch-bound, ~8 launches x 24 layers for a few
+    short questions).  A batch of n sequences of at most l tokens runs in the
+    (B >= n, L >= l) bucket: sequence b occupies rows [b*L, b*L + len_b), the
+    padding rows ride along in the GEMMs but are masked out of attention and
+    pooling by seq_len, and bucket rows past n are 1-token dummies.  Position ids
+    and sequence starts are constants of the bucket; only token ids and lengths
+    are copied in (one pinned H2D copy) before the replay."""
+
+    B_BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128)
+    L_BUCKETS = (16, 32, 64, 128)
+
+    def __init__(self, enc: "BertEncoder"):
+        self.enc = enc
+        self.graphs: dict = {}
+        self.pool = None
+        self._events: dict = {}
+        self.stats = {"replays": 0, "captures": 0}
+
+    def bucket(self, n: int, lmax: int):
+        B = next((b for b in self.B_BUCKETS if b >= n), None)
+        L = next((x for x in self.L_BUCKETS if x >= lmax and x <= self.enc.cfg.max_position), None)
+        return None if B is None or L is None else (B, L)
+
+    def bucket_for(self, batch: list[list[int]]):
+        maxp = self.enc.cfg.max_position
+        return self.bucket(len(batch), max(max(1, min(len(x), maxp)) for x in batch)) if batch else None
+
+    def has(self, bk) -> bool:
+        return bk in self.graphs
+
+    def capture(self, B: int, L: int):
+        """Capture bucket (B, L); the caller holds the capture guard (gpu_guard)."""
+        return self.graphs.get((B, L)) or self._capture(B, L)
+
+    def _capture(self, B: int, L: int):
+        dev = self.enc.device
+        n_in = 2 * B * L + 2 * B + 1
+        host = torch.zeros(n_in, dtype=torch.int32).pin_memory()
+        dbuf = torch.zeros(n_in, dtype=torch.int32, device=dev)
+        ids, pos = dbuf[: B * L], dbuf[B * L: 2 * B * L]
+        starts, lens = dbuf[2 * B * L: 2 * B * L + B + 1], dbuf[2 * B * L + B + 1:]
+        pos.copy_(torch.arange(L, dtype=torch.int32, device=dev).repeat(B))
+        starts.copy_(torch.arange(B + 1, dtype=torch.int32, device=dev) * L)
+        lens.fill_(1)
+        host.copy_(dbuf.cpu())
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        s = torch.cuda.current_stream(dev)
+        self.enc.forward(ids, pos, starts, lens, L, want_bf16=True)  # eager warm-up sizes workspaces
+        s.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
+            outf, outb = self.enc.forward(ids, pos, starts, lens, L, want_bf16=True)
+        self.stats["captures"] += 1
+        ent = (g, host, dbuf, outf, outb)
+        self.graphs[(B, L)] = ent
+        return ent
+
+    def run(self, batch: list[list[int]], allow_capture: bool = True):
+        """-> (fp32 [n, H], bf16 [n, H]) views into the bucket's static outputs
+        (valid until the next replay of that bucket on this stream); None when no
+        bucket fits (the caller runs eagerly)."""
+        n = len(batch)
+        maxp = self.enc.cfg.max_position
+        lens = [max(1, min(len(x), maxp)) for x in batch]
+        bk = self.bucket(n, max(lens))
+        if bk is None:
+            return None
+        B, L = bk
+        ent = self.graphs.get(bk)
+        if ent is None:
+            if not allow_capture:
+                return None
+            ent = self._capture(B, L)
+        g, host, dbuf, outf, outb = ent
+        ev = self._events.get(bk)
+        if ev is not None:
+            ev.synchronize()  # the previous replay's H2D copy has read the pinned buffer
+        h = host.numpy()
+        h[: B * L] = 0
+        for b, (x, ln) in enumerate(zip(batch, lens)):
+            if x:
+                h[b * L: b * L + ln] = x[:ln]
+        lo = 2 * B * L + B + 1
+        h[lo: lo + n] = lens
+        h[lo + n: lo + B] = 1
+        dbuf.copy_(host, non_blocking=True)
+        ev = self._events[bk] = torch.cuda.Event()
+        ev.record()
+        g.replay()
+        self.stats["replays"] += 1
+        return outf[:n], outb[:n]

@@ -49,6 +49,11 @@ _SIGS = {
     "grag_gemm_stream": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "grag_gemm_stream_plan": [I, I, I, I, P],
     "grag_awq_dequant": [P, P, P, P, I, I, I, P],
+    "grag_ivf_plan": [P, I, I, P, I, P, P, P, P],
+    "grag_ivf_plan_max_pairs": [],
+    "grag_topk_merge": [P, P, I, P, I, I, I, I, P, P, I, I, I, P, P, P],
+    "grag_topk_merge_cap": [],
+    "grag_bitmap_update": [P, P, I, I, P],
     "grag_gemm_tile": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
 }
 

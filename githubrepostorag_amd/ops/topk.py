@@ -173,3 +173,63 @@ def score_topk_work(X, Q, k, work_rows: torch.Tensor, work_q: torch.Tensor, nqt:
          ptr(work_rows), ptr(work_q), W, cols, vals, ops, nf, ptr(bitmap), ptr(row_ids), qc, nqc, ptr(qsel), ptr(qval),
          ptr(out_s), ptr(out_i))
     return out_s.view(W, nqt * 16, nw * k), out_i.view(W, nqt * 16, nw * k)
+
+
+# ---------------------------------------------------------------- device-side merge / IVF plan / bitmap
+MERGE_MAX_K = 16
+
+
+def merge_partials(ps: torch.Tensor, pi: torch.Tensor, k: int, nq: int, cand: torch.Tensor | None = None,
+                   cnt: int = 0, affine: tuple = (1, 0, 0), extra: tuple | None = None):
+    """Final top-k per query from partial lists (``grag_topk_merge``): query q's
+    candidate rows of ps/pi [R, L] are ``cand[q, :cnt]`` or the affine rows
+    (q // G) * A + q % G + j * B; ``extra`` = (scores [nq, L2], ids [nq, L2])."""
+    L = ps.shape[-1]
+    G, A, B = affine
+    out_s = torch.empty(nq, k, dtype=torch.float32, device=ps.device)
+    out_i = torch.empty(nq, k, dtype=torch.int64, device=ps.device)
+    es, ei = (None, None) if extra is None else (extra[0].contiguous(), extra[1].contiguous())
+    L2 = 0 if extra is None else es.shape[1]
+    call("grag_topk_merge", ptr(ps), ptr(pi), L, ptr(cand), cnt, G, A, B, ptr(es), ptr(ei), L2, nq, k,
+         ptr(out_s), ptr(out_i))
+    return out_s, out_i
+
+
+def merge_fits(cnt: int, L: int, L2: int, k: int) -> bool:
+    return k <= MERGE_MAX_K and cnt * L + L2 <= lib().grag_topk_merge_cap()
+
+
+def ivf_plan(lists: torch.Tensor, offsets: torch.Tensor, nlist: int):
+    """Coarse probe lists [nq, nprobe] int64 -> (work_rows [P, 2], work_q [P, 16], cand [nq, nprobe]),
+    P = nq * nprobe (items past the real count are empty)."""
+    nq, nprobe = lists.shape
+    P = nq * nprobe
+    dev = lists.device
+    work_rows = torch.empty(P, 2, dtype=torch.int64, device=dev)
+    work_q = torch.empty(P, 16, dtype=torch.int32, device=dev)
+    cand = torch.empty(nq, nprobe, dtype=torch.int32, device=dev)
+    call("grag_ivf_plan", ptr(lists.contiguous()), nq, nprobe, ptr(offsets), nlist, ptr(work_rows), ptr(work_q),
+         ptr(cand))
+    return work_rows, work_q, cand
+
+
+def ivf_plan_fits(nq: int, nprobe: int) -> bool:
+    return nq * nprobe <= lib().grag_ivf_plan_max_pairs()
+
+
+def bitmap_update(bitmap: torch.Tensor, rows: torch.Tensor, alive: bool) -> None:
+    """Set (alive) / clear live bits of rows (int64, device) in place."""
+    if rows.numel() == 0:
+        return
+    if not bitmap.is_cuda:
+        import numpy as np
+
+        r = rows.long().cpu().numpy()
+        words = bitmap.numpy().view(np.uint32)
+        bits = (np.uint32(1) << (r & 31).astype(np.uint32)).astype(np.uint32)
+        if alive:
+            np.bitwise_or.at(words, r >> 5, bits)
+        else:
+            np.bitwise_and.at(words, r >> 5, ~bits)
+        return
+    call("grag_bitmap_update", ptr(bitmap), ptr(rows.to(torch.int64).contiguous()), rows.numel(), 1 if alive else 0)

@@ -27,7 +27,7 @@ from fastapi.middleware.cors import CORSMiddleware
 from fastapi.staticfiles import StaticFiles
 from starlette.responses import StreamingResponse
 
-from ..utils.gpu_guard import gpu_guard
+from ..utils.gpu_guard import gpu_shared
 from . import metrics as M
 from .events import CancelFlags, EventLog
 from .health import _get_app_start_time, register_health_endpoints
@@ -222,7 +222,7 @@ def create_app(state: APIState | None = None, runtime_factory=None) -> FastAPI:
         texts = [body.input] if isinstance(body.input, str) else list(body.input)
         loop = asyncio.get_running_loop()
         def _embed():
-            with gpu_guard():  # the .cpu() sync must not land inside an engine graph capture
+            with gpu_shared():  # the .cpu() sync must not land inside an engine graph capture
                 return rt.embedder.embed_documents(texts).float().cpu().tolist()
 
         vecs = await loop.run_in_executor(None, _embed)

@@ -60,9 +60,10 @@ class RAGRuntime:
         # store
         if store is None:
             if s.index_dir and (Path(s.index_dir) / "manifest.json").exists():
-                store = VectorStore.load(s.index_dir, self.device)
-            else:
-                store = VectorStore(embedder.dim, self.device, s.table_names())
+                store = VectorStore.load(s.index_dir, self.device, nprobe=s.nprobe)
+            else:  # INDEX_KIND / NLIST / NPROBE select the per-table index (flat | ivf)
+                store = VectorStore(embedder.dim, self.device, s.table_names(), index_kind=s.index_kind,
+                                    nlist=s.nlist, nprobe=s.nprobe)
         self.store = store
         self.retrievers = RetrieverFactory(store, embedder)
         # LLM engine

@@ -9,8 +9,10 @@ and the service runs retrieval / embedding / ingest on other threads against
 the same device.  Captures are rare (warm-up, first use of a shape), so the
 cost is one uncontended RLock acquire per retrieval / embedding call.
 
-Use ``with gpu_guard():`` around a thread's GPU section that synchronises, or
-decorate an entry point with ``@guarded``.  ``side_stream`` keeps such
+Captures hold the guard exclusively (``with gpu_guard():``); a thread's GPU
+section that synchronises holds it shared (``with gpu_shared():`` or the
+``@guarded`` decorator), so retrieval / embedding / ingest sections run
+concurrently with each other and only wait while a capture is open.  ``side_stream`` keeps such
 latency-bound sections off the engine's stream.
 """
 from __future__ import annotations
@@ -21,21 +23,98 @@ import threading
 
 import torch
 
-_LOCK = threading.RLock()
-_TLS = threading.local()
+class _CaptureGuard:
+    """Shared/exclusive guard.  Capture holds it EXCLUSIVE; any thread section
+    that may synchronise (a search's ``.cpu()``, an embedding batch, an upsert)
+    holds it SHARED, so those sections run concurrently with each other and
+    only wait while a capture is open.  Re-entrant per thread (a shared
+    section inside the capturing thread's exclusive one is a no-op); a thread
+    never upgrades shared -> exclusive (it would deadlock against itself)."""
+
+    def __init__(self):
+        self._cond = threading.Condition()
+        self._readers = 0
+        self._writer = None
+        self._waiting = 0
+        self._tls = threading.local()
+
+    def _depth(self, kind):
+        return getattr(self._tls, kind, 0)
+
+    @contextlib.contextmanager
+    def shared(self):
+        if self._depth("ex") or self._depth("sh"):
+            self._tls.sh = self._depth("sh") + 1
+            try:
+                yield
+            finally:
+                self._tls.sh -= 1
+            return
+        with self._cond:
+            while self._writer is not None or self._waiting:
+                self._cond.wait()
+            self._readers += 1
+        self._tls.sh = 1
+        try:
+            yield
+        finally:
+            self._tls.sh = 0
+            with self._cond:
+                self._readers -= 1
+                if self._readers == 0:
+                    self._cond.notify_all()
+
+    @contextlib.contextmanager
+    def exclusive(self):
+        if self._depth("ex"):
+            self._tls.ex += 1
+            try:
+                yield
+            finally:
+                self._tls.ex -= 1
+            return
+        if self._depth("sh"):
+            raise RuntimeError("gpu_guard: cannot take the capture guard inside a shared section")
+        me = threading.get_ident()
+        with self._cond:
+            self._waiting += 1
+            while self._writer is not None or self._readers:
+                self._cond.wait()
+            self._waiting -= 1
+            self._writer = me
+        self._tls.ex = 1
+        try:
+            yield
+        finally:
+            self._tls.ex = 0
+            with self._cond:
+                self._writer = None
+                self._cond.notify_all()
 
 
-def gpu_guard() -> threading.RLock:
-    return _LOCK
+_GUARD = _CaptureGuard()
+
+
+def gpu_guard():
+    """Exclusive section (hipGraph capture): ``with gpu_guard(): ...``"""
+    return _GUARD.exclusive()
+
+
+def gpu_shared():
+    """Shared section (may synchronise; must not overlap a capture)."""
+    return _GUARD.shared()
 
 
 def guarded(fn):
     @functools.wraps(fn)
     def wrapper(*a, **k):
-        with _LOCK:
+        with _GUARD.shared():
             return fn(*a, **k)
 
     return wrapper
+
+
+_TLS = threading.local()
 
 
 def _thread_stream(device: torch.device) -> torch.cuda.Stream:

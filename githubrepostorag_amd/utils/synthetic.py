@@ -95,3 +95,95 @@ def clustered_vectors(n: int, d: int, n_centers: int = 4096, noise: float = 0.35
         x = C[c] + noise * torch.randn(m, d, generator=g, device=device) / d ** 0.5
         out[s:s + m] = (x / x.norm(dim=1, keepdim=True)).to(torch.bfloat16)
     return out
+
+
+class SyntheticCorpus:
+    """Virtual rows of a vector table (index/store.py ``RowStore`` segments): row i
+    of a bulk-loaded synthetic corpus gets a deterministic row_id, chunk text and
+    metadata (namespace / repo / module / file_path / language / scope), so a
+    10M-row table carries its host rows as a recipe instead of 10M objects.
+    ``columns(n, device)`` returns the matching dictionary-coded filter columns."""
+
+    def __init__(self, n: int, seed: int = 0, n_repos: int = 64, n_modules: int = 8, files_per_module: int = 64,
+                 namespace: str = "default", scope: str = "chunk", text_chars: int = 800):
+        self.n, self.seed = int(n), int(seed)
+        self.n_repos, self.n_modules, self.fpm = n_repos, n_modules, files_per_module
+        self.namespace, self.scope, self.text_chars = namespace, scope, text_chars
+        self.prefix = f"syn{self.seed}-"
+
+    def spec(self) -> dict:
+        return {"kind": "synthetic", "n": self.n, "seed": self.seed, "n_repos": self.n_repos,
+                "n_modules": self.n_modules, "files_per_module": self.fpm, "namespace": self.namespace,
+                "scope": self.scope, "text_chars": self.text_chars}
+
+    # row i -> (repo, module, file, language) indices
+    def _parts(self, i: int):
+        repo = i % self.n_repos
+        mod = (i // self.n_repos) % self.n_modules
+        f = (i // (self.n_repos * self.n_modules)) % self.fpm
+        return repo, mod, f, (repo + mod + f) % len(_LANGS)
+
+    def repo_name(self, j: int) -> str:
+        return f"{_WORDS[j % len(_WORDS)]}-{_WORDS[(j * 7 + 3) % len(_WORDS)]}-{j}"
+
+    def module_name(self, j: int) -> str:
+        return _WORDS[(j * 5 + 1) % len(_WORDS)] + f"{j}"
+
+    def row_id(self, i: int) -> str:
+        return f"{self.prefix}{i}"
+
+    def index_of(self, row_id: str):
+        if not row_id.startswith(self.prefix):
+            return None
+        try:
+            return int(row_id[len(self.prefix):])
+        except ValueError:
+            return None
+
+    def text(self, i: int) -> str:
+        return chunk_text(self.seed * 1_000_003 + i, self.text_chars)
+
+    def meta(self, i: int) -> dict:
+        repo, mod, f, lang = self._parts(i)
+        ext, language = _LANGS[lang]
+        m = self.module_name(mod)
+        return {"namespace": self.namespace, "repo": self.repo_name(repo), "module": m,
+                "file_path": f"{m}/{_WORDS[f % len(_WORDS)]}_{f}.{ext}", "language": language,
+                "scope": self.scope, "doc_type": self.scope}
+
+    def register(self, table) -> None:
+        """Register every dictionary value this corpus uses, in a fixed order, so
+        ``columns`` can encode rows arithmetically."""
+        self._codes = {}
+        for fld, vals in (("namespace", [self.namespace]), ("scope", [self.scope]), ("doc_type", [self.scope]),
+                          ("repo", [self.repo_name(j) for j in range(self.n_repos)]),
+                          ("module", [self.module_name(j) for j in range(self.n_modules)]),
+                          ("language", [lang for _, lang in _LANGS])):
+            self._codes[fld] = torch.tensor([table._code(fld, v) for v in vals], dtype=torch.int32)
+        fp = []
+        for mod in range(self.n_modules):
+            for f in range(self.fpm):
+                for lang in range(len(_LANGS)):
+                    m = self.module_name(mod)
+                    fp.append(table._code("file_path", f"{m}/{_WORDS[f % len(_WORDS)]}_{f}.{_LANGS[lang][0]}"))
+        self._codes["file_path"] = torch.tensor(fp, dtype=torch.int32)
+
+    def columns(self, device) -> dict:
+        i = torch.arange(self.n, device=device, dtype=torch.int64)
+        repo = i % self.n_repos
+        mod = (i // self.n_repos) % self.n_modules
+        f = (i // (self.n_repos * self.n_modules)) % self.fpm
+        lang = (repo + mod + f) % len(_LANGS)
+        c = {k: v.to(device) for k, v in self._codes.items()}
+        return {"namespace": c["namespace"][torch.zeros_like(i)], "scope": c["scope"][torch.zeros_like(i)],
+                "doc_type": c["doc_type"][torch.zeros_like(i)], "repo": c["repo"][repo], "module": c["module"][mod],
+                "language": c["language"][lang],
+                "file_path": c["file_path"][(mod * self.fpm + f) * len(_LANGS) + lang]}
+
+
+def provider_from_spec(spec: dict):
+    if spec.get("kind") == "synthetic":
+        kw = {k: v for k, v in spec.items() if k not in ("kind", "n", "seed")}
+        kw["files_per_module"] = kw.pop("files_per_module", 64)
+        return SyntheticCorpus(spec["n"], spec["seed"], **kw)
+    raise ValueError(f"unknown virtual row provider {spec!r}")

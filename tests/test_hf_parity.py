@@ -193,3 +193,22 @@ def test_bert_hip_bf16_matches_hf_fp32(dev):
     ref = _hf_pooled(hf, BATCH)
     cos = torch.nn.functional.cosine_similarity(got.float().cpu(), ref, dim=1)
     assert cos.min().item() >= 0.999, cos
+
+
+@pytest.mark.gpu
+def test_encoder_graph_replay_matches_eager(dev):
+    """Captured (bucketed, padded) encoder passes == eager varlen passes."""
+    from githubrepostorag_amd.models.encoder import BertEncoder, EncoderGraphs
+
+    cfg, hf = _hf_bert(seed=4)
+    enc = BertEncoder(cfg, device=dev, dtype=torch.bfloat16, state_dict=hf.state_dict())
+    gr = EncoderGraphs(enc)
+    g = torch.Generator().manual_seed(0)
+    for n in (3, 8, 5, 8):  # re-uses the (8, 16) bucket with different contents
+        batch = [torch.randint(1, cfg.vocab_size, (int(torch.randint(1, 14, (1,), generator=g)),),
+                               generator=g).tolist() for _ in range(n)]
+        ef, _ = enc.encode_ids(batch)
+        gf, _ = gr.run(batch)
+        assert gf.shape == ef.shape
+        assert torch.allclose(gf.float().cpu(), ef.float().cpu(), atol=2e-3), (gf.float() - ef.float()).abs().max()
+    assert gr.stats["captures"] == 2 and gr.stats["replays"] == 4  # buckets (4, 16) and (8, 16)

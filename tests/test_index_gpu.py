@@ -1,0 +1,135 @@
+"""GPU vector store: the IVF table behind the service store (INDEX_KIND=ivf)
+against the exact flat scan, the device probe plan / merge / bitmap kernels
+against torch references, and upsert / delete / compaction / snapshot."""
+import pytest
+import torch
+
+from githubrepostorag_amd.index.store import VectorStore, VectorTable
+from githubrepostorag_amd.ops import topk as T
+from githubrepostorag_amd.utils.synthetic import SyntheticCorpus, clustered_vectors
+
+pytestmark = pytest.mark.gpu
+
+
+def test_ivf_plan_covers_every_pair(dev):
+    g = torch.Generator(device="cpu").manual_seed(0)
+    nq, nprobe, nlist = 37, 16, 64
+    lists = torch.randint(0, nlist, (nq, nprobe), generator=g)
+    lists[3, 5] = -1  # fewer lists than nprobe
+    offsets = torch.cumsum(torch.cat([torch.zeros(1, dtype=torch.long), torch.randint(0, 50, (nlist,), generator=g)]),
+                           0)
+    rows, wq, cand = T.ivf_plan(lists.to(dev), offsets.to(dev), nlist)
+    rows, wq, cand = rows.cpu(), wq.cpu(), cand.cpu()
+    seen = set()
+    for q in range(nq):
+        for p in range(nprobe):
+            c = int(cand[q, p])
+            item, slot = c // 16, c % 16
+            l = int(lists[q, p])
+            if l < 0:
+                assert int(wq[item, slot]) == -1 and rows[item, 0] == rows[item, 1]
+                continue
+            assert int(wq[item, slot]) == q
+            assert (int(rows[item, 0]), int(rows[item, 1])) == (int(offsets[l]), int(offsets[l + 1]))
+            assert c not in seen
+            seen.add(c)
+    # every non-empty slot belongs to exactly one pair
+    assert int((wq >= 0).sum()) == len(seen)
+
+
+@pytest.mark.parametrize("k", [1, 10, 16])
+def test_topk_merge_matches_torch(dev, k):
+    g = torch.Generator(device="cpu").manual_seed(k)
+    R, L, nq, cnt = 300, 64, 20, 12
+    ps = torch.randn(R, L, generator=g)
+    pi = torch.randint(0, 1 << 40, (R, L), generator=g)
+    ps[pi % 7 == 0] = float("-inf")
+    pi[pi % 7 == 0] = -1
+    cand = torch.randint(0, R, (nq, cnt), generator=g, dtype=torch.int32)
+    es, ei = torch.randn(nq, 5, generator=g), torch.randint(0, 1 << 40, (nq, 5), generator=g)
+    s, i = T.merge_partials(ps.to(dev), pi.to(dev), k, nq, cand=cand.to(dev), cnt=cnt, extra=(es.to(dev), ei.to(dev)))
+    for q in range(nq):
+        allv = torch.cat([ps[cand[q].long()].reshape(-1), es[q]])
+        alli = torch.cat([pi[cand[q].long()].reshape(-1), ei[q]])
+        ok = alli >= 0
+        v, j = allv[ok].topk(k)
+        assert torch.allclose(s[q].cpu(), v), (q, s[q], v)
+        assert set(i[q].cpu().tolist()) == set(alli[ok][j].tolist())
+
+
+def test_bitmap_update(dev):
+    bm = torch.zeros(8, dtype=torch.int32, device=dev)
+    T.bitmap_update(bm, torch.tensor([0, 31, 32, 200, 255], device=dev), True)
+    T.bitmap_update(bm, torch.tensor([31, 200], device=dev), False)
+    ref = torch.zeros(8, dtype=torch.int32)
+    T.bitmap_update(ref, torch.tensor([0, 31, 32, 200, 255]), True)
+    T.bitmap_update(ref, torch.tensor([31, 200]), False)
+    assert torch.equal(bm.cpu(), ref)
+
+
+def _tables(dev, n, d, nlist, nprobe, seed=0):
+    corp = SyntheticCorpus(n, seed=seed, n_repos=16)
+    X = clustered_vectors(n, d, n_centers=2048, seed=seed, device=dev)
+    flat = VectorTable("flat", d, dev, index_kind="flat")
+    ivf = VectorTable("ivf", d, dev, index_kind="ivf", nlist=nlist, nprobe=nprobe)
+    flat.add_virtual(corp, X)
+    ivf.add_virtual(SyntheticCorpus(n, seed=seed, n_repos=16), X)
+    ivf.compact(train_iters=8)
+    return corp, X, flat, ivf
+
+
+def test_ivf_filtered_recall_vs_flat(dev):
+    """filtered IVF recall >= 0.9 against the flat scan."""
+    n, d = 1 << 21, 1024
+    corp, X, flat, ivf = _tables(dev, n, d, nlist=1024, nprobe=32)
+    assert ivf.nc == n and ivf.offsets[-1].item() == n
+    g = torch.Generator(device="cpu").manual_seed(1)
+    qi = torch.randint(0, n, (64,), generator=g)
+    Q = X[qi.to(dev)].float() + 0.02 * torch.randn(64, d, device=dev) / d ** 0.5
+    for flt in (None, {"repo": corp.repo_name(3)}, {"repo": corp.repo_name(5), "language": "python"}):
+        a = flat.search(Q, 10, flt)
+        b = ivf.search(Q, 10, flt)
+        inter = tot = 0
+        for ha, hb in zip(a, b):
+            sa = {h.row_id for h in ha}
+            inter += len(sa & {h.row_id for h in hb})
+            tot += len(sa)
+            for h in hb:
+                for k, v in (flt or {}).items():
+                    assert h.metadata[k] == v
+        assert tot > 0 and inter / tot >= 0.9, (flt, inter / tot)
+
+
+def test_ivf_upsert_delete_compact_snapshot(dev, tmp_path):
+    n, d = 1 << 16, 256
+    corp, X, flat, ivf = _tables(dev, n, d, nlist=128, nprobe=16, seed=3)
+    ivf.compact_min = 1 << 30  # keep the appended rows in the append region for this test
+    new = torch.nn.functional.normalize(torch.randn(50, d, device=dev), dim=1)
+    ivf.upsert([f"new{i}" for i in range(50)], [f"text {i}" for i in range(50)], new,
+               [{"repo": "fresh", "namespace": "default"} for _ in range(50)])
+    assert ivf.n == n + 50 and ivf.nc == n
+    hits = ivf.search(new[:8], 1)
+    assert [h[0].row_id for h in hits] == [f"new{i}" for i in range(8)]
+    assert all(h[0].metadata["repo"] == "fresh" for h in ivf.search(new[:8], 1, {"repo": "fresh"}))
+    # overwrite a clustered synthetic row: the old slot is tombstoned, the new vector wins
+    rid = corp.row_id(123)
+    ivf.upsert([rid], ["rewritten"], new[10:11], [{"repo": "fresh"}])
+    h = ivf.search(new[10:11], 2)[0]
+    assert h[0].row_id in (rid, "new10") and {x.row_id for x in h} == {rid, "new10"}
+    assert ivf.search(new[10:11], 2)[0][0].text in ("rewritten", "text 10")
+    assert ivf.delete(["new3", "new4"]) == 2
+    assert all(x.row_id not in ("new3", "new4") for x in ivf.search(new[3:5], 5)[0] + ivf.search(new[3:5], 5)[1])
+    ivf.compact()
+    assert ivf.nc == ivf.n == n + 50 - 2 and ivf.deleted == 0
+    assert ivf.search(new[:1], 1)[0][0].row_id == "new0"
+    ivf.save(tmp_path / "t")
+    back = VectorTable.load(tmp_path / "t", dev)
+    assert back.ivf and back.nc == ivf.nc
+    a = [[x.row_id for x in hs] for hs in ivf.search(new[:16], 5)]
+    b = [[x.row_id for x in hs] for hs in back.search(new[:16], 5)]
+    assert a == b
+
+
+def test_store_honours_index_kind(dev):
+    st = VectorStore(64, dev, index_kind="ivf", nlist=16, nprobe=4)
+    assert all(t.index_kind == "ivf" for t in st.tables.values())
