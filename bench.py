@@ -72,6 +72,11 @@ def parse():
                     help="Python GIL switch interval (s): the engine thread re-takes the GIL quickly after a GPU wait")
     ap.add_argument("--prefetch", type=int, default=1,
                     help="1: the next group's retrieval overlaps engine steps on a helper thread")
+    ap.add_argument("--agent-jobs", type=int, default=64,
+                    help="end-to-end phase: agent-loop jobs through POST /rag/jobs + SSE over real HTTP "
+                         "(0 disables); secondary fields e2e_ttft_p50_ms / p90 / agent_jobs_per_s")
+    ap.add_argument("--agent-concurrency", type=int, default=64)
+    ap.add_argument("--agent-gen-len", type=int, default=32, help="token cap of every agent LLM call")
     ap.add_argument("--out", default=None)
     return ap.parse_args()
 
@@ -135,13 +140,18 @@ def main():
     n_local = args.index_size // world + (1 if rank < args.index_size % world else 0)
     t0 = time.perf_counter()
     X = synthetic.clustered_vectors(n_local, emb.dim, seed=1000 + rank, device=dev)
+    # the product table (index/store.py) per shard: IVF lists + metadata filter columns; the
+    # corpus rows (row id, chunk text, repo/module/file metadata) are a deterministic recipe
+    corpus = synthetic.SyntheticCorpus(args.index_size, seed=7)
     index = ShardedIndex(emb.dim, group, dev, kind=args.index_kind, nlist=args.nlist, nprobe=args.nprobe)
-    index.build(X, seed=7)
+    index.build_corpus(corpus, X, seed=7)
     del X
     torch.cuda.synchronize() if dev.type == "cuda" else None
     log(f"index shard ready: {n_local} rows ({args.index_kind}) in {time.perf_counter() - t0:.1f}s")
 
     max_len = args.prompt_len + args.gen_len + 64
+    if args.agent_jobs > 0:  # the agent phase's synthesize prompts carry 5 context blocks
+        max_len = max(max_len, 4096)
     D = max(1, min(args.inflight, args.gen_len))
     A = max(1, min(args.arrival_groups, args.batch, max(1, args.gen_len // D)))
     while args.batch % A:
@@ -158,12 +168,12 @@ def main():
                   "say so clearly and suggest looking in specific repos/modules that might contain the answer.")
 
     # row texts: the index's body_blob column (the reference stores chunk text
-    # next to the vector, vector_write_service.py:166-198) — a pool generated
-    # once here, so the timed loop does a lookup, not synthetic text generation
-    text_pool = [synthetic.chunk_text(i) for i in range(4096)]
+    # next to the vector, vector_write_service.py:166-198) — the corpus rows of a
+    # pool generated once here, so the timed loop does a lookup, not text generation
+    text_pool = [corpus.text(i) for i in range(4096)]
 
-    def row_text(d: int) -> str:
-        return text_pool[d % len(text_pool)]
+    def row_block(d: int) -> tuple[str, dict]:
+        return text_pool[d % len(text_pool)], corpus.meta(d)
 
     qcounter = [dp_rank * 1_000_000]
     phase = {"embed": 0.0, "search": 0.0, "prompt": 0.0, "generate": 0.0}
@@ -192,13 +202,16 @@ def main():
             qcounter[0] += B
             qv = emb.embed_queries(qs)
             t_e = time.perf_counter()
-            scores, ids = index.search(qv, args.top_k)
+            # every reference retrieval carries the namespace filter (agent_graph.py:249): fused in the scan
+            scores, ids = index.search(qv, args.top_k, {"namespace": corpus.namespace})
             ids = ids.cpu().tolist()
             t_s = time.perf_counter()
         prompts = []
         for q, row in zip(qs, ids):
-            blocks = [f"[{j + 1}] repo=synthetic module=m{d % 97} file=f{d}.py\n{row_text(d)}"
-                      for j, d in enumerate([x for x in row if x >= 0][:5])]
+            blocks = []
+            for j, d in enumerate([x for x in row if x >= 0][:5]):
+                text, md = row_block(d)
+                blocks.append(f"[{j + 1}] repo={md['repo']} module={md['module']} file={md['file_path']}\n{text}")
             text = tok.apply_chat_template([{"role": "user", "content": f"{sys_prompt}\n\nQuestion: {q}\n\n"
                                              "Context:\n" + "\n\n".join(blocks) + "\n\nAnswer:"}])
             pid = tok.encode(text)
@@ -330,6 +343,22 @@ def main():
     timed_engine = {k: round((v - stats0.get(k, 0)) / args.steps, 4) for k, v in stats1.items()
                     if isinstance(v, (int, float))}
 
+    # ---- end-to-end phase (reported separately): the reference's job path over real HTTP --
+    # uvicorn serving service/api.py on 127.0.0.1, jobs through the queue + worker + GraphAgent
+    # (plan / retrieve / judge / rewrite / synthesize, SSE token streaming) on this engine,
+    # encoder and the 10M-row IVF chunk table (namespace filter fused in the scan)
+    agent_res = None
+    if args.agent_jobs > 0 and tp == 1:
+        agent_res = agent_phase(args, rank, dev, eng, tok, emb, index, corpus, log)
+        tt = torch.tensor([agent_res["wall_s"]], dtype=torch.float64, device=dev)
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        agent_res["agent_jobs_per_s"] = round(args.agent_jobs * world / float(tt.item()), 3)
+        log(f"agent e2e: {agent_res['agent_jobs_per_s']} jobs/s, e2e TTFT p50 {agent_res['e2e_ttft_p50_ms']} ms "
+            f"p90 {agent_res['e2e_ttft_p90_ms']} ms, errors {agent_res['errors']}")
+
     # ---- ingest phase (reported separately)
     ingest_dps = None
     ingest_stages = None
@@ -386,6 +415,10 @@ def main():
                                         "engine_decode": round(timed_engine.get("decode_s", 0) * 1000, 2)},
             "retrieval_prefetch": bool(args.prefetch),
             "ingest_stage_s": ingest_stages,
+            "e2e_ttft_p50_ms": None if agent_res is None else agent_res["e2e_ttft_p50_ms"],
+            "e2e_ttft_p90_ms": None if agent_res is None else agent_res["e2e_ttft_p90_ms"],
+            "agent_jobs_per_s": None if agent_res is None else agent_res["agent_jobs_per_s"],
+            "agent_e2e": agent_res,
         }
         line = json.dumps(res)
         print(line, flush=True)
@@ -396,6 +429,47 @@ def main():
         import torch.distributed as dist
 
         dist.destroy_process_group()
+
+
+def agent_phase(args, rank, dev, eng, tok, emb, index, corpus, log):
+    """POST /rag/jobs -> SSE over real HTTP for ``--agent-jobs`` 3-round agent jobs."""
+    from githubrepostorag_amd.agent.llm import EngineLLM, MeteredLLM
+    from githubrepostorag_amd.config import Settings
+    from githubrepostorag_amd.engine.runner import EngineRunner
+    from githubrepostorag_amd.index.store import VectorStore
+    from githubrepostorag_amd.service.api import APIState, create_app
+    from githubrepostorag_amd.service.e2e import run_e2e
+    from githubrepostorag_amd.service.runtime import RAGRuntime
+    from githubrepostorag_amd.utils import synthetic
+
+    conc = args.agent_concurrency
+    s = Settings(qwen_model=args.model, embed_model=args.encoder, qwen_max_output=args.agent_gen_len,
+                 worker_max_jobs=conc, max_rag_attempts=3, default_namespace=corpus.namespace, job_timeout_s=1800,
+                 llm_retries=0, stream_tokens=True, index_kind=args.index_kind, nlist=args.nlist, nprobe=args.nprobe,
+                 embed_batch_window_ms=1.0, data_dir=None, seed=rank)
+    store = VectorStore(emb.dim, dev)  # project/package/file tables empty: code questions plan to the chunk scope
+    store.tables["chunk"] = index.table
+    runner = EngineRunner(eng, watchdog_s=600)
+    llm = MeteredLLM(EngineLLM(runner, tok, max_tokens=args.agent_gen_len, timeout_s=1800, retries=0))
+    rt = RAGRuntime(s, device=str(dev), llm=llm, embedder=emb, store=store, build_engine=False)
+    rt.engine, rt.runner = eng, runner
+    app = create_app(APIState(runtime=rt))
+    import logging
+
+    logging.getLogger("githubrepostorag_amd.agent").setLevel(logging.ERROR)  # random weights: parse fallbacks
+    q0 = 50_000_000 + rank * 1_000_000
+    warm = [synthetic.code_question(q0 + 500_000 + i) for i in range(min(conc, 16))]
+    qs = [synthetic.code_question(q0 + i) for i in range(args.agent_jobs)]
+    try:
+        res = run_e2e(app, qs, conc, warmup=warm)
+    finally:
+        runner.shutdown()
+        emb.close()  # the runtime turned on query-embedding batching for this phase
+    res["concurrency"] = conc
+    res["llm_token_cap"] = args.agent_gen_len
+    res["chunk_table"] = {"rows": index.table.count(), "index": index.table.index_kind,
+                          "searches": index.table.stats["searches"]}
+    return res
 
 
 if __name__ == "__main__":

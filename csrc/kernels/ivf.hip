@@ -21,7 +21,7 @@ using namespace grag;
 
 namespace {
 
-constexpr int kPlanThreads = 1024;
+constexpr int kPlanThreads = 256;  // one wave per SIMD: fits beside a resident GEMM workgroup
 constexpr int kMaxPairs = 16384;  // nq * nprobe handled by one plan workgroup
 
 __global__ __launch_bounds__(kPlanThreads) void ivf_plan_kernel(const int64_t* __restrict__ lists, int nq, int nprobe,
@@ -29,8 +29,11 @@ __global__ __launch_bounds__(kPlanThreads) void ivf_plan_kernel(const int64_t* _
                                                                 int64_t* __restrict__ work_rows,
                                                                 int32_t* __restrict__ work_q,
                                                                 int32_t* __restrict__ cand) {
-  __shared__ unsigned long long key[kMaxPairs];  // (list << 20) | pair; padding = all ones
-  __shared__ int scan[kPlanThreads];
+  // dynamic LDS sized to the plan (a 256-pair plan takes 6 KB, so it co-resides with the
+  // 128-KB GEMM workgroups of the engine stream instead of waiting for a free CU)
+  extern __shared__ __attribute__((aligned(16))) char plan_lds[];
+  int* scan = reinterpret_cast<int*>(plan_lds);
+  unsigned long long* key = reinterpret_cast<unsigned long long*>(plan_lds + kPlanThreads * sizeof(int));
   const int P = nq * nprobe;
   int np2 = 1;
   while (np2 < P) np2 <<= 1;
@@ -159,9 +162,11 @@ __global__ __launch_bounds__(kMergeThreads) void topk_merge_kernel(const float* 
                                                                    const int64_t* __restrict__ ex_i, int L2, int k,
                                                                    float* __restrict__ out_s,
                                                                    int64_t* __restrict__ out_i) {
-  __shared__ float cs[kMergeCap];
-  __shared__ float ws[4 * 32];
-  __shared__ int64_t wi[4 * 32];
+  // dynamic LDS: C candidate scores (sized per launch: small merges co-reside with GEMM workgroups)
+  extern __shared__ __attribute__((aligned(16))) char merge_lds[];
+  int64_t* wi = reinterpret_cast<int64_t*>(merge_lds);
+  float* ws = reinterpret_cast<float*>(merge_lds + 4 * 32 * sizeof(int64_t));
+  float* cs = ws + 4 * 32;
   const int q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int C = cnt * L + L2;
@@ -250,7 +255,15 @@ GRAG_API int grag_ivf_plan(const int64_t* lists, int nq, int nprobe, const int64
                            int64_t* work_rows, int32_t* work_q, int32_t* cand, hipStream_t stream) {
   if (nq <= 0 || nprobe <= 0) return 0;
   if ((long)nq * nprobe > kMaxPairs || nlist >= (1 << 30)) return (int)hipErrorInvalidValue;
-  ivf_plan_kernel<<<1, kPlanThreads, 0, stream>>>(lists, nq, nprobe, offsets, nlist, work_rows, work_q, cand);
+  int np2 = 1;
+  while (np2 < nq * nprobe) np2 <<= 1;
+  const size_t lds = kPlanThreads * sizeof(int) + (size_t)np2 * sizeof(unsigned long long);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)ivf_plan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  ivf_plan_kernel<<<1, kPlanThreads, lds, stream>>>(lists, nq, nprobe, offsets, nlist, work_rows, work_q, cand);
   return (int)hipGetLastError();
 }
 
@@ -263,8 +276,14 @@ GRAG_API int grag_topk_merge(const float* ps, const int64_t* pi, int L, const in
   if (k < 1 || k > 32 || L < 0 || L2 < 0 || (long)cnt * L + L2 > kMergeCap || 4 * k > 64 * 2)
     return (int)hipErrorInvalidValue;
   if (4 * k > 64) return (int)hipErrorInvalidValue;  // wave-0 merge holds 4 lists of k in one wave
-  topk_merge_kernel<<<nq, kMergeThreads, 0, stream>>>(ps, pi, L, cand, cnt, G, A, B, ex_s, ex_i, L2, k, out_s,
-                                                      out_i);
+  const size_t lds = 4 * 32 * (sizeof(int64_t) + sizeof(float)) + ((size_t)cnt * L + L2) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)topk_merge_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  topk_merge_kernel<<<nq, kMergeThreads, lds, stream>>>(ps, pi, L, cand, cnt, G, A, B, ex_s, ex_i, L2, k, out_s,
+                                                        out_i);
   return (int)hipGetLastError();
 }
 

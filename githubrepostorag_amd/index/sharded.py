@@ -1,25 +1,63 @@
-"""Data-parallel sharded index: each rank keeps a shard of the vectors in its
-own HBM (288 GB per MI355X: a 10M x 1024 bf16 shard is 20.5 GB) and searches
+"""Data-parallel sharded index over the product vector table: each rank keeps
+a shard of the rows in its own HBM (288 GB per MI355X: a 10M x 1024 bf16
+shard is 20.5 GB) as an ``index/store.py`` VectorTable (flat or IVF, with the
+metadata columns, live bitmap and filters of the service store), and searches
 it locally with the fused kernels.  Every rank brings its own query batch, so
 one search is three steps over xGMI:
   C4  all-gather the query embeddings ([W, nq, d] bf16: every shard scores
       every rank's queries),
-      local fused score + top-k of all W*nq queries against this shard,
+      local fused score + filter + top-k of all W*nq queries against this shard,
   C3  all-to-all of the per-shard lists (slice j = the lists for rank j's
       queries: W*nq*k (score, id) pairs in, the same out, never the whole
       W x W*nq x k gather), then a local merge to the global top-k.
 Query batches of different sizes are padded to the largest.  Global ids are
 interleaved: global = local * world + rank, so shards never collide and no id
-exchange is needed at insert time.
+exchange is needed at insert time.  The IVF quantiser is trained jointly:
+the k-means sums/counts are all-reduced every iteration (C6), so every shard
+probes the same lists.
 """
 from __future__ import annotations
 
 import torch
 
-from ..ops.topk import score_topk
+from ..ops.topk import merge_fits, merge_partials
 from ..parallel.comm import Group
 from ..utils.gpu_guard import guarded
-from .ivf import IVFIndex
+from .store import VectorTable
+
+
+class ShardView:
+    """Virtual rows of one shard: local row j = global corpus row j * world + rank."""
+
+    def __init__(self, corpus, rank: int, world: int):
+        self.corpus, self.rank, self.world = corpus, rank, world
+
+    def _g(self, j: int) -> int:
+        return j * self.world + self.rank
+
+    def row_id(self, j: int) -> str:
+        return self.corpus.row_id(self._g(j))
+
+    def text(self, j: int) -> str:
+        return self.corpus.text(self._g(j))
+
+    def meta(self, j: int) -> dict:
+        return self.corpus.meta(self._g(j))
+
+    def index_of(self, row_id: str):
+        i = self.corpus.index_of(row_id)
+        return None if i is None or i % self.world != self.rank else i // self.world
+
+    def spec(self) -> dict:
+        return {"kind": "shard", "corpus": self.corpus.spec(), "rank": self.rank, "world": self.world}
+
+    def register(self, table) -> None:
+        self.corpus.register(table)
+
+    def columns(self, device) -> dict:
+        n_local = self.n
+        idx = torch.arange(n_local, device=device, dtype=torch.int64) * self.world + self.rank
+        return {k: v[idx] for k, v in self.corpus.columns(device).items()}
 
 
 class ShardedIndex:
@@ -30,57 +68,79 @@ class ShardedIndex:
         self.device = torch.device(device)
         self.kind = kind
         self.nprobe = nprobe
-        self.ivf = IVFIndex(dim, nlist, device) if kind == "ivf" else None
-        self.flat = torch.zeros(0, dim, dtype=torch.bfloat16, device=self.device)
+        self.table = VectorTable("shard", dim, self.device, index_kind=kind, nlist=nlist, nprobe=nprobe,
+                                 compact_min=1 << 62)
 
     def global_ids(self, local: torch.Tensor) -> torch.Tensor:
         return torch.where(local >= 0, local * self.group.size + self.group.rank, local)
 
+    def _finish(self, train_sample: int, iters: int, seed: int) -> None:
+        if self.kind == "ivf":
+            self.table.compact(train_iters=iters, sample=train_sample, seed=seed,
+                               group=None if self.group.trivial else self.group)
+
     @torch.inference_mode()
     def build(self, X: torch.Tensor, train_sample: int = 131072, iters: int = 8, seed: int = 0) -> None:
-        if self.kind == "ivf":
-            m = min(train_sample, X.shape[0])
-            g = torch.Generator(device="cpu")
-            g.manual_seed(seed + self.group.rank)
-            idx = torch.randperm(X.shape[0], generator=g)[:m].to(X.device)
-            self.ivf.train(X[idx], iters=iters, seed=seed, group=self.group)
-            self.ivf.add(X)
-        else:
-            self.flat = X.to(self.device, torch.bfloat16).contiguous()
+        """Shard of anonymous vectors (local row j = global j * world + rank)."""
+        from ..utils.synthetic import SyntheticCorpus
+
+        view = ShardView(SyntheticCorpus(X.shape[0] * self.group.size, seed=seed), self.group.rank, self.group.size)
+        self.table.add_virtual(view, X.to(self.device, torch.bfloat16), columns={})
+        self._finish(train_sample, iters, seed)
+
+    @torch.inference_mode()
+    def build_corpus(self, corpus, X_local: torch.Tensor, train_sample: int = 131072, iters: int = 8,
+                     seed: int = 0) -> None:
+        """This rank's shard of a virtual corpus (rows i = rank (mod world)), with its
+        metadata columns, so filtered searches run inside the scan."""
+        view = ShardView(corpus, self.group.rank, self.group.size)
+        view.n = X_local.shape[0]
+        self.table.add_virtual(view, X_local)
+        self._finish(train_sample, iters, seed)
 
     @property
     def local_size(self) -> int:
-        return self.ivf.ntotal if self.kind == "ivf" else int(self.flat.shape[0])
+        return self.table.count()
 
-    def _local(self, Q: torch.Tensor, k: int):
-        if self.kind == "ivf":
-            s, i = self.ivf.search(Q, k, self.nprobe)
-        else:
-            s, i = score_topk(self.flat, Q.to(self.device, torch.bfloat16), k)
+    def _local(self, Q: torch.Tensor, k: int, flt: dict | None = None):
+        t = self.table
+        nq = Q.shape[0]
+        with t.lock:
+            pc = t.predicates(flt)
+            if pc is None or t.n == 0:
+                return (torch.full((nq, k), float("-inf"), device=Q.device),
+                        torch.full((nq, k), -1, dtype=torch.long, device=Q.device))
+            s, i = t._scan(Q.to(self.device, t.dtype), k, pc[0][:4], t.live, None)
         return s.float(), self.global_ids(i)
 
     @guarded
     @torch.inference_mode()
-    def search(self, Q: torch.Tensor, k: int):
+    def search(self, Q: torch.Tensor, k: int, flt: dict | None = None):
         """This rank's queries Q [nq, d] -> global top-k (scores fp32, ids int64)."""
         g = self.group
         Q = Q.to(self.device, torch.bfloat16)
         if g.trivial:
-            return self._local(Q, k)
+            return self._local(Q, k, flt)
         nq = Q.shape[0]
         sizes = g.all_gather(torch.tensor([nq], dtype=torch.int64, device=self.device)).view(-1)
         qmax = int(sizes.max())
         Qp = torch.zeros(qmax, Q.shape[1], dtype=Q.dtype, device=self.device)
         Qp[:nq] = Q
         Qall = g.all_gather(Qp).view(g.size * qmax, -1)  # C4
-        s, i = self._local(Qall, k)
+        s, i = self._local(Qall, k, flt)
         kk = s.shape[1]
         packed = torch.empty(g.size * qmax, kk, 2, dtype=torch.int64, device=self.device)
         packed[..., 0] = i
         packed[..., 1] = s.view(torch.int32).to(torch.int64)
         recv = g.all_to_all(packed.view(g.size, qmax, kk, 2))  # C3: [shard, my query, k, 2]
-        ids = recv[..., 0].permute(1, 0, 2).reshape(qmax, -1)[:nq]
-        sc = recv[..., 1].to(torch.int32).view(torch.float32).permute(1, 0, 2).reshape(qmax, -1)[:nq]
+        ids = recv[..., 0]
+        sc = recv[..., 1].to(torch.int32).view(torch.float32)
+        if Q.is_cuda and merge_fits(g.size, kk, 0, k):  # device merge: query q's lists are rows q + j*qmax
+            ms, mi = merge_partials(sc.reshape(-1, kk).contiguous(), ids.reshape(-1, kk).contiguous(), k, qmax,
+                                    cnt=g.size, affine=(qmax, 0, qmax))
+            return ms[:nq], mi[:nq]
+        ids = ids.permute(1, 0, 2).reshape(qmax, -1)[:nq]
+        sc = sc.permute(1, 0, 2).reshape(qmax, -1)[:nq]
         sc = torch.where(ids >= 0, sc, torch.full_like(sc, float("-inf")))
         top, sel = sc.topk(min(k, sc.shape[1]), dim=1)
         return top, ids.gather(1, sel)

@@ -454,13 +454,14 @@ class VectorTable:
         return app > max(self.compact_min, self.compact_frac * self.nc)
 
     @guarded
-    def compact(self, train_iters: int = 10, sample: int = 1 << 18, seed: int = 0) -> None:
-        """(ivf) train the quantiser if needed, assign the append region, and re-sort
-        every live slot by inverted list (tombstones dropped)."""
+    def compact(self, train_iters: int = 10, sample: int = 1 << 18, seed: int = 0, group=None) -> None:
+        """(ivf) train the quantiser if needed (k-means sums all-reduced over ``group``
+        when the table is one shard of a DP index), assign the append
+        region, and re-sort every live slot by inverted list (tombstones dropped)."""
         with self.lock, side_stream(self.device):
-            self._compact_locked(train_iters, sample, seed)
+            self._compact_locked(train_iters, sample, seed, group)
 
-    def _compact_locked(self, train_iters: int = 10, sample: int = 1 << 18, seed: int = 0) -> None:
+    def _compact_locked(self, train_iters: int = 10, sample: int = 1 << 18, seed: int = 0, group=None) -> None:
         if not self.ivf or self.n == 0:
             return
         from .ivf import IVFIndex
@@ -473,7 +474,7 @@ class VectorTable:
             g = torch.Generator(device="cpu").manual_seed(seed)
             pick = live[torch.randperm(live.numel(), generator=g)[: min(sample, live.numel())].to(dev)]
             q = IVFIndex(self.dim, self.nlist, dev, self.dtype)
-            q.train(self.vectors[pick], iters=train_iters, seed=seed)
+            q.train(self.vectors[pick], iters=train_iters, seed=seed, group=group)
             self.centroids = q.centroids
         lists = self.slot_list[live].clone()
         need = lists < 0

@@ -200,12 +200,16 @@ class EncoderGraphs:
         host.copy_(dbuf.cpu())
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
-        s = torch.cuda.current_stream(dev)
-        self.enc.forward(ids, pos, starts, lens, L, want_bf16=True)  # eager warm-up sizes workspaces
-        s.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
-            outf, outb = self.enc.forward(ids, pos, starts, lens, L, want_bf16=True)
+        cur = torch.cuda.current_stream(dev)
+        s = cur if cur != torch.cuda.default_stream(dev) else torch.cuda.Stream(device=dev)  # capture needs a side stream
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            self.enc.forward(ids, pos, starts, lens, L, want_bf16=True)  # eager warm-up sizes workspaces
+            s.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
+                outf, outb = self.enc.forward(ids, pos, starts, lens, L, want_bf16=True)
+        cur.wait_stream(s)
         self.stats["captures"] += 1
         ent = (g, host, dbuf, outf, outb)
         self.graphs[(B, L)] = ent

@@ -1,0 +1,120 @@
+"""End-to-end serving measurement over real HTTP (SURVEY §6 metric
+definitions): a uvicorn server on 127.0.0.1 in a
+background thread serves ``service/api.py`` over a runtime, and an async
+httpx client drives N concurrent jobs exactly as the UI does
+(rest_api/src/app/static/index.html:215-224): ``POST /rag/jobs`` ->
+``GET /rag/jobs/{id}/events`` (SSE) until the ``final`` event.
+
+  TTFT    = POST issued -> first ``token`` SSE frame received by the client
+            (reference: the first visible output is the final event,
+            rag_worker/src/worker/worker.py:170, qwen_llm.py:149-151)
+  jobs/s  = completed jobs / wall time of the run
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import socket
+import statistics
+import threading
+import time
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class ServerThread:
+    """uvicorn in a daemon thread (its own event loop); ``url`` once started."""
+
+    def __init__(self, app, port: int | None = None):
+        import uvicorn
+
+        self.port = port or _free_port()
+        cfg = uvicorn.Config(app, host="127.0.0.1", port=self.port, log_level="warning", lifespan="on",
+                             timeout_keep_alive=600)
+        self.server = uvicorn.Server(cfg)
+        self.thread = threading.Thread(target=self.server.run, name="e2e-uvicorn", daemon=True)
+
+    @property
+    def url(self) -> str:
+        return f"http://127.0.0.1:{self.port}"
+
+    def __enter__(self):
+        self.thread.start()
+        t0 = time.time()
+        while not self.server.started:
+            if not self.thread.is_alive() or time.time() - t0 > 120:
+                raise RuntimeError("e2e: uvicorn did not start")
+            time.sleep(0.01)
+        return self
+
+    def __exit__(self, *exc):
+        self.server.should_exit = True
+        self.thread.join(timeout=30)
+
+
+async def _drive(url: str, questions: list[str], concurrency: int, timeout_s: float) -> list[dict]:
+    import httpx
+
+    sem = asyncio.Semaphore(concurrency)
+    limits = httpx.Limits(max_connections=2 * concurrency + 8, max_keepalive_connections=2 * concurrency + 8)
+    async with httpx.AsyncClient(base_url=url, timeout=timeout_s, limits=limits) as client:
+        async def one(q: str) -> dict:
+            async with sem:
+                t0 = time.perf_counter()
+                r = await client.post("/rag/jobs", json={"query": q})
+                r.raise_for_status()
+                jid = r.json()["job_id"]
+                first = final = None
+                err = False
+                ntok = 0
+                async with client.stream("GET", f"/rag/jobs/{jid}/events") as resp:
+                    async for line in resp.aiter_lines():
+                        if not line.startswith("data:"):
+                            continue
+                        ev = json.loads(line[5:])
+                        now = time.perf_counter()
+                        if ev.get("event") == "token":
+                            ntok += 1
+                            if first is None:
+                                first = now
+                        elif ev.get("event") == "final":
+                            final = now
+                            err = bool((ev.get("data") or {}).get("error"))
+                            break
+                return {"t0": t0, "first_token": first, "final": final, "error": err, "tokens": ntok}
+
+        return await asyncio.gather(*[one(q) for q in questions])
+
+
+def _pct(xs: list[float], p: float) -> float | None:
+    if not xs:
+        return None
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(round(p * (len(xs) - 1))))]
+
+
+def run_e2e(app, questions: list[str], concurrency: int, warmup: list[str] | None = None,
+            timeout_s: float = 1800.0) -> dict:
+    """Serve ``app`` on localhost and push ``questions`` through the HTTP API."""
+    with ServerThread(app) as srv:
+        loop = asyncio.new_event_loop()
+        try:
+            if warmup:
+                loop.run_until_complete(_drive(srv.url, warmup, concurrency, timeout_s))
+            t0 = time.perf_counter()
+            res = loop.run_until_complete(_drive(srv.url, questions, concurrency, timeout_s))
+            wall = time.perf_counter() - t0
+        finally:
+            loop.close()
+    ttft = [(r["first_token"] - r["t0"]) * 1e3 for r in res if r["first_token"] is not None]
+    lat = [(r["final"] - r["t0"]) * 1e3 for r in res if r["final"] is not None]
+    return {"jobs": len(res), "wall_s": round(wall, 3), "jobs_per_s": round(len(res) / wall, 3),
+            "e2e_ttft_p50_ms": round(statistics.median(ttft), 1) if ttft else None,
+            "e2e_ttft_p90_ms": round(_pct(ttft, 0.9), 1) if ttft else None,
+            "job_latency_p50_ms": round(statistics.median(lat), 1) if lat else None,
+            "errors": sum(r["error"] for r in res), "mean_tokens_streamed": round(
+                statistics.mean(r["tokens"] for r in res), 1) if res else 0}

@@ -182,8 +182,21 @@ class SyntheticCorpus:
 
 
 def provider_from_spec(spec: dict):
+    if spec.get("kind") == "shard":
+        from ..index.sharded import ShardView
+
+        return ShardView(provider_from_spec(spec["corpus"]), spec["rank"], spec["world"])
     if spec.get("kind") == "synthetic":
         kw = {k: v for k, v in spec.items() if k not in ("kind", "n", "seed")}
         kw["files_per_module"] = kw.pop("files_per_module", 64)
         return SyntheticCorpus(spec["n"], spec["seed"], **kw)
     raise ValueError(f"unknown virtual row provider {spec!r}")
+
+
+def code_question(i: int) -> str:
+    """A debugging-style question: the agent's planner routes it to the code scope
+    (agent_graph.py:33-38 keyword fallback), so every refinement round searches
+    the chunk table."""
+    r = _rng(20_000_033 + i)
+    return (f"Why does {r.choice(_WORDS)}_{r.choice(_WORDS)} raise an exception on retry when the "
+            f"{r.choice(_WORDS)} {r.choice(_WORDS)} hits a timeout?")
