@@ -1,0 +1,343 @@
+// Decode-regime MFMA GEMM (SURVEY §2.7 N1c, N1h, N1i, N1j at 32 < M <= 256):
+//
+//   D[M, N] = A[M, K] · W[N, K]^T        bf16 in, fp32 accumulate
+//
+// Regime.  At decode batches every weight byte is read once per step and the
+// whole A (M x K, <= 1.8 MB) sits in L2, so the kernel is bound by how many W
+// bytes each CU keeps in flight (Little's law: 5.5 TB/s over ~3 us of loaded
+// HBM latency = ~64 KB per CU).  The 256x256 tile kernel (gemm_tile.hip) keeps
+// ~32 KB of W in flight behind one LDS ring shared with A and measured 2.5-2.9
+// TB/s on the Qwen2-7B projections (profiles/gemm_tile_ab_v2.jsonl).
+//
+// Design:
+//   * W goes HBM -> VGPRs directly (no LDS): each wave owns 32 W rows (two
+//     16-row MFMA tiles) and keeps D+1 K-steps (64 deep) of them in a register
+//     ring, D steps in flight.  The loads are inline-asm `global_load_dwordx4 nt`
+//     (hidden from hipcc's waitcnt bookkeeping, which would otherwise drain the
+//     ring with vmcnt(0) beside the LDS-DMA: cdna guide §5 trap (b)), retired by
+//     ONE counted `s_waitcnt vmcnt(N)` per K-step that names the consumed
+//     registers ("+v"), so no MFMA can be scheduled above it (guide §5.7 item 1).
+//   * A (all M rows, 16*MT padded) arrives per K-step by LDS-DMA into a D+1 deep
+//     LDS ring (one 1-KiB wave instruction = 8 rows x 128 B, source-side XOR
+//     swizzle -> conflict-free ds_read_b128), fetched once per workgroup and read
+//     by all its waves; one raw s_barrier per K-step (the refill goes into the
+//     slot every wave finished before that barrier).
+//   * The MFMA takes the W fragment as operand A, so each lane ends with 4
+//     consecutive output columns of one row (8-byte bf16 / 16-byte fp32 stores).
+//   * Work: (N / (32*NWV)) column tiles x ksplit K-ranges, XCD-remapped.  ksplit
+//     > 1 writes fp32 partial planes ws[split][M][N]; grag_splitk_reduce (in
+//     gemm_tile.hip) sums them and applies the epilogue.
+//   * Epilogues fused in the kernel: bias + act (none / gelu-erf / gelu-tanh),
+//     SiLU(gate)*up for the gate/up weight stored interleaved in 32-row blocks
+//     (ops/gemm.py interleave_gate_up): a wave's two n-tiles are then the 16
+//     gate rows and the 16 matching up rows, so the product forms in registers.
+#include "common.h"
+
+using namespace grag;
+
+GRAG_API int grag_splitk_reduce(const void* ws, const void* bias, void* C, int ldc, int M, int N, int S, int epi,
+                                int act, hipStream_t stream);
+
+namespace {
+
+enum { EPI_STORE = 0, EPI_SILU = 1, EPI_PARTIAL = 2 };
+enum { ACT_NONE = 0, ACT_GELU = 1, ACT_GELU_TANH = 3 };
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ float gelu_erf_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_tanh_f(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (2.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u)));
+}
+template <int ACT>
+__device__ __forceinline__ float act_f(float x) {
+  if constexpr (ACT == ACT_GELU) return gelu_erf_f(x);
+  else if constexpr (ACT == ACT_GELU_TANH) return gelu_tanh_f(x);
+  else return x;
+}
+
+// LDS-DMA piece (1 KiB per wave instruction, lane-linear at wave-uniform lds_dst); M0 saved/set/restored in
+// one statement; completion tracked only by the caller's counted vmcnt.
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_dst)
+      : "memory");
+}
+
+// Two 16-B W loads of one row: k [32s + 8 h4, +8) for s = 0, 1 (bytes 16 h4 and 64 + 16 h4 of the 128-B line).
+// Two 16-B W loads of one row: k [32s + 8 h4, +8) for s = 0, 1 (bytes 16 h4 and 64 + 16 h4 of the 128-B
+// line).  Default cache policy: the two half-line requests of a row share the L2 line (nontemporal loads
+// measured 5-20 % slower here: profiles/gemm_decode_ab_v2.jsonl).
+__device__ __forceinline__ void ldw2(bf16x8_t& lo, bf16x8_t& hi, const bf16* p) {
+  asm volatile(
+      "global_load_dwordx4 %0, %2, off\n\t"
+      "global_load_dwordx4 %1, %2, off offset:64"
+      : "=&v"(lo), "=&v"(hi)
+      : "v"(p)
+      : "memory");
+}
+
+// Retire everything but the N youngest vector-memory ops; the named W registers are read-write here, so
+// nothing that consumes them can be scheduled above the wait.
+template <int N, int G>
+__device__ __forceinline__ void wait_w(bf16x8_t (&w)[G]) {
+  if constexpr (G == 4)
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : "n"(N) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7])
+                 : "n"(N)
+                 : "memory");
+}
+
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+constexpr int kDepth = 3;  // K-steps of W and A in flight (ring of kDepth + 1)
+
+struct DArgs {
+  const bf16* A;
+  const bf16* W;
+  const bf16* bias;
+  void* C;
+  int lda, ldw, ldc;
+  int M, N, K;
+  int tiles_n, ksplit, kt_split;
+};
+
+// NTW 16-row n-tiles per wave (32 or 64 W rows): the A fragment read from LDS feeds NTW MFMAs, so NTW = 4
+// halves the LDS read traffic per MFMA (at NTW = 2 it equals the LDS bandwidth at full MFMA rate).
+template <int EPI, int ACT, int MT, int D, int NWV, int NTW>
+__global__ __launch_bounds__(64 * NWV, (NWV == 4 && NTW == 2 && (D + 1) * MT * 2 <= 80) ? 2 : 1)
+void gemm_dec_kernel(DArgs p) {
+  constexpr int NST = D + 1;            // LDS stages = W register slots
+  constexpr int ABYTES = MT * 16 * 128;  // one K-step of A
+  constexpr int GA = (MT * 2) / NWV;     // A pieces (1 KiB) per wave per K-step
+  constexpr int GW = 2 * NTW;            // W dwordx4 per lane per K-step
+  constexpr int BN = 16 * NTW * NWV;
+  static_assert((MT * 2) % NWV == 0, "A pieces must split evenly over the waves");
+  static_assert(NTW == 2 || NTW == 4, "NTW");
+  __shared__ __attribute__((aligned(16))) char smem[NST * ABYTES];
+
+  const int tid = threadIdx.x;
+  const int L = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = L & 15, h4 = L >> 4;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = b / p.ksplit, split = b % p.ksplit;
+  const int n0 = tile * BN;
+  const int ks = p.K >> 6;
+  const int kb = split * p.kt_split;
+  const int ke = min(ks, kb + p.kt_split);
+  const int nsteps = ke - kb;
+
+  // W rows of this wave's n-tiles.  SiLU at NTW = 2: the 16 gate rows of a 16-wide output group and the
+  // matching up rows (+32); at NTW = 4 the wave owns one whole 64-row gate/up block (tiles 0,1 gate, 2,3 up).
+  int wr[NTW];
+  if constexpr (EPI == EPI_SILU && NTW == 2) {
+    const int q = (n0 >> 5) + w;
+    wr[0] = (q >> 1) * 64 + (q & 1) * 16;
+    wr[1] = wr[0] + 32;
+  } else {
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) wr[nt] = n0 + 16 * NTW * w + 16 * nt;
+  }
+  const bf16* wp[NTW];
+#pragma unroll
+  for (int nt = 0; nt < NTW; ++nt)
+    wp[nt] = p.W + (size_t)min(wr[nt] + li, p.N - 1) * p.ldw + (size_t)kb * 64 + 8 * h4;
+
+  // A pieces: piece q = w*GA + i covers rows [8q, 8q+8); lane -> row 8q + L/8, physical chunk L%8
+  const bf16* ap[GA];
+  uint32_t adst[GA];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int q = w * GA + i;
+    const int row = q * 8 + (L >> 3);
+    const int c = (L & 7) ^ ((row >> 1) & 7);
+    ap[i] = p.A + (size_t)min(row, p.M - 1) * p.lda + (size_t)kb * 64 + c * 8;
+    adst[i] = __builtin_amdgcn_readfirstlane(lds0 + q * 1024);
+  }
+
+  bf16x8_t wf[NST][GW];  // [slot][2 nt + s]
+  f32x4_t acc[MT][NTW];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // issue K-step `step` into ring slot `slot`; a step past the range (the last D iterations) re-reads
+  // L2-resident bytes (A's own rows, one W line) so every iteration issues the same ops and the counted
+  // waits stay exact without a branch (a conditional load would make hipcc merge the ring registers through
+  // copies that read an asm destination before its data lands)
+  auto issue = [&](int step, int slot, bf16x8_t (&wreg)[GW]) {
+    const bool live = step < nsteps;
+    const int so = live ? step * 64 : 0;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) glds16(ap[i] + so, adst[i] + slot * ABYTES);
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) ldw2(wreg[2 * nt], wreg[2 * nt + 1], live ? wp[nt] + so : p.W);
+  };
+
+  // A fragment of rows 16 mt + li, logical chunk 4 s + h4 (swizzle depends on li only)
+  const int sw = (li >> 1) & 7;
+  const int aoff0 = li * 128 + ((h4 ^ sw) << 4);
+  const int aoff1 = li * 128 + (((4 + h4) ^ sw) << 4);
+  auto compute = [&](int slot, bf16x8_t (&wreg)[GW]) {
+    const char* As = smem + slot * ABYTES;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(As + mt * 2048 + aoff0);
+      const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(As + mt * 2048 + aoff1);
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[2 * nt], a0, acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[2 * nt + 1], a1, acc[mt][nt], 0, 0, 0);
+      }
+    }
+  };
+
+  // prologue: steps 0 .. D-1 in flight (nsteps >= NST, checked by the launcher)
+#pragma unroll
+  for (int d = 0; d < D; ++d) issue(d, d, wf[d]);
+
+  // nsteps is a multiple of NST (launcher), so ring slots are compile-time in the unrolled body and no
+  // step is conditional
+  for (int t0 = 0; t0 < nsteps; t0 += NST) {
+#pragma unroll
+    for (int u = 0; u < NST; ++u) {
+      // steps t+1 .. t+D-1 were issued after step t: (D-1)(GA+GW) younger ops
+      wait_w<(D - 1) * (GA + GW)>(wf[u]);
+      bar();  // step t's A pieces visible to every wave; every wave is done with slot (u + D) % NST
+      issue(t0 + u + D, (u + D) % NST, wf[(u + D) % NST]);
+      compute(u, wf[u]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-reads land before the workgroup retires
+
+  // ---- epilogue: acc[mt][nt][r] = D[W row (wr[nt] + 4 h4 + r)][A row (16 mt + li)]
+  if constexpr (EPI == EPI_SILU) {
+    bf16* C = (bf16*)p.C;
+    constexpr int NP = NTW / 2;  // gate/up tile pairs: (nt, nt + NP)
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int gr = wr[j] + 4 * h4, ur = wr[j + NP] + 4 * h4;
+      if (ur >= p.N) continue;
+      const int oc = (gr >> 6) * 32 + (gr & 31);  // gate row 64 q + c  ->  output column 32 q + c
+      float bg[4], bu[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bg[r] = p.bias ? (float)p.bias[gr + r] : 0.f;
+        bu[r] = p.bias ? (float)p.bias[ur + r] : 0.f;
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = mt * 16 + li;
+        if (m >= p.M) continue;
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bits(silu_f(acc[mt][j][r] + bg[r]) * (acc[mt][j + NP][r] + bu[r]));
+        *reinterpret_cast<bf16x4_t*>(C + (size_t)m * p.ldc + oc) = o;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      const int n = wr[nt] + 4 * h4;
+      if (n >= p.N) continue;
+      float bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = (EPI == EPI_STORE && p.bias) ? (float)p.bias[n + r] : 0.f;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = mt * 16 + li;
+        if (m >= p.M) continue;
+        if constexpr (EPI == EPI_PARTIAL) {
+          float* ws = (float*)p.C + ((size_t)split * p.M + m) * p.N + n;
+          *reinterpret_cast<f32x4_t*>(ws) = acc[mt][nt];
+        } else {
+          bf16x4_t o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = f2bits(act_f<ACT>(acc[mt][nt][r] + bv[r]));
+          *reinterpret_cast<bf16x4_t*>((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+        }
+      }
+    }
+  }
+}
+
+template <int MT, int D, int NWV, int NTW>
+int launch_v(const DArgs& a, int epi, int act, int nwg, hipStream_t s) {
+#define GO(E, AC) gemm_dec_kernel<E, AC, MT, D, NWV, NTW><<<nwg, 64 * NWV, 0, s>>>(a)
+  if (epi == EPI_PARTIAL) GO(EPI_PARTIAL, ACT_NONE);
+  else if (epi == EPI_SILU) GO(EPI_SILU, ACT_NONE);
+  else if (act == ACT_GELU) GO(EPI_STORE, ACT_GELU);
+  else if (act == ACT_GELU_TANH) GO(EPI_STORE, ACT_GELU_TANH);
+  else GO(EPI_STORE, ACT_NONE);
+#undef GO
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Variants compiled (mt = 16-row tiles of M, nwv = waves per workgroup, ntw = 16-row W tiles per wave;
+// depth kDepth): (nwv 4, ntw 2): mt 4, 8, 16;  (nwv 8, ntw 2): mt 12.  ntw = 4 measured no faster than 2 at
+// M = 192 (profiles/gemm_decode_ab_v3.jsonl) and is not instantiated.
+GRAG_API int grag_gemm_decode_has(int mt, int nwv, int ntw) {
+  if (nwv == 4 && ntw == 2) return mt == 4 || mt == 8 || mt == 16;
+  if (nwv == 8 && ntw == 2) return mt == 12;
+  return 0;
+}
+
+// y = epilogue(x @ w^T) for M <= 16 * mt rows.  epi 0 store (act 0/1/3), 1 silu*mul (w gate/up interleaved in
+// 32-row blocks, out [M, N/2]).  ksplit > 1: fp32 planes into ws (ksplit * M * N floats), then
+// grag_splitk_reduce applies the epilogue.  Requirements (checked): K % 256 == 0 (whole ring rounds per
+// split), N % (16 * ntw * nwv) == 0, lda/ldw % 8 == 0, ldc % 4 == 0, 16-B aligned A/W.
+GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, void* C, int lda, int ldw, int ldc,
+                              int M, int N, int K, int epi, int act, int mt, int nwv, int ntw, int ksplit, void* ws,
+                              hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (!grag_gemm_decode_has(mt, nwv, ntw) || M > 16 * mt) return (int)hipErrorInvalidValue;
+  if (K % 64 != 0 || K < 64 || N % (16 * ntw * nwv) != 0 || lda % 8 != 0 || ldw % 8 != 0 || ldc % 4 != 0)
+    return (int)hipErrorInvalidValue;
+  if (epi != EPI_STORE && epi != EPI_SILU) return (int)hipErrorInvalidValue;
+  if (act != ACT_NONE && act != ACT_GELU && act != ACT_GELU_TANH) return (int)hipErrorInvalidValue;
+  if (epi == EPI_SILU && act != ACT_NONE) return (int)hipErrorInvalidValue;
+  constexpr int NST = kDepth + 1;
+  const int kt = K / 64;
+  if (kt % NST != 0) return (int)hipErrorInvalidValue;
+  if (ksplit < 1) ksplit = 1;
+  const int kts = ((kt / NST + ksplit - 1) / ksplit) * NST;
+  ksplit = (kt + kts - 1) / kts;  // effective splits (ops/gemm.py dec_ksplit computes the same)
+  if (ksplit > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
+  DArgs a;
+  a.A = (const bf16*)A;
+  a.W = (const bf16*)W;
+  a.bias = ksplit > 1 ? nullptr : (const bf16*)bias;
+  a.C = ksplit > 1 ? ws : C;
+  a.lda = lda; a.ldw = ldw; a.ldc = ldc;
+  a.M = M; a.N = N; a.K = K;
+  a.tiles_n = N / (16 * ntw * nwv);
+  a.ksplit = ksplit;
+  a.kt_split = kts;
+  const int nwg = a.tiles_n * ksplit;
+  const int e = ksplit > 1 ? EPI_PARTIAL : epi;
+  int err;
+  if (nwv == 4) err = mt == 4 ? launch_v<4, kDepth, 4, 2>(a, e, act, nwg, stream)
+                     : mt == 8 ? launch_v<8, kDepth, 4, 2>(a, e, act, nwg, stream)
+                               : launch_v<16, kDepth, 4, 2>(a, e, act, nwg, stream);
+  else err = launch_v<12, kDepth, 8, 2>(a, e, act, nwg, stream);
+  if (err || ksplit == 1) return err;
+  return grag_splitk_reduce(ws, bias, C, ldc, M, N, ksplit, epi, act, stream);
+}

@@ -485,6 +485,23 @@ int launch(const Args& a, hipStream_t stream) {
 
 }  // namespace
 
+// out = epilogue(sum_s ws[s]) for fp32 split-K planes ws[S][M][N] (also used by gemm_decode.hip).
+GRAG_API int grag_splitk_reduce(const void* ws, const void* bias, void* C, int ldc, int M, int N, int S, int epi,
+                                int act, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (N % 8 != 0 || ldc % 8 != 0 || (epi == EPI_SILU && N % 64 != 0) || S < 1) return (int)hipErrorInvalidValue;
+  const int NO = epi == EPI_SILU ? N / 2 : N;
+  const long n8 = (long)M * (NO / 8);
+  const int blocks = (int)((n8 + 255) / 256);
+#define RED(E, AC) splitk_reduce_kernel<E, AC><<<blocks, 256, 0, stream>>>((const float*)ws, (const bf16*)bias, (bf16*)C, ldc, M, N, S)
+  if (epi == EPI_SILU) RED(EPI_SILU, ACT_NONE);
+  else if (act == ACT_GELU) RED(EPI_STORE, ACT_GELU);
+  else if (act == ACT_GELU_TANH) RED(EPI_STORE, ACT_GELU_TANH);
+  else RED(EPI_STORE, ACT_NONE);
+#undef RED
+  return (int)hipGetLastError();
+}
+
 // y = epilogue(x @ w^T).  epi: 0 store (act: 0 none, 1 gelu-erf, 3 gelu-tanh), 1 silu*mul
 // (w rows interleaved in 32-row gate/up blocks, out [M, N/2]).
 //   ksplit > 1: K split into ksplit parts, fp32 planes into ws (ksplit * M * N floats) and

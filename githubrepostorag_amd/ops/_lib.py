@@ -55,6 +55,9 @@ _SIGS = {
     "grag_topk_merge_cap": [],
     "grag_bitmap_update": [P, P, I, I, P],
     "grag_gemm_tile": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
+    "grag_splitk_reduce": [P, P, P, I, I, I, I, I, I, P],
+    "grag_gemm_decode": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P],
+    "grag_gemm_decode_has": [I, I, I],
 }
 
 

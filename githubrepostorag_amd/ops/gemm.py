@@ -204,6 +204,84 @@ def gemm_silu(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None = N
     return _launch(x, w_gu, b_gu, out, EPI_SILU, ACT_NONE, ksplit, sk)
 
 
+# ---------------------------------------------------------------- decode regime (csrc/kernels/gemm_decode.hip)
+DEC_DEPTH = 3  # K-steps in flight; a K-split covers whole rings of DEC_DEPTH + 1 steps
+_DEC_ON = os.environ.get("GRAG_DECODE_GEMM", "1") != "0"
+# (mt, nwv, ntw) compiled: mt 16-row tiles of M, nwv waves per workgroup, ntw 16-row W tiles per wave
+DEC_VARIANTS = [(4, 4, 2), (8, 4, 2), (12, 8, 2), (16, 4, 2)]
+DEC_MAX_M = int(os.environ.get("GRAG_DECODE_MAX_M", "128"))
+
+
+def dec_variants(M: int) -> list[tuple[int, int, int]]:
+    """Compiled variants that take an M-row batch, smallest padded row count first."""
+    need = -(-M // 16)
+    vs = [v for v in DEC_VARIANTS if v[0] >= need]
+    if not vs:
+        return []
+    mt = min(v[0] for v in vs)
+    return [v for v in vs if v[0] == mt]
+
+
+def dec_ksplit(K: int, ksplit: int) -> int:
+    """Effective K-splits after rounding each split to whole rings (same rule as the launcher)."""
+    kt = K // 64
+    nst = DEC_DEPTH + 1
+    kts = -(-(kt // nst) // max(1, ksplit)) * nst
+    return -(-kt // kts)
+
+
+def dec_plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int, int, int] | None:
+    """(mt, nwv, ntw, ksplit) for the decode kernel, or None when another path is faster.
+
+    Measured (scripts/bench_gemm_decode.py, cold weights, profiles/gemm_decode_ab_v4.jsonl): at 33..128 rows
+    the 4-wave variant with about one workgroup per CU beats the 256x256 tile kernel by 1.2-1.3x on the
+    Qwen2-7B qkv / o projections and 1.05-1.2x on down_proj; at 192 rows it only ties (v3), and on the
+    vocab- or FFN-wide outputs (>= one 128-column tile per CU) the tile kernel / library win."""
+    if not _DEC_ON or M < 1 or M > DEC_MAX_M or K % 256 or (silu and N % 64):
+        return None
+    vs = [v for v in dec_variants(M) if v[1] == 4 and N % (16 * v[1] * v[2]) == 0]
+    if not vs:
+        return None
+    mt, nwv, ntw = vs[0]
+    tiles = N // (16 * nwv * ntw)
+    ncu = _num_cus()
+    if tiles >= ncu:
+        return None
+    return mt, nwv, ntw, dec_ksplit(K, max(1, ncu // tiles))
+
+
+def dec_ws_floats(M: int, N: int, ksplit: int) -> int:
+    return ksplit * M * N if ksplit > 1 else 0
+
+
+def gemm_decode(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, act: int = ACT_NONE,
+                epi: int = EPI_STORE, plan: tuple[int, int, int, int] | None = None,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    """Decode-regime GEMM: y = act(x @ w.T + b) (epi EPI_STORE) or the SwiGLU product of an interleaved
+    gate/up weight (epi EPI_SILU, out [M, N/2]).  ``plan`` = (mt, nwv, ntw, ksplit) overrides dec_plan."""
+    M, K = x.shape
+    N = w.shape[0]
+    if not x.is_cuda:
+        return gemm_silu(x, w, b) if epi == EPI_SILU else gemm(x, w, b, act)
+    mt, nwv, ntw, ks = plan or dec_plan(M, N, K, epi == EPI_SILU)
+    ks = dec_ksplit(K, ks)
+    if out is None:
+        out = torch.empty(M, N // 2 if epi == EPI_SILU else N, dtype=x.dtype, device=x.device)
+    fl = dec_ws_floats(M, N, ks)
+    ws = WS.get(x.device, fl) if fl else None
+    call("grag_gemm_decode", ptr(x), ptr(w), ptr(b), ptr(out), x.stride(0), w.stride(0), out.stride(0),
+         M, N, K, epi, act, mt, nwv, ntw, ks, ptr(ws))
+    return out
+
+
+def dec_capture_ok(dev: torch.device, M: int, N: int, K: int, silu: bool = False) -> bool:
+    p = dec_plan(M, N, K, silu)
+    if p is None:
+        return False
+    fl = dec_ws_floats(M, N, p[3])
+    return fl == 0 or not torch.cuda.is_current_stream_capturing() or WS.ready(dev, fl)
+
+
 def capture_ok(dev: torch.device, M: int, N: int, K: int) -> bool:
     """False only inside a hipGraph capture whose split-K slab was not sized by an eager step."""
     ks, sk = plan(M, N, K)

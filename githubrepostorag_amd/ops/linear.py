@@ -8,8 +8,12 @@ A/B in scripts/bench_gemm.py:
 * ``grag_gemm_stream`` (deep-K projections such as down_proj, and the LM head
   at M <= 32): stream-K over (tile, 64-k) iterations, full-line LDS-DMA ring,
   in-launch split-tile combine;
-* ``grag_gemm_tile`` (ops/gemm.py, 256x256 MFMA tiles + split-K slabs) for
-  decode batches 32 < M <= 256: 1.1-1.5x the library on every Qwen2-7B
+* ``grag_gemm_decode`` (ops/gemm.py, W streamed HBM -> registers 3 K-steps
+  deep, A through an LDS-DMA ring) for 32 < M <= 128 on projections narrower
+  than one 128-column tile per CU (qkv, o, down): 1.05-1.3x the tile kernel
+  (profiles/gemm_decode_ab_v4.jsonl);
+* ``grag_gemm_tile`` (ops/gemm.py, 256x256 MFMA tiles + split-K slabs) for the
+  other decode batches 32 < M <= 256: 1.1-1.5x the library on every Qwen2-7B
   projection (profiles/gemm_tile_ab_v1.jsonl);
 * larger M (prefill, encoder batches): plain GEMMs go to hipBLASLt through
   ``torch.nn.functional.linear`` — the library is used only for plain
@@ -265,6 +269,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> t
             and x.stride(1) == 1 and w.stride(1) == 1):
         M, K = x.shape
         N = w.shape[0]
+        if (TILE_MIN_M <= M and _tile.supported(x, w) and _tile.dec_plan(M, N, K) is not None
+                and _tile.dec_capture_ok(x.device, M, N, K)):
+            return _tile.gemm_decode(x, w, b)
         if use_tile(M, N, K) and _tile.supported(x, w) and _tile.capture_ok(x.device, M, N, K):
             return _tile.gemm(x, w, b)
         parts = splitk_parts(M, N, K)

@@ -1,0 +1,123 @@
+"""A/B of the decode-regime GEMM (csrc/kernels/gemm_decode.hip) against the
+256x256 tile kernel and the library GEMM on the Qwen2-7B projections at decode
+batches (M = 64..256).  Every variant (mt, waves, K-splits) is timed, so the
+output doubles as the dispatch sweep for ops/gemm.py dec_plan.
+
+Weights rotate over enough copies to exceed the 256 MB Infinity Cache (timed
+cold, as in serving); all arms interleave in one process on the same operands.
+Prints one JSON line per (shape, arm).
+
+usage: python scripts/bench_gemm_decode.py [--ms 64,128,192,256] [--reps 30] [--out f.jsonl]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from githubrepostorag_amd.ops import gemm as G  # noqa: E402
+from githubrepostorag_amd.ops.linear import enable_tuned_gemms  # noqa: E402
+
+Q7 = {"qkv": (4608, 3584), "o": (3584, 3584), "gate_up": (37888, 3584), "down": (3584, 18944)}
+
+
+def timeit(fn, reps):
+    ts = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e) * 1e3)
+    return statistics.median(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ms", default="64,128,192,256")
+    ap.add_argument("--shapes", default="qkv,o,gate_up,down")
+    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--splits", default="1,2,3,4,5,7,9,14,18,28")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    enable_tuned_gemms()
+    torch.manual_seed(0)
+    rows = []
+    for sname in args.shapes.split(","):
+        N, K = Q7[sname]
+        silu = sname == "gate_up"
+        wbytes = N * K * 2
+        ncopy = max(2, min(10, (700 << 20) // wbytes + 1))
+        ws = [(torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16) * 0.05 for _ in range(ncopy)]
+        for M in map(int, args.ms.split(",")):
+            x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+            ref = torch.nn.functional.linear(x.float(), ws[0].float())
+            if silu:
+                g, u = G.deinterleave_gate_up(ws[0].float())
+                ref = torch.nn.functional.silu(x.float() @ g.T) * (x.float() @ u.T)
+            it = {"i": 0}
+
+            def nxt():
+                it["i"] += 1
+                return ws[it["i"] % ncopy]
+
+            arms = {"lib": lambda w=None: torch.nn.functional.linear(x, w if w is not None else nxt())}
+            S, SK = G.plan(M, N, K)
+            G.WS.reserve(dev, G._ws_floats(M, N, S, SK))
+            arms["tile"] = (lambda w=None: G.gemm_silu(x, w if w is not None else nxt(), ksplit=S, sk=SK)) if silu \
+                else (lambda w=None: G.gemm(x, w if w is not None else nxt(), ksplit=S, sk=SK))
+            for mt, nwv, ntw in G.dec_variants(M):
+                if N % (16 * nwv * ntw):
+                    continue
+                tiles = N // (16 * nwv * ntw)
+                seen = set()
+                for req in map(int, args.splits.split(",")):
+                    ks = G.dec_ksplit(K, req)
+                    if ks in seen or tiles * ks > 1200:
+                        continue
+                    seen.add(ks)
+                    G.WS.reserve(dev, G.dec_ws_floats(M, N, ks))
+                    plan = (mt, nwv, ntw, ks)
+                    epi = G.EPI_SILU if silu else G.EPI_STORE
+                    arms[f"dec_mt{mt}_w{nwv}_n{ntw}_s{ks}"] = (
+                        lambda w=None, plan=plan, epi=epi: G.gemm_decode(x, w if w is not None else nxt(), epi=epi,
+                                                                         plan=plan))
+            errs = {}
+            for name, fn in arms.items():
+                if name == "lib":
+                    continue
+                y = fn(ws[0]).float()
+                errs[name] = ((y - ref).abs().max() / (ref.abs().max() + 1e-9)).item()
+            for _ in range(3):
+                for fn in arms.values():
+                    fn()
+            torch.cuda.synchronize()
+            times = {n: [] for n in arms}
+            for _ in range(3):
+                for n, fn in arms.items():
+                    times[n].append(timeit(fn, max(1, args.reps // 3)))
+            lib_us = statistics.median(times["lib"])
+            for n in arms:
+                us = statistics.median(times[n])
+                row = {"shape": sname, "M": M, "N": N, "K": K, "arm": n, "us": round(us, 2),
+                       "TBps": round((wbytes + M * K * 2) / us / 1e6, 2), "vs_lib": round(lib_us / us, 3),
+                       "relerr": None if n == "lib" else round(errs[n], 5)}
+                print(json.dumps(row), flush=True)
+                rows.append(row)
+        del ws
+    if args.out:
+        with open(args.out, "w") as f:
+            for r in rows:
+                f.write(json.dumps(r) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -130,3 +130,68 @@ def test_plan_stream_k():
     assert G.plan(192, 37888, 3584) == (1, 0)     # 148 tiles: whole tiles (all-stream-K measured slower)
     assert G.plan(16384, 4608, 3584) == (1, 256)  # 1152 tiles = 4.5 rounds
     assert G.plan(16384, 37888, 3584) == (1, 0)   # 9472 tiles = 37 full rounds
+
+
+# ---------------------------------------------------------------- decode kernel (csrc/kernels/gemm_decode.hip)
+@pytest.mark.parametrize("M,N,K,plan", [(1, 256, 256, (4, 4, 2, 1)), (37, 512, 1024, (4, 4, 2, 2)),
+                                        (128, 1024, 512, (8, 4, 2, 1)), (192, 4608, 3584, (12, 8, 2, 14)),
+                                        (64, 3584, 3584, (4, 4, 2, 7)), (256, 1536, 1024, (16, 4, 2, 2)),
+                                        (100, 512, 256, (8, 4, 2, 1)), (120, 1024, 1024, (8, 4, 2, 3)),
+                                        (96, 3584, 18944, (8, 4, 2, 9))])
+def test_gemm_decode_plain(dev, M, N, K, plan):
+    x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+    G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, plan[3])))
+    y = G.gemm_decode(x, w, b, plan=plan)
+    check(y, ref(x, w, b), K)
+
+
+def test_gemm_decode_identity_asymmetric(dev):
+    # A = I with an asymmetric W catches a transposed C write
+    K = 256
+    w = (torch.arange(K * 256, dtype=torch.float32).reshape(256, K) % 251 - 125).to(torch.bfloat16).to(dev)
+    for M, plan in ((200, (16, 4, 2, 1)), (190, (12, 8, 2, 1))):
+        x = torch.eye(K, dtype=torch.bfloat16, device=dev)[:M].contiguous()
+        y = G.gemm_decode(x, w, plan=plan)
+        assert torch.equal(y.cpu(), w.float().T[:M].to(torch.bfloat16).cpu())
+
+
+@pytest.mark.parametrize("act", [G.ACT_GELU, G.ACT_GELU_TANH])
+def test_gemm_decode_gelu(dev, act):
+    M, N, K = 77, 1024, 512
+    x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+    for ks in (1, 2):
+        G.WS.reserve(dev, G.dec_ws_floats(M, N, ks))
+        y = G.gemm_decode(x, w, b, act=act, plan=(8, 4, 2, ks))
+        r = torch.nn.functional.gelu(ref(x, w, b), approximate="tanh" if act == G.ACT_GELU_TANH else "none")
+        check(y, r, K)
+
+
+@pytest.mark.parametrize("M,plan", [(5, (4, 4, 2, 1)), (192, (12, 8, 2, 1)), (250, (16, 4, 2, 1)),
+                                    (160, (12, 8, 2, 2)), (100, (8, 4, 2, 1))])
+def test_gemm_decode_silu(dev, M, plan):
+    I, K = 1024, 1024
+    x = rnd(M, K, dev=dev, scale=0.5)
+    wg, wu = rnd(I, K, dev=dev, seed=1, scale=0.2), rnd(I, K, dev=dev, seed=2, scale=0.2)
+    bg, bu = rnd(I, dev=dev, seed=3), rnd(I, dev=dev, seed=4)
+    wgu = G.interleave_gate_up(wg, wu)
+    bgu = G.interleave_gate_up(bg.view(I, 1), bu.view(I, 1)).view(2 * I)
+    G.WS.reserve(dev, G.dec_ws_floats(M, 2 * I, plan[3]))
+    h = G.gemm_decode(x, wgu, bgu, epi=G.EPI_SILU, plan=plan)
+    check(h, torch.nn.functional.silu(ref(x, wg, bg)) * ref(x, wu, bu), K)
+
+
+def test_gemm_decode_graph_replay(dev):
+    M, N, K = 96, 3584, 3584
+    x, w = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3)
+    plan = G.dec_plan(M, N, K)
+    G.WS.reserve(dev, G.dec_ws_floats(M, N, plan[3]))
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    G.gemm_decode(x, w, out=out)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        G.gemm_decode(x, w, out=out)
+    x.copy_(rnd(M, K, dev=dev, seed=7, scale=0.3))
+    g.replay()
+    torch.cuda.synchronize()
+    check(out, ref(x, w), K)

@@ -23,3 +23,17 @@ def test_two_slice_splitk_only_for_measured_shape():
     assert splitk_parts(64, 1536, 8960) == 0  # Qwen2-1.5B down_proj
     assert splitk_parts(64, 2048, 11008) == 0  # Qwen2.5-3B down_proj
     assert splitk_parts(64, 3584, 18944) == 2
+
+
+def test_decode_gemm_plan_rules():
+    from githubrepostorag_amd.ops import gemm as G
+
+    assert G.dec_plan(96, 4608, 1000) is None             # K % 256
+    assert G.dec_plan(192, 4608, 3584) is None            # M > 128: tile kernel
+    assert G.dec_plan(64, 37888, 3584, silu=True) is None  # FFN-wide: >= one tile per CU
+    assert G.dec_ksplit(3584, 9) == 7                     # 14 rings of 4 steps -> 2 rings per split
+    assert G.dec_variants(100) == [(8, 4, 2)]
+    assert G.dec_variants(190) == [(12, 8, 2)]
+    if G._num_cus() == 256:
+        assert G.dec_plan(64, 4608, 3584) == (4, 4, 2, 7)   # 36 tiles x 7 splits
+        assert G.dec_plan(128, 3584, 18944) == (8, 4, 2, 9)  # 28 tiles x 9 splits
