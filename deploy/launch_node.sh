@@ -1,6 +1,7 @@
 #!/bin/bash
 # Bare-metal launcher for one 8 x MI355X node (no Kubernetes):
-#   ./deploy/launch_node.sh serve    -> one API+engine process per GPU on ports 8000..8007
+#   ./deploy/launch_node.sh serve    -> one front door on :8000 (one /rag/jobs + SSE endpoint, one queue)
+#                                       over NGPU replica processes, one per GPU (service/cluster.py)
 #   ./deploy/launch_node.sh ingest   -> ingest on GPU 0, snapshot to $INDEX_DIR
 #   ./deploy/launch_node.sh bench N  -> the multi-GPU bench (torchrun, one rank per GPU, RCCL)
 set -euo pipefail
@@ -9,10 +10,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 NGPU=${NGPU:-8}
 case "${1:-serve}" in
   serve)
-    for i in $(seq 0 $((NGPU - 1))); do
-      HIP_VISIBLE_DEVICES=$i python -m githubrepostorag_amd serve --port $((8000 + i)) > "serve_$i.log" 2>&1 &
-    done
-    wait ;;
+    GPUS=$(seq -s, 0 $((NGPU - 1))) exec python -m githubrepostorag_amd serve --replicas "$NGPU" --port "${PORT:-8000}" ;;
   ingest)
     HIP_VISIBLE_DEVICES=0 python -m githubrepostorag_amd ingest "${@:2}" ;;
   bench)

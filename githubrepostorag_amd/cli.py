@@ -10,6 +10,11 @@ engine, encoder, index, job workers and API together:
            with the in-process job workers; the runtime (models, index) is
            built once at startup on this process's GPU.  With TP=N under
            torchrun the engine is sharded over N GPUs and TP rank 0 serves.
+           With --replicas N (or DP=N) this process is a GPU-less front door:
+           one /rag/jobs + SSE endpoint, one job queue and event log, and N
+           replica child processes (one per GPU) that run the jobs
+           (service/cluster.py).
+  replica  one per-GPU replica of a front door (started by serve --replicas).
   ingest   ingest repositories (github | local dir | synthetic) into the
            index and optionally snapshot it to INDEX_DIR.
   ask      one RAG query through the agent, printing events as they arrive.
@@ -51,6 +56,9 @@ def cmd_serve(args) -> int:
 
     s = _settings(args)
     logging.basicConfig(level=s.log_level, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    replicas = args.replicas if args.replicas is not None else s.dp
+    if replicas > 1:
+        return _serve_front_door(args, s, replicas)
     def factory():
         rt = _runtime(args)
         n = rt.warmup()  # decode graphs captured before the first request, not inside one
@@ -72,9 +80,65 @@ def cmd_serve(args) -> int:
         uvicorn.run(app, host=args.host, port=port, log_level=s.log_level.lower())
         rt.close()
         return 0
-    app = create_app(runtime_factory=factory)
+    from .service.api import APIState
+
+    app = create_app(APIState(ping_seconds=s.sse_ping_seconds), runtime_factory=factory)
     uvicorn.run(app, host=args.host, port=args.port, log_level=s.log_level.lower())
     return 0
+
+
+def _serve_front_door(args, s, replicas: int) -> int:
+    """One API + queue + event log for N per-GPU replica processes (service/cluster.py)."""
+    import uvicorn
+
+    from .service.api import APIState, create_app
+    from .service.cluster import ClusterRuntimeView, ReplicaHub, spawn_replicas
+    from .service.events import EventLog
+
+    events = EventLog(keep_seconds=s.keep_result_s)
+    hub = ReplicaHub(events, job_timeout=s.job_timeout_s, keep_result=s.keep_result_s)
+    gpus = [int(g) for g in os.environ.get("GPUS", "").split(",") if g.strip()] or list(range(replicas))
+    fwd = []
+    for k in ("qwen_model", "embed_model", "index_dir", "model_dir", "encoder_dir"):
+        v = getattr(args, k, None)
+        if v:
+            fwd += [f"--{k.replace('_', '-')}", v]
+    procs = spawn_replicas(replicas, hub.address, hub.authkey, fwd, gpus=gpus[:replicas])
+    state = APIState(runtime=ClusterRuntimeView(hub, s), queue=hub.queue, events=events, flags=hub.flags,
+                     ping_seconds=s.sse_ping_seconds)
+    app = create_app(state)
+    try:
+        uvicorn.run(app, host=args.host, port=args.port, log_level=s.log_level.lower())
+    finally:
+        hub.close()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except Exception:
+                p.terminate()
+    return 0
+
+
+def cmd_replica(args) -> int:
+    from .service.cluster import run_replica
+
+    s = _settings(args)
+    logging.basicConfig(level=s.log_level, format=f"%(asctime)s %(levelname)s replica{args.rank} %(name)s: %(message)s")
+    if args.factory:
+        import importlib
+
+        mod, fn = args.factory.split(":")
+        rt = getattr(importlib.import_module(mod), fn)(s)
+    else:
+        rt = _runtime(args)
+        rt.warmup()
+    host, port = args.hub.rsplit(":", 1)
+    key = bytes.fromhex(os.environ["GRAG_HUB_AUTHKEY"])
+    try:
+        return run_replica(rt, (host, int(port)), key, args.rank)
+    finally:
+        if hasattr(rt, "close"):
+            rt.close()
 
 
 def cmd_ingest(args) -> int:
@@ -150,6 +214,13 @@ def main(argv=None) -> int:
     common(p)
     p.add_argument("--host", default="0.0.0.0")
     p.add_argument("--port", type=int, default=8000)
+    p.add_argument("--replicas", type=int, default=None,
+                   help="front door over N per-GPU replica processes (default DP; GPUS=0,1,.. picks devices)")
+    p = sub.add_parser("replica", help="one per-GPU replica of a front door (internal)")
+    common(p)
+    p.add_argument("--hub", required=True, help="host:port of the front door's replica hub")
+    p.add_argument("--rank", type=int, default=0)
+    p.add_argument("--factory", default=None, help="module:function(settings) -> runtime (tests)")
     p = sub.add_parser("ingest", help="ingest repositories into the index")
     common(p)
     p.add_argument("--source", choices=["github", "local", "synthetic"], default="synthetic")
@@ -175,7 +246,7 @@ def main(argv=None) -> int:
     if argv and argv[0] == "bench":
         return cmd_bench(None, argv[1:])
     args = ap.parse_args(argv)
-    return {"serve": cmd_serve, "ingest": cmd_ingest, "ask": cmd_ask, "build": cmd_build,
+    return {"serve": cmd_serve, "replica": cmd_replica, "ingest": cmd_ingest, "ask": cmd_ask, "build": cmd_build,
             "config": cmd_config}[args.cmd](args)
 
 

@@ -75,7 +75,7 @@ class Settings:
     index_dir: str | None = field(default_factory=lambda: os.environ.get("INDEX_DIR"))
     device: str = field(default_factory=lambda: _env("DEVICE", "auto"))
     tp: int = field(default_factory=lambda: _int("TP", 1))
-    dp: int = field(default_factory=lambda: _int("DP", 1))
+    dp: int = field(default_factory=lambda: _int("DP", 1))  # serve: replicas behind one front door
     max_num_seqs: int = field(default_factory=lambda: _int("MAX_NUM_SEQS", 64))
     max_model_len: int = field(default_factory=lambda: _int("MAX_MODEL_LEN", 11712))
     max_num_batched_tokens: int = field(default_factory=lambda: _int("MAX_NUM_BATCHED_TOKENS", 16384))
@@ -91,8 +91,7 @@ class Settings:
     job_timeout_s: int = field(default_factory=lambda: _int("JOB_TIMEOUT", 300))
     engine_watchdog_s: int = field(default_factory=lambda: _int("ENGINE_WATCHDOG_S", 120))
     keep_result_s: int = field(default_factory=lambda: _int("KEEP_RESULT", 3600))
-    event_bus: str = field(default_factory=lambda: _env("EVENT_BUS", "memory"))  # memory | redis
-    llm_timeout_s: float = field(default_factory=lambda: _float("LLM_TIMEOUT", 60.0))
+    llm_timeout_s: float = field(default_factory=lambda: _float("LLM_TIMEOUT", 60.0))  # remote (HTTP) LLM calls
     llm_retries: int = field(default_factory=lambda: _int("LLM_RETRIES", 1))
     stream_tokens: bool = field(default_factory=lambda: _bool("STREAM_TOKENS", True))
     # coalesce concurrent jobs' query embeddings into one encoder pass (0 disables)

@@ -269,6 +269,8 @@ class VectorTable:
         self.max_probe_boost = 8.0
         self._version = 0
         self._counts: dict = {}
+        # write hook (service/cluster.py mirrors ingest writes to the other replicas): fn(op, args)
+        self.on_write = None
 
     @property
     def ivf(self) -> bool:
@@ -395,7 +397,9 @@ class VectorTable:
                 torch.cuda.current_stream(self.device).synchronize()
             if self.ivf and self._needs_compaction():
                 self._compact_locked()
-            return len(fresh)
+        if self.on_write is not None:
+            self.on_write("upsert", (list(row_ids), list(texts), vecs.to("cpu", torch.float16), metadatas))
+        return len(fresh)
 
     @guarded
     def delete(self, row_ids: list[str]) -> int:
@@ -415,7 +419,9 @@ class VectorTable:
                 self._version += 1
             if self.device.type == "cuda":
                 torch.cuda.current_stream(self.device).synchronize()
-            return int(slots.size)
+        if self.on_write is not None:
+            self.on_write("delete", (list(row_ids),))
+        return int(slots.size)
 
     def count(self) -> int:
         return self.n - self.deleted
@@ -802,6 +808,37 @@ class VectorStore:
 
     def table(self, scope: str) -> VectorTable:
         return self.tables[scope]
+
+    # ------------------------------------------------------------------ replica mirroring
+    def add_listener(self, fn) -> None:
+        """fn(scope, (op, args)) after every upsert/delete made through this store (not for writes
+        applied with ``apply_remote``), so a front door can mirror one replica's ingest on the others."""
+        self._remote = threading.local()
+
+        def hook(scope):
+            def on_write(op, args):
+                if not getattr(self._remote, "active", False):
+                    fn(scope, (op, args))
+            return on_write
+
+        for scope, t in self.tables.items():
+            t.on_write = hook(scope)
+
+    def apply_remote(self, scope: str, payload) -> None:
+        """Apply a write mirrored from another replica (not re-broadcast)."""
+        op, args = payload
+        remote = getattr(self, "_remote", None)
+        if remote is not None:
+            remote.active = True
+        try:
+            t = self.tables[scope]
+            if op == "upsert":
+                t.upsert(*args)
+            elif op == "delete":
+                t.delete(*args)
+        finally:
+            if remote is not None:
+                remote.active = False
 
     def counts(self) -> dict:
         return {self.table_names[s]: t.count() for s, t in self.tables.items()}

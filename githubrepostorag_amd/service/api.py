@@ -98,7 +98,7 @@ def create_app(state: APIState | None = None, runtime_factory=None) -> FastAPI:
         body = req.model_dump()
         if "top_k" not in req.model_fields_set:
             body["top_k"] = None  # only an explicit top_k caps the retrieved documents
-        await state.queue.enqueue_job("run_rag_job", job_id, body)
+        await state.queue.enqueue_job("run_rag_job", job_id, body, _job_id=job_id)
         return {"job_id": job_id}
 
     @app.get("/rag/jobs/{job_id}/events")

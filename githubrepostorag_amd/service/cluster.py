@@ -1,0 +1,465 @@
+"""One front door for N per-GPU replicas (SURVEY §2.9 "DP replicas").
+
+The reference decouples its API from N ARQ workers through Redis: the API
+enqueues ``run_rag_job`` (rest_api/src/app/controllers/jobs_controller.py:15-20),
+any worker pod picks it up (rag_worker/src/worker/worker.py:182-187) and
+progress flows back over pub/sub (rag_shared/bus.py:8-40).  Here:
+
+  front door (no GPU):  FastAPI (service/api.py) + JobQueue + EventLog +
+                        CancelFlags + ReplicaHub (this module)
+  replica r (GPU r):    a child process (``python -m githubrepostorag_amd
+                        replica``) holding one RAGRuntime (engine, encoder,
+                        store) and a RAGWorker, connected to the hub over a
+                        local authenticated socket (multiprocessing.connection)
+
+Scheduling: the hub's job function ``run_rag_job`` waits for a live replica
+with a free slot (each replica advertises WORKER_MAX_JOBS), sends the job to
+the least-loaded one and returns when that replica reports the job's ``final``
+event.  Every event a replica's worker emits is forwarded and appended to the
+front door's replayable EventLog, so ``GET /rag/jobs/{id}/events`` is one SSE
+endpoint for the whole node; cancels are forwarded to the owning replica; a
+replica that disconnects fails its in-flight jobs (``error`` + ``final``) and
+the hub stops dispatching to it.  Ingest writes (``VectorStore`` upserts made on
+one replica) are broadcast to the others so every replica serves the same
+index (288 GB of HBM holds a full 10M-vector table per GPU, so replicas keep
+full copies and a search never crosses xGMI).
+
+Wire messages (pickled tuples over the authenticated socket, our own processes
+only):
+  replica -> hub: ("hello", rank, capacity, info) | ("event", job, name, data)
+                  | ("health", info) | ("upsert", table, payload)
+  hub -> replica: ("run", job, request) | ("cancel", job) | ("upsert", table, payload) | ("stop",)
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import secrets
+import subprocess
+import sys
+import threading
+import time
+from multiprocessing.connection import Client, Listener
+
+from . import metrics as M
+from .events import CancelFlags, EventLog
+
+log = logging.getLogger(__name__)
+
+
+class _Replica:
+    __slots__ = ("rank", "conn", "capacity", "inflight", "alive", "info", "lock", "jobs")
+
+    def __init__(self, rank: int, conn, capacity: int, info: dict):
+        self.rank = rank
+        self.conn = conn
+        self.capacity = max(1, int(capacity))
+        self.inflight = 0
+        self.alive = True
+        self.info = info
+        self.lock = threading.Lock()
+        self.jobs: set[str] = set()
+
+    def send(self, msg) -> bool:
+        with self.lock:
+            if not self.alive:
+                return False
+            try:
+                self.conn.send(msg)
+                return True
+            except (OSError, EOFError, BrokenPipeError):
+                self.alive = False
+                return False
+
+
+class HubCancelFlags(CancelFlags):
+    """Front-door cancel flags: a cancel is also forwarded to the replica that runs the job."""
+
+    def __init__(self, hub: "ReplicaHub", ttl: float = 3600.0):
+        super().__init__(ttl)
+        self.hub = hub
+
+    def cancel_sync(self, job_id: str) -> None:
+        super().cancel_sync(job_id)
+        self.hub.forward_cancel(job_id)
+
+
+class ReplicaHub:
+    """Accepts replica connections and dispatches jobs to them."""
+
+    def __init__(self, events: EventLog, host: str = "127.0.0.1", port: int = 0, authkey: bytes | None = None,
+                 job_timeout: float = 300.0, keep_result: float = 3600.0):
+        from .worker import JobQueue
+
+        self.events = events
+        self.authkey = authkey or secrets.token_bytes(16)
+        self.listener = Listener((host, port), authkey=self.authkey)
+        self.address = self.listener.address
+        self.replicas: dict[int, _Replica] = {}
+        self.owner: dict[str, _Replica] = {}
+        self._done: dict[str, tuple[asyncio.AbstractEventLoop, asyncio.Future]] = {}
+        self._lock = threading.Lock()
+        self._loop: asyncio.AbstractEventLoop | None = None
+        self._slot_cond: asyncio.Condition | None = None
+        self.flags = HubCancelFlags(self)
+        # the front door's queue admits as many jobs as the replicas have slots; the rest wait in FIFO order
+        self.queue = JobQueue({"run_rag_job": self.run_rag_job}, max_jobs=256, job_timeout=job_timeout,
+                              keep_result=keep_result)
+        self.queue.ctx["on_timeout"] = self._on_timeout
+        self._closed = False
+        self._acceptor = threading.Thread(target=self._accept_loop, name="replica-hub-accept", daemon=True)
+        self._acceptor.start()
+
+    # ------------------------------------------------------------------ connections
+    def _accept_loop(self) -> None:
+        while not self._closed:
+            try:
+                conn = self.listener.accept()
+            except (OSError, EOFError):
+                if self._closed:
+                    return
+                continue
+            except Exception:  # authentication failure of a stray connection
+                log.warning("replica hub: rejected a connection", exc_info=True)
+                continue
+            threading.Thread(target=self._reader, args=(conn,), name="replica-hub-reader", daemon=True).start()
+
+    def _reader(self, conn) -> None:
+        rep = None
+        try:
+            hello = conn.recv()
+            if not (isinstance(hello, tuple) and hello and hello[0] == "hello"):
+                conn.close()
+                return
+            _, rank, capacity, info = hello
+            rep = _Replica(int(rank), conn, capacity, info or {})
+            with self._lock:
+                old = self.replicas.get(rep.rank)
+                self.replicas[rep.rank] = rep
+            if old is not None:
+                self._fail_replica(old, "replica re-registered")
+            log.info("replica %d connected (capacity %d)", rep.rank, rep.capacity)
+            M.CLUSTER_REPLICAS.set(self.live_count())
+            self._notify_slots()
+            while True:
+                msg = conn.recv()
+                kind = msg[0]
+                if kind == "event":
+                    _, job_id, name, data = msg
+                    self.events.emit_sync(job_id, name, data)
+                    if name == "final":
+                        self._finish(job_id)
+                elif kind == "health":
+                    rep.info = msg[1]
+                elif kind == "upsert":  # an ingest on this replica: mirror it on every other replica
+                    for other in self.live_replicas():
+                        if other is not rep:
+                            other.send(msg)
+        except (EOFError, OSError, ConnectionResetError):
+            pass
+        finally:
+            if rep is not None:
+                self._fail_replica(rep, "replica disconnected")
+
+    def _fail_replica(self, rep: _Replica, why: str) -> None:
+        with rep.lock:
+            was_alive = rep.alive
+            rep.alive = False
+        with self._lock:
+            if self.replicas.get(rep.rank) is rep:
+                self.replicas.pop(rep.rank, None)
+            jobs = [j for j, r in self.owner.items() if r is rep]
+        if was_alive:
+            log.warning("replica %d: %s (%d jobs in flight)", rep.rank, why, len(jobs))
+        for j in jobs:
+            if not self.events.is_closed(j):
+                self.events.emit_sync(j, "error", {"message": f"replica {rep.rank} lost: {why}"})
+                self.events.emit_sync(j, "final", {"answer": "", "sources": None, "error": True})
+            self._finish(j)
+        M.CLUSTER_REPLICAS.set(self.live_count())
+        self._notify_slots()
+
+    # ------------------------------------------------------------------ scheduling
+    def live_replicas(self) -> list[_Replica]:
+        with self._lock:
+            return [r for r in self.replicas.values() if r.alive]
+
+    def live_count(self) -> int:
+        return len(self.live_replicas())
+
+    def capacity(self) -> int:
+        return sum(r.capacity for r in self.live_replicas())
+
+    def _notify_slots(self) -> None:
+        loop, cond = self._loop, self._slot_cond
+        if loop is None or cond is None:
+            return
+
+        async def _n():
+            async with cond:
+                cond.notify_all()
+
+        coro = _n()
+        try:
+            asyncio.run_coroutine_threadsafe(coro, loop)
+        except RuntimeError:  # loop closed
+            coro.close()
+
+    def _pick(self) -> _Replica | None:
+        free = [r for r in self.live_replicas() if r.inflight < r.capacity]
+        return min(free, key=lambda r: (r.inflight / r.capacity, r.rank)) if free else None
+
+    def _finish(self, job_id: str) -> None:
+        with self._lock:
+            rep = self.owner.pop(job_id, None)
+            fut = self._done.pop(job_id, None)
+        if rep is not None:
+            with rep.lock:
+                rep.inflight = max(0, rep.inflight - 1)
+                rep.jobs.discard(job_id)
+            M.CLUSTER_INFLIGHT.labels(replica=str(rep.rank)).set(rep.inflight)
+        if fut is not None:
+            loop, f = fut
+            loop.call_soon_threadsafe(lambda: f.done() or f.set_result(True))
+        self._notify_slots()
+
+    async def wait_for_replicas(self, n: int, timeout: float = 600.0) -> None:
+        self._bind_loop()
+        t0 = time.time()
+        while self.live_count() < n:
+            if time.time() - t0 > timeout:
+                raise TimeoutError(f"only {self.live_count()} of {n} replicas connected")
+            await asyncio.sleep(0.05)
+
+    def _bind_loop(self) -> None:
+        if self._loop is None:
+            self._loop = asyncio.get_running_loop()
+            self._slot_cond = asyncio.Condition()
+
+    async def run_rag_job(self, ctx, job_id: str, req: dict):
+        """JobQueue function: place the job on a replica and wait for its final event."""
+        self._bind_loop()
+        loop = asyncio.get_running_loop()
+        t0 = time.perf_counter()
+        async with self._slot_cond:
+            while True:
+                rep = self._pick()
+                if rep is not None:
+                    break
+                if self.live_count() == 0 and time.perf_counter() - t0 > 30.0:
+                    self.events.emit_sync(job_id, "error", {"message": "no replica available"})
+                    self.events.emit_sync(job_id, "final", {"answer": "", "sources": None, "error": True})
+                    return None
+                try:
+                    await asyncio.wait_for(self._slot_cond.wait(), timeout=1.0)
+                except asyncio.TimeoutError:
+                    pass
+            fut = loop.create_future()
+            with self._lock:
+                self.owner[job_id] = rep
+                self._done[job_id] = (loop, fut)
+            with rep.lock:
+                rep.inflight += 1
+                rep.jobs.add(job_id)
+        M.CLUSTER_INFLIGHT.labels(replica=str(rep.rank)).set(rep.inflight)
+        M.CLUSTER_DISPATCH.labels(replica=str(rep.rank)).inc()
+        req = dict(req, _enqueued=(self.queue.results.get(job_id) or {}).get("enqueued"))
+        if not rep.send(("run", job_id, req)):
+            self._fail_replica(rep, "send failed")
+        if self.flags.is_cancelled_sync(job_id):
+            rep.send(("cancel", job_id))
+        await fut
+        return {"replica": rep.rank}
+
+    def forward_cancel(self, job_id: str) -> None:
+        with self._lock:
+            rep = self.owner.get(job_id)
+        if rep is not None:
+            rep.send(("cancel", job_id))
+
+    async def _on_timeout(self, job_id: str, req: dict) -> None:
+        self.flags.cancel_sync(job_id)
+        if not self.events.is_closed(job_id):
+            await self.events.emit(job_id, "error", {"message": f"job timed out after {self.queue.job_timeout}s"})
+            await self.events.emit(job_id, "final", {"answer": "", "sources": None, "error": True})
+        self._finish(job_id)
+
+    def health(self) -> dict:
+        reps = sorted(self.live_replicas(), key=lambda r: r.rank)
+        return {"replicas": [{"rank": r.rank, "capacity": r.capacity, "inflight": r.inflight, **r.info}
+                             for r in reps], "live": len(reps)}
+
+    def close(self) -> None:
+        self._closed = True
+        for r in self.live_replicas():
+            r.send(("stop",))
+        try:
+            self.listener.close()
+        except OSError:
+            pass
+
+
+class ClusterRuntimeView:
+    """What the API and /health need from a runtime, at a front door that holds no model."""
+
+    def __init__(self, hub: ReplicaHub, settings):
+        self.hub = hub
+        self.settings = settings
+        self.runner = None
+
+    def health(self) -> dict:
+        return self.hub.health()
+
+
+# ---------------------------------------------------------------------- replica side
+class _ForwardingEvents(EventLog):
+    """A replica's event log: every event is also forwarded to the hub (the replica keeps its own copy so
+    its worker's timeout / cancel paths behave exactly as in a single-process server)."""
+
+    def __init__(self, send):
+        super().__init__()
+        self._send = send
+
+    def emit_sync(self, job_id: str, event: str, data) -> None:
+        super().emit_sync(job_id, event, data)
+        self._send(("event", job_id, event, data))
+
+    emit_threadsafe = emit_sync
+
+
+def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | None = None,
+                health_every: float = 5.0) -> int:
+    """Serve jobs from the hub until it says stop or the connection drops (blocking)."""
+    from .worker import RAGWorker
+
+    s = runtime.settings
+    cap = capacity or s.worker_max_jobs
+    conn = Client(tuple(address) if isinstance(address, list) else address, authkey=authkey)
+    send_lock = threading.Lock()
+
+    def send(msg):
+        with send_lock:
+            conn.send(msg)
+
+    events = _ForwardingEvents(send)
+    flags = CancelFlags()
+    worker = RAGWorker(runtime, events, flags, cap, s.job_timeout_s, s.keep_result_s, s.stream_tokens)
+    store = getattr(runtime, "store", None)
+    if store is not None and hasattr(store, "add_listener"):
+        store.add_listener(lambda table, payload: send(("upsert", table, payload)))
+    send(("hello", rank, cap, {"device": str(getattr(runtime, "device", "cpu")), "pid": os.getpid()}))
+
+    async def main():
+        loop = asyncio.get_running_loop()
+        inbox: asyncio.Queue = asyncio.Queue()
+
+        def reader():
+            try:
+                while True:
+                    loop.call_soon_threadsafe(inbox.put_nowait, conn.recv())
+            except (EOFError, OSError):
+                loop.call_soon_threadsafe(inbox.put_nowait, ("stop",))
+
+        threading.Thread(target=reader, name="replica-reader", daemon=True).start()
+        tasks = set()
+        last_h = 0.0
+        while True:
+            try:
+                msg = await asyncio.wait_for(inbox.get(), timeout=health_every)
+            except asyncio.TimeoutError:
+                msg = None
+            if time.time() - last_h >= health_every:
+                last_h = time.time()
+                try:
+                    h = runtime.health() if hasattr(runtime, "health") else {}
+                    send(("health", {"device": str(getattr(runtime, "device", "cpu")), **h}))
+                except Exception:  # pragma: no cover
+                    pass
+            if msg is None:
+                continue
+            kind = msg[0]
+            if kind == "run":
+                _, job_id, req = msg
+                enq = req.pop("_enqueued", None)
+                worker.queue.results[job_id] = {"status": "running", "enqueued": enq or time.time()}
+
+                async def _run(job_id=job_id, req=req):
+                    try:
+                        await asyncio.wait_for(worker.run_rag_job(worker.queue.ctx, job_id, req),
+                                               timeout=worker.queue.job_timeout)
+                    except asyncio.TimeoutError:
+                        await worker._on_timeout(job_id, req)
+                    finally:
+                        worker.queue.results.pop(job_id, None)
+
+                t = asyncio.create_task(_run())
+                tasks.add(t)
+                t.add_done_callback(tasks.discard)
+            elif kind == "cancel":
+                flags.cancel_sync(msg[1])
+            elif kind == "upsert" and store is not None and hasattr(store, "apply_remote"):
+                store.apply_remote(msg[1], msg[2])
+            elif kind == "stop":
+                for t in list(tasks):
+                    t.cancel()
+                return
+
+    try:
+        asyncio.run(main())
+    finally:
+        try:
+            conn.close()
+        except OSError:
+            pass
+    return 0
+
+
+def spawn_replicas(n: int, address, authkey: bytes, extra_args=(), gpus: list[int] | None = None,
+                   env: dict | None = None) -> list[subprocess.Popen]:
+    """Start one replica child process per GPU (HIP_VISIBLE_DEVICES pins it; never an exec of this
+    process).  The authkey travels in the environment, not on the command line."""
+    procs = []
+    for r in range(n):
+        e = dict(os.environ, **(env or {}))
+        e["GRAG_HUB_AUTHKEY"] = authkey.hex()
+        if gpus is not None:
+            e["HIP_VISIBLE_DEVICES"] = str(gpus[r])
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        cmd = [sys.executable, "-m", "githubrepostorag_amd", "replica", "--hub", f"{address[0]}:{address[1]}",
+               "--rank", str(r), *extra_args]
+        procs.append(subprocess.Popen(cmd, env=e))
+    return procs
+
+
+def demo_runtime(settings):
+    """A CPU replica runtime with a scripted LLM and a tiny encoder over three chunks (tests, and a
+    GPU-less rehearsal of ``serve --replicas``: ``replica --factory
+    githubrepostorag_amd.service.cluster:demo_runtime``).  GRAG_DEMO_LLM_DELAY (s) slows each LLM call."""
+    from ..agent.llm import ScriptedLLM
+    from ..embed.service import Embedder
+    from ..index.store import VectorStore
+    from .runtime import RAGRuntime
+
+    delay = float(os.environ.get("GRAG_DEMO_LLM_DELAY", "0"))
+
+    def router(p):
+        if delay:
+            time.sleep(delay)
+        if p.startswith("Choose the best search scope"):
+            return '{"scope": "code"}'
+        if p.startswith("Judge if"):
+            return '{"coverage": 0.9, "needs_more": false}'
+        if p.startswith("Generate 3-4"):
+            return '["alt query"]'
+        return f"Widgets are handled in [1] (replica pid {os.getpid()})."
+
+    emb = Embedder.from_name("encoder-tiny", device="cpu", seed=3)
+    store = VectorStore(emb.dim, "cpu")
+    texts = ["widgets code", "gadget service", "billing module"]
+    store.table("chunk").upsert(["a", "b", "c"], texts, emb.embed_documents(texts),
+                                [{"namespace": "default", "repo": "r", "module": "m", "file_path": f"{x}.py"}
+                                 for x in "abc"])
+    settings.worker_max_jobs = int(os.environ.get("GRAG_DEMO_SLOTS", settings.worker_max_jobs))
+    return RAGRuntime(settings, device="cpu", llm=ScriptedLLM(router), embedder=emb, store=store,
+                      build_engine=False)

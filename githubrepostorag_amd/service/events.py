@@ -10,6 +10,9 @@ sleep), keep-alive pings go out only when idle, and the stream ends after the
 ``final`` event.  Producers may be asyncio code or agent threads
 (``emit_threadsafe``).  The wire format is unchanged:
 ``data: {"event": E, "data": D}\\n\\n`` frames and ``: ping\\n\\n`` comments.
+Across processes (one front door, N per-GPU replicas) the replicas forward
+their events to the front door's log over the replica hub (service/cluster.py)
+instead of Redis.
 """
 from __future__ import annotations
 
@@ -151,43 +154,3 @@ class CancelFlags:
         job's in-flight LLM requests so cancel takes effect mid-decode)."""
         with self._lock:
             self._listeners[job_id].append(fn)
-
-
-class RedisEventLog:  # pragma: no cover - redis is not installed in this image
-    """Wire-compatible Redis transport (multi-process API/worker split):
-    events go to a Redis Stream ``job:{id}:events`` so late subscribers replay
-    history with XRANGE/XREAD instead of losing pub/sub messages."""
-
-    def __init__(self, url: str):
-        import redis.asyncio as redis  # noqa: F401
-
-        self.url = url
-
-    async def _r(self):
-        import redis.asyncio as redis
-
-        return await redis.from_url(self.url, decode_responses=True)
-
-    async def emit(self, job_id: str, event: str, data) -> None:
-        r = await self._r()
-        await r.xadd(f"job:{job_id}:events", {"p": json.dumps({"event": event, "data": data}, default=str)})
-        await r.expire(f"job:{job_id}:events", 3600)
-        await r.close()
-
-    async def stream(self, job_id: str, ping_seconds: float = 15.0) -> AsyncIterator[str]:
-        r = await self._r()
-        last = "0-0"
-        try:
-            while True:
-                res = await r.xread({f"job:{job_id}:events": last}, block=int(ping_seconds * 1000), count=100)
-                if not res:
-                    yield ": ping\n\n"
-                    continue
-                for _, entries in res:
-                    for eid, fields in entries:
-                        last = eid
-                        yield f"data: {fields['p']}\n\n"
-                        if json.loads(fields["p"]).get("event") == "final":
-                            return
-        finally:
-            await r.close()

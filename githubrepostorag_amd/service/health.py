@@ -79,6 +79,25 @@ def _probe_index(runtime) -> dict:
     return {"status": "UP", "details": {"initialized": True, "test_results_count": len(hits)}}
 
 
+def _probe_replicas(view, component: str) -> dict:
+    """At a front door every component lives on the replicas: UP while at least one replica is connected
+    (and, for the LLM, its engine reports healthy); details list each replica's last health report."""
+    h = view.hub.health()
+    reps = h["replicas"]
+    if not reps:
+        return {"status": "DOWN", "details": {"error": "no replica connected"}}
+    if component == "qwen":
+        ok = [r for r in reps if (r.get("engine") or {}).get("healthy", True)]
+        return {"status": "UP" if ok else "DOWN",
+                "details": {"endpoint": "replicas", "healthy": len(ok), "replicas": len(reps)}}
+    if component == "vector_store":
+        return {"status": "UP", "details": {"tables": reps[0].get("tables", {}), "replicas": len(reps)}}
+    if component == "gpu":
+        return {"status": "UP", "details": {"devices": [r.get("device") for r in reps]}}
+    return {"status": "UP", "details": {"replicas": [{"rank": r["rank"], "inflight": r["inflight"],
+                                                      "capacity": r["capacity"]} for r in reps]}}
+
+
 def _probe_gpu() -> dict:
     try:
         import torch
@@ -110,8 +129,12 @@ def register_health_endpoints(app: FastAPI, runtime_getter, requests_mod=None) -
                          "system": {"cpu_percent": psutil.cpu_percent(), "memory_percent": psutil.virtual_memory().percent,
                                     "disk_usage": psutil.disk_usage("/").percent}}}
         runtime = runtime_getter()
-        probes = [("vector_store", lambda: _probe_store(runtime)), ("qwen", lambda: _probe_llm(runtime, req)),
-                  ("vector_index", lambda: _probe_index(runtime)), ("gpu", _probe_gpu)]
+        if hasattr(runtime, "hub"):  # front door over replica processes (service/cluster.py)
+            probes = [(name, lambda name=name: _probe_replicas(runtime, name))
+                      for name in ("vector_store", "qwen", "vector_index", "gpu")]
+        else:
+            probes = [("vector_store", lambda: _probe_store(runtime)), ("qwen", lambda: _probe_llm(runtime, req)),
+                      ("vector_index", lambda: _probe_index(runtime)), ("gpu", _probe_gpu)]
         for name, fn in probes:
             try:
                 if runtime is None and name != "gpu":

@@ -74,3 +74,10 @@ def render() -> bytes:
     except Exception:
         pass
     return generate_latest(REGISTRY)
+
+# front door over N replicas (service/cluster.py)
+CLUSTER_REPLICAS = Gauge("grag_cluster_replicas_live", "Replicas connected to the front door", registry=REGISTRY)
+CLUSTER_INFLIGHT = Gauge("grag_cluster_replica_inflight_jobs", "Jobs running on a replica", ["replica"],
+                         registry=REGISTRY)
+CLUSTER_DISPATCH = Counter("grag_cluster_dispatched_jobs_total", "Jobs dispatched to a replica", ["replica"],
+                           registry=REGISTRY)

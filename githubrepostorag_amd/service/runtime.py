@@ -11,7 +11,7 @@ from pathlib import Path
 import torch
 
 from ..agent.graph_agent import GraphAgent
-from ..agent.llm import EngineLLM, MeteredLLM
+from ..agent.llm import EngineLLM, HTTPLLM, MeteredLLM
 from ..config import Settings, settings as get_settings
 from ..embed.service import Embedder
 from ..engine.llm_engine import EngineConfig, LLMEngine
@@ -68,7 +68,16 @@ class RAGRuntime:
         self.retrievers = RetrieverFactory(store, embedder)
         # LLM engine
         self.engine = self.runner = None
-        if llm is None and build_engine:
+        self.tokenizer = None
+        remote = s.qwen_endpoint.startswith(("http://", "https://"))
+        if llm is None and remote:
+            # remote mode (the reference's worker -> vLLM split, qwen_llm.py:104-148): an OpenAI-compatible
+            # server elsewhere (e.g. another node's `serve`) answers the agent's and ingest's LLM calls
+            llm = MeteredLLM(HTTPLLM(s.qwen_endpoint, s.qwen_model, max_tokens=s.qwen_max_output,
+                                     timeout_s=s.llm_timeout_s, allow_thinking=s.allow_thinking))
+            ingest_llm = HTTPLLM(s.qwen_endpoint, s.qwen_model, max_tokens=2048, mode="ingest",
+                                 timeout_s=s.llm_timeout_s, allow_thinking=s.allow_thinking)
+        elif llm is None and build_engine:
             dcfg = decoder_config(s.qwen_model)
             sd = load_state_dict(s.model_dir, device=self.device) if s.model_dir else None
             model = build_decoder(dcfg, device=self.device, dtype=dtype, seed=s.seed + 1, state_dict=sd,

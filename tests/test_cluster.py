@@ -1,0 +1,167 @@
+"""Front door over N replica processes (service/cluster.py) on CPU: one
+/rag/jobs + SSE endpoint dispatching to 2 replica child processes over the
+replica hub, least-loaded placement, cancel forwarding, a dying replica
+failing its in-flight jobs, and ingest-write mirroring between replicas.
+Reference split: rest_api/src/app/controllers/jobs_controller.py:15-20 (API
+enqueues), rag_worker/src/worker/worker.py:182-187 (N workers consume)."""
+import asyncio
+import json
+import os
+import time
+
+import pytest
+import torch
+from fastapi.testclient import TestClient
+
+from githubrepostorag_amd.config import Settings
+from githubrepostorag_amd.index.store import VectorStore
+from githubrepostorag_amd.service.api import APIState, create_app
+from githubrepostorag_amd.service.cluster import ClusterRuntimeView, ReplicaHub, spawn_replicas
+from githubrepostorag_amd.service.events import EventLog
+
+FACTORY = ["--factory", "githubrepostorag_amd.service.cluster:demo_runtime", "--device", "cpu"]
+
+
+def _sse(client, job_id, timeout=60.0):
+    events = []
+    with client.stream("GET", f"/rag/jobs/{job_id}/events") as r:
+        for line in r.iter_lines():
+            if line.startswith("data:"):
+                msg = json.loads(line.split(":", 1)[1])
+                events.append((msg["event"], msg["data"]))
+                if msg["event"] == "final":
+                    break
+    return events
+
+
+@pytest.fixture()
+def cluster():
+    def make(n=2, delay=0.0, slots=2):
+        events = EventLog()
+        hub = ReplicaHub(events, job_timeout=60.0)
+        env = {"GRAG_DEMO_LLM_DELAY": str(delay), "GRAG_DEMO_SLOTS": str(slots), "CUDA_VISIBLE_DEVICES": "",
+               "HIP_VISIBLE_DEVICES": "", "OMP_NUM_THREADS": "1"}
+        procs = spawn_replicas(n, hub.address, hub.authkey, FACTORY, env=env)
+        s = Settings(index_dir=None, data_dir=None)
+        state = APIState(runtime=ClusterRuntimeView(hub, s), queue=hub.queue, events=events, flags=hub.flags,
+                         ping_seconds=0.5)
+        client = TestClient(create_app(state))
+        client.__enter__()
+        t0 = time.time()
+        while hub.live_count() < n:
+            assert time.time() - t0 < 120, "replicas did not connect"
+            assert all(p.poll() is None for p in procs), "a replica exited during startup"
+            time.sleep(0.1)
+        made.append((hub, procs, client))
+        return hub, procs, client
+
+    made = []
+    yield make
+    for hub, procs, client in made:
+        client.__exit__(None, None, None)
+        hub.close()
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except Exception:
+                p.kill()
+
+
+def test_front_door_dispatches_over_replicas(cluster):
+    hub, procs, client = cluster(n=2, delay=0.05, slots=2)
+    ids = [client.post("/rag/jobs", json={"query": f"where are widgets {i}"}).json()["job_id"] for i in range(6)]
+    pids = set()
+    for jid in ids:
+        ev = _sse(client, jid)
+        names = [e for e, _ in ev]
+        assert names[0] == "started" and names[-1] == "final", names
+        final = ev[-1][1]
+        assert "Widgets are handled" in final["answer"]
+        pids.add(final["answer"].split("pid ")[1].rstrip(")."))
+    assert len(pids) == 2, "both replicas must have served jobs"
+    assert sum(hub.queue.results[j]["result"]["replica"] in (0, 1) for j in ids) == 6
+    r = client.get("/health")
+    assert r.status_code == 200 and r.json()["status"] == "UP", r.json()
+    assert len(r.json()["components"]["vector_index"]["details"]["replicas"]) == 2
+
+
+def test_front_door_cancel_reaches_replica(cluster):
+    hub, procs, client = cluster(n=2, delay=0.4, slots=1)
+    jid = client.post("/rag/jobs", json={"query": "slow question"}).json()["job_id"]
+    time.sleep(0.3)
+    assert client.post(f"/rag/jobs/{jid}/cancel").json()["status"] == "cancelling"
+    ev = _sse(client, jid)
+    assert ev[-1][0] == "final"
+    assert ev[-1][1].get("cancelled") or ev[-1][1].get("answer") == ""
+
+
+def test_replica_loss_fails_inflight_jobs(cluster):
+    hub, procs, client = cluster(n=2, delay=1.0, slots=4)
+    ids = [client.post("/rag/jobs", json={"query": f"q{i}"}).json()["job_id"] for i in range(4)]
+    time.sleep(0.6)
+    victim = next(r for r in hub.live_replicas() if r.inflight > 0)
+    procs[victim.rank].kill()
+    outcomes = [_sse(client, j)[-1][1] for j in ids]
+    assert any(o.get("error") for o in outcomes), "jobs of the dead replica must fail"
+    assert any("Widgets" in (o.get("answer") or "") for o in outcomes), "the live replica keeps serving"
+    assert hub.live_count() == 1
+    # new work goes to the survivor
+    jid = client.post("/rag/jobs", json={"query": "after"}).json()["job_id"]
+    assert "Widgets" in _sse(client, jid)[-1][1]["answer"]
+
+
+def test_store_write_mirroring():
+    a, b = VectorStore(8, "cpu"), VectorStore(8, "cpu")
+    sent = []
+    a.add_listener(lambda scope, payload: sent.append((scope, payload)))
+    b.add_listener(lambda scope, payload: pytest.fail("a mirrored write must not be re-broadcast"))
+    v = torch.randn(2, 8)
+    a.table("chunk").upsert(["x", "y"], ["tx", "ty"], v, [{"repo": "r"}, {"repo": "r"}])
+    a.table("chunk").delete(["y"])
+    assert [s for s, _ in sent] == ["chunk", "chunk"]
+    for scope, payload in sent:
+        b.apply_remote(scope, payload)
+    assert b.table("chunk").count() == 1
+    hit = b.table("chunk").search(v[:1], 1)[0][0]
+    assert hit.row_id == "x" and hit.text == "tx"
+
+
+def test_remote_llm_mode_uses_http_client():
+    """QWEN_ENDPOINT=http://... selects the OpenAI-compatible client (reference worker -> vLLM split,
+    rag_worker/src/worker/services/qwen_llm.py:104-148) with LLM_TIMEOUT as its request timeout."""
+    import threading
+    from http.server import BaseHTTPRequestHandler, HTTPServer
+
+    from githubrepostorag_amd.agent.llm import HTTPLLM
+    from githubrepostorag_amd.embed.service import Embedder
+    from githubrepostorag_amd.service.runtime import RAGRuntime
+
+    seen = []
+
+    class H(BaseHTTPRequestHandler):
+        def do_POST(self):
+            body = json.loads(self.rfile.read(int(self.headers["Content-Length"])))
+            seen.append((self.path, body))
+            out = json.dumps({"choices": [{"message": {"role": "assistant", "content": "remote says hi"}}]}).encode()
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(out)))
+            self.end_headers()
+            self.wfile.write(out)
+
+        def log_message(self, *a):
+            pass
+
+    srv = HTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        url = f"http://127.0.0.1:{srv.server_address[1]}"
+        s = Settings(index_dir=None, data_dir=None, qwen_endpoint=url, llm_timeout_s=7.0)
+        emb = Embedder.from_name("encoder-tiny", device="cpu", seed=3)
+        rt = RAGRuntime(s, device="cpu", embedder=emb)
+        assert rt.engine is None and isinstance(rt.llm._base, HTTPLLM) and rt.llm._base.timeout_s == 7.0
+        assert rt.llm.complete("hello there").text == "remote says hi"
+        assert isinstance(rt.ingest_llm, HTTPLLM) and rt.ingest_llm.mode == "ingest"
+        assert seen[0][0] == "/v1/chat/completions" and seen[0][1]["messages"][-1]["content"] == "hello there"
+    finally:
+        srv.shutdown()
