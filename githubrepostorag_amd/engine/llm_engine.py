@@ -388,8 +388,9 @@ class LLMEngine:
     def _run_decode(self, seqs, max_window: int | None = None) -> list[Sequence]:
         t0 = time.perf_counter()
         n = len(seqs)
-        use_graph = (self.on_gpu and self.cfg.use_cuda_graph and self.model.tp.trivial
-                     and n <= max(self.cfg.graph_batch_sizes))
+        # under TP the graphs hold the decode's collectives (one-shot IPC all-reduce, RCCL logits gather);
+        # replicated scheduling makes every TP rank pick, capture and replay the same graph in lockstep
+        use_graph = self.on_gpu and self.cfg.use_cuda_graph and n <= max(self.cfg.graph_batch_sizes)
         K = self._window(seqs, max_window) if use_graph else 1
         max_ctx = max(s.total_len for s in seqs) + K - 1
         if use_graph:
@@ -492,7 +493,7 @@ class LLMEngine:
         sampler's current launch chain: call it once requests with the
         serving sampling parameters have been admitted.  Returns the number
         of graphs captured."""
-        if not (self.on_gpu and self.cfg.use_cuda_graph and self.model.tp.trivial):
+        if not (self.on_gpu and self.cfg.use_cuda_graph):
             return 0
         n = 0
         for B in batch_sizes or self.cfg.graph_batch_sizes:

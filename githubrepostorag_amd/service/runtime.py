@@ -113,9 +113,12 @@ class RAGRuntime:
         given context lengths), as vLLM does, so no capture stalls a live
         request.  The engine thread must be idle (call before serving)."""
         eng = self.engine
-        if eng is None or not eng.on_gpu or (self.tp_group is not None and not self.tp_group.trivial):
-            return 0  # TP: the engine threads already step in lockstep; graphs capture on first use
+        if eng is None or not eng.on_gpu:
+            return 0
         from ..engine.sequence import SamplingParams
+
+        if self.tp_group is not None and not self.tp_group.trivial:
+            return self._warmup_tp()
 
         # admit one request with the worker's sampling knobs first: graphs are keyed on the sampler chain
         eng.generate([[1, 2, 3, 4]], SamplingParams(max_tokens=2, temperature=0.4, top_p=0.8,
@@ -126,6 +129,23 @@ class RAGRuntime:
             if ctx <= eng.cfg.max_model_len:
                 n += eng.warmup_graphs(buckets, ctx, windows)
         return n
+
+    def _warmup_tp(self) -> int:
+        """TP: every rank's engine thread already steps in lockstep (the followers mirror the leader), so
+        the leader warms the decode graphs by serving one batch per graph bucket through the runner —
+        each bucket's graph (with its all-reduces) is captured by all TP ranks in the same step."""
+        if not self.runner.leader:
+            return 0
+        from ..engine.sequence import SamplingParams
+
+        eng = self.engine
+        before = eng.stats["graph_captures"]
+        sp = SamplingParams(max_tokens=3, temperature=0.4, top_p=0.8, repetition_penalty=1.2, ignore_eos=True)
+        for B in [b for b in eng.cfg.graph_batch_sizes if b <= max(1, eng.cfg.max_num_seqs)]:
+            hs = [self.runner.submit([1, 2, 3, 4 + i], sp) for i in range(B)]
+            for h in hs:
+                h.wait(self.settings.job_timeout_s)
+        return eng.stats["graph_captures"] - before
 
     def agent(self) -> GraphAgent:
         """A fresh agent per job (cheap: it only holds references)."""

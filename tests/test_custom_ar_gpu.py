@@ -112,3 +112,78 @@ def test_ipc_regions_two_processes():
     for p in procs:
         p.join(timeout=30)
     assert all(ok for _, ok, _ in res), res
+
+
+def _graph_ar_worker(rank, world, port, q):
+    """One TP 'rank' process: IPC communicator over gloo, a hipGraph holding [producer -> one-shot
+    all-reduce], replayed several times in step with the peer process and checked against the sum."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from githubrepostorag_amd.parallel.custom_ar import IpcAllReduce
+
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        ar = IpcAllReduce.create(dist.group.WORLD, rank, world, dev, slot_bytes=1 << 20, grid=32)
+        n = 3584 * 16
+        x = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        buf = torch.empty_like(x)
+        s = torch.cuda.Stream(device=dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            torch.mul(x, 2, out=buf)
+            ar.all_reduce(buf, stream=s)
+        torch.cuda.synchronize()
+        ok, msg = True, ""
+        for it in range(5):
+            xs = [(torch.randn(n, generator=torch.Generator().manual_seed(100 * it + r)) * (r + 1)).to(torch.bfloat16)
+                  for r in range(world)]
+            x.copy_(xs[rank])
+            ref = sum(2 * v.float() for v in xs)
+            torch.cuda.synchronize()
+            dist.barrier()
+            g.replay()
+            torch.cuda.synchronize()
+            if ar.failed():
+                ok, msg = False, f"replay {it}: timed out waiting for the peer"
+                break
+            if not torch.allclose(buf.float().cpu(), ref, atol=0.1 * world, rtol=1e-2):
+                ok, msg = False, f"replay {it}: wrong sum"
+                break
+            # an eager call between replays advances the same epoch counters
+            dist.barrier()
+            ar.all_reduce(x.clone())
+            torch.cuda.synchronize()
+            ok = ok and not ar.failed()
+        dist.barrier()
+        del g
+        ar.close()
+        dist.destroy_process_group()
+        q.put((rank, ok, msg))
+    except Exception as e:  # report, never hang the parent
+        q.put((rank, False, repr(e)))
+
+
+def test_oneshot_inside_hipgraph_two_processes():
+    """The TP decode graph holds the one-shot all-reduce (engine/llm_engine.py captures decode under TP):
+    two rank processes (separate hardware queues, as TP ranks on separate GPUs are) each replay their
+    captured graph repeatedly; epochs advance inside the replays and interleave with eager calls."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_graph_ar_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+    assert all(ok for _, ok, _ in res), res
