@@ -124,6 +124,40 @@ class EngineLLM:
         return SamplingParams(max_tokens=int(mt), stop=list(kw.get("stop") or self.stop),
                               ignore_eos=bool(kw.get("ignore_eos", False)), **d)
 
+    def _post(self, prompt: str, out: str) -> str:
+        if self.mode == "ingest":
+            return sanitize(out) or "No response generated"
+        if is_selector_prompt(prompt):
+            return clean_selector_response(out)
+        return out
+
+    def complete_many(self, prompt_list: list[str], **kw) -> list[CompletionResponse]:
+        """A wave of independent completions (ingest extractors, roll-ups): tokenised here, in the
+        caller's thread, and submitted to the engine together — no thread per call, no tokenising on
+        the engine thread — then awaited; failed items are retried as one smaller wave."""
+        sp = self.params(**kw)
+        ids = [self.tok.encode(self.tok.apply_chat_template(self._messages(p), True,
+                                                             None if self.allow_thinking else False))
+               for p in prompt_list]
+        out: list[CompletionResponse | None] = [None] * len(prompt_list)
+        todo = list(range(len(prompt_list)))
+        for attempt in range(self.retries + 1):
+            hs = [(i, self.runner.submit(ids[i], sp)) for i in todo]
+            failed = []
+            for i, h in hs:
+                try:
+                    c = h.wait(self.timeout_s)
+                    out[i] = CompletionResponse(self._post(prompt_list[i], c.text), False, c.ttft_s, len(c.token_ids))
+                except Exception as e:
+                    log.warning("LLM call failed (attempt %d): %s", attempt + 1, e)
+                    h.cancel()
+                    out[i] = CompletionResponse(f"Error: {e}", True)
+                    failed.append(i)
+            todo = failed
+            if not todo:
+                break
+        return out
+
     def complete(self, prompt: str, on_token: Callable[[str], None] | None = None, **kw) -> CompletionResponse:
         text = self.tok.apply_chat_template(self._messages(prompt), True,
                                             None if self.allow_thinking else False)
@@ -147,12 +181,7 @@ class EngineLLM:
                                 raise Cancelled()
                             raise TimeoutError("generation timed out")
                     c = h.wait(0)
-                out = c.text
-                if self.mode == "ingest":
-                    out = sanitize(out) or "No response generated"
-                elif is_selector_prompt(prompt):
-                    out = clean_selector_response(out)
-                return CompletionResponse(out, False, c.ttft_s, len(c.token_ids))
+                return CompletionResponse(self._post(prompt, c.text), False, c.ttft_s, len(c.token_ids))
             except Exception as e:  # bounded retry, then the reference's "errors become content"
                 if type(e).__name__ == "Cancelled":
                     raise

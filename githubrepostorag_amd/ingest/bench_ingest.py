@@ -52,7 +52,11 @@ def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs:
         if dev.type == "cuda":
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        return res["documents"], dt, res["stage_seconds"]
+        st = dict(res["stage_seconds"])
+        st["engine"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()
+                        if isinstance(v, (int, float))}
+        st["llm_calls"] = ctl.extractors.wave.calls + ctl.hier.wave.calls + ctl.hier.extract.wave.calls
+        return res["documents"], dt, st
     finally:
         runner.shutdown()
         del eng

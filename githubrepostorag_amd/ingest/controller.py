@@ -55,14 +55,17 @@ class stage_timer:
         return self
 
     def __exit__(self, exc_type, exc, tb):
-        dt = time.perf_counter() - self.t0
+        self.record(time.perf_counter() - self.t0)
+        return False
+
+    def record(self, dt: float) -> None:
+        """Report a stage duration measured elsewhere (a stage that overlaps another)."""
         if not math.isfinite(dt):
-            return False
+            return
         self.timings[self.level] = dt
         M.INGEST_STAGE_SECONDS.labels(level=self.level, **self.labels).set(dt)
         _push("ingest_stage_run_seconds", "Duration (seconds) of a single ingest stage for a single run",
               {"level": self.level, **self.labels}, dt, self.push_addr)
-        return False
 
 
 def _push(name: str, help_text: str, labels: dict, value: float, addr: str | None) -> None:
@@ -195,11 +198,14 @@ class IngestController:
                 return split_nodes, cat
 
             f_code = pool.submit(code_branch)
-            with timer("file_summaries"):
-                file_nodes = self.hier.file_summary_nodes(split_nodes, repo, namespace, branch, kind)
-            f_file_ext = pool.submit(self.hier.extract.run, file_nodes)
+            # file -> module roll-ups pipelined per module (a module's summary starts when its own files
+            # are summarised); stage marks record when the last file / module summary finished
+            marks: dict = {}
             with timer("module_summaries"):
-                module_nodes = self.hier.module_summary_nodes(file_nodes, repo, namespace, branch, kind)
+                file_nodes, module_nodes = self.hier.file_module_pipeline(split_nodes, repo, namespace, branch, kind,
+                                                                          marks=marks)
+            timer("file_summaries").record(marks.get("file_summaries", 0.0))
+            f_file_ext = pool.submit(self.hier.extract.run, file_nodes)
             f_mod_ext = pool.submit(self.hier.extract.run, module_nodes)
             with timer("repo_summaries"):
                 repo_nodes = self.hier.extract.run(

@@ -36,6 +36,13 @@ class LLMWave:
         if not prompt_list:
             return []
         self.calls += len(prompt_list)
+        many = getattr(self.llm, "complete_many", None)
+        if many is not None:  # engine client: one submission of the whole wave
+            try:
+                return [r.text.strip() for r in many(prompt_list, **kw)]
+            except Exception as e:  # extractor failures never abort ingest
+                log.warning("extractor wave failed: %s", e)
+                return [f"Error: {e}"] * len(prompt_list)
 
         def one(p):
             try:

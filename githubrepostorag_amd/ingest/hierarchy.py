@@ -3,7 +3,8 @@ document (ingest/src/app/services/hierarchy_summary_service.py:13-202,
 catalog/catalog_builder.py:8-194, services/catalog_service.py:12-39).
 
 Each level is one batched LLM wave (every file summary of a repo at once,
-then every module summary), then the "catalog pipeline"
+then every module summary; the ingest controller pipelines the two per module,
+``file_module_pipeline``), then the "catalog pipeline"
 (SentenceSplitter(1500,100) + Summary + Title(3) + Keyword extractors,
 pipelines/catalog_pipeline.py:10-23) runs over the produced documents.
 Truncation semantics match the reference: 25 000 chars per roll-up input,
@@ -13,6 +14,9 @@ quality check on the first 1 000 chars, <= 10 code summaries for the catalog.
 from __future__ import annotations
 
 import logging
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
 
 from ..agent import prompts
 from .extractors import ExtractorPipeline, LLMWave
@@ -34,7 +38,8 @@ class HierarchyBuilder:
         self.splitter = SentenceSplitter(1500, 100)
 
     def _catalog_pipeline(self, docs: list[Document]) -> list[Node]:
-        return self.extract.run(self.splitter.get_nodes_from_documents(docs))
+        # the catalog sits on the ingest critical path: its extractor pass jumps the bulk chunk waves
+        return self.extract.run(self.splitter.get_nodes_from_documents(docs), priority=ROLLUP_PRIORITY)
 
     def file_nodes(self, code_nodes: list[Node], repo: str, namespace: str, branch: str, kind: str) -> list[Node]:
         return self.extract.run(self.file_summary_nodes(code_nodes, repo, namespace, branch, kind))
@@ -84,6 +89,57 @@ class HierarchyBuilder:
                 for (m, fs), t in zip(mods, texts)]
         return self.splitter.get_nodes_from_documents(docs)
 
+    def file_module_pipeline(self, code_nodes: list[Node], repo: str, namespace: str, branch: str, kind: str,
+                             depth: int = 1, max_files: int = 40, marks: dict | None = None
+                             ) -> tuple[list[Node], list[Node]]:
+        """file_summary_nodes then module_summary_nodes, pipelined per module: a module's summary is
+        submitted as soon as ITS files' summaries are back, not after the slowest file of the repo, so
+        the file -> module -> repo chain costs about one file wave + one module wave on its slowest
+        module instead of two full waves (same prompts, same outputs as the two level functions).
+        ``marks`` receives the wall times when the last file / module summary finished."""
+        files = [(fp, ns) for fp, ns in group_nodes_by_file(code_nodes).items() if fp]
+        by_mod = group_files_by_module([fp for fp, _ in files], depth)
+        nodes_of = dict(files)
+        t0 = time.perf_counter()
+        done_files = [0.0]
+        lock = threading.Lock()
+
+        def one_module(item):
+            m, fps = item
+            concat = ["\n\n".join(n.get_content() for n in nodes_of[fp])[:25000] for fp in fps]
+            texts = self.wave.map([prompts.file_summary(fp) + "\n\n" + c for fp, c in zip(fps, concat)],
+                                  max_tokens=self.summary_tokens, priority=ROLLUP_PRIORITY)
+            with lock:
+                done_files[0] = max(done_files[0], time.perf_counter() - t0)
+            fdocs = [Document(t or f"{fp} summary unavailable.",
+                              {"namespace": namespace, "repo": repo, "branch": branch, "file_path": fp,
+                               "module": top_directory(fp, 1), "component_kind": kind, "doc_type": "file",
+                               "rollup_of": [n.id for n in nodes_of[fp]], "rollup_count": len(nodes_of[fp])})
+                     for fp, t in zip(fps, texts)]
+            fnodes = self.splitter.get_nodes_from_documents(fdocs)
+            if not m:  # root-level files have no module roll-up
+                return fnodes, []
+            first = {}
+            for n in fnodes:
+                first.setdefault(n.metadata.get("file_path"), n)
+            keep = [fp for fp in fps if fp in first][:max_files]
+            joined = "\n\n".join(first[fp].get_content() for fp in keep)[:25000]
+            t = self.wave.map([prompts.module_summary(m, repo) + "\n\n" + joined], max_tokens=self.summary_tokens,
+                              priority=ROLLUP_PRIORITY)[0]
+            mdoc = Document(t or f"{m} module summary unavailable.",
+                            {"namespace": namespace, "repo": repo, "branch": branch, "module": m,
+                             "component_kind": kind, "doc_type": "module",
+                             "rollup_of": [first[fp].id for fp in keep], "constituent_files": keep})
+            return fnodes, self.splitter.get_nodes_from_documents([mdoc])
+
+        items = list(by_mod.items())
+        with ThreadPoolExecutor(max_workers=max(1, min(64, len(items)))) as ex:
+            res = list(ex.map(one_module, items))
+        if marks is not None:
+            marks["file_summaries"] = done_files[0]
+            marks["module_summaries"] = time.perf_counter() - t0
+        return [n for f, _ in res for n in f], [n for _, mn in res for n in mn]
+
     def repo_summary_nodes(self, docs: list[Document], module_nodes: list[Node], repo: str, namespace: str,
                            branch: str, kind: str, readme_limit: int = 3, module_limit: int = 10) -> list[Node]:
         readmes = [d.text for d in docs if d.metadata.get("file_path", "").lower().endswith("readme.md")][:readme_limit]
@@ -105,7 +161,7 @@ class HierarchyBuilder:
                              or d.metadata.get("file_path", "").lower() == "readme")
         good = False
         if readme and len(readme.strip()) >= 50:
-            verdict = self.wave.map([prompts.readme_quality(readme)], max_tokens=8)[0]
+            verdict = self.wave.map([prompts.readme_quality(readme)], max_tokens=8, priority=ROLLUP_PRIORITY)[0]
             if verdict.startswith("Error"):
                 good = len(readme.strip()) > 200 and "todo" not in readme.lower()
             else:
@@ -123,7 +179,7 @@ class HierarchyBuilder:
                     exts.add(fp.rsplit(".", 1)[-1].lower())
             tech = ", ".join(sorted(exts)) or "unknown"
             text = self.wave.map([prompts.catalog_from_summaries(repo, tech, "\n\n---\n\n".join(sums[:10]))],
-                                 max_tokens=self.summary_tokens)[0]
+                                 max_tokens=self.summary_tokens, priority=ROLLUP_PRIORITY)[0]
         else:
             text = f"# PROJECT OVERVIEW\n{readme}" if readme else f"Component summary placeholder for {repo}."
         doc = Document(text, {"doc_type": "catalog", "repo": repo, "layer": layer or "unspecified",

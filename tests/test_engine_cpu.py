@@ -206,3 +206,22 @@ def test_mixed_prefill_decode_steps_identical(model, tok):
     a, n_mixed = run(True)
     b, n_sep = run(False)
     assert a == b and n_mixed > 0 and n_sep == 0
+
+
+def test_complete_many_wave_matches_single_calls(model, tok):
+    """EngineLLM.complete_many (ingest waves: tokenised in the caller, submitted together) returns the
+    same greedy completions as one complete() call per prompt."""
+    from githubrepostorag_amd.agent.llm import EngineLLM
+    from githubrepostorag_amd.engine.runner import EngineRunner
+
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_num_batched_tokens=64, use_cuda_graph=False))
+    runner = EngineRunner(eng)
+    try:
+        llm = EngineLLM(runner, tok, max_tokens=5, mode="worker", timeout_s=60.0)
+        ps = ["def retry(policy):", "explain the cache", "widgets", "billing module", "x = 1"]
+        many = llm.complete_many(ps, temperature=0.0, repetition_penalty=1.0)
+        single = [llm.complete(p, temperature=0.0, repetition_penalty=1.0) for p in ps]
+        assert [m.text for m in many] == [s.text for s in single]
+        assert all(not m.error for m in many)
+    finally:
+        runner.shutdown()
