@@ -77,6 +77,9 @@ def parse():
                          "(0 disables); secondary fields e2e_ttft_p50_ms / p90 / agent_jobs_per_s")
     ap.add_argument("--agent-concurrency", type=int, default=64)
     ap.add_argument("--agent-gen-len", type=int, default=32, help="token cap of every agent LLM call")
+    ap.add_argument("--quant", default="none", choices=["none", "w4"],
+                    help="w4: AWQ-format W4A16 decoder weights (group-128 scales + zero points, the reference's "
+                         "precision: helm/values.yaml:67) on the decode GEMMs; reported as its own config line")
     ap.add_argument("--out", default=None)
     return ap.parse_args()
 
@@ -132,6 +135,9 @@ def main():
     t_setup = time.perf_counter()
     dcfg = decoder_config(args.model)
     model = Qwen2Model(dcfg, device=dev, seed=1, tp=tp_group)
+    w4_bytes = model.quantize_w4() if args.quant == "w4" else 0
+    if w4_bytes:
+        log(f"W4A16 decode weights: {w4_bytes / 1e9:.2f} GB packed (+ bf16 copy of the same values for prefill)")
     tok = load_tokenizer(None, dcfg.vocab_size)
     emb = Embedder.from_name(args.encoder, device=dev, seed=2)
     log(f"models ready {time.perf_counter() - t_setup:.1f}s  decoder={model.param_bytes() / 1e9:.1f} GB")
@@ -391,7 +397,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if args.quant == "none" else "w4a16 (AWQ format, group 128) decode / bf16 prefill",
             "data": "synthetic (random-init weights, clustered synthetic vectors, generated chunk texts/questions)",
             "p50_ttft_ms": round(p50, 2),
             "ingest_docs_per_s": None if ingest_dps is None else round(ingest_dps, 3),
@@ -406,6 +412,8 @@ def main():
                 "gen_len": args.gen_len,
                 "top_k": args.top_k,
                 "parallelism": f"tp{tp}dp{dp_size}" if tp > 1 else f"dp{world}",
+                **({"quant": "w4a16 awq-format (round-to-nearest group-128 codes of the random-init weights)",
+                    "decode_weight_gb": round(w4_bytes / 1e9, 3)} if args.quant == "w4" else {}),
             },
             "engine": eng_stats,
             "engine_per_timed_step": timed_engine,

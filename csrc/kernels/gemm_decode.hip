@@ -65,7 +65,8 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
       "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
+      "s_mov_b32 m0, %0\n\t"
+      "s_nop 2"  // hipcc may hand the address VGPRs to the very next VALU: let the DMA read them first
       : "=&s"(keep)
       : "v"(src), "s"(lds_dst)
       : "memory");
@@ -97,8 +98,10 @@ __device__ __forceinline__ void wait_w(bf16x8_t (&w)[G]) {
                  : "memory");
 }
 
+// raw barrier that never drains the LDS-DMA in flight; the wave's own ds_reads of the slot the next issue
+// refills must be complete before it (hipcc may otherwise sink their lgkmcnt waits below the barrier)
 __device__ __forceinline__ void bar() {
-  asm volatile("" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }

@@ -38,7 +38,7 @@ from .configs import DecoderConfig
 
 
 class _Layer:
-    __slots__ = ("in_norm", "qkv_w", "qkv_b", "o_w", "post_norm", "gu_w", "down_w")
+    __slots__ = ("in_norm", "qkv_w", "qkv_b", "o_w", "post_norm", "gu_w", "down_w", "w4")
 
 
 class Qwen2Model:
@@ -67,6 +67,7 @@ class Qwen2Model:
         self.vocab0 = tr * self.vocab_shard
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         self.cos_sin = rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device)
+        self.w4_enabled = False
         if state_dict is not None:
             self._load(state_dict)
         else:
@@ -149,6 +150,46 @@ class Qwen2Model:
         head = self.embed if cfg.tie_word_embeddings or "lm_head.weight" not in sd else get("lm_head.weight")
         self.lm_head = self._pad_rows(head[self.vocab0:self.vocab0 + self.vocab_shard].contiguous())
 
+    # ------------------------------------------------------------------ W4A16 (AWQ precision)
+    def quantize_w4(self) -> int:
+        """4-bit weights (group-128 scales + zero points, AWQ's format) for the decode GEMMs
+        (csrc/kernels/gemm_w4.hip); the bf16 weights are replaced by the values the 4-bit codes
+        represent, so prefill (bf16 GEMMs) and decode compute with the same quantised model.
+        Returns the bytes of packed 4-bit weights + scales."""
+        from ..ops.w4 import W4Linear
+
+        total = 0
+        for L in self.layers:
+            w4 = {}
+            for name, silu in (("qkv_w", False), ("o_w", False), ("gu_w", self.gu_interleaved), ("down_w", False)):
+                w = getattr(L, name)
+                if w.shape[0] % 32 or w.shape[1] % 256:
+                    continue
+                q = W4Linear.quantize(w, silu=silu)
+                setattr(L, name, q.dequant(w.dtype).contiguous())
+                if w.is_cuda:  # the GPU kernel reads the packed copy; CPU keeps the codes for its reference
+                    q.release_codes()
+                w4[name] = q
+                total += q.bytes()
+            L.w4 = w4
+        self.w4_enabled = True
+        return total
+
+    def _proj(self, x: torch.Tensor, L, name: str, bias=None) -> torch.Tensor:
+        """A layer projection: the W4A16 decode GEMM at decode-sized batches when the model is
+        quantised, else the bf16 path (ops/linear.py)."""
+        w4 = getattr(L, "w4", None) if self.w4_enabled else None
+        q = w4.get(name) if w4 else None
+        if q is not None and x.is_cuda:
+            from ..ops import w4 as W4
+
+            if W4.plan(x.shape[0], q.N, q.K, q.silu) is not None and W4.capture_ok(x.device, x.shape[0], q):
+                return W4.gemm_w4(x, q, bias)
+        w = getattr(L, name)
+        if name == "gu_w":
+            return mlp_gate_up(x, w) if self.gu_interleaved else silu_mul(linear(x, w))
+        return linear(x, w, bias)
+
     def gate_up_weights(self, L) -> tuple[torch.Tensor, torch.Tensor]:
         """(gate [I, H], up [I, H]) of a layer in plain HF row order."""
         if self.gu_interleaved:
@@ -185,14 +226,14 @@ class Qwen2Model:
                 x = rmsnorm(h, L.in_norm, eps)
             else:
                 x = rmsnorm(h, L.in_norm, eps, residual=residual)
-            qkv = linear(x, L.qkv_w)
+            qkv = self._proj(x, L, "qkv_w")
             q = qkv_rope_kvstore(qkv, L.qkv_b, positions, self.cos_sin, meta.slot_mapping, kc, vc,
                                  self.hq, self.hkv, self.head_dim)
             a = paged_attention(q, kc, vc, meta, self.scale, causal=True)
-            h = self.tp.all_reduce(linear(a, L.o_w))
+            h = self.tp.all_reduce(self._proj(a, L, "o_w"))
             x = rmsnorm(h, L.post_norm, eps, residual=residual)
-            m = mlp_gate_up(x, L.gu_w) if self.gu_interleaved else silu_mul(linear(x, L.gu_w))
-            h = self.tp.all_reduce(linear(m, L.down_w))
+            m = self._proj(x, L, "gu_w")
+            h = self.tp.all_reduce(self._proj(m, L, "down_w"))
         return rmsnorm(h, self.norm, eps, residual=residual)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:

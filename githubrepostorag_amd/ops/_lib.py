@@ -58,6 +58,8 @@ _SIGS = {
     "grag_splitk_reduce": [P, P, P, I, I, I, I, I, I, P],
     "grag_gemm_decode": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_decode_has": [I, I, I],
+    "grag_gemm_w4": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P],
+    "grag_gemm_w4_has": [I, I],
 }
 
 
