@@ -1,17 +1,15 @@
 #!/bin/bash
-# rocprofv3 kernel-trace + stats of a short bench run -> gpurun_out/prof_<tag>
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-R=$(pwd)
-TAG=${TAG:-bench}
-mkdir -p gpurun_out/prof_$TAG
+# rocprofv3 kernel trace + stats over a short bench (no PMC counters: those go in their own passes,
+# scripts/pmc_gemm.sh).  Only the stats CSVs are copied to gpurun_out/ (the full trace is large).
+#   bash scripts/profile_bench.sh [bench args...]
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p "$R/gpurun_out"
 export TMPDIR=/tmp
 cd /tmp
-timeout -k 10 ${PROF_TIMEOUT:-900} rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py ${BENCH_ARGS:---steps 1 --warmup 1 --no-ingest} > $R/gpurun_out/prof_$TAG/bench_stdout.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_bench -o run -- \
+  python3 "$R/bench.py" --steps 2 --warmup 1 --no-ingest --agent-jobs 0 "$@" > "$R/gpurun_out/profile_bench.log" 2>&1
 rc=$?
-echo "rc=$rc"
-# the per-dispatch trace is large; keep only the summaries
-find $R/gpurun_out/prof_$TAG -name "*kernel_trace.csv" -delete
-tail -5 $R/gpurun_out/prof_$TAG/bench_stdout.log
-f=$(find $R/gpurun_out/prof_$TAG -name "*kernel_stats.csv" | head -1)
-[ -n "$f" ] && python3 $R/scripts/summarize_prof.py "$f" 40
+find /tmp/prof_bench -name "*kernel_stats.csv" -exec cp {} "$R/gpurun_out/" \;
+[ $rc -eq 0 ] && python3 "$R/scripts/summarize_prof.py" "$R/gpurun_out/run_kernel_stats.csv" "rocprofv3 kernel stats: bench.py --steps 2 --warmup 1 --no-ingest --agent-jobs 0 $*"
 exit $rc
