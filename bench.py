@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--quant", default="none", choices=["none", "w4"],
                     help="w4: AWQ-format W4A16 decoder weights (group-128 scales + zero points, the reference's "
                          "precision: helm/values.yaml:67) on the decode GEMMs; reported as its own config line")
+    ap.add_argument("--pysample", type=float, default=0.0,
+                    help="ms between stack samples of the engine thread over the timed steps (0: off; diagnostics)")
     ap.add_argument("--out", default=None)
     return ap.parse_args()
 
@@ -310,6 +312,10 @@ def main():
     for k in phase:  # phase breakdown over the timed steps only
         phase[k] = 0.0
     stats0 = dict(eng.stats)
+    sampler = None
+    if args.pysample:  # diagnostics: where the engine thread spends the timed steps
+        from githubrepostorag_amd.utils.pysample import StackSampler
+        sampler = StackSampler(interval=args.pysample / 1000.0, depth=4, all_threads=True).start()
     t_start = time.perf_counter()
     phase["admit"] = 0.0
     ttfts = []
@@ -317,6 +323,12 @@ def main():
         ttfts += run_step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    if sampler is not None:
+        sampler.stop()
+        for share, where in sampler.top(30):
+            log(f"pysample {share:7.4f}  {where}")
+        for share, where in sampler.top_other(40):
+            log(f"pysample-other {share:7.4f}  {where}")
     stats1 = dict(eng.stats)
     comm.barrier()
     elapsed = time.perf_counter() - t_start

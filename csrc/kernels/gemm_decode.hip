@@ -24,9 +24,16 @@
 //     slot every wave finished before that barrier).
 //   * The MFMA takes the W fragment as operand A, so each lane ends with 4
 //     consecutive output columns of one row (8-byte bf16 / 16-byte fp32 stores).
-//   * Work: (N / (32*NWV)) column tiles x ksplit K-ranges, XCD-remapped.  ksplit
-//     > 1 writes fp32 partial planes ws[split][M][N]; grag_splitk_reduce (in
-//     gemm_tile.hip) sums them and applies the epilogue.
+//   * Work: the N / (16*NTW) wave units (16*NTW W rows each) of every K-range
+//     are dealt to `gs` workgroups per K-range in contiguous, balanced runs
+//     (floor(g U / gs) .. floor((g+1) U / gs), at most NWV each), XCD-remapped.
+//     gs = U / NWV is the plain tiling; a smaller unit count per workgroup lets
+//     the grid match the 256 CUs when U / NWV does not (Qwen2-7B gate/up at
+//     M > 128: 1184 units = 148 full 8-wave tiles, 58 % of the CUs; dealt as 4-5
+//     units to each of 256 five-wave workgroups every CU streams its share).
+//     A wave without a unit repeats its neighbour's loads (L2 hits) and stores
+//     nothing.  ksplit > 1 writes fp32 partial planes ws[split][M][N];
+//     grag_splitk_reduce (in gemm_tile.hip) sums them and applies the epilogue.
 //   * Epilogues fused in the kernel: bias + act (none / gelu-erf / gelu-tanh),
 //     SiLU(gate)*up for the gate/up weight stored interleaved in 32-row blocks
 //     (ops/gemm.py interleave_gate_up): a wave's two n-tiles are then the 16
@@ -115,7 +122,9 @@ struct DArgs {
   void* C;
   int lda, ldw, ldc;
   int M, N, K;
-  int tiles_n, ksplit, kt_split;
+  int units, gs, ksplit, kt_split;  // wave units per K-range, workgroups per K-range
+  int msplit;                       // row blocks of 16*MT (adjacent on one XCD: the W lines are shared in L2)
+  int packed;                       // W in the unit-packed layout (grag_gemm_decode doc)
 };
 
 // NTW 16-row n-tiles per wave (32 or 64 W rows): the A fragment read from LDS feeds NTW MFMAs, so NTW = 4
@@ -125,10 +134,9 @@ __global__ __launch_bounds__(64 * NWV, (NWV == 4 && NTW == 2 && (D + 1) * MT * 2
 void gemm_dec_kernel(DArgs p) {
   constexpr int NST = D + 1;            // LDS stages = W register slots
   constexpr int ABYTES = MT * 16 * 128;  // one K-step of A
-  constexpr int GA = (MT * 2) / NWV;     // A pieces (1 KiB) per wave per K-step
-  constexpr int GW = 2 * NTW;            // W dwordx4 per lane per K-step
-  constexpr int BN = 16 * NTW * NWV;
-  static_assert((MT * 2) % NWV == 0, "A pieces must split evenly over the waves");
+  constexpr int NPC = MT * 2;                  // A pieces (1 KiB = 8 rows x 128 B) per K-step
+  constexpr int GA = (NPC + NWV - 1) / NWV;    // per wave (the last wave may repeat its final piece)
+  constexpr int GW = 2 * NTW;                  // W dwordx4 per lane per K-step
   static_assert(NTW == 2 || NTW == 4, "NTW");
   __shared__ __attribute__((aligned(16))) char smem[NST * ABYTES];
 
@@ -137,8 +145,13 @@ void gemm_dec_kernel(DArgs p) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = L & 15, h4 = L >> 4;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = b / p.ksplit, split = b % p.ksplit;
-  const int n0 = tile * BN;
+  const int split = b % p.ksplit;
+  const int mb = (b / p.ksplit) % p.msplit, g = b / (p.ksplit * p.msplit);
+  const int m0 = mb * 16 * MT;
+  const int u0 = (int)((long)g * p.units / p.gs);
+  const int cnt = (int)((long)(g + 1) * p.units / p.gs) - u0;
+  const bool active = w < cnt;                    // wave-uniform
+  const int q = u0 + min(w, cnt - 1);             // this wave's unit (an idle wave repeats the last one)
   const int ks = p.K >> 6;
   const int kb = split * p.kt_split;
   const int ke = min(ks, kb + p.kt_split);
@@ -147,30 +160,36 @@ void gemm_dec_kernel(DArgs p) {
   // W rows of this wave's n-tiles.  SiLU at NTW = 2: the 16 gate rows of a 16-wide output group and the
   // matching up rows (+32); at NTW = 4 the wave owns one whole 64-row gate/up block (tiles 0,1 gate, 2,3 up).
   int wr[NTW];
-  if constexpr (EPI == EPI_SILU && NTW == 2) {
-    const int q = (n0 >> 5) + w;
+  // gate/up units: the SiLU epilogue, or fp32 partials of a weight packed in gate/up units (packed == 2)
+  if (NTW == 2 && (EPI == EPI_SILU || p.packed == 2)) {
     wr[0] = (q >> 1) * 64 + (q & 1) * 16;
     wr[1] = wr[0] + 32;
   } else {
 #pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) wr[nt] = n0 + 16 * NTW * w + 16 * nt;
+    for (int nt = 0; nt < NTW; ++nt) wr[nt] = 16 * NTW * q + 16 * nt;
   }
+  // natural layout: row stride ldw, K-step stride 64 elements; unit-packed: the unit's 16*NTW rows x 64 k
+  // of one K-step are one contiguous block (row stride 64), the unit's K-steps follow each other, so a
+  // wave streams one contiguous region (DRAM pages are read whole, not 128 B per row per K-step)
+  const int kstride = p.packed ? 16 * NTW * 64 : 64;
   const bf16* wp[NTW];
 #pragma unroll
   for (int nt = 0; nt < NTW; ++nt)
-    wp[nt] = p.W + (size_t)min(wr[nt] + li, p.N - 1) * p.ldw + (size_t)kb * 64 + 8 * h4;
+    wp[nt] = p.packed ? p.W + (size_t)q * ks * kstride + (size_t)kb * kstride + (16 * nt + li) * 64 + 8 * h4
+                      : p.W + (size_t)min(wr[nt] + li, p.N - 1) * p.ldw + (size_t)kb * 64 + 8 * h4;
 
   // A pieces: piece q = w*GA + i covers rows [8q, 8q+8); lane -> row 8q + L/8, physical chunk L%8
-  const bf16* ap[GA];
+  // 32-bit element offsets (not 64-bit pointers): the MT = 16, 5-wave variant needs the registers
+  uint32_t ao[GA];
   uint32_t adst[GA];
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
-    const int q = w * GA + i;
-    const int row = q * 8 + (L >> 3);
+    const int pc = min(w * GA + i, NPC - 1);
+    const int row = pc * 8 + (L >> 3);
     const int c = (L & 7) ^ ((row >> 1) & 7);
-    ap[i] = p.A + (size_t)min(row, p.M - 1) * p.lda + (size_t)kb * 64 + c * 8;
-    adst[i] = __builtin_amdgcn_readfirstlane(lds0 + q * 1024);
+    ao[i] = (uint32_t)min(m0 + row, p.M - 1) * p.lda + kb * 64 + c * 8;
+    adst[i] = __builtin_amdgcn_readfirstlane(lds0 + pc * 1024);
   }
 
   bf16x8_t wf[NST][GW];  // [slot][2 nt + s]
@@ -188,26 +207,42 @@ void gemm_dec_kernel(DArgs p) {
     const bool live = step < nsteps;
     const int so = live ? step * 64 : 0;
 #pragma unroll
-    for (int i = 0; i < GA; ++i) glds16(ap[i] + so, adst[i] + slot * ABYTES);
+    for (int i = 0; i < GA; ++i) glds16(p.A + (ao[i] + so), adst[i] + slot * ABYTES);
 #pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) ldw2(wreg[2 * nt], wreg[2 * nt + 1], live ? wp[nt] + so : p.W);
+    for (int nt = 0; nt < NTW; ++nt) ldw2(wreg[2 * nt], wreg[2 * nt + 1], live ? wp[nt] + step * kstride : p.W);
   };
 
   // A fragment of rows 16 mt + li, logical chunk 4 s + h4 (swizzle depends on li only)
   const int sw = (li >> 1) & 7;
   const int aoff0 = li * 128 + ((h4 ^ sw) << 4);
   const int aoff1 = li * 128 + (((4 + h4) ^ sw) << 4);
+  // A fragments are read APF row tiles ahead of their MFMAs into a small register ring, with a scheduling
+  // fence between each read group and the MFMA group before it: left alone, hipcc (short of registers at two
+  // waves per SIMD) reads one fragment, waits lgkmcnt(0) and issues two MFMAs, exposing the LDS latency
+  // before every MFMA pair (measured: the MFMA pipe idle about half the time at M = 192).
+  constexpr int APF = MT >= 8 ? 2 : 1;
   auto compute = [&](int slot, bf16x8_t (&wreg)[GW]) {
     const char* As = smem + slot * ABYTES;
+    bf16x8_t af[APF + 1][2];
+#pragma unroll
+    for (int j = 0; j < APF; ++j) {
+      af[j][0] = *reinterpret_cast<const bf16x8_t*>(As + j * 2048 + aoff0);
+      af[j][1] = *reinterpret_cast<const bf16x8_t*>(As + j * 2048 + aoff1);
+    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const bf16x8_t a0 = *reinterpret_cast<const bf16x8_t*>(As + mt * 2048 + aoff0);
-      const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(As + mt * 2048 + aoff1);
+      if (mt + APF < MT) {
+        af[(mt + APF) % (APF + 1)][0] = *reinterpret_cast<const bf16x8_t*>(As + (mt + APF) * 2048 + aoff0);
+        af[(mt + APF) % (APF + 1)][1] = *reinterpret_cast<const bf16x8_t*>(As + (mt + APF) * 2048 + aoff1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8_t a0 = af[mt % (APF + 1)][0], a1 = af[mt % (APF + 1)][1];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[2 * nt], a0, acc[mt][nt], 0, 0, 0);
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[2 * nt + 1], a1, acc[mt][nt], 0, 0, 0);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -230,6 +265,7 @@ void gemm_dec_kernel(DArgs p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-reads land before the workgroup retires
 
   // ---- epilogue: acc[mt][nt][r] = D[W row (wr[nt] + 4 h4 + r)][A row (16 mt + li)]
+  if (!active) return;
   if constexpr (EPI == EPI_SILU) {
     bf16* C = (bf16*)p.C;
     constexpr int NP = NTW / 2;  // gate/up tile pairs: (nt, nt + NP)
@@ -246,7 +282,7 @@ void gemm_dec_kernel(DArgs p) {
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int m = mt * 16 + li;
+        const int m = m0 + mt * 16 + li;
         if (m >= p.M) continue;
         bf16x4_t o;
 #pragma unroll
@@ -264,7 +300,7 @@ void gemm_dec_kernel(DArgs p) {
       for (int r = 0; r < 4; ++r) bv[r] = (EPI == EPI_STORE && p.bias) ? (float)p.bias[n + r] : 0.f;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int m = mt * 16 + li;
+        const int m = m0 + mt * 16 + li;
         if (m >= p.M) continue;
         if constexpr (EPI == EPI_PARTIAL) {
           float* ws = (float*)p.C + ((size_t)split * p.M + m) * p.N + n;
@@ -295,25 +331,43 @@ int launch_v(const DArgs& a, int epi, int act, int nwg, hipStream_t s) {
 }  // namespace
 
 // Variants compiled (mt = 16-row tiles of M, nwv = waves per workgroup, ntw = 16-row W tiles per wave;
-// depth kDepth): (nwv 4, ntw 2): mt 4, 8, 16;  (nwv 8, ntw 2): mt 12.  ntw = 4 measured no faster than 2 at
-// M = 192 (profiles/gemm_decode_ab_v3.jsonl) and is not instantiated.
+// depth kDepth): (nwv 4, ntw 2): mt 4, 8, 16;  (nwv 5, ntw 2): mt 4, 8, 12 (balanced grids; mt 16 needs
+// more than the 256 registers a wave gets at two waves per SIMD);  (nwv 8, ntw 2): mt 12.  ntw = 4 measured no faster than 2 at M = 192 (profiles/gemm_decode_ab_v3.jsonl) and is
+// not instantiated.
 GRAG_API int grag_gemm_decode_has(int mt, int nwv, int ntw) {
-  if (nwv == 4 && ntw == 2) return mt == 4 || mt == 8 || mt == 16;
-  if (nwv == 8 && ntw == 2) return mt == 12;
+  if (ntw != 2) return 0;
+  if (nwv == 4) return mt == 4 || mt == 8 || mt == 16;
+  if (nwv == 5) return mt == 4 || mt == 8 || mt == 12;
+  if (nwv == 8) return mt == 12;
   return 0;
 }
 
 // y = epilogue(x @ w^T) for M <= 16 * mt rows.  epi 0 store (act 0/1/3), 1 silu*mul (w gate/up interleaved in
 // 32-row blocks, out [M, N/2]).  ksplit > 1: fp32 planes into ws (ksplit * M * N floats), then
-// grag_splitk_reduce applies the epilogue.  Requirements (checked): K % 256 == 0 (whole ring rounds per
-// split), N % (16 * ntw * nwv) == 0, lda/ldw % 8 == 0, ldc % 4 == 0, 16-B aligned A/W.
+// grag_splitk_reduce applies the epilogue.  gs = workgroups per K-range over the N / (16 ntw) wave units
+// (0: N / (16 ntw nwv), the plain tiling; otherwise ceil(units / gs) <= nwv).  M > 16 mt: the rows go to
+// ceil(M / (16 mt)) workgroups per unit run (at most 4).  packed = 1: W in the unit-packed layout
+// [N / (16 ntw)][K / 64][16 ntw][64] (ops/gemm.py dec_pack), ldw ignored; packed = 2: the same for an
+// interleaved gate/up weight packed in gate/up units (16 gate rows then their 16 up rows; ntw 2).
+// Requirements (checked):
+// K % 256 == 0 (whole ring rounds per split), N % (16 * ntw) == 0 (silu: N % 64 == 0), lda/ldw % 8 == 0,
+// ldc % 4 == 0, 16-B aligned A/W.
 GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, void* C, int lda, int ldw, int ldc,
-                              int M, int N, int K, int epi, int act, int mt, int nwv, int ntw, int ksplit, void* ws,
-                              hipStream_t stream) {
+                              int M, int N, int K, int epi, int act, int mt, int nwv, int ntw, int ksplit, int gs,
+                              int packed, void* ws, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (!grag_gemm_decode_has(mt, nwv, ntw) || M > 16 * mt) return (int)hipErrorInvalidValue;
-  if (K % 64 != 0 || K < 64 || N % (16 * ntw * nwv) != 0 || lda % 8 != 0 || ldw % 8 != 0 || ldc % 4 != 0)
+  const int msplit = (M + 16 * mt - 1) / (16 * mt);
+  if (!grag_gemm_decode_has(mt, nwv, ntw) || msplit > 4) return (int)hipErrorInvalidValue;
+  if (K % 64 != 0 || K < 64 || N % (16 * ntw) != 0 || lda % 8 != 0 || ldw % 8 != 0 || ldc % 4 != 0)
     return (int)hipErrorInvalidValue;
+  if (epi == EPI_SILU && N % 64 != 0) return (int)hipErrorInvalidValue;
+  if (packed < 0 || packed > 2 || (packed == 2 && (ntw != 2 || N % 64 != 0))) return (int)hipErrorInvalidValue;
+  const int units = N / (16 * ntw);
+  if (gs <= 0) {
+    if (units % nwv != 0) return (int)hipErrorInvalidValue;
+    gs = units / nwv;
+  }
+  if (gs > units || (units + gs - 1) / gs > nwv) return (int)hipErrorInvalidValue;
   if (epi != EPI_STORE && epi != EPI_SILU) return (int)hipErrorInvalidValue;
   if (act != ACT_NONE && act != ACT_GELU && act != ACT_GELU_TANH) return (int)hipErrorInvalidValue;
   if (epi == EPI_SILU && act != ACT_NONE) return (int)hipErrorInvalidValue;
@@ -331,15 +385,21 @@ GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, vo
   a.C = ksplit > 1 ? ws : C;
   a.lda = lda; a.ldw = ldw; a.ldc = ldc;
   a.M = M; a.N = N; a.K = K;
-  a.tiles_n = N / (16 * ntw * nwv);
+  a.units = units;
+  a.gs = gs;
+  a.msplit = msplit;
+  a.packed = packed;
   a.ksplit = ksplit;
   a.kt_split = kts;
-  const int nwg = a.tiles_n * ksplit;
+  const int nwg = gs * ksplit * msplit;
   const int e = ksplit > 1 ? EPI_PARTIAL : epi;
   int err;
   if (nwv == 4) err = mt == 4 ? launch_v<4, kDepth, 4, 2>(a, e, act, nwg, stream)
                      : mt == 8 ? launch_v<8, kDepth, 4, 2>(a, e, act, nwg, stream)
                                : launch_v<16, kDepth, 4, 2>(a, e, act, nwg, stream);
+  else if (nwv == 5) err = mt == 4 ? launch_v<4, kDepth, 5, 2>(a, e, act, nwg, stream)
+                          : mt == 8 ? launch_v<8, kDepth, 5, 2>(a, e, act, nwg, stream)
+                                    : launch_v<12, kDepth, 5, 2>(a, e, act, nwg, stream);
   else err = launch_v<12, kDepth, 8, 2>(a, e, act, nwg, stream);
   if (err || ksplit == 1) return err;
   return grag_splitk_reduce(ws, bias, C, ldc, M, N, ksplit, epi, act, stream);

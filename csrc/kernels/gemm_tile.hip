@@ -510,6 +510,8 @@ GRAG_API int grag_splitk_reduce(const void* ws, const void* bias, void* C, int l
 //               workgroups share the last (tiles - dp) tiles, dp = (tiles / sk_grid - 1) * sk_grid
 //               (all tiles when tiles < sk_grid); ws >= 2 * sk_grid * 65536 floats, cnt >= tiles
 //               zero-initialised words (each reset by its tile's last arriver);
+//   ksplit == 1, sk_grid < 0: the same with dp = (tiles / |sk_grid|) * |sk_grid| (only the partial
+//               last round is streamed; shares down to a quarter tile);
 //   otherwise every tile is one workgroup.
 // Requirements (checked): K % 64 == 0, every split >= 2 K-tiles, lda/ldw % 8 == 0,
 // N % 8 == 0 (silu: N % 64 == 0), ldc % 8 == 0, 16-B aligned pointers.
@@ -546,13 +548,17 @@ GRAG_API int grag_gemm_tile(const void* A, const void* W, const void* bias, void
   if (tiles * ksplit >= (1L << 30)) return (int)hipErrorInvalidValue;
   a.dp_tiles = (int)(tiles * ksplit);
   a.sk_grid = 0;
-  if (ksplit == 1 && sk_grid > 0 && tiles % sk_grid != 0) {
+  // sk_grid > 0: the last full round and the remainder are streamed (shares >= half a tile);
+  // sk_grid < 0: every full round is data-parallel and only the remainder is streamed over |sk_grid|
+  // workgroups (shares >= a quarter tile: <= 5 parts per tile, the last arriver folds <= 4 slabs)
+  const int skg = sk_grid < 0 ? -sk_grid : sk_grid;
+  if (ksplit == 1 && skg > 0 && tiles % skg != 0) {
     if (ws == nullptr || cnt == nullptr) return (int)hipErrorInvalidValue;
-    const long rounds = tiles / sk_grid;
-    a.dp_tiles = rounds >= 1 ? (int)((rounds - 1) * sk_grid) : 0;
-    a.sk_grid = sk_grid;
-    // every stream-K share must cover >= half a tile (<= 3 parts per tile, bounded fixup reads)
-    if ((tiles - a.dp_tiles) * kt < (long)sk_grid * ((kt + 1) / 2)) return (int)hipErrorInvalidValue;
+    const long rounds = tiles / skg;
+    a.dp_tiles = sk_grid < 0 ? (int)(rounds * skg) : rounds >= 1 ? (int)((rounds - 1) * skg) : 0;
+    a.sk_grid = skg;
+    const long min_share = sk_grid < 0 ? (kt + 3) / 4 : (kt + 1) / 2;
+    if ((tiles - a.dp_tiles) * kt < (long)skg * min_share) return (int)hipErrorInvalidValue;
   }
   int err;
   if (ksplit > 1) {

@@ -19,6 +19,8 @@ discarded.
 """
 from __future__ import annotations
 
+import contextlib
+
 import logging
 import threading
 import time
@@ -107,16 +109,27 @@ class LLMEngine:
         self._static = None
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0, "steps": 0,
                       "graph_replays": 0, "graph_captures": 0, "decode_steps": 0, "decode_wait_s": 0.0,
-                      "step_s": 0.0, "mixed_steps": 0}
+                      "step_s": 0.0, "mixed_steps": 0,
+                      # host-side time by section (the GPU idles whenever one of these outlasts the queued work)
+                      "host_sched_s": 0.0, "host_prefill_prep_s": 0.0, "host_prefill_launch_s": 0.0,
+                      "host_prefill_sample_s": 0.0, "host_prefill_post_s": 0.0, "host_decode_prep_s": 0.0,
+                      "host_decode_post_s": 0.0}
         self._eos = set(getattr(tokenizer, "eos_token_ids", set()))
         self._lock = threading.RLock()
         max_split = -(-cfg.max_model_len // KV_TILE)
         self._max_b = max(cfg.graph_batch_sizes) if cfg.use_cuda_graph else cfg.max_num_seqs
         self._max_b = max(self._max_b, cfg.max_num_seqs)
+        self.stream = None
         if self.on_gpu:
             hq, d = model.hq, model.head_dim
             self._part_o = torch.empty(max_split * self._max_b * hq * d, dtype=torch.float32, device=self.device)
             self._part_ml = torch.empty(max_split * self._max_b * hq * 2, dtype=torch.float32, device=self.device)
+            # the engine's own (non-default) stream: retrieval / API threads issue their copies and syncs
+            # on other streams; with the engine on the legacy default stream their runtime calls stalled
+            # the engine thread (profiles/timeline_r2_*.txt).  Weights and the KV cache were written on
+            # the default stream: drain it once before the first engine launch.
+            torch.cuda.synchronize(self.device)
+            self.stream = torch.cuda.Stream(self.device)
 
     # ------------------------------------------------------------------ setup
     def _plan_blocks(self) -> int:
@@ -187,12 +200,17 @@ class LLMEngine:
         ``max_window`` caps the decode window (tokens per sequence this step)."""
         t0 = time.perf_counter()
         try:
-            return self._step(max_window)
+            with self._on_stream():
+                return self._step(max_window)
         finally:
             self.stats["step_s"] += time.perf_counter() - t0
 
+    def _on_stream(self):
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
     @torch.inference_mode()
     def _step(self, max_window: int | None = None) -> list[Sequence]:
+        th = time.perf_counter()
         finished = self.sched.reap_cancelled()
         for s in finished:
             self._notify(s, None, True)
@@ -204,6 +222,7 @@ class LLMEngine:
         for s in getattr(self.sched, "last_admitted", []):
             self.sampler.reset_slot(s.slot, s.params.temperature, s.params.top_p, s.params.top_k,
                                     s.params.repetition_penalty, s.all_ids, seed=s.params.seed)
+        self.stats["host_sched_s"] += time.perf_counter() - th
         if not items:
             return finished
         self.stats["steps"] += 1
@@ -249,6 +268,8 @@ class LLMEngine:
                                  np.asarray(q_start, dtype=np.int32), np.asarray(ctx, dtype=np.int32),
                                  self._block_table(seqs, width).reshape(-1)])
         dev = self._to_dev(packed)
+        th = time.perf_counter()
+        self.stats["host_prefill_prep_s"] += th - t0
         T, n = q_start[-1], len(seqs)
         o = 0
         d_ids = dev[o:o + T]; o += T
@@ -277,6 +298,8 @@ class LLMEngine:
             meta.num_seqs, meta.num_tokens = n_pref, Tp
             meta.max_q_len = max(b - a for _, a, b in items[:n_pref])
         hidden = self.model.forward(d_ids, d_pos, meta, self.kv_caches)
+        t1 = time.perf_counter()
+        self.stats["host_prefill_launch_s"] += t1 - th
         # sample for sequences whose prompt is now complete (first token) and for decode rows (next token)
         samp_rows, samp_seqs = [], []
         for i, (s, a, b) in enumerate(items):
@@ -295,9 +318,11 @@ class LLMEngine:
             toks = sample(logits, self.sampler, slot_t).tolist()
             tp.check_health()
             now = time.perf_counter()
+            self.stats["host_prefill_sample_s"] += now - t1
             for s, t in zip(samp_seqs, toks):
                 if self._append(s, int(t), now):
                     finished.append(s)
+            self.stats["host_prefill_post_s"] += time.perf_counter() - now
         self.stats["prefill_tokens"] += T - n_dec
         if n_dec:
             self.stats["decode_tokens"] += n_dec
@@ -406,6 +431,7 @@ class LLMEngine:
             self._static_dev[: packed.size].copy_(self._static_host[: packed.size], non_blocking=True)
             g.graph.replay()
             tw = time.perf_counter()
+            self.stats["host_decode_prep_s"] += tw - t0
             self.model.tp.stage_health()
             toks = g.out_tokens[:K, :n].cpu().numpy()
             self.model.tp.check_health()
@@ -440,6 +466,7 @@ class LLMEngine:
                 break
         self.stats["decode_steps"] += K
         self.stats["decode_s"] += now - t0
+        self.stats["host_decode_post_s"] += time.perf_counter() - now
         return finished
 
     def _ensure_static(self):
@@ -495,6 +522,10 @@ class LLMEngine:
         of graphs captured."""
         if not (self.on_gpu and self.cfg.use_cuda_graph):
             return 0
+        with self._on_stream():
+            return self._warmup_graphs(batch_sizes, max_ctx, windows)
+
+    def _warmup_graphs(self, batch_sizes, max_ctx, windows) -> int:
         n = 0
         for B in batch_sizes or self.cfg.graph_batch_sizes:
             split_len = _split_len_for(B)

@@ -56,7 +56,7 @@ _SIGS = {
     "grag_bitmap_update": [P, P, I, I, P],
     "grag_gemm_tile": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "grag_splitk_reduce": [P, P, P, I, I, I, I, I, I, P],
-    "grag_gemm_decode": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P],
+    "grag_gemm_decode": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_decode_has": [I, I, I],
     "grag_gemm_w4": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_w4_has": [I, I],

@@ -105,7 +105,7 @@ def plan(M: int, N: int, K: int) -> tuple[int, int]:
 
 
 def _ws_floats(M: int, N: int, ksplit: int, sk: int) -> int:
-    return ksplit * M * N if ksplit > 1 else (2 * sk * 65536 if sk else 0)
+    return ksplit * M * N if ksplit > 1 else (2 * abs(sk) * 65536 if sk else 0)
 
 
 class _Workspace:
@@ -208,7 +208,7 @@ def gemm_silu(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None = N
 DEC_DEPTH = 3  # K-steps in flight; a K-split covers whole rings of DEC_DEPTH + 1 steps
 _DEC_ON = os.environ.get("GRAG_DECODE_GEMM", "1") != "0"
 # (mt, nwv, ntw) compiled: mt 16-row tiles of M, nwv waves per workgroup, ntw 16-row W tiles per wave
-DEC_VARIANTS = [(4, 4, 2), (8, 4, 2), (12, 8, 2), (16, 4, 2)]
+DEC_VARIANTS = [(4, 4, 2), (4, 5, 2), (8, 4, 2), (8, 5, 2), (12, 5, 2), (12, 8, 2), (16, 4, 2)]
 DEC_MAX_M = int(os.environ.get("GRAG_DECODE_MAX_M", "128"))
 
 
@@ -254,24 +254,66 @@ def dec_ws_floats(M: int, N: int, ksplit: int) -> int:
     return ksplit * M * N if ksplit > 1 else 0
 
 
+def dec_unit_rows(N: int, silu: bool, ntw: int = 2) -> torch.Tensor:
+    """Weight rows of every decode-kernel wave unit, in unit order ([N] index): 16*ntw consecutive rows, or
+    for the interleaved gate/up weight (ntw 2) the 16 gate rows of a 16-column output group then its 16 up
+    rows (the kernel's silu unit q: rows 64 (q >> 1) + 16 (q & 1) + [0, 16) and the same + 32)."""
+    if not silu:
+        return torch.arange(N)
+    q = torch.arange(N // 32)
+    g0 = (q >> 1) * 64 + (q & 1) * 16
+    g = g0[:, None] + torch.arange(16)
+    return torch.cat([g, g + 32], 1).reshape(-1)
+
+
+def dec_pack(w: torch.Tensor, silu: bool = False, ntw: int = 2) -> torch.Tensor:
+    """[N, K] weight -> the decode kernel's unit-packed layout [N / (16 ntw), K / 64, 16 ntw, 64]: each wave
+    streams one contiguous region instead of 128 B per row per K-step."""
+    N, K = w.shape
+    r = 16 * ntw
+    idx = dec_unit_rows(N, silu, ntw).to(w.device)
+    return w[idx].view(N // r, r, K // 64, 64).permute(0, 2, 1, 3).contiguous()
+
+
+class DecPacked:
+    """A weight kept twice: natural [N, K] (prefill GEMMs) and unit-packed for the decode kernel."""
+
+    def __init__(self, w: torch.Tensor, silu: bool = False):
+        self.shape = w.shape
+        self.silu = silu
+        self.data = dec_pack(w, silu)
+
+
 def gemm_decode(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, act: int = ACT_NONE,
                 epi: int = EPI_STORE, plan: tuple[int, int, int, int] | None = None,
-                out: torch.Tensor | None = None) -> torch.Tensor:
+                out: torch.Tensor | None = None, packed: "DecPacked | None" = None) -> torch.Tensor:
     """Decode-regime GEMM: y = act(x @ w.T + b) (epi EPI_STORE) or the SwiGLU product of an interleaved
-    gate/up weight (epi EPI_SILU, out [M, N/2]).  ``plan`` = (mt, nwv, ntw, ksplit) overrides dec_plan."""
+    gate/up weight (epi EPI_SILU, out [M, N/2]).  ``plan`` = (mt, nwv, ntw, ksplit[, gs]) overrides dec_plan
+    (gs: workgroups per K-range over the N / (16 ntw) wave units; 0 = the plain N / (16 ntw nwv) tiling)."""
     M, K = x.shape
     N = w.shape[0]
     if not x.is_cuda:
         return gemm_silu(x, w, b) if epi == EPI_SILU else gemm(x, w, b, act)
-    mt, nwv, ntw, ks = plan or dec_plan(M, N, K, epi == EPI_SILU)
+    mt, nwv, ntw, ks, *rest = plan or dec_plan(M, N, K, epi == EPI_SILU)
+    gs = rest[0] if rest else 0
     ks = dec_ksplit(K, ks)
     if out is None:
         out = torch.empty(M, N // 2 if epi == EPI_SILU else N, dtype=x.dtype, device=x.device)
     fl = dec_ws_floats(M, N, ks)
     ws = WS.get(x.device, fl) if fl else None
-    call("grag_gemm_decode", ptr(x), ptr(w), ptr(b), ptr(out), x.stride(0), w.stride(0), out.stride(0),
-         M, N, K, epi, act, mt, nwv, ntw, ks, ptr(ws))
+    wsrc = w if packed is None else packed.data
+    call("grag_gemm_decode", ptr(x), ptr(wsrc), ptr(b), ptr(out), x.stride(0), w.stride(0), out.stride(0),
+         M, N, K, epi, act, mt, nwv, ntw, ks, gs, 0 if packed is None else 2 if packed.silu else 1, ptr(ws))
     return out
+
+
+def dec_balanced_gs(N: int, ntw: int, nwv: int, ksplit: int, ncu: int | None = None) -> int | None:
+    """Workgroups per K-range that put about one workgroup on every CU with at most ``nwv`` wave units each
+    (None when the units do not fill ``nwv``-wave groups even at one workgroup per CU)."""
+    units = N // (16 * ntw)
+    ncu = ncu or _num_cus()
+    gs = max(-(-units // nwv), ncu // max(1, ksplit))
+    return min(gs, units) if -(-units // min(gs, units)) <= nwv else None
 
 
 def dec_capture_ok(dev: torch.device, M: int, N: int, K: int, silu: bool = False) -> bool:

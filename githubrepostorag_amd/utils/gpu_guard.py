@@ -129,7 +129,7 @@ def _thread_stream(device: torch.device) -> torch.cuda.Stream:
 
 
 @contextlib.contextmanager
-def side_stream(device, wait_caller: bool = False):
+def side_stream(device, wait_caller: bool = False, join: str = "sync"):
     """Run a thread's latency-bound GPU work (query embedding, index search,
     graph traversal) on a per-thread, high-priority, non-blocking stream.
 
@@ -138,9 +138,16 @@ def side_stream(device, wait_caller: bool = False):
     ``.cpu()`` waits for it.  On a side stream the search's sync only waits
     for the search.  Re-entrant: nested blocks on the same thread stay on the
     same stream.  ``wait_caller``: the block consumes device tensors made on
-    the caller's stream, so the side stream first waits for that stream.  On
-    exit the caller's stream is made to wait for the side work (no host
-    sync), so results are safe to consume there."""
+    the caller's stream, so the side stream first waits for that stream.
+
+    ``join`` (on exit): "sync" (default) waits on the host for the side
+    stream alone (the wait releases the GIL), so results are complete for any
+    stream or thread; "event" makes the caller's stream wait for the side work
+    without a host sync.  "event" enqueues into the caller's stream, which for
+    a retrieval thread is the default stream the engine keeps full: measured
+    on ROCm, that enqueue blocked the retrieval thread ~12 ms per block with
+    the GIL held, and the engine thread (needing the GIL to launch) left the
+    GPU idle for the whole time (profiles/timeline_r2_*.txt)."""
     dev = torch.device(device)
     if dev.type != "cuda":
         yield None
@@ -156,4 +163,7 @@ def side_stream(device, wait_caller: bool = False):
         s.wait_stream(prev)
     with torch.cuda.stream(s):
         yield s
-    prev.wait_stream(s)
+    if join == "event":
+        prev.wait_stream(s)
+    else:
+        s.synchronize()

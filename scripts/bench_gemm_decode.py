@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--splits", default="1,2,3,4,5,7,9,14,18,28")
     ap.add_argument("--w4", action="store_true", help="add W4A16 (ops/w4.py) arms; their error is vs the 4-bit weight")
+    ap.add_argument("--packed", action="store_true", help="add unit-packed weight arms (pk_*)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -71,26 +72,39 @@ def main():
                 return ws[it["i"] % ncopy]
 
             arms = {"lib": lambda w=None: torch.nn.functional.linear(x, w if w is not None else nxt())}
+            pks = [G.DecPacked(w_, silu) for w_ in ws] if args.packed else []
             S, SK = G.plan(M, N, K)
             G.WS.reserve(dev, G._ws_floats(M, N, S, SK))
             arms["tile"] = (lambda w=None: G.gemm_silu(x, w if w is not None else nxt(), ksplit=S, sk=SK)) if silu \
                 else (lambda w=None: G.gemm(x, w if w is not None else nxt(), ksplit=S, sk=SK))
-            for mt, nwv, ntw in G.dec_variants(M):
-                if N % (16 * nwv * ntw):
-                    continue
-                tiles = N // (16 * nwv * ntw)
+            for mt, nwv, ntw in G.dec_variants(M) + [v for v in G.DEC_VARIANTS if v[1] == 5 and 16 * v[0] < M
+                                                     and -(-M // (16 * v[0])) <= 4]:
                 seen = set()
                 for req in map(int, args.splits.split(",")):
                     ks = G.dec_ksplit(K, req)
-                    if ks in seen or tiles * ks > 1200:
+                    if ks in seen or (silu and ks > 1):
                         continue
                     seen.add(ks)
-                    G.WS.reserve(dev, G.dec_ws_floats(M, N, ks))
-                    plan = (mt, nwv, ntw, ks)
-                    epi = G.EPI_SILU if silu else G.EPI_STORE
-                    arms[f"dec_mt{mt}_w{nwv}_n{ntw}_s{ks}"] = (
-                        lambda w=None, plan=plan, epi=epi: G.gemm_decode(x, w if w is not None else nxt(), epi=epi,
-                                                                         plan=plan))
+                    # plain tiling (nwv units per workgroup) and the balanced grid (about one workgroup per CU)
+                    gss = {0: N // (16 * nwv * ntw)} if N % (16 * nwv * ntw) == 0 else {}
+                    gb = G.dec_balanced_gs(N, ntw, nwv, ks)
+                    if gb is not None and gb not in gss.values():
+                        gss[gb] = gb
+                    for gs, ngroups in gss.items():
+                        if ngroups * ks * -(-M // (16 * mt)) > 1200:
+                            continue
+                        G.WS.reserve(dev, G.dec_ws_floats(M, N, ks))
+                        plan = (mt, nwv, ntw, ks, gs)
+                        epi = G.EPI_SILU if silu else G.EPI_STORE
+                        arms[f"dec_mt{mt}_w{nwv}_n{ntw}_s{ks}" + (f"_g{gs}" if gs else "")] = (
+                            lambda w=None, plan=plan, epi=epi: G.gemm_decode(x, w if w is not None else nxt(),
+                                                                             epi=epi, plan=plan))
+                        if args.packed:
+                            arms[f"pk_mt{mt}_w{nwv}_n{ntw}_s{ks}" + (f"_g{gs}" if gs else "")] = (
+                                lambda w=None, plan=plan, epi=epi: G.gemm_decode(
+                                    x, ws[0], epi=epi, plan=plan,
+                                    packed=pks[0] if w is not None else pks[it.__setitem__("i", it["i"] + 1)
+                                                                            or it["i"] % len(pks)]))
             if args.w4:
                 from githubrepostorag_amd.ops import w4 as W4
 

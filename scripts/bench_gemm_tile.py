@@ -27,10 +27,10 @@ Q7 = {"qkv": (4608, 3584), "o": (3584, 3584), "gate_up": (37888, 3584), "down": 
 ENC = {"qkv": (3072, 1024), "o": (1024, 1024), "ffn1": (4096, 1024), "ffn2": (1024, 4096)}
 
 
-def shapes(which):
+def shapes(which, prefill_ms=(4096, 16384)):
     out = []
     if which in ("prefill", "all"):
-        for M in (4096, 16384):
+        for M in prefill_ms:
             for name, (N, K) in Q7.items():
                 out.append((f"q7_{name}_M{M}", M, N, K, name == "gate_up"))
     if which in ("decode", "all"):
@@ -59,13 +59,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="all")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--prefill-ms", default="4096,16384")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     enable_tuned_gemms()
     torch.manual_seed(0)
     rows = []
-    for name, M, N, K, silu in shapes(args.shapes):
+    for name, M, N, K, silu in shapes(args.shapes, tuple(map(int, args.prefill_ms.split(",")))):
         wbytes = N * K * 2
         ncopy = max(1, min(8, (600 << 20) // wbytes + 1))
         ws = [(torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16) * 0.05 for _ in range(ncopy)]
@@ -88,6 +89,17 @@ def main():
             it["i"] += 1
             return G.gemm_silu(x, w, ksplit=S, sk=SK) if silu else G.gemm(x, w, ksplit=S, sk=SK)
 
+        def own_nosk_fn(w):
+            return G.gemm_silu(x, w, ksplit=1, sk=0) if silu else G.gemm(x, w, ksplit=1, sk=0)
+
+        def own_tail_fn(w):
+            return G.gemm_silu(x, w, ksplit=1, sk=-G._num_cus()) if silu else G.gemm(x, w, ksplit=1, sk=-G._num_cus())
+
+        def own_tail():  # full rounds data-parallel, only the partial last round streamed
+            w = ws[it["i"] % ncopy]
+            it["i"] += 1
+            return G.gemm_silu(x, w, ksplit=1, sk=-G._num_cus()) if silu else G.gemm(x, w, ksplit=1, sk=-G._num_cus())
+
         def own_nosk():
             w = ws[it["i"] % ncopy]
             it["i"] += 1
@@ -103,17 +115,29 @@ def main():
         for _ in range(3):
             lib_fn(); own_fn()
         torch.cuda.synchronize()
-        tl, to, tn = [], [], []
+        tiles = -(-M // 256) * -(-N // 256)
+        tail_ok = S == 1 and tiles % G._num_cus() != 0 and tiles > G._num_cus() and \
+            (tiles % G._num_cus()) * (K // 64) >= G._num_cus() * ((K // 64 + 3) // 4)
+        if tail_ok:
+            G.WS.reserve(dev, G._ws_floats(M, N, 1, G._num_cus()))
+        tail_err = None
+        if tail_ok:  # against the whole-tile schedule (deterministic reference of the same kernel)
+            y0, y1 = own_nosk_fn(ws[0]), own_tail_fn(ws[0])
+            tail_err = ((y1.float() - y0.float()).abs().max() / (y0.float().abs().max() + 1e-6)).item()
+        tl, to, tn, tt = [], [], [], []
         for _ in range(args.reps):
             tl += timeit(lib_fn, 1)
             to += timeit(own_fn, 1)
             if SK:
                 tn += timeit(own_nosk, 1)
+            if tail_ok:
+                tt += timeit(own_tail, 1)
         ml, mo = statistics.median(tl), statistics.median(to)
         flop = 2.0 * M * N * K
         byts = wbytes + M * K * 2 + M * N * 2
         row = {"shape": name, "M": M, "N": N, "K": K, "ksplit": S, "sk": SK, "silu_fused": silu,
                "own_nosk_us": round(statistics.median(tn), 1) if tn else None,
+               "own_tail_us": round(statistics.median(tt), 1) if tt else None, "tail_err": tail_err,
                "lib_us": round(ml, 1), "own_us": round(mo, 1), "speedup": round(ml / mo, 3),
                "own_tflops": round(flop / mo / 1e6, 1), "lib_tflops": round(flop / ml / 1e6, 1),
                "own_TBps": round(byts / mo / 1e6, 2), "lib_TBps": round(byts / ml / 1e6, 2), "relerr": err}

@@ -17,8 +17,11 @@ import os
 import sys
 from collections import defaultdict
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from summarize_prof import short  # noqa: E402
+
+
+def short(name: str, n: int = 90) -> str:
+    """Kernel name without the argument list, cut to n characters."""
+    return name.split("(")[0][:n]
 
 
 def load(out):

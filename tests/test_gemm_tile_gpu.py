@@ -107,7 +107,9 @@ def test_gemm_graph_replay(dev):
 
 
 @pytest.mark.parametrize("M,N,K,sk", [(512, 1536, 512, 16), (512, 1536, 512, 20), (2560, 1024, 384, 16),
-                                      (4096, 4608, 1024, 256), (192, 37888, 1024, 256)])
+                                      (4096, 4608, 1024, 256), (192, 37888, 1024, 256),
+                                      # sk < 0: whole rounds data-parallel, only the remainder streamed
+                                      (512, 1536, 512, -20), (2560, 1024, 384, -16), (1280, 4608, 1024, -64)])
 def test_gemm_stream_k(dev, M, N, K, sk):
     x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
     y = G.gemm(x, w, b, ksplit=1, sk=sk)
@@ -116,11 +118,12 @@ def test_gemm_stream_k(dev, M, N, K, sk):
     assert torch.equal(y, y2), "stream-K fixup must be bitwise reproducible"
 
 
-def test_gemm_silu_stream_k(dev):
-    M, I, K = 192, 4096, 1024  # 32 tiles over 48 stream-K workgroups: every tile split
+@pytest.mark.parametrize("M,I,sk", [(192, 4096, 48), (768, 2048, -20)])
+def test_gemm_silu_stream_k(dev, M, I, sk):
+    K = 1024  # (192, 48): 32 tiles over 48 stream-K workgroups, every tile split; (768, -20): 8-tile remainder
     x = rnd(M, K, dev=dev, scale=0.3)
     wg, wu = rnd(I, K, dev=dev, seed=1, scale=0.2), rnd(I, K, dev=dev, seed=2, scale=0.2)
-    h = G.gemm_silu(x, G.interleave_gate_up(wg, wu), ksplit=1, sk=48)
+    h = G.gemm_silu(x, G.interleave_gate_up(wg, wu), ksplit=1, sk=sk)
     check(h, torch.nn.functional.silu(ref(x, wg)) * ref(x, wu), K)
 
 
@@ -145,11 +148,59 @@ def test_gemm_decode_plain(dev, M, N, K, plan):
     check(y, ref(x, w, b), K)
 
 
+# balanced grids: (mt, nwv, ntw, ksplit, gs) with 1..nwv wave units per workgroup (idle waves store nothing)
+@pytest.mark.parametrize("M,N,K,plan", [(192, 4608, 3584, (12, 5, 2, 7, 36)), (200, 3584, 18944, (8, 5, 2, 9, 28)),
+                                        (100, 1024, 512, (8, 5, 2, 1, 7)), (129, 1536, 1024, (12, 5, 2, 2, 13)),
+                                        (256, 2048, 1024, (8, 5, 2, 1, 64)), (150, 1056, 512, (12, 5, 2, 1, 8)),
+                                        (250, 1024, 512, (4, 5, 2, 2, 8)), (77, 1024, 512, (8, 4, 2, 1))])
+def test_gemm_decode_balanced(dev, M, N, K, plan):
+    x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+    G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, plan[3])))
+    y = G.gemm_decode(x, w, b, plan=plan)
+    check(y, ref(x, w, b), K)
+
+
+@pytest.mark.parametrize("M,plan", [(192, (12, 5, 2, 1, 14)), (250, (8, 5, 2, 1, 16)), (100, (8, 5, 2, 1, 33)),
+                                    (230, (16, 4, 2, 1, 17)), (200, (12, 8, 2, 2, 9))])
+def test_gemm_decode_silu_balanced(dev, M, plan):
+    I, K = 1056, 1024  # 66 wave units: 4-5, 4-5, 2 per workgroup
+    x = rnd(M, K, dev=dev, scale=0.5)
+    wg, wu = rnd(I, K, dev=dev, seed=1, scale=0.2), rnd(I, K, dev=dev, seed=2, scale=0.2)
+    wgu = G.interleave_gate_up(wg, wu)
+    h = G.gemm_decode(x, wgu, None, epi=G.EPI_SILU, plan=plan)
+    check(h, torch.nn.functional.silu(ref(x, wg)) * ref(x, wu), K)
+
+
+# unit-packed weights (ops/gemm.py dec_pack): same results as the natural layout
+@pytest.mark.parametrize("M,N,K,plan,silu", [(192, 4608, 3584, (12, 5, 2, 7, 36), False),
+                                             (64, 3584, 18944, (4, 4, 2, 9), False),
+                                             (250, 2048, 1024, (8, 5, 2, 1, 64), False),
+                                             (192, 2112, 1024, (12, 5, 2, 1, 14), True),
+                                             (100, 2048, 512, (8, 4, 2, 2), True)])
+def test_gemm_decode_packed(dev, M, N, K, plan, silu):
+    x, w = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3)
+    b = rnd(N, dev=dev, seed=2)
+    G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, plan[3])))
+    epi = G.EPI_SILU if silu else G.EPI_STORE
+    y0 = G.gemm_decode(x, w, b, epi=epi, plan=plan)
+    y1 = G.gemm_decode(x, w, b, epi=epi, plan=plan, packed=G.DecPacked(w, silu))
+    if silu:
+        wg, wu = G.deinterleave_gate_up(w.float())
+        bg, bu = G.deinterleave_gate_up(b.float().view(N, 1))
+        r = torch.nn.functional.silu(ref(x, wg.bfloat16(), bg.view(-1).bfloat16())) * ref(x, wu.bfloat16(), bu.view(-1).bfloat16())
+    else:
+        r = ref(x, w, b)
+    check(y0, r, K)
+    check(y1, r, K)
+    assert torch.equal(y0.cpu(), y1.cpu())
+
+
 def test_gemm_decode_identity_asymmetric(dev):
     # A = I with an asymmetric W catches a transposed C write
     K = 256
     w = (torch.arange(K * 256, dtype=torch.float32).reshape(256, K) % 251 - 125).to(torch.bfloat16).to(dev)
-    for M, plan in ((200, (16, 4, 2, 1)), (190, (12, 8, 2, 1))):
+    for M, plan in ((200, (16, 4, 2, 1)), (190, (12, 8, 2, 1)), (190, (12, 5, 2, 1, 4)), (120, (8, 5, 2, 1, 3)),
+                    (250, (4, 5, 2, 1, 2))):
         x = torch.eye(K, dtype=torch.bfloat16, device=dev)[:M].contiguous()
         y = G.gemm_decode(x, w, plan=plan)
         assert torch.equal(y.cpu(), w.float().T[:M].to(torch.bfloat16).cpu())

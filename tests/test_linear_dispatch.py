@@ -1,6 +1,9 @@
 """Decode-GEMM dispatch rules of ops/linear.py (CPU: predicates only; the
 numerics of every path are in tests/test_kernels_gpu.py)."""
+import torch
+
 from githubrepostorag_amd.ops.linear import splitk_parts, use_splitk
+from githubrepostorag_amd.ops import gemm as G
 
 
 def test_splitk_only_for_decode_sized_deep_k_down_proj():
@@ -32,8 +35,19 @@ def test_decode_gemm_plan_rules():
     assert G.dec_plan(192, 4608, 3584) is None            # M > 128: tile kernel
     assert G.dec_plan(64, 37888, 3584, silu=True) is None  # FFN-wide: >= one tile per CU
     assert G.dec_ksplit(3584, 9) == 7                     # 14 rings of 4 steps -> 2 rings per split
-    assert G.dec_variants(100) == [(8, 4, 2)]
-    assert G.dec_variants(190) == [(12, 8, 2)]
+    assert G.dec_variants(100) == [(8, 4, 2), (8, 5, 2)]
+    assert G.dec_variants(190) == [(12, 5, 2), (12, 8, 2)]
     if G._num_cus() == 256:
         assert G.dec_plan(64, 4608, 3584) == (4, 4, 2, 7)   # 36 tiles x 7 splits
         assert G.dec_plan(128, 3584, 18944) == (8, 4, 2, 9)  # 28 tiles x 9 splits
+
+
+def test_dec_pack_layout():
+    N, K = 128, 256
+    w = torch.arange(N * K, dtype=torch.float32).reshape(N, K)
+    pk = G.dec_pack(w)
+    assert pk.shape == (4, 4, 32, 64)
+    assert torch.equal(pk[1, 2, 5], w[32 + 5, 128:192])
+    pks = G.dec_pack(w, silu=True)
+    # silu unit 3: block 1, second 16-wide group -> gate rows 80..95, up rows 112..127
+    assert torch.equal(pks[3, 0, 0], w[80, :64]) and torch.equal(pks[3, 0, 16], w[112, :64])
