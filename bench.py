@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--quant", default="none", choices=["none", "w4"],
                     help="w4: AWQ-format W4A16 decoder weights (group-128 scales + zero points, the reference's "
                          "precision: helm/values.yaml:67) on the decode GEMMs; reported as its own config line")
+    ap.add_argument("--gc-freeze", type=int, default=1,
+                    help="1: gc.freeze() the setup objects before the timed steps (serving does the same at startup)")
     ap.add_argument("--pysample", type=float, default=0.0,
                     help="ms between stack samples of the engine thread over the timed steps (0: off; diagnostics)")
     ap.add_argument("--out", default=None)
@@ -311,6 +313,22 @@ def main():
         torch.cuda.synchronize()
     for k in phase:  # phase breakdown over the timed steps only
         phase[k] = 0.0
+    # long-lived setup objects (corpus tables, tokenizer tables, index metadata) leave the cyclic GC's
+    # generations: a gen-2 pass over them runs in whichever thread triggers it, holding the GIL, and the
+    # engine thread cannot launch meanwhile
+    import gc
+    gc.collect()
+    if args.gc_freeze:
+        gc.freeze()
+    gc_ms = collections.Counter()
+    gc_t0 = {}
+
+    def _gc_cb(phase_, info):
+        if phase_ == "start":
+            gc_t0["t"] = time.perf_counter()
+        elif "t" in gc_t0:
+            gc_ms[info.get("generation", -1)] += (time.perf_counter() - gc_t0.pop("t")) * 1000
+    gc.callbacks.append(_gc_cb)
     stats0 = dict(eng.stats)
     sampler = None
     if args.pysample:  # diagnostics: where the engine thread spends the timed steps
@@ -330,6 +348,7 @@ def main():
         for share, where in sampler.top_other(40):
             log(f"pysample-other {share:7.4f}  {where}")
     stats1 = dict(eng.stats)
+    gc.callbacks.remove(_gc_cb)
     comm.barrier()
     elapsed = time.perf_counter() - t_start
     phase_timed = dict(phase)
@@ -430,6 +449,7 @@ def main():
             "engine": eng_stats,
             "engine_per_timed_step": timed_engine,
             "phase_ms_per_step": {k: round(v / args.steps * 1000, 2) for k, v in phase_timed.items()},
+            "gc_pause_ms_per_step": {f"gen{k}": round(v / args.steps, 2) for k, v in sorted(gc_ms.items())},
             "main_thread_ms_per_step": {"engine_step": round(timed_engine.get("step_s", 0) * 1000, 2),
                                         "engine_prefill": round(timed_engine.get("prefill_s", 0) * 1000, 2),
                                         "engine_decode": round(timed_engine.get("decode_s", 0) * 1000, 2)},

@@ -246,6 +246,23 @@ class LLMEngine:
             bt[i, :n] = s.blocks[:n]
         return bt
 
+    def _read_host(self, t: torch.Tensor) -> np.ndarray:
+        """Device int tensor -> host numpy through a persistent pinned buffer (a non-blocking copy and an
+        event wait that releases the GIL).  A pageable .cpu() is staged by the runtime through a shared
+        bounce buffer, where it queued behind other threads' copies (retrieval) while the GPU idled."""
+        if not self.on_gpu:
+            return t.cpu().numpy()
+        n = t.numel()
+        buf = getattr(self, "_pinned_out", None)
+        if buf is None or buf.numel() < n or buf.dtype != t.dtype:
+            buf = self._pinned_out = torch.empty(max(n, 4096), dtype=t.dtype, pin_memory=True)
+            self._pinned_ev = torch.cuda.Event()
+        dst = buf[:n].view(t.shape)
+        dst.copy_(t, non_blocking=True)
+        self._pinned_ev.record()
+        self._pinned_ev.synchronize()
+        return dst.numpy().copy()
+
     def _to_dev(self, arr: np.ndarray) -> torch.Tensor:
         t = torch.from_numpy(arr)
         if self.on_gpu:
@@ -315,7 +332,7 @@ class LLMEngine:
             slot_t = self._to_dev(np.asarray([s.slot for s in samp_seqs], dtype=np.int32))
             tp = self.model.tp
             tp.stage_health()
-            toks = sample(logits, self.sampler, slot_t).tolist()
+            toks = self._read_host(sample(logits, self.sampler, slot_t)).reshape(-1).tolist()
             tp.check_health()
             now = time.perf_counter()
             self.stats["host_prefill_sample_s"] += now - t1
@@ -433,7 +450,7 @@ class LLMEngine:
             tw = time.perf_counter()
             self.stats["host_decode_prep_s"] += tw - t0
             self.model.tp.stage_health()
-            toks = g.out_tokens[:K, :n].cpu().numpy()
+            toks = self._read_host(g.out_tokens[:K, :n])
             self.model.tp.check_health()
             self.stats["decode_wait_s"] += time.perf_counter() - tw
             self.stats["graph_replays"] += 1

@@ -209,7 +209,7 @@ DEC_DEPTH = 3  # K-steps in flight; a K-split covers whole rings of DEC_DEPTH + 
 _DEC_ON = os.environ.get("GRAG_DECODE_GEMM", "1") != "0"
 # (mt, nwv, ntw) compiled: mt 16-row tiles of M, nwv waves per workgroup, ntw 16-row W tiles per wave
 DEC_VARIANTS = [(4, 4, 2), (4, 5, 2), (8, 4, 2), (8, 5, 2), (12, 5, 2), (12, 8, 2), (16, 4, 2)]
-DEC_MAX_M = int(os.environ.get("GRAG_DECODE_MAX_M", "128"))
+DEC_MAX_M = int(os.environ.get("GRAG_DECODE_MAX_M", "256"))
 
 
 def dec_variants(M: int) -> list[tuple[int, int, int]]:
@@ -230,24 +230,51 @@ def dec_ksplit(K: int, ksplit: int) -> int:
     return -(-kt // kts)
 
 
-def dec_plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int, int, int] | None:
-    """(mt, nwv, ntw, ksplit) for the decode kernel, or None when another path is faster.
+def dec_plan(M: int, N: int, K: int, silu: bool = False) -> tuple | None:
+    """(mt, nwv, ntw, ksplit[, gs]) for the decode kernel, or None when another path is faster.
 
-    Measured (scripts/bench_gemm_decode.py, cold weights, profiles/gemm_decode_ab_v4.jsonl): at 33..128 rows
-    the 4-wave variant with about one workgroup per CU beats the 256x256 tile kernel by 1.2-1.3x on the
-    Qwen2-7B qkv / o projections and 1.05-1.2x on down_proj; at 192 rows it only ties (v3), and on the
-    vocab- or FFN-wide outputs (>= one 128-column tile per CU) the tile kernel / library win."""
-    if not _DEC_ON or M < 1 or M > DEC_MAX_M or K % 256 or (silu and N % 64):
+    Measured (scripts/bench_gemm_decode.py, cold weights, profiles/gemm_decode_ab_v4.jsonl and
+    gemm_decode_ab_v6.jsonl; Qwen2-7B projections, us):
+      * <= 128 rows, qkv / o / down: 4 waves, about one workgroup per CU via K-splits (1.2-1.3x the
+        256x256 tile kernel); gate/up (1184 wave units): the balanced 5-wave grid, 4-5 units on every CU
+        (M = 128: 72.6 vs tile 88.8, library 84.6);
+      * 129-192 rows: qkv / o on balanced 5-wave grids, 4 units x 7 K-splits (M = 192: qkv 33.7 vs tile
+        39.0, o 32.2 vs 36.0); gate/up balanced (81.9 vs 85.6); down_proj (K = 5.3 N) stays on the tile
+        kernel's split-K (58.0 vs 63.4);
+      * 193-256 rows: qkv / o on 16-row-tile 4-wave groups x 7 K-splits (M = 256: 36.5 vs 42.7, 34.7 vs
+        39.0); gate/up and down_proj stay on the tile kernel (88.3 vs 110, 64.3 vs 68.1)."""
+    if not _DEC_ON or M < 1 or M > DEC_MAX_M or K % 256 or N % 32 or (silu and N % 64):
         return None
-    vs = [v for v in dec_variants(M) if v[1] == 4 and N % (16 * v[1] * v[2]) == 0]
-    if not vs:
-        return None
-    mt, nwv, ntw = vs[0]
-    tiles = N // (16 * nwv * ntw)
     ncu = _num_cus()
-    if tiles >= ncu:
+    units = N // 32
+    deep = K >= 4 * N  # down_proj-like
+    if M <= 128:
+        if silu or units >= 4 * ncu:  # FFN-wide: balanced 5-wave grid over every CU, no K-split
+            mt = 4 if M <= 64 else 8
+            gs = dec_balanced_gs(N, 2, 5, 1, ncu)
+            return None if gs is None else (mt, 5, 2, 1, gs)
+        vs = [v for v in dec_variants(M) if v[1] == 4 and N % (16 * v[1] * v[2]) == 0]
+        if not vs:
+            return None
+        mt, nwv, ntw = vs[0]
+        tiles = N // (16 * nwv * ntw)
+        if tiles >= ncu:
+            return None
+        return mt, nwv, ntw, dec_ksplit(K, max(1, ncu // tiles))
+    if M <= 192:
+        if deep:
+            return None
+        if silu:
+            gs = dec_balanced_gs(N, 2, 5, 1, ncu)
+            return None if gs is None else (12, 5, 2, 1, gs)
+        if units >= 4 * ncu:
+            return None
+        ks = dec_ksplit(K, max(1, round(ncu / max(1, units / 4))))
+        gs = dec_balanced_gs(N, 2, 5, ks, ncu)
+        return None if gs is None else (12, 5, 2, ks, gs)
+    if silu or deep or units % 4 or units // 4 >= ncu:
         return None
-    return mt, nwv, ntw, dec_ksplit(K, max(1, ncu // tiles))
+    return 16, 4, 2, dec_ksplit(K, max(1, ncu // (units // 4)))
 
 
 def dec_ws_floats(M: int, N: int, ksplit: int) -> int:
@@ -320,7 +347,7 @@ def dec_capture_ok(dev: torch.device, M: int, N: int, K: int, silu: bool = False
     p = dec_plan(M, N, K, silu)
     if p is None:
         return False
-    fl = dec_ws_floats(M, N, p[3])
+    fl = dec_ws_floats(M, N, dec_ksplit(K, p[3]))
     return fl == 0 or not torch.cuda.is_current_stream_capturing() or WS.ready(dev, fl)
 
 
@@ -336,6 +363,9 @@ def mlp_gate_up(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None =
     """SwiGLU input half for an interleaved gate/up weight: the fused tile
     kernel when it takes the shape, else library GEMM + reshape (same math)."""
     M, K = x.shape
+    if x.is_cuda and M >= 33 and supported(x, w_gu) and dec_plan(M, w_gu.shape[0], K, True) is not None \
+            and dec_capture_ok(x.device, M, w_gu.shape[0], K, True):
+        return gemm_decode(x, w_gu, b_gu, epi=EPI_SILU)
     if not x.is_cuda or (supported(x, w_gu) and capture_ok(x.device, M, w_gu.shape[0], K)):
         return gemm_silu(x, w_gu, b_gu)
     y = torch.nn.functional.linear(x, w_gu, b_gu).view(M, -1, 2, 32)

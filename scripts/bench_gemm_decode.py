@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--splits", default="1,2,3,4,5,7,9,14,18,28")
     ap.add_argument("--w4", action="store_true", help="add W4A16 (ops/w4.py) arms; their error is vs the 4-bit weight")
     ap.add_argument("--packed", action="store_true", help="add unit-packed weight arms (pk_*)")
+    ap.add_argument("--dispatch", action="store_true", help="arms: library, tile kernel, dec_plan's choice")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -77,8 +78,15 @@ def main():
             G.WS.reserve(dev, G._ws_floats(M, N, S, SK))
             arms["tile"] = (lambda w=None: G.gemm_silu(x, w if w is not None else nxt(), ksplit=S, sk=SK)) if silu \
                 else (lambda w=None: G.gemm(x, w if w is not None else nxt(), ksplit=S, sk=SK))
-            for mt, nwv, ntw in G.dec_variants(M) + [v for v in G.DEC_VARIANTS if v[1] == 5 and 16 * v[0] < M
-                                                     and -(-M // (16 * v[0])) <= 4]:
+            if args.dispatch:  # only the plan ops/gemm.py dec_plan picks
+                pl = G.dec_plan(M, N, K, silu)
+                if pl is not None:
+                    G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, pl[3])))
+                    arms["plan_" + "_".join(map(str, pl))] = (
+                        lambda w=None, plan=pl: G.gemm_decode(x, w if w is not None else nxt(),
+                                                              epi=G.EPI_SILU if silu else G.EPI_STORE, plan=plan))
+            for mt, nwv, ntw in [] if args.dispatch else G.dec_variants(M) + [
+                    v for v in G.DEC_VARIANTS if v[1] == 5 and 16 * v[0] < M and -(-M // (16 * v[0])) <= 4]:
                 seen = set()
                 for req in map(int, args.splits.split(",")):
                     ks = G.dec_ksplit(K, req)

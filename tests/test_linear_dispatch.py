@@ -32,14 +32,23 @@ def test_decode_gemm_plan_rules():
     from githubrepostorag_amd.ops import gemm as G
 
     assert G.dec_plan(96, 4608, 1000) is None             # K % 256
-    assert G.dec_plan(192, 4608, 3584) is None            # M > 128: tile kernel
-    assert G.dec_plan(64, 37888, 3584, silu=True) is None  # FFN-wide: >= one tile per CU
     assert G.dec_ksplit(3584, 9) == 7                     # 14 rings of 4 steps -> 2 rings per split
     assert G.dec_variants(100) == [(8, 4, 2), (8, 5, 2)]
     assert G.dec_variants(190) == [(12, 5, 2), (12, 8, 2)]
-    if G._num_cus() == 256:
+    G_ncu = G._num_cus
+    try:
+        G._num_cus = lambda: 256
         assert G.dec_plan(64, 4608, 3584) == (4, 4, 2, 7)   # 36 tiles x 7 splits
         assert G.dec_plan(128, 3584, 18944) == (8, 4, 2, 9)  # 28 tiles x 9 splits
+        assert G.dec_plan(128, 37888, 3584, silu=True) == (8, 5, 2, 1, 256)  # 1184 units: 4-5 per CU
+        assert G.dec_plan(192, 4608, 3584) == (12, 5, 2, 7, 36)  # 144 units: 4 per group x 7 splits
+        assert G.dec_plan(192, 37888, 3584, silu=True) == (12, 5, 2, 1, 256)
+        assert G.dec_plan(192, 3584, 18944) is None          # deep-K down_proj: tile kernel split-K
+        assert G.dec_plan(256, 3584, 3584) == (16, 4, 2, 7)
+        assert G.dec_plan(256, 37888, 3584, silu=True) is None  # gate/up at 193..256: tile kernel
+        assert G.dec_plan(300, 4608, 3584) is None
+    finally:
+        G._num_cus = G_ncu
 
 
 def test_dec_pack_layout():
