@@ -15,8 +15,11 @@ covers the chip.
 """
 from __future__ import annotations
 
+import bisect
+import json
 import os
 import threading
+from pathlib import Path
 
 import torch
 
@@ -104,6 +107,74 @@ def plan(M: int, N: int, K: int) -> tuple[int, int]:
     return (1, ncu) if eff < SK_EFF else (1, 0)
 
 
+def sk_ok(M: int, N: int, K: int, ksplit: int, sk: int) -> bool:
+    """The launcher's schedule rule (grag_gemm_tile): a stream-K round must give every workgroup at least
+    half a tile of K-steps (a quarter for the tail-only mode, sk < 0)."""
+    kt = K // 64
+    if ksplit > 1:
+        kts = -(-kt // ksplit)
+        return kts >= 2 and (ksplit - 1) * kts < kt and kt - (ksplit - 1) * kts >= 2
+    tiles = -(-M // 256) * -(-N // 256)
+    skg = abs(sk)
+    if skg == 0 or tiles % skg == 0:
+        return True
+    rounds = tiles // skg
+    dp = rounds * skg if sk < 0 else (rounds - 1) * skg if rounds >= 1 else 0
+    return (tiles - dp) * kt >= skg * ((kt + 3) // 4 if sk < 0 else (kt + 1) // 2)
+
+
+_PREFILL = {"table": None}
+PREFILL_TABLE = Path(__file__).resolve().parents[1] / "tuning" / "gemm_prefill_gfx950.json"
+
+
+def _prefill_table() -> dict:
+    if _PREFILL["table"] is None:
+        t = {}
+        if os.environ.get("GRAG_PREFILL_TABLE", "1") != "0" and PREFILL_TABLE.exists():
+            for k, rows in json.loads(PREFILL_TABLE.read_text())["table"].items():
+                t[tuple(map(int, k.split(",")))] = ([r[0] for r in rows], rows)
+        _PREFILL["table"] = t
+    return _PREFILL["table"]
+
+
+def prefill_plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int] | None:
+    """(ksplit, sk) of the owned kernel for a prefill-sized GEMM, or None for the library.
+
+    From the dense M sweep of scripts/sweep_prefill_gemm.py (tuning/gemm_prefill_gfx950.json; library
+    with the TunableOp solutions loaded vs every owned schedule, 256-row buckets).  The library's
+    heuristic swings with M (Qwen2-7B down_proj: 605 us at M = 5504, 1103 us at 6016, 678 us at 6784,
+    1131 us at 7040; owned 650-770 us across the range), so the library is taken only where it won at
+    both buckets around M; otherwise the owned schedule measured at the bucket at or above M (re-checked
+    against the launcher rule at this M).  SwiGLU shapes are always owned (the library needs a separate
+    SiLU*mul pass: owned won all 63 buckets on Qwen2-7B / 1.5B).  Unmeasured shapes: None (library) for
+    plain GEMMs, ``plan`` for SwiGLU."""
+    t = _prefill_table().get((N, K, int(silu)))
+    if t is None:
+        return plan(M, N, K) if silu else None
+    ms, rows = t
+    i = bisect.bisect_left(ms, M)
+    cand = [rows[min(i, len(rows) - 1)]]
+    if 0 < i < len(rows) and ms[i] != M:
+        cand.append(rows[i - 1])
+    won = [r for r in cand if r[2] is not None and r[2] < r[1]]
+    if not won:
+        return plan(M, N, K) if silu else None
+    ks, sk = won[0][3], won[0][4]
+    return (ks, sk) if sk_ok(M, N, K, ks, sk) else (1, 0)
+
+
+PREFILL_MIN_M = 257  # above one 256-row tile: the prefill regime (decode batches use plan())
+
+
+def schedule(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int]:
+    """(ksplit, sk) the owned kernel runs a shape with when the caller does not pin one."""
+    if M >= PREFILL_MIN_M:
+        p = prefill_plan(M, N, K, silu)
+        if p is not None:
+            return p
+    return plan(M, N, K)
+
+
 def _ws_floats(M: int, N: int, ksplit: int, sk: int) -> int:
     return ksplit * M * N if ksplit > 1 else (2 * abs(sk) * 65536 if sk else 0)
 
@@ -179,7 +250,7 @@ def gemm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, act: i
         return y.to(x.dtype)
     M, K = x.shape
     N = w.shape[0]
-    ksplit, sk = plan(M, N, K) if ksplit is None else (ksplit, sk or 0)
+    ksplit, sk = schedule(M, N, K) if ksplit is None else (ksplit, sk or 0)
     if out is None:
         out = torch.empty(M, N, dtype=x.dtype, device=x.device)
     return _launch(x, w, b, out, EPI_STORE, act, ksplit, sk)
@@ -198,7 +269,7 @@ def gemm_silu(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None = N
         return (torch.nn.functional.silu(g) * u).to(x.dtype)
     if N2 % 64:
         raise ValueError("gemm_silu: 2I must be a multiple of 64")
-    ksplit, sk = plan(M, N2, K) if ksplit is None else (ksplit, sk or 0)
+    ksplit, sk = schedule(M, N2, K, True) if ksplit is None else (ksplit, sk or 0)
     if out is None:
         out = torch.empty(M, N2 // 2, dtype=x.dtype, device=x.device)
     return _launch(x, w_gu, b_gu, out, EPI_SILU, ACT_NONE, ksplit, sk)
@@ -351,9 +422,9 @@ def dec_capture_ok(dev: torch.device, M: int, N: int, K: int, silu: bool = False
     return fl == 0 or not torch.cuda.is_current_stream_capturing() or WS.ready(dev, fl)
 
 
-def capture_ok(dev: torch.device, M: int, N: int, K: int) -> bool:
+def capture_ok(dev: torch.device, M: int, N: int, K: int, silu: bool = False) -> bool:
     """False only inside a hipGraph capture whose split-K slab was not sized by an eager step."""
-    ks, sk = plan(M, N, K)
+    ks, sk = schedule(M, N, K, silu)
     fl = _ws_floats(M, N, ks, sk)
     return fl == 0 or not torch.cuda.is_current_stream_capturing() or (WS.ready(dev, fl) and (
         not sk or getattr(WS._tls, "cnts", {}).get(dev.index) is not None))
@@ -366,7 +437,7 @@ def mlp_gate_up(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None =
     if x.is_cuda and M >= 33 and supported(x, w_gu) and dec_plan(M, w_gu.shape[0], K, True) is not None \
             and dec_capture_ok(x.device, M, w_gu.shape[0], K, True):
         return gemm_decode(x, w_gu, b_gu, epi=EPI_SILU)
-    if not x.is_cuda or (supported(x, w_gu) and capture_ok(x.device, M, w_gu.shape[0], K)):
+    if not x.is_cuda or (supported(x, w_gu) and capture_ok(x.device, M, w_gu.shape[0], K, True)):
         return gemm_silu(x, w_gu, b_gu)
     y = torch.nn.functional.linear(x, w_gu, b_gu).view(M, -1, 2, 32)
     return (torch.nn.functional.silu(y[:, :, 0].float()) * y[:, :, 1].float()).to(x.dtype).reshape(M, -1)

@@ -15,7 +15,10 @@ A/B in scripts/bench_gemm.py:
 * ``grag_gemm_tile`` (ops/gemm.py, 256x256 MFMA tiles + split-K slabs) for the
   other decode batches 32 < M <= 256: 1.1-1.5x the library on every Qwen2-7B
   projection (profiles/gemm_tile_ab_v1.jsonl);
-* larger M (prefill, encoder batches): plain GEMMs go to hipBLASLt through
+* larger M (prefill, encoder batches): the owned tile kernel wherever the
+  dense M sweep of scripts/sweep_prefill_gemm.py measured it faster
+  (``gemm.prefill_plan``; e.g. Qwen2-7B down_proj at the bench's ~7.1K-row
+  prefill steps: 771 vs 1131 us), else hipBLASLt through
   ``torch.nn.functional.linear`` — the library is used only for plain
   (epilogue-free / bias-only) GEMMs; everything fused around them
   (bias+RoPE+KV store, SiLU*mul, bias+GELU, bias+residual+LayerNorm,
@@ -274,6 +277,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> t
             return _tile.gemm_decode(x, w, b)
         if use_tile(M, N, K) and _tile.supported(x, w) and _tile.capture_ok(x.device, M, N, K):
             return _tile.gemm(x, w, b)
+        if M >= _tile.PREFILL_MIN_M and _tile.supported(x, w):
+            p = _tile.prefill_plan(M, N, K)
+            if p is not None and _tile.capture_ok(x.device, M, N, K):
+                return _tile.gemm(x, w, b, ksplit=p[0], sk=p[1])
         parts = splitk_parts(M, N, K)
         if parts:
             return gemm_splitk(x, w, b, parts)

@@ -1,0 +1,193 @@
+"""Measured prefill-GEMM dispatch: owned 256x256 tile kernel vs the library.
+
+For every prefill/encoder weight shape and a dense sweep of row counts M
+(the engine's prefill steps carry arbitrary token counts, and the library's
+heuristic choice swings with M: Qwen2-7B down_proj runs at 1504 TF/s at
+M = 4096 and 863 TF/s at M = 7104, profiles/gemm_tile_prefill_7k.jsonl),
+time hipBLASLt (TunableOp results loaded, as in serving) and the owned kernel
+under each tail schedule it has (whole tiles; stream-K round; tail-only
+stream-K), check each owned arm against the library output, and record the
+fastest arm per M.  Writes githubrepostorag_amd/tuning/gemm_prefill_gfx950.json,
+which ops/linear.py (plain projections) and ops/gemm.py (fused SwiGLU) read.
+
+Both arms run interleaved in one process on the same random operands
+(cdna guide §5.4 rules 24/25); medians of CUDA-event timings.
+
+usage: python scripts/sweep_prefill_gemm.py [--models qwen2-7b,bge-large] [--mmin 384 --mmax 16384 --mstep 256]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from githubrepostorag_amd.ops import gemm as G  # noqa: E402
+from githubrepostorag_amd.ops.linear import enable_tuned_gemms  # noqa: E402
+
+SHAPES = {
+    # name: [(label, N, K, silu)]  (N, K) of the [N, K] weight; silu: interleaved gate/up + SwiGLU epilogue
+    "qwen2-7b": [("qkv", 4608, 3584, False), ("o", 3584, 3584, False), ("gate_up", 37888, 3584, True),
+                 ("down", 3584, 18944, False)],
+    "qwen2-1.5b": [("qkv", 2048, 1536, False), ("o", 1536, 1536, False), ("gate_up", 17920, 1536, True),
+                   ("down", 1536, 8960, False)],
+    "bge-large": [("qkv", 3072, 1024, False), ("o", 1024, 1024, False), ("ffn1", 4096, 1024, False),
+                  ("ffn2", 1024, 4096, False)],
+}
+
+
+def med_us(fn, reps):
+    ts = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e) * 1e3)
+    return statistics.median(ts)
+
+
+def own_arms(M, N, K):
+    """(ksplit, sk) schedules the owned kernel can run this shape with."""
+    ncu = G._num_cus()
+    arms = {(1, 0)}
+    arms.add(G.plan(M, N, K))
+    tiles = -(-M // 256) * -(-N // 256)
+    if tiles > 2 * ncu and tiles % ncu:
+        arms.add((1, ncu))
+    kt = K // 64
+    if tiles > ncu and tiles % ncu and (tiles % ncu) * kt >= ncu * ((kt + 3) // 4):
+        arms.add((1, -ncu))
+    return sorted(arms)
+
+
+def table_row(M, med):
+    """[M, lib_us, best owned us, its ksplit, its sk] (owned fields null when no arm passed numerics)."""
+    own = {a: t for a, t in med.items() if a != "lib"}
+    if not own:
+        return [M, round(med["lib"], 1), None, 1, 0]
+    a = min(own, key=own.get)
+    return [M, round(med["lib"], 1), round(own[a], 1), a[0], a[1]]
+
+
+def table_from_log(path):
+    """Rebuild the dispatch table from a --log file of an earlier sweep."""
+    table = {}
+    for line in open(path):
+        r = json.loads(line)
+        model, label = r["shape"].split("/")
+        N, K, silu = next((n, k, s) for lb, n, k, s in SHAPES[model] if lb == label)
+        med = {"lib": r["lib_us"]}
+        for k, v in r.items():
+            if k.startswith("own_") and k.endswith("_us"):
+                ks, sk = k[4:-3].split("_")
+                med[(int(ks), int(sk))] = v
+        table.setdefault(f"{N},{K},{int(silu)}", []).append(table_row(r["M"], med))
+    return table
+
+
+def write_table(path, table, mstep, extra=None):
+    out = {"arch": "gfx950", "note": "scripts/sweep_prefill_gemm.py: per (N, K, silu) and M bucket "
+           "[M, library us, best owned us, its ksplit, its sk]; ops/linear.py prefill_plan() takes the library "
+           "only where it won at both buckets around M", "mstep": mstep, "table": table, **(extra or {})}
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    with open(path, "w") as f:
+        json.dump(out, f)
+    print(f"wrote {path} ({sum(len(v) for v in table.values())} buckets)", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--models", default="qwen2-7b,bge-large")
+    ap.add_argument("--mmin", type=int, default=384)
+    ap.add_argument("--mmax", type=int, default=16384)
+    ap.add_argument("--mstep", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--out", default="githubrepostorag_amd/tuning/gemm_prefill_gfx950.json")
+    ap.add_argument("--log", default=None)
+    ap.add_argument("--from-log", default=None, help="rebuild --out from an earlier sweep's --log, no GPU")
+    args = ap.parse_args()
+    if args.from_log:
+        write_table(args.out, table_from_log(args.from_log), args.mstep)
+        return
+    dev = torch.device("cuda", 0)
+    enable_tuned_gemms()
+    torch.manual_seed(0)
+    table, times = {}, {}
+    logf = open(args.log, "w") if args.log else None
+    t_start = time.time()
+    for model in args.models.split(","):
+        for label, N, K, silu in SHAPES[model]:
+            key = f"{N},{K},{int(silu)}"
+            ws = [((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(2)]
+            xfull = (torch.rand(args.mmax, K, device=dev) * 2 - 1).to(torch.bfloat16)
+            rows, trow = [], []
+            for M in range(args.mmin, args.mmax + 1, args.mstep):
+                x = xfull[:M]
+                arms = own_arms(M, N, K)
+                for ks, sk in arms:
+                    G.WS.reserve(dev, G._ws_floats(M, N, ks, sk))
+                    if sk:
+                        G.WS.counters(dev)
+                it = {"i": 0}
+
+                def lib():
+                    w = ws[it["i"] & 1]
+                    it["i"] += 1
+                    y = torch.nn.functional.linear(x, w)
+                    if silu:
+                        y = y.view(M, -1, 2, 32)
+                        y = (torch.nn.functional.silu(y[:, :, 0].float()) * y[:, :, 1].float()).to(x.dtype).reshape(M, -1)
+                    return y
+
+                def own(ks, sk):
+                    def f():
+                        w = ws[it["i"] & 1]
+                        it["i"] += 1
+                        return G.gemm_silu(x, w, ksplit=ks, sk=sk) if silu else G.gemm(x, w, ksplit=ks, sk=sk)
+                    return f
+
+                # numerics: each owned arm against the library on the same weight
+                it["i"] = 0
+                ref = lib().float()
+                scale = ref.abs().max().item() + 1e-6
+                ok = {}
+                for a in arms:
+                    it["i"] = 0
+                    y = own(*a)().float()
+                    ok[a] = ((y - ref).abs().max().item() / scale) < 2e-2
+                fns = {"lib": lib, **{a: own(*a) for a in arms if ok[a]}}
+                for f in fns.values():  # warm
+                    f()
+                torch.cuda.synchronize()
+                t = {k: [] for k in fns}
+                for _ in range(args.reps):  # interleaved rounds
+                    for k, f in fns.items():
+                        t[k].append(med_us(f, 1))
+                med = {k: statistics.median(v) for k, v in t.items()}
+                best = min(med, key=med.get)
+                choice = ["lib", 1, 0] if best == "lib" else ["own", best[0], best[1]]
+                rows.append(table_row(M, med))
+                trow.append({"M": M, "lib_us": round(med["lib"], 1),
+                             **{f"own_{a[0]}_{a[1]}_us": round(med[a], 1) for a in arms if a in med},
+                             "bad_arms": [list(a) for a in arms if not ok[a]], "best": choice})
+                line = json.dumps({"shape": f"{model}/{label}", **trow[-1]})
+                print(line, flush=True)
+                if logf:
+                    logf.write(line + "\n")
+                    logf.flush()
+            table[key] = rows
+            times[f"{model}/{label}"] = trow
+            del ws, xfull
+            torch.cuda.empty_cache()
+    write_table(args.out, table, args.mstep, {"sweep_s": round(time.time() - t_start, 1)})
+
+if __name__ == "__main__":
+    main()

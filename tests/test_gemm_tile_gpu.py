@@ -246,3 +246,20 @@ def test_gemm_decode_graph_replay(dev):
     g.replay()
     torch.cuda.synchronize()
     check(out, ref(x, w), K)
+
+
+@pytest.mark.parametrize("M,N,K", [(7104, 3584, 18944), (6016, 3584, 18944), (7296, 4608, 3584), (5000, 3584, 3584),
+                                   (3000, 1024, 4096)])
+def test_linear_prefill_dispatch(dev, M, N, K):
+    """linear() at prefill-sized M routes by the measured table (owned kernel where it won) — same numbers
+    as the fp32 reference whichever arm is taken; the Qwen2-7B down_proj at 7104 rows must be owned."""
+    from githubrepostorag_amd.ops.linear import linear
+
+    x, w = rnd(M, K, dev=dev, scale=0.5), rnd(N, K, dev=dev, seed=1, scale=0.05)
+    b = rnd(N, dev=dev, seed=2)
+    p = G.prefill_plan(M, N, K)
+    if (M, N, K) == (7104, 3584, 18944):
+        assert p is not None
+    y = linear(x, w, b)
+    rows = torch.arange(0, M, 37)
+    check(y[rows], ref(x[rows], w, b), K)

@@ -60,3 +60,46 @@ def test_dec_pack_layout():
     pks = G.dec_pack(w, silu=True)
     # silu unit 3: block 1, second 16-wide group -> gate rows 80..95, up rows 112..127
     assert torch.equal(pks[3, 0, 0], w[80, :64]) and torch.equal(pks[3, 0, 16], w[112, :64])
+
+
+def test_prefill_plan_from_measured_table():
+    """Prefill GEMMs (M > 256) follow the dense M sweep (tuning/gemm_prefill_gfx950.json)."""
+    ms, rows = G._prefill_table()[(3584, 18944, 0)]  # Qwen2-7B down_proj
+    assert ms == sorted(ms) and ms[0] <= 512 and ms[-1] >= 16000
+    # the bench's ~7.1K-row prefill steps: the library's heuristic is ~1.45x slower there
+    assert G.prefill_plan(7104, 3584, 18944) is not None
+    # the library is kept only where it won at both buckets around M
+    for i in range(1, len(ms)):
+        lo, hi = rows[i - 1], rows[i]
+        p = G.prefill_plan(ms[i] - 1, 3584, 18944)
+        lib_both = all(r[2] is None or r[2] >= r[1] for r in (lo, hi))
+        assert (p is None) == lib_both
+    # SwiGLU shapes are always owned; unmeasured plain shapes stay on the library
+    assert G.prefill_plan(5000, 37888, 3584, silu=True) is not None
+    assert G.prefill_plan(5000, 1000, 1024) is None
+    assert G.prefill_plan(5000, 1000, 1024, silu=True) == G.plan(5000, 1000, 1024)
+    # decode-sized M keeps the split-K planner
+    assert G.schedule(192, 3584, 18944) == G.plan(192, 3584, 18944)
+
+
+def test_prefill_plan_schedules_pass_launcher_rule():
+    G_ncu = G._num_cus
+    try:
+        G._num_cus = lambda: 256
+        for (N, K, silu), (ms, _) in G._prefill_table().items():
+            for M in range(300, 16500, 97):
+                p = G.prefill_plan(M, N, K, bool(silu))
+                if p is not None:
+                    assert G.sk_ok(M, N, K, *p), (M, N, K, p)
+    finally:
+        G._num_cus = G_ncu
+
+
+def test_sk_ok_mirrors_launcher():
+    # 28 x 14 = 392 tiles on 256 CUs, K = 18944 (296 K-steps): tail-only needs 136 * 296 >= 256 * 74
+    assert G.sk_ok(7104, 3584, 18944, 1, -256)
+    assert G.sk_ok(7104, 3584, 18944, 1, 0)
+    # 17 x 14 = 238 tiles < one round: the stream-K round gets all of them, 238 * 56 >= 256 * 28
+    assert G.sk_ok(4352, 3584, 3584, 1, 256)
+    # 257 tiles, tail of 1 tile over 256 workgroups: far below a quarter tile each
+    assert not G.sk_ok(257 * 256, 256, 3584, 1, -256)
