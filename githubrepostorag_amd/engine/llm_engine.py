@@ -51,7 +51,7 @@ class EngineConfig:
     gpu_memory_fraction: float = 0.5
     enable_prefix_caching: bool = True
     use_cuda_graph: bool = True
-    graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
+    graph_batch_sizes: tuple = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256, 320, 384, 448, 512)
     decode_window: int = 8  # max decode steps per graph replay (power of two)
     # decode tokens ride along in prefill steps (one weight pass for both).  Off by
     # default: measured on the headline bench the odd GEMM M (4096 + live rows)
@@ -124,6 +124,8 @@ class LLMEngine:
             hq, d = model.hq, model.head_dim
             self._part_o = torch.empty(max_split * self._max_b * hq * d, dtype=torch.float32, device=self.device)
             self._part_ml = torch.empty(max_split * self._max_b * hq * 2, dtype=torch.float32, device=self.device)
+            # sampler scratch for the largest decode batch up front: graphs captured later all see one buffer
+            self.sampler.workspace(self._max_b)
             # the engine's own (non-default) stream: retrieval / API threads issue their copies and syncs
             # on other streams; with the engine on the legacy default stream their runtime calls stalled
             # the engine thread (profiles/timeline_r2_*.txt).  Weights and the KV cache were written on

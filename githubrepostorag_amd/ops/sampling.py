@@ -24,6 +24,7 @@ class SamplerState:
         self.seen = torch.zeros(max_slots, self.words, dtype=torch.int32, device=device)
         self.rng = torch.zeros(max_slots, dtype=torch.int64, device=device)
         self._ws = None  # device scratch of the multi-workgroup sampler (sized on first use)
+        self._retired = []  # outgrown scratch stays alive: captured decode graphs still point at it
         # host mirror of which slots use top-k / top-p: the kernel chain only
         # launches the radix rounds some slot needs (decode graphs are keyed on it)
         self._uses_topk = [False] * max_slots
@@ -35,12 +36,18 @@ class SamplerState:
 
     def workspace(self, rows: int) -> torch.Tensor:
         """Scratch for a ``rows``-row call of grag_sample; sized for the
-        largest batch seen so far (>= 256 rows: every decode graph bucket) and
-        only grown outside hipGraph capture."""
+        largest batch seen so far (at least 256 rows; the engine reserves its
+        largest decode-graph bucket up front) and only grown outside hipGraph
+        capture.  An outgrown buffer is retired, not freed: decode graphs
+        captured at smaller buckets replay with its address (freeing it made a
+        384-row graph, captured before a 448-row warm-up grew the scratch,
+        fault on replay)."""
         need = int(lib().grag_sample_ws_floats(max(rows, 256), self.vocab))
         if self._ws is None or self._ws.numel() < need:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("sampler workspace must be sized before hipGraph capture")
+            if self._ws is not None:
+                self._retired.append(self._ws)
             self._ws = torch.empty(need, dtype=torch.float32, device=self.device)
         return self._ws
 

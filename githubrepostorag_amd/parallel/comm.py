@@ -56,7 +56,9 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600) -> DistIn
             torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         return _INFO
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # GRAG_DIST_BACKEND=gloo: rehearse a multi-rank run with every rank on one shared GPU (RCCL refuses
+        # two ranks on one device); ranks then map to devices local % device_count
+        backend = os.environ.get("GRAG_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     if backend == "nccl":
@@ -66,6 +68,9 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600) -> DistIn
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(**kw)
+    if backend != "nccl" and torch.cuda.is_available():
+        local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
     _INFO = DistInfo(rank, world, local, backend)
     return _INFO
 

@@ -108,3 +108,31 @@ def test_long_context_chunked_prefill_and_split_kv_decode(dev):
             agree += int(r[0].token_ids[0] == o.token_ids[j])
             total += 1
     assert agree / total >= 0.75, (agree, total)
+
+
+def test_sampler_scratch_outlives_graphs_captured_before_it_grew(setup, dev):
+    """A decode graph captured at a small bucket keeps replaying after a larger bucket's warm-up grew the
+    sampler scratch (the outgrown buffer is retired, not freed; the engine also reserves its largest
+    bucket up front).  Replays must match the eager engine token for token."""
+    from githubrepostorag_amd.ops.sampling import SamplerState
+
+    s = SamplerState(4, 1000, dev)
+    w1 = s.workspace(8)
+    w2 = s.workspace(4096)
+    assert w2.numel() > w1.numel() and any(r is w1 for r in s._retired)
+
+    model, tok = setup
+    sp = SamplingParams(max_tokens=10, temperature=0.7, top_p=0.9, ignore_eos=True, seed=3)
+    cfg = dict(max_num_seqs=8, max_model_len=2048, num_blocks=1024,
+               graph_batch_sizes=(1, 2, 4, 8, 320, 512))
+    eng = LLMEngine(model, tok, EngineConfig(use_cuda_graph=True, **cfg))
+    assert eng.sampler._ws.numel() >= int(__import__("githubrepostorag_amd.ops._lib", fromlist=["lib"]).lib()
+                                          .grag_sample_ws_floats(512, model.cfg.vocab_size))
+    eng.warmup_graphs([4, 8], max_ctx=2048, windows=(1,))
+    old = eng.sampler._ws
+    eng.sampler.workspace(2048)  # a regrowth after the small graphs were captured
+    assert eng.sampler._ws is not old and any(r is old for r in eng.sampler._retired)
+    eng.warmup_graphs([512], max_ctx=2048, windows=(1,))
+    a = eng.generate(_prompts(tok), sp)
+    b = LLMEngine(model, tok, EngineConfig(use_cuda_graph=False, **cfg)).generate(_prompts(tok), sp)
+    assert [x.token_ids for x in a] == [x.token_ids for x in b]
