@@ -368,16 +368,21 @@ GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, vo
     gs = units / nwv;
   }
   if (gs > units || (units + gs - 1) / gs > nwv) return (int)hipErrorInvalidValue;
-  if (epi != EPI_STORE && epi != EPI_SILU) return (int)hipErrorInvalidValue;
+  // epi 2 (EPI_PARTIAL): leave the fp32 planes in ws for a consumer that reduces them itself
+  // (grag_splitk_add_rmsnorm: split-K reduce + residual add + RMSNorm in one pass)
+  const bool keep = epi == EPI_PARTIAL;
+  if (epi != EPI_STORE && epi != EPI_SILU && !keep) return (int)hipErrorInvalidValue;
   if (act != ACT_NONE && act != ACT_GELU && act != ACT_GELU_TANH) return (int)hipErrorInvalidValue;
-  if (epi == EPI_SILU && act != ACT_NONE) return (int)hipErrorInvalidValue;
+  if ((epi == EPI_SILU || keep) && act != ACT_NONE) return (int)hipErrorInvalidValue;
+  if (keep && bias != nullptr) return (int)hipErrorInvalidValue;
   constexpr int NST = kDepth + 1;
   const int kt = K / 64;
   if (kt % NST != 0) return (int)hipErrorInvalidValue;
   if (ksplit < 1) ksplit = 1;
   const int kts = ((kt / NST + ksplit - 1) / ksplit) * NST;
   ksplit = (kt + kts - 1) / kts;  // effective splits (ops/gemm.py dec_ksplit computes the same)
-  if (ksplit > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
+  if ((ksplit > 1 || keep) && ws == nullptr) return (int)hipErrorInvalidValue;
+  if (keep && ksplit == 1) return (int)hipErrorInvalidValue;
   DArgs a;
   a.A = (const bf16*)A;
   a.W = (const bf16*)W;
@@ -401,6 +406,6 @@ GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, vo
                           : mt == 8 ? launch_v<8, kDepth, 5, 2>(a, e, act, nwg, stream)
                                     : launch_v<12, kDepth, 5, 2>(a, e, act, nwg, stream);
   else err = launch_v<12, kDepth, 8, 2>(a, e, act, nwg, stream);
-  if (err || ksplit == 1) return err;
+  if (err || ksplit == 1 || keep) return err;
   return grag_splitk_reduce(ws, bias, C, ldc, M, N, ksplit, epi, act, stream);
 }

@@ -522,9 +522,13 @@ GRAG_API int grag_gemm_tile(const void* A, const void* W, const void* bias, void
   if (K % 64 != 0 || K < 128 || lda % 8 != 0 || ldw % 8 != 0 || ldc % 8 != 0 || N % 8 != 0)
     return (int)hipErrorInvalidValue;
   if (epi == EPI_SILU && N % 64 != 0) return (int)hipErrorInvalidValue;
-  if (epi != EPI_STORE && epi != EPI_SILU) return (int)hipErrorInvalidValue;
+  // epi 2 (EPI_PARTIAL, ksplit > 1 only): leave the fp32 planes in ws for a consumer that reduces
+  // them itself (grag_splitk_add_rmsnorm)
+  const bool keep = epi == EPI_PARTIAL;
+  if (epi != EPI_STORE && epi != EPI_SILU && !keep) return (int)hipErrorInvalidValue;
   if (act != ACT_NONE && act != ACT_GELU && act != ACT_GELU_TANH) return (int)hipErrorInvalidValue;
-  if (epi == EPI_SILU && act != ACT_NONE) return (int)hipErrorInvalidValue;
+  if ((epi == EPI_SILU || keep) && act != ACT_NONE) return (int)hipErrorInvalidValue;
+  if (keep && (ksplit <= 1 || bias != nullptr)) return (int)hipErrorInvalidValue;
   const int kt = K / 64;
   if (ksplit < 1) ksplit = 1;
   const int kts = (kt + ksplit - 1) / ksplit;
@@ -563,7 +567,7 @@ GRAG_API int grag_gemm_tile(const void* A, const void* W, const void* bias, void
   int err;
   if (ksplit > 1) {
     err = launch<EPI_PARTIAL, ACT_NONE>(a, stream);
-    if (err) return err;
+    if (err || keep) return err;
     const int NO = epi == EPI_SILU ? N / 2 : N;
     const long n8 = (long)M * (NO / 8);
     const int blocks = (int)((n8 + 255) / 256);

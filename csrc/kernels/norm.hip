@@ -70,6 +70,66 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_kernel(
   }
 }
 
+// Split-K reduce fused into the decoder's block boundary: h = sum_s ws[s] (fp32
+// planes a split-K projection left behind, ops/linear.py linear_deferred),
+// residual += h (rounded to bf16, the residual stream's precision), out =
+// RMSNorm(residual) * w.  Replaces splitk_reduce (fp32 planes -> bf16 h) +
+// rmsnorm (h + residual): one launch and one bf16 round trip of h fewer per
+// o_proj / down_proj at decode batches, and h is never rounded before the add.
+template <int VPT>
+__global__ __launch_bounds__(kThreads) void splitk_rmsnorm_kernel(
+    const float* __restrict__ ws, int S, size_t plane, bf16* __restrict__ residual,
+    const bf16* __restrict__ w, bf16* __restrict__ out, int H, float eps) {
+  __shared__ float red[kThreads / 64];
+  const int row = blockIdx.x;
+  const int nvec = H >> 3;
+  const float* hr = ws + (size_t)row * H;
+  bf16x8_t* rr = reinterpret_cast<bf16x8_t*>(residual + (size_t)row * H);
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) {
+      float a[8];
+      unpack8(rr[idx], a);
+#pragma unroll 4
+      for (int sp = 0; sp < S; ++sp) {
+        const float* q = hr + sp * plane + idx * 8;
+        const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(q), x1 = *reinterpret_cast<const f32x4_t*>(q + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { a[j] += x0[j]; a[j + 4] += x1[j]; }
+      }
+      bf16x8_t sum = pack8(a);
+      rr[idx] = sum;
+      unpack8(sum, a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = a[j];
+        ss += a[j] * a[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  ss = block_sum(ss, red);
+  const float inv = rsqrtf(ss / (float)H + eps);
+  const bf16x8_t* wr = reinterpret_cast<const bf16x8_t*>(w);
+  bf16x8_t* orow = reinterpret_cast<bf16x8_t*>(out + (size_t)row * H);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) {
+      float g[8], o[8];
+      unpack8(wr[idx], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * g[j];
+      orow[idx] = pack8(o);
+    }
+  }
+}
+
 // y = LN(x [+ bias] [+ residual]) * gamma + beta.
 // WRITEBACK (pre-LN decoders, GPT-2): the bf16-rounded sum x + bias + residual
 // is stored back into `residual` (the residual stream) before it is
@@ -248,6 +308,26 @@ GRAG_API int grag_rmsnorm(const void* x, void* residual, const void* w, void* ou
     case 4: rmsnorm_kernel<4><<<T, kThreads, 0, stream>>>(xp, rp, (const bf16*)w, (bf16*)out, H, eps); break;
     default: rmsnorm_kernel<8><<<T, kThreads, 0, stream>>>(xp, rp, (const bf16*)w, (bf16*)out, H, eps); break;
   }
+  return (int)hipGetLastError();
+}
+
+// residual += sum_s ws[s] ; out = RMSNorm(residual) * w   (ws: S fp32 planes [T][H], 16-B aligned)
+GRAG_API int grag_splitk_add_rmsnorm(const void* ws, int S, void* residual, const void* w, void* out, int T,
+                                     int H, float eps, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8 != 0 || H > 8 * 8 * kThreads || S < 1 || ws == nullptr || residual == nullptr)
+    return (int)hipErrorInvalidValue;
+  const size_t plane = (size_t)T * H;
+  const float* wp = (const float*)ws;
+  bf16* rp = (bf16*)residual;
+#define SRN(V) splitk_rmsnorm_kernel<V><<<T, kThreads, 0, stream>>>(wp, S, plane, rp, (const bf16*)w, (bf16*)out, H, eps)
+  switch (vpt_for(H)) {
+    case 1: SRN(1); break;
+    case 2: SRN(2); break;
+    case 4: SRN(4); break;
+    default: SRN(8); break;
+  }
+#undef SRN
   return (int)hipGetLastError();
 }
 

@@ -31,7 +31,7 @@ import torch
 from ..ops.attention import AttnMetadata, paged_attention
 from ..ops.elementwise import qkv_rope_kvstore, rope_cos_sin, silu_mul
 from ..ops.gemm import deinterleave_gate_up, interleave_gate_up, mlp_gate_up
-from ..ops.linear import linear
+from ..ops.linear import linear, linear_deferred
 from ..ops.norm import embed_gather, rmsnorm
 from ..parallel.comm import Group
 from .configs import DecoderConfig
@@ -175,7 +175,7 @@ class Qwen2Model:
         self.w4_enabled = True
         return total
 
-    def _proj(self, x: torch.Tensor, L, name: str, bias=None) -> torch.Tensor:
+    def _proj(self, x: torch.Tensor, L, name: str, bias=None, defer: bool = False):
         """A layer projection: the W4A16 decode GEMM at decode-sized batches when the model is
         quantised, else the bf16 path (ops/linear.py)."""
         w4 = getattr(L, "w4", None) if self.w4_enabled else None
@@ -186,6 +186,8 @@ class Qwen2Model:
             if W4.plan(x.shape[0], q.N, q.K, q.silu) is not None and W4.capture_ok(x.device, x.shape[0], q):
                 return W4.gemm_w4(x, q, bias)
         w = getattr(L, name)
+        if defer and bias is None:  # o / down feeding residual add + RMSNorm: split-K reduce folded into the norm
+            return linear_deferred(x, w)
         if name == "gu_w":
             return mlp_gate_up(x, w) if self.gu_interleaved else silu_mul(linear(x, w))
         return linear(x, w, bias)
@@ -220,6 +222,7 @@ class Qwen2Model:
         eps = cfg.rms_norm_eps
         h = embed_gather(input_ids, self.embed)
         residual = None
+        defer = self.tp.trivial  # under TP the all-reduce sits between the projection and the norm
         for L, (kc, vc) in zip(self.layers, kv_caches):
             if residual is None:
                 residual = h
@@ -230,10 +233,10 @@ class Qwen2Model:
             q = qkv_rope_kvstore(qkv, L.qkv_b, positions, self.cos_sin, meta.slot_mapping, kc, vc,
                                  self.hq, self.hkv, self.head_dim)
             a = paged_attention(q, kc, vc, meta, self.scale, causal=True)
-            h = self.tp.all_reduce(self._proj(a, L, "o_w"))
+            h = self.tp.all_reduce(self._proj(a, L, "o_w", defer=defer))
             x = rmsnorm(h, L.post_norm, eps, residual=residual)
             m = self._proj(x, L, "gu_w")
-            h = self.tp.all_reduce(self._proj(m, L, "down_w"))
+            h = self.tp.all_reduce(self._proj(m, L, "down_w", defer=defer))
         return rmsnorm(h, self.norm, eps, residual=residual)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:

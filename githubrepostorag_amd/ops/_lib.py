@@ -28,6 +28,7 @@ F = ctypes.c_float
 
 _SIGS = {
     "grag_rmsnorm": [P, P, P, P, I, I, F, P],
+    "grag_splitk_add_rmsnorm": [P, I, P, P, P, I, I, F, P],
     "grag_layernorm": [P, P, P, P, P, P, I, I, F, P],
     "grag_add_layernorm": [P, P, P, P, P, P, I, I, F, P],
     "grag_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, P],

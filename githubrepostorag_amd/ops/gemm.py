@@ -26,7 +26,7 @@ import torch
 from ._lib import call, ptr
 
 ACT_NONE, ACT_GELU, ACT_SILU, ACT_GELU_TANH = 0, 1, 2, 3
-EPI_STORE, EPI_SILU = 0, 1
+EPI_STORE, EPI_SILU, EPI_PARTIAL = 0, 1, 2
 _ON = os.environ.get("GRAG_TILE_GEMM", "1") != "0"
 
 
@@ -403,6 +403,58 @@ def gemm_decode(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
     call("grag_gemm_decode", ptr(x), ptr(wsrc), ptr(b), ptr(out), x.stride(0), w.stride(0), out.stride(0),
          M, N, K, epi, act, mt, nwv, ntw, ks, gs, 0 if packed is None else 2 if packed.silu else 1, ptr(ws))
     return out
+
+
+class SplitKPartial:
+    """The fp32 split-K planes [S, M, N] of a projection whose reduce was deferred to its consumer
+    (ops/norm.py rmsnorm: split-K reduce + residual add + RMSNorm in one kernel).  The planes live in the
+    thread's split-K workspace: the consumer must be the next launch that touches it on this stream."""
+
+    __slots__ = ("planes", "S", "M", "N", "dtype", "device")
+
+    def __init__(self, planes: torch.Tensor, S: int, M: int, N: int, dtype):
+        self.planes, self.S, self.M, self.N, self.dtype = planes, S, M, N, dtype
+        self.device = planes.device
+
+    @property
+    def shape(self):
+        return (self.M, self.N)
+
+    def materialize(self) -> torch.Tensor:
+        return self.planes.view(self.S, self.M, self.N).sum(0).to(self.dtype)
+
+
+def deferred_plan(M: int, N: int, K: int) -> tuple[str, int, tuple] | None:
+    """("decode" | "tile", effective K-splits, plan) when ops/linear.py linear() would run this bias-free
+    bf16 projection as a K-split on an owned kernel (its splitk_reduce is then deferrable); else None."""
+    p = dec_plan(M, N, K)
+    if p is not None:
+        ks = dec_ksplit(K, p[3])
+        return ("decode", ks, p) if ks > 1 else None
+    from .linear import use_tile  # noqa: PLC0415 (linear imports this module)
+
+    if use_tile(M, N, K):
+        ks, sk = schedule(M, N, K)
+        return ("tile", ks, (ks, sk)) if ks > 1 and not sk else None
+    return None
+
+
+def gemm_deferred(x: torch.Tensor, w: torch.Tensor, how: tuple[str, int, tuple]) -> SplitKPartial:
+    """Run a K-split projection (deferred_plan) and leave its fp32 planes in the workspace (epi
+    EPI_PARTIAL: no splitk_reduce launch)."""
+    M, K = x.shape
+    N = w.shape[0]
+    kind, ks, p = how
+    fl = ks * M * N
+    ws = WS.get(x.device, fl)
+    if kind == "decode":
+        mt, nwv, ntw, ksp, *rest = p
+        call("grag_gemm_decode", ptr(x), ptr(w), ptr(None), ptr(None), x.stride(0), w.stride(0), N,
+             M, N, K, EPI_PARTIAL, ACT_NONE, mt, nwv, ntw, ksp, rest[0] if rest else 0, 0, ptr(ws))
+    else:
+        call("grag_gemm_tile", ptr(x), ptr(w), ptr(None), ptr(None), x.stride(0), w.stride(0), N,
+             M, N, K, EPI_PARTIAL, ACT_NONE, ks, 0, ptr(ws), ptr(None))
+    return SplitKPartial(ws[:fl], ks, M, N, x.dtype)
 
 
 def dec_balanced_gs(N: int, ntw: int, nwv: int, ksplit: int, ncu: int | None = None) -> int | None:

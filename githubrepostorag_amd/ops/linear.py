@@ -298,3 +298,23 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> t
                 and (not torch.cuda.is_current_stream_capturing() or _WS.ready(x.device, M, N, K))):
             return gemm_stream(x, w, b)
     return torch.nn.functional.linear(x, w, b)
+
+
+def linear_deferred(x: torch.Tensor, w: torch.Tensor):
+    """linear(x, w) for a bias-free projection whose output only feeds the decoder's residual add +
+    RMSNorm: when linear() would run it as a K-split on an owned kernel, the fp32 planes are returned
+    unreduced (ops/gemm.py SplitKPartial) and rmsnorm() folds the reduce into its pass; otherwise the
+    plain bf16 result.  Same dispatch predicates as linear()."""
+    if (x.is_cuda and _SKINNY_ON and _DEFER_ON and x.dim() == 2 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and x.stride(1) == 1 and w.stride(1) == 1 and _tile.supported(x, w)):
+        M, K = x.shape
+        N = w.shape[0]
+        if M >= TILE_MIN_M:
+            how = _tile.deferred_plan(M, N, K)
+            if how is not None and (not torch.cuda.is_current_stream_capturing()
+                                    or _tile.WS.ready(x.device, how[1] * M * N)):
+                return _tile.gemm_deferred(x, w, how)
+    return linear(x, w)
+
+
+_DEFER_ON = os.environ.get("GRAG_DEFER_SPLITK", "1") != "0"

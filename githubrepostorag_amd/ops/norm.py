@@ -4,6 +4,7 @@ from __future__ import annotations
 import torch
 
 from ._lib import call, ptr
+from .gemm import SplitKPartial
 
 
 def _on_gpu(t: torch.Tensor) -> bool:
@@ -25,6 +26,14 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
             out: torch.Tensor | None = None) -> torch.Tensor:
     """y = RMSNorm(x [+ residual]) * w.  With ``residual`` the sum is written
     back into ``residual`` (the decoder's residual stream), fused in one pass."""
+    if isinstance(x, SplitKPartial):  # deferred split-K projection: reduce + residual add + norm in one pass
+        if residual is None:
+            x = x.materialize()
+        else:
+            out = torch.empty(x.M, x.N, dtype=x.dtype, device=x.device) if out is None else out
+            call("grag_splitk_add_rmsnorm", ptr(x.planes), x.S, ptr(residual), ptr(w), ptr(out), x.M, x.N,
+                 float(eps))
+            return out
     if not _on_gpu(x):
         return rmsnorm_ref(x, w, eps, residual)
     x = x.contiguous()

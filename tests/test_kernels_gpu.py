@@ -341,3 +341,58 @@ def test_linear_splitk_down_proj(dev, M):
     close(linear(x, w), ref, 3e-2, 2e-2)
     close(gemm_splitk(x, w, b), ref + b.float().cpu(), 3e-2, 2e-2)
     close(gemm_splitk(x, w, None, 2), ref, 3e-2, 2e-2)
+
+
+@pytest.mark.parametrize("M,Nn,K", [(48, 3584, 3584), (128, 3584, 18944), (190, 3584, 3584), (190, 3584, 18944),
+                                   (240, 3584, 3584)])
+def test_splitk_deferred_rmsnorm(dev, M, Nn, K):
+    """o_proj / down_proj at decode batches: the K-split planes left unreduced (EPI_PARTIAL) and reduced
+    inside the residual-add + RMSNorm kernel; vs the fp32 reference of linear -> residual add -> RMSNorm
+    and vs the unfused bf16 path (splitk_reduce + rmsnorm)."""
+    from githubrepostorag_amd.ops import gemm as G
+    from githubrepostorag_amd.ops.linear import linear, linear_deferred
+
+    how = G.deferred_plan(M, Nn, K)
+    assert how is not None and how[1] > 1, how
+    x = rnd(M, K, dev=dev, scale=0.5)
+    w = rnd(Nn, K, dev=dev, scale=0.05, seed=1)
+    r = rnd(M, Nn, dev=dev, seed=2)
+    g = rnd(Nn, dev=dev, seed=3)
+    part = linear_deferred(x, w)
+    assert isinstance(part, G.SplitKPartial) and part.S == how[1]
+    r1 = r.clone()
+    y = N.rmsnorm(part, g, 1e-6, residual=r1)
+    h32 = x.float().cpu() @ w.float().cpu().T
+    s32 = (h32 + r.float().cpu()).to(torch.bfloat16).float()
+    y32 = s32 * torch.rsqrt(s32.pow(2).mean(-1, keepdim=True) + 1e-6) * g.float().cpu()
+    close(r1, s32, 3e-2)
+    close(y, y32, 5e-2)
+    r2 = r.clone()  # the unfused path agrees to bf16 rounding of h
+    y2 = N.rmsnorm(linear(x, w), g, 1e-6, residual=r2)
+    close(r1, r2, 3e-2)
+    close(y, y2, 5e-2)
+
+
+def test_splitk_deferred_in_graph(dev):
+    """The deferred projection + fused norm replay correctly inside a hipGraph (workspace sized eagerly)."""
+    from githubrepostorag_amd.ops.linear import linear_deferred
+
+    M, Nn, K = 190, 3584, 3584
+    x = rnd(M, K, dev=dev, scale=0.5)
+    w = rnd(Nn, K, dev=dev, scale=0.05, seed=1)
+    r0 = rnd(M, Nn, dev=dev, seed=2)
+    g = rnd(Nn, dev=dev, seed=3)
+    r = r0.clone()
+    eager = N.rmsnorm(linear_deferred(x, w), g, 1e-6, residual=r)
+    r_g = r0.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph):
+            out = N.rmsnorm(linear_deferred(x, w), g, 1e-6, residual=r_g)
+    torch.cuda.current_stream().wait_stream(s)
+    r_g.copy_(r0)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager) and torch.equal(r_g, r)

@@ -103,3 +103,13 @@ def test_sk_ok_mirrors_launcher():
     assert G.sk_ok(4352, 3584, 3584, 1, 256)
     # 257 tiles, tail of 1 tile over 256 workgroups: far below a quarter tile each
     assert not G.sk_ok(257 * 256, 256, 3584, 1, -256)
+
+
+def test_deferred_splitk_plan():
+    """o_proj / down_proj K-splits whose reduce folds into the residual-add + RMSNorm kernel: exactly the
+    owned-kernel K-split cases of linear(); prefill sizes, the fused gate/up and un-split shapes are not."""
+    assert G.deferred_plan(190, 3584, 3584)[:2] == ("decode", 7)
+    assert G.deferred_plan(128, 3584, 18944)[:2] == ("decode", 9)
+    assert G.deferred_plan(190, 3584, 18944)[0] == "tile"
+    assert G.deferred_plan(4096, 3584, 3584) is None
+    assert G.deferred_plan(190, 37888, 3584) is None
