@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--ingest-files", type=int, default=192, help="source files in the synthetic repo to ingest")
     ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--ingest-seqs", type=int, default=256, help="concurrent sequences of the ingest engine")
+    ap.add_argument("--ingest-mixed", type=int, default=0,
+                    help="1: the ingest engine piggybacks decode tokens on prefill steps (mixed batches)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--switch-interval", type=float, default=0.0,
                     help="Python GIL switch interval (s): the engine thread re-takes the GIL quickly after a GPU wait")
@@ -410,7 +412,8 @@ def main():
             torch.cuda.empty_cache()
         comm.barrier()
         n_docs, secs, ingest_stages = run_ingest_bench(model, tok, emb, args.ingest_files, seed=rank,
-                                                       max_num_seqs=args.ingest_seqs, use_graph=not args.no_graph)
+                                                       max_num_seqs=args.ingest_seqs, use_graph=not args.no_graph,
+                                                       mixed_batches=bool(args.ingest_mixed))
         tt = torch.tensor([secs], dtype=torch.float64, device=dev)
         if world > 1:
             import torch.distributed as dist

@@ -27,12 +27,14 @@ from .readers import Document
 
 
 def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs: int = 256,
-                     max_model_len: int = 8192, use_graph: bool = True, summary_tokens: int = 128) -> tuple[int, float, dict]:
+                     max_model_len: int = 8192, use_graph: bool = True, summary_tokens: int = 128,
+                     mixed_batches: bool = False) -> tuple[int, float, dict]:
     """Returns (documents ingested, seconds, per-stage seconds)."""
     dev = next(model.parameters()).device if hasattr(model, "parameters") else torch.device("cpu")
     sizes = tuple(sorted({*EngineConfig.graph_batch_sizes, *range(256, max_num_seqs + 1, 128), max_num_seqs}))
     eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max_num_seqs, max_num_batched_tokens=16384,
                                              max_model_len=max_model_len, use_cuda_graph=use_graph, seed=seed,
+                                             mixed_batches=mixed_batches,
                                              graph_batch_sizes=tuple(b for b in sizes if b <= max_num_seqs)))
     if use_graph and dev.type == "cuda":
         eng.warmup_graphs()

@@ -436,6 +436,10 @@ def deferred_plan(M: int, N: int, K: int) -> tuple[str, int, tuple] | None:
     if use_tile(M, N, K):
         ks, sk = schedule(M, N, K)
         return ("tile", ks, (ks, sk)) if ks > 1 and not sk else None
+    if M >= PREFILL_MIN_M:  # 257-512-row decode batches run the measured prefill plans (K-split tile kernel)
+        p = prefill_plan(M, N, K)
+        if p is not None and p[0] > 1 and not p[1]:
+            return "tile", p[0], p
     return None
 
 

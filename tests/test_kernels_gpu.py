@@ -344,7 +344,7 @@ def test_linear_splitk_down_proj(dev, M):
 
 
 @pytest.mark.parametrize("M,Nn,K", [(48, 3584, 3584), (128, 3584, 18944), (190, 3584, 3584), (190, 3584, 18944),
-                                   (240, 3584, 3584)])
+                                   (240, 3584, 3584), (384, 3584, 18944), (512, 3584, 3584)])
 def test_splitk_deferred_rmsnorm(dev, M, Nn, K):
     """o_proj / down_proj at decode batches: the K-split planes left unreduced (EPI_PARTIAL) and reduced
     inside the residual-add + RMSNorm kernel; vs the fp32 reference of linear -> residual add -> RMSNorm

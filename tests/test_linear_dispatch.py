@@ -111,5 +111,6 @@ def test_deferred_splitk_plan():
     assert G.deferred_plan(190, 3584, 3584)[:2] == ("decode", 7)
     assert G.deferred_plan(128, 3584, 18944)[:2] == ("decode", 9)
     assert G.deferred_plan(190, 3584, 18944)[0] == "tile"
+    assert G.deferred_plan(384, 3584, 18944)[0] == "tile"  # 257-512-row decode: measured K-split plans
     assert G.deferred_plan(4096, 3584, 3584) is None
     assert G.deferred_plan(190, 37888, 3584) is None
