@@ -59,10 +59,7 @@ def parse():
     ap.add_argument("--nlist", type=int, default=4096)
     ap.add_argument("--nprobe", type=int, default=32)
     ap.add_argument("--batch", type=int, default=64, help="queries per GPU per step")
-    ap.add_argument("--inflight", type=int, default=8,
-                    help="batches' worth of queries in flight (1 = closed batch).  Default 8 = 512 live sequences "
-                         "(the largest decode graph): measured 3 -> 60.0, 6 -> 72.8, 7 -> 75.0, 8 -> 78.0 queries/s "
-                         "at an unchanged p50 TTFT of 87-88 ms (profiles/sweep_inflight_r2.txt)")
+    ap.add_argument("--inflight", type=int, default=3, help="batches' worth of queries in flight (1 = closed batch)")
     ap.add_argument("--arrival-groups", type=int, default=8, help="queries of a step arrive in this many groups")
     ap.add_argument("--prompt-len", type=int, default=1024)
     ap.add_argument("--gen-len", type=int, default=128)
@@ -292,13 +289,17 @@ def main():
                 assert len(s.output_ids) == args.gen_len, (len(s.output_ids), s.finish_reason)
         return ttft
 
-    # pipeline fill: U-1 groups staggered by gen_len / U tokens (exact,
-    # rounded cumulatively), so the in-flight ages are the steady state's and
-    # every timed step does the same work whatever --warmup is
+    # pipeline fill: U-1 groups staggered by s = (gen_len - 1) / U decode tokens (rounded
+    # cumulatively).  Steady state: a group gets its first token from prefill and s decode tokens in
+    # each of the U sub-steps it is in flight (its arrival's included), 1 + U s = gen_len; so before
+    # a sub-step the in-flight ages are 1 + s j, j = 1..U-1.  Each fill round decodes s tokens for
+    # every group: the newest (1 token after its prefill) is run to 1 + s.  Every timed step then
+    # decodes about B (gen_len - 1) tokens (reported as steady_state_decode_ratio ~ 1.0).
+    S = (args.gen_len - 1) / U
     for k in range(U - 1):
         submit()
-        d = max(1, round((k + 1) * args.gen_len / U) - round(k * args.gen_len / U))
-        run_until(inflight[-1][0], d)
+        d = max(1, round((k + 1) * S) - round(k * S))
+        run_until(inflight[-1][0], 1 + d)
 
     # capture the decode graphs of the steady state now (batch buckets the
     # live count can reach x every decode window), not inside a timed step
@@ -454,6 +455,10 @@ def main():
             },
             "engine": eng_stats,
             "engine_per_timed_step": timed_engine,
+            # timed decode tokens / (completed queries x (gen_len - 1)): ~1.0 when the timed steps did the
+            # steady state's decode work (no backlog from the fill drained or built inside the timed region)
+            "steady_state_decode_ratio": round(timed_engine.get("decode_tokens", 0) * dp_size * args.steps
+                                               / max(1, total_q * (args.gen_len - 1)), 3),
             "phase_ms_per_step": {k: round(v / args.steps * 1000, 2) for k, v in phase_timed.items()},
             "gc_pause_ms_per_step": {f"gen{k}": round(v / args.steps, 2) for k, v in sorted(gc_ms.items())},
             "main_thread_ms_per_step": {"engine_step": round(timed_engine.get("step_s", 0) * 1000, 2),
