@@ -156,7 +156,7 @@ def prefill_plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int] 
     cand = [rows[min(i, len(rows) - 1)]]
     if 0 < i < len(rows) and ms[i] != M:
         cand.append(rows[i - 1])
-    won = [r for r in cand if r[2] is not None and r[2] < r[1]]
+    won = [r for r in cand if r[2] is not None and (silu or r[2] < r[1])]  # SwiGLU: owned at every bucket
     if not won:
         return plan(M, N, K) if silu else None
     ks, sk = won[0][3], won[0][4]
