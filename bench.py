@@ -267,7 +267,13 @@ def main():
             have = min(len(eng.get(r).output_ids) for r in rids)
             if have >= ntok:
                 break
-            eng.step(max_window=ntok - have)
+            cap = ntok - have
+            if arrival is not None and not arrival.done():
+                # an arrival's retrieval is in flight: one decode step per replay, so the engine looks
+                # for its prompts every ~step instead of every window (TTFT no longer depends on
+                # whether retrieval beats a multi-step window)
+                cap = 1
+            eng.step(max_window=cap)
             if arrival is not None and arrival.done():
                 admit(arrival.result())
                 arrival = None
