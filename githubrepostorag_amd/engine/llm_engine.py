@@ -369,16 +369,33 @@ class LLMEngine:
         sl = buf[o:o + B]; o += B
         buf[o:o + B + 1] = np.arange(B + 1, dtype=np.int32); o += B + 1
         bt = buf[o:].reshape(B, width)
-        bt.fill(0)
+        bt[n:].fill(0)
         ids[n:] = 0
         pos[:, n:] = 0
         slot[:, n:] = -1
         ctx[:, n:] = 1
         sl[n:] = self.scratch_slot
         if n:
-            for i, s in enumerate(seqs):
+            # block-table rows come from a per-slot table kept across steps: a running sequence only
+            # appends to its block list (KVCacheManager.ensure extends in place; free / prefix match
+            # install a new list), so a step writes just the new tail, a full row when the slot's list
+            # object changed, and the batch is one row gather
+            tab, owner, have = self._slot_block_table()
+            tw = tab.shape[1]
+            for s in seqs:
+                r = s.slot
                 b = s.blocks
-                bt[i, :len(b)] = b if len(b) <= width else b[:width]
+                nb = min(len(b), tw)
+                h = have[r]
+                if owner[r] is not b or h > nb:
+                    tab[r, :nb] = b[:nb]
+                    owner[r] = b
+                    have[r] = nb
+                elif h < nb:
+                    tab[r, h:nb] = b[h:nb]
+                    have[r] = nb
+            rows = np.fromiter((s.slot for s in seqs), dtype=np.int64, count=n)
+            bt[:n] = tab[rows, :width] if width <= tw else np.pad(tab[rows], ((0, 0), (0, width - tw)))
             ids[:n] = [self._last_id(s) for s in seqs]
             sl[:n] = [s.slot for s in seqs]
             L = np.fromiter((s.total_len for s in seqs), dtype=np.int64, count=n)
@@ -387,6 +404,15 @@ class LLMEngine:
             ctx[:, :n] = p + 1
             slot[:, :n] = bt[np.arange(n)[None, :], p // bs].astype(np.int64) * bs + p % bs
         return buf
+
+    def _slot_block_table(self):
+        """(table [slots, max blocks], row owner, row length) behind _decode_inputs."""
+        t = getattr(self, "_sbt", None)
+        if t is None:
+            rows = self.cfg.max_num_seqs + 1
+            t = self._sbt = (np.zeros((rows, self.max_blocks_per_seq + 1), dtype=np.int32), [None] * rows,
+                             [0] * rows)
+        return t
 
     def _views(self, buf: torch.Tensor, B: int, width: int, K: int = 1):
         o = 0
