@@ -60,9 +60,17 @@ class GenerationHandle:
 
 
 class EngineRunner:
+    # arrival-aware decode window: while requests keep arriving (one submitted within the last
+    # ARRIVAL_RECENT_S) a decode replay runs at most ARRIVAL_WINDOW steps, so a new prompt waits for
+    # ~2 decode steps before its prefill instead of a whole 8-step window (bench.py measured p50 TTFT
+    # 123 -> 102 ms with the same cap); an idle stream keeps the full window
+    ARRIVAL_RECENT_S = 0.05
+    ARRIVAL_WINDOW = 2
+
     def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005, watchdog_s: float = 120.0,
                  on_health=None, tp=None, start: bool = True):
         self.engine = engine
+        self._last_submit = -1e9
         self.tp = tp if tp is not None and not tp.trivial else None
         self.leader = self.tp is None or self.tp.rank == 0
         self._aborts: list[str] = []
@@ -96,8 +104,12 @@ class EngineRunner:
         with self._cv:
             self._handles[rid] = h
             self._pending.append((rid, prompt, params, on_token))
+            self._last_submit = time.monotonic()
             self._cv.notify()
         return h
+
+    def _window(self) -> int | None:
+        return self.ARRIVAL_WINDOW if time.monotonic() - self._last_submit < self.ARRIVAL_RECENT_S else None
 
     def generate(self, prompt, params: SamplingParams | None = None, on_token=None,
                  timeout: float | None = None) -> Completion:
@@ -170,7 +182,7 @@ class EngineRunner:
                 continue
             ok = True
             try:
-                self.engine.step()
+                self.engine.step(max_window=msg.get("window"))
             except Exception as e:
                 log.exception("TP follower step failed")
                 self.last_error = e
@@ -208,12 +220,14 @@ class EngineRunner:
                 pending, self._pending = self._pending, []
                 aborts, self._aborts = self._aborts, []
             will_step = bool(pending) or self.engine.has_unfinished()
+            win = self._window()  # decided before the TP broadcast: every rank replays the same graph
             if self.tp is not None:
                 adds = []
                 for rid, prompt, params, cb in pending:
                     ids = self.engine.tok.encode(prompt) if isinstance(prompt, str) else list(prompt)
                     adds.append((rid, ids, params or SamplingParams()))
-                self._bcast({"add": adds, "abort": aborts, "stop": stop, "step": will_step and not stop})
+                self._bcast({"add": adds, "abort": aborts, "stop": stop, "step": will_step and not stop,
+                             "window": win})
                 pending = [(rid, ids, p, cb) for (rid, ids, p), (_, _, _, cb) in zip(adds, pending)]
             if stop:
                 break
@@ -233,7 +247,7 @@ class EngineRunner:
             self._step_t0 = time.monotonic()
             err = None
             try:
-                self.engine.step()
+                self.engine.step(max_window=win)
             except Exception as e:  # engine fault: fail every in-flight request, keep serving
                 log.exception("engine step failed")
                 err = e

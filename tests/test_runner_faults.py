@@ -47,7 +47,7 @@ class FakeEngine:
     def completion(self, seq):
         return Completion(seq.req_id, "done", [1], "length", 1, 0.0, 0.0)
 
-    def step(self):
+    def step(self, max_window=None):
         if self.mode == "raise":
             self.mode = "ok"
             self.reqs.clear()
