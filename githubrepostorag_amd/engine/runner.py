@@ -27,6 +27,7 @@ returns, the engine is marked healthy again.
 from __future__ import annotations
 
 import logging
+import os
 import threading
 import time
 
@@ -60,12 +61,14 @@ class GenerationHandle:
 
 
 class EngineRunner:
-    # arrival-aware decode window: while requests keep arriving (one submitted within the last
-    # ARRIVAL_RECENT_S) a decode replay runs at most ARRIVAL_WINDOW steps, so a new prompt waits for
-    # ~2 decode steps before its prefill instead of a whole 8-step window (bench.py measured p50 TTFT
-    # 123 -> 102 ms with the same cap); an idle stream keeps the full window
+    # arrival-aware decode window (GRAG_ARRIVAL_WINDOW=N): while requests keep arriving (one submitted
+    # within the last ARRIVAL_RECENT_S) a decode replay runs at most N steps, so a new prompt waits ~N
+    # decode steps before its prefill instead of a whole 8-step window.  Off by default: on the bench's
+    # agent e2e phase (64 concurrent 3-round jobs of short calls) N = 2 measured 11.1-11.9 vs 11.8-12.4
+    # jobs/s and p50 first-answer-token 4.26-4.59 vs 4.01-4.28 s (same box, profiles/ab_arrival_window_r2.txt):
+    # a chain of short calls pays for the extra replays more than it gains on admission
     ARRIVAL_RECENT_S = 0.05
-    ARRIVAL_WINDOW = 2
+    ARRIVAL_WINDOW = int(os.environ.get("GRAG_ARRIVAL_WINDOW", "0"))
 
     def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005, watchdog_s: float = 120.0,
                  on_health=None, tp=None, start: bool = True):
@@ -109,6 +112,8 @@ class EngineRunner:
         return h
 
     def _window(self) -> int | None:
+        if self.ARRIVAL_WINDOW <= 0:
+            return None
         return self.ARRIVAL_WINDOW if time.monotonic() - self._last_submit < self.ARRIVAL_RECENT_S else None
 
     def generate(self, prompt, params: SamplingParams | None = None, on_token=None,
