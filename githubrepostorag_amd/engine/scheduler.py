@@ -223,7 +223,8 @@ class Scheduler:
             for seq in self.running:
                 if budget <= 0:
                     break
-                if seq.is_prefill:
+                out_ids = seq.output_ids
+                if seq.num_computed < len(seq.prompt_ids) + len(out_ids) - (1 if out_ids else 0):  # is_prefill
                     tgt = self.prefill_target(seq)
                     n = min(tgt - seq.num_computed, budget)
                     if n > 0 and self.kv.ensure(seq, seq.num_computed + n):
@@ -286,10 +287,14 @@ class Scheduler:
             out = []
             preempted = False
             bs = self.kv.block_size
+            running = SeqStatus.RUNNING
             for seq in list(self.running):
-                if seq.status != SeqStatus.RUNNING or seq.is_prefill:  # preempted earlier in this loop
+                if seq.status != running:  # preempted earlier in this loop
                     continue
-                L = seq.total_len
+                out_ids = seq.output_ids
+                L = len(seq.prompt_ids) + len(out_ids)  # total_len / is_prefill inlined: 512-row hot loop
+                if seq.num_computed < L - (1 if out_ids else 0):
+                    continue
                 if len(seq.blocks) * bs < L:
                     while not self.kv.ensure(seq, L):
                         if not self._preempt_one(seq):
