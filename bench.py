@@ -89,12 +89,71 @@ def parse():
                     help="1: gc.freeze() the setup objects before the timed steps (serving does the same at startup)")
     ap.add_argument("--pysample", type=float, default=0.0,
                     help="ms between stack samples of the engine thread over the timed steps (0: off; diagnostics)")
+    ap.add_argument("--arrival-cap", type=int, default=1,
+                    help="1: the harness caps the decode window to one step while an arrival's retrieval is in "
+                         "flight (an admission policy of this bench loop; the serving runner's equivalent, "
+                         "GRAG_ARRIVAL_WINDOW, is off by default).  Reported as ttft_admission_policy")
     ap.add_argument("--out", default=None)
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """``python bench.py --gpus N`` without a launcher: start N rank processes
+    of this same script (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* in their env), forward rank 0's stdout, wait for all of them and
+    return the worst exit status.  This parent imports nothing that touches
+    the GPU (no torch) and never execs: the ranks are children.  If one rank
+    fails the others are terminated (by pid) so the job cannot hang."""
+    import signal
+    import subprocess
+
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port,
+                   GRAG_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in live:  # a failed rank leaves its peers blocked in a collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        rc = 130
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     if args.switch_interval > 0:
         sys.setswitchinterval(args.switch_interval)
     import torch
@@ -268,7 +327,7 @@ def main():
             if have >= ntok:
                 break
             cap = ntok - have
-            if arrival is not None and not arrival.done():
+            if arrival is not None and not arrival.done() and args.arrival_cap:
                 # an arrival's retrieval is in flight: one decode step per replay, so the engine looks
                 # for its prompts every ~step instead of every window (TTFT no longer depends on
                 # whether retrieval beats a multi-step window)
@@ -447,6 +506,10 @@ def main():
             "dtype": "bf16" if args.quant == "none" else "w4a16 (AWQ format, group 128) decode / bf16 prefill",
             "data": "synthetic (random-init weights, clustered synthetic vectors, generated chunk texts/questions)",
             "p50_ttft_ms": round(p50, 2),
+            # p50_ttft_ms is measured under this bench loop's admission policy, not the serving runner's default
+            "ttft_admission_policy": ("harness: decode window capped to 1 step while an arrival's retrieval is in "
+                                      "flight (serving runner default: uncapped 8-step windows)")
+            if args.arrival_cap else "uncapped decode windows (serving runner default)",
             "ingest_docs_per_s": None if ingest_dps is None else round(ingest_dps, 3),
             "config": {
                 "model": f"{args.model} TP={tp} + {args.encoder}, {args.index_size}-vec {args.index_kind} index "

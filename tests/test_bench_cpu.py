@@ -11,7 +11,7 @@ from dist_utils import free_port
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TINY = ["--model", "qwen2-tiny", "--encoder", "encoder-tiny", "--index-size", "4000", "--index-kind", "ivf",
         "--nlist", "16", "--nprobe", "4", "--batch", "3", "--prompt-len", "48", "--gen-len", "5",
-        "--ingest-files", "4", "--steps", "2", "--warmup", "1"]
+        "--ingest-files", "4", "--steps", "2", "--warmup", "1", "--agent-jobs", "8", "--agent-concurrency", "4"]
 
 
 def _run(cmd, env):
@@ -49,3 +49,15 @@ def test_bench_tensor_parallel_two_ranks_gloo():
                 "--tp", "2", *TINY], env)
     assert res["config"]["parallelism"] == "tp2dp1" and res["config"]["global_batch"] == 3
     assert res["value"] > 0 and res["ingest_docs_per_s"] is None and "TP=2" in res["config"]["model"]
+
+
+def test_bench_self_launch_two_ranks():
+    """``python bench.py --gpus 2`` with no launcher spawns two rank processes
+    itself (the driver's BENCH command form): the JSON reports n_gpus 2."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2",
+               GRAG_DIST_BACKEND="gloo")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    res = _run([sys.executable, "bench.py", "--gpus", "2", *TINY], env)
+    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 6 and res["config"]["parallelism"] == "dp2"
+    assert res["value"] > 0 and "ttft_admission_policy" in res
