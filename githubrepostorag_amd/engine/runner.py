@@ -89,6 +89,9 @@ class EngineRunner:
         self.hung = False
         self.num_faults = 0
         self._step_t0: float | None = None
+        self._step_failed: BaseException | None = None  # TP: reported in the next control all-reduce
+        self._ar_failed = False
+        self.ctrl_stats = {"iterations": 0, "bytes": 0, "payloads": 0}
         self._thread = threading.Thread(target=self._loop if self.leader else self.follow, name="grag-engine",
                                         daemon=True)
         if start:
@@ -154,13 +157,80 @@ class EngineRunner:
                     h.done.set()
         return cb
 
-    # ------------------------------------------------------------------ TP
-    def _bcast(self, msg):
+    # ------------------------------------------------------------------ TP control plane
+    # One iteration of a TP group = ONE int64 SUM all-reduce of a small header over the TP group (the
+    # leader writes the control words, every rank adds its own status words; a SUM is a broadcast for
+    # the leader's words and a count for the status words), plus, only when the leader has new requests
+    # or aborts, one uint8 broadcast of their pickled payload.  A steady decode iteration therefore moves
+    # 48 bytes and syncs the host once (round 2: a pickled broadcast_object_list AND an agree() MIN
+    # all-reduce per iteration: two collectives, two host syncs).  Step status is reported in the NEXT
+    # header, so every rank applies a failure (fail / drop every in-flight request, detach the one-shot
+    # all-reduce, drop the decode graphs that captured it) at the same iteration.
+    HDR_FLAGS, HDR_WINDOW, HDR_PAYLOAD, HDR_FAILED, HDR_AR_ERR, HDR_ITER = range(6)
+    HDR_WORDS = 6
+    FLAG_STOP, FLAG_STEP = 1, 2
+
+    def _control(self, msg: dict | None) -> tuple[dict, int, int]:
+        """Collective over the TP group.  ``msg`` (leader only): {"add", "abort", "stop", "step", "window"}.
+        Returns (message, ranks whose previous step failed, ranks whose one-shot all-reduce timed out)."""
+        import pickle
+
         import torch.distributed as dist
 
-        obj = [msg]
-        dist.broadcast_object_list(obj, src=self.tp.ranks[0], group=self.tp.pg)
-        return obj[0]
+        dev = self.tp.ctrl_device(self.engine.device)
+        h = torch.zeros(self.HDR_WORDS, dtype=torch.int64)
+        payload = b""
+        if self.leader:
+            if msg["add"] or msg["abort"]:
+                payload = pickle.dumps((msg["add"], msg["abort"]), protocol=pickle.HIGHEST_PROTOCOL)
+            h[self.HDR_FLAGS] = (self.FLAG_STOP if msg["stop"] else 0) | (self.FLAG_STEP if msg["step"] else 0)
+            h[self.HDR_WINDOW] = msg["window"] or 0
+            h[self.HDR_PAYLOAD] = len(payload)
+            h[self.HDR_ITER] = self.ctrl_stats["iterations"]
+        h[self.HDR_FAILED] = 1 if self._step_failed is not None else 0
+        h[self.HDR_AR_ERR] = 1 if self._ar_failed else 0
+        t = h.to(dev)
+        dist.all_reduce(t, group=self.tp.pg)
+        h = t.tolist()
+        self.ctrl_stats["iterations"] += 1
+        self.ctrl_stats["bytes"] += 8 * self.HDR_WORDS
+        adds, aborts = [], []
+        n = h[self.HDR_PAYLOAD]
+        if n:
+            if self.leader:
+                buf = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev)
+            else:
+                buf = torch.empty(n, dtype=torch.uint8, device=dev)
+            dist.broadcast(buf, src=self.tp.ranks[0], group=self.tp.pg)
+            self.ctrl_stats["bytes"] += n
+            self.ctrl_stats["payloads"] += 1
+            if not self.leader:
+                adds, aborts = pickle.loads(buf.cpu().numpy().tobytes())
+        flags = h[self.HDR_FLAGS]
+        out = {"add": adds, "abort": aborts, "stop": bool(flags & self.FLAG_STOP),
+               "step": bool(flags & self.FLAG_STEP), "window": h[self.HDR_WINDOW] or None}
+        return out, h[self.HDR_FAILED], h[self.HDR_AR_ERR]
+
+    def _apply_group_status(self, failed: int, ar_err: int) -> None:
+        """Every rank, same iteration: a step failed somewhere in the group last iteration."""
+        local = self._step_failed
+        self._step_failed, self._ar_failed = None, False
+        if not failed and not ar_err:
+            return
+        if ar_err and self.tp.detach_custom_ar():
+            # the decode graphs captured the IPC kernel: recapture them on RCCL
+            self.engine._graphs.clear()
+            log.warning("one-shot all-reduce reported a peer timeout on %d rank(s): the TP group is back on RCCL",
+                        ar_err)
+        err = local or RuntimeError(f"{failed} TP rank(s) failed the previous engine step")
+        if self.leader:
+            self.last_error = err
+            if local is None:
+                self.num_faults += 1
+            self._set_health(False)
+            self._fail_inflight(err)
+        else:
+            self._drop_all()
 
     def follow(self) -> None:
         """Follower loop of a TP rank: mirror the leader's request stream and
@@ -173,7 +243,8 @@ class EngineRunner:
                 self.engine.pop(seq.req_id)
 
         while True:
-            msg = self._bcast(None)
+            msg, failed, ar_err = self._control(None)
+            self._apply_group_status(failed, ar_err)
             for rid, ids, params in msg["add"]:
                 try:
                     self.engine.add_request(ids, params, req_id=rid, on_token=drop)
@@ -183,24 +254,25 @@ class EngineRunner:
                 self.engine.abort(rid)
             if msg["stop"]:
                 break
-            if not msg.get("step", True):
+            if not msg["step"]:
                 continue
-            ok = True
             try:
-                self.engine.step(max_window=msg.get("window"))
+                self.engine.step(max_window=msg["window"])
             except Exception as e:
                 log.exception("TP follower step failed")
                 self.last_error = e
                 self.num_faults += 1
-                ok = False
-            # every rank learns whether the step succeeded everywhere, so all
-            # ranks fail the same requests and stay in lockstep
-            if not self.tp.agree(ok, self.engine.device):
-                self._drop_all()
+                self._note_failure(e)
+
+    def _note_failure(self, e: BaseException) -> None:
+        from ..parallel.custom_ar import CommError
+
+        self._step_failed = e
+        self._ar_failed = self._ar_failed or isinstance(e, CommError)
 
     def _drop_all(self) -> None:
         """Follower side of a failed step: cancel every in-flight sequence
-        (the leader fails the same requests in _fail_all)."""
+        (the leader fails the same requests in _fail_inflight)."""
         for rid in list(self.engine._seqs):
             self.engine.abort(rid)
         try:
@@ -217,10 +289,11 @@ class EngineRunner:
             torch.cuda.set_device(self.engine.device)
         while True:
             with self._cv:
-                while not self._stop and not self._pending and not self._aborts and not self.engine.has_unfinished():
+                while (not self._stop and not self._pending and not self._aborts
+                       and not self.engine.has_unfinished() and self._step_failed is None):
                     self._cv.wait(timeout=1.0)
                     if self.tp is not None:
-                        break  # idle heartbeat: followers block in the broadcast meanwhile
+                        break  # idle heartbeat: followers block in the control all-reduce meanwhile
                 stop = self._stop
                 pending, self._pending = self._pending, []
                 aborts, self._aborts = self._aborts, []
@@ -231,8 +304,9 @@ class EngineRunner:
                 for rid, prompt, params, cb in pending:
                     ids = self.engine.tok.encode(prompt) if isinstance(prompt, str) else list(prompt)
                     adds.append((rid, ids, params or SamplingParams()))
-                self._bcast({"add": adds, "abort": aborts, "stop": stop, "step": will_step and not stop,
-                             "window": win})
+                _, failed, ar_err = self._control({"add": adds, "abort": aborts, "stop": stop,
+                                                   "step": will_step and not stop, "window": win})
+                self._apply_group_status(failed, ar_err)
                 pending = [(rid, ids, p, cb) for (rid, ids, p), (_, _, _, cb) in zip(adds, pending)]
             if stop:
                 break
@@ -257,8 +331,17 @@ class EngineRunner:
                 log.exception("engine step failed")
                 err = e
             self._step_t0 = None
-            if self.tp is not None and not self.tp.agree(err is None, self.engine.device) and err is None:
-                err = RuntimeError("a TP follower rank failed this engine step")
+            if self.tp is not None:
+                # under TP the outcome is applied by every rank at the next control all-reduce
+                if err is not None:
+                    self.last_error = err
+                    self.num_faults += 1
+                    self._note_failure(err)
+                elif self.hung:
+                    self.hung = False
+                elif self._step_failed is None:
+                    self._set_health(True)
+                continue
             if err is None:
                 if self.hung:
                     log.warning("engine step returned after the watchdog fired; marking healthy again")
@@ -309,6 +392,22 @@ class EngineRunner:
                 self._aborts.append(rid)
         else:
             self.engine.abort(rid)
+
+    def _fail_inflight(self, err: BaseException) -> None:
+        """Fail the requests already inside the engine (not the ones still queued for admission)."""
+        with self._cv:
+            rids = [r for r in list(self.engine._seqs) if r in self._handles]
+            handles = [(r, self._handles.pop(r)) for r in rids]
+        for rid in list(self.engine._seqs):
+            self.engine.abort(rid)
+        for rid, h in handles:
+            h.error = err
+            h.done.set()
+        try:
+            for s in self.engine.sched.reap_cancelled():
+                self.engine.pop(s.req_id)
+        except Exception:
+            pass
 
     def _fail_all(self, err: BaseException) -> None:
         with self._cv:

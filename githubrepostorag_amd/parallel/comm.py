@@ -121,17 +121,34 @@ class Group:
             ar.stage_error_check()
 
     def check_health(self) -> None:
-        """After the step's sync: raise if a one-shot all-reduce of this step
-        timed out on a peer.  The custom all-reduce is then detached for good
-        (RCCL from here on) so the failure cannot repeat with stale epochs."""
+        """After the step's sync: raise ``CommError`` if a one-shot all-reduce
+        of this step timed out on a peer.  The detach is NOT decided here: one
+        rank's error word says nothing about its peers, and a rank that went
+        back to RCCL alone would meet its peers' IPC kernels in the next
+        collective.  The engine runner counts the error in its next control
+        all-reduce and every rank calls ``detach_custom_ar`` at that same
+        iteration (engine/runner.py)."""
+        ar = self.custom_ar
+        if ar is not None:
+            ar.raise_if_failed()
+
+    def detach_custom_ar(self) -> bool:
+        """Leave the one-shot all-reduce for RCCL (every rank of the group at the
+        same iteration; decode graphs that captured the IPC kernel must be
+        dropped by the caller).  The IPC regions stay mapped: graphs or peers
+        may still hold their addresses until they are gone."""
         ar = self.custom_ar
         if ar is None:
-            return
-        try:
-            ar.raise_if_failed()
-        except Exception:
-            self.custom_ar = None
-            raise
+            return False
+        ar.reset_error()
+        self.custom_ar = None
+        return True
+
+    def ctrl_device(self, device=None):
+        """Where a small control tensor of this group lives (RCCL: the GPU, gloo: the host)."""
+        if device is not None and torch.device(device).type == "cuda" and _INFO.backend == "nccl":
+            return torch.device(device)
+        return torch.device("cpu")
 
     def agree(self, ok: bool, device=None) -> bool:
         """All ranks learn whether every rank's step succeeded (MIN all-reduce
@@ -143,9 +160,7 @@ class Group:
         replicated scheduling needs identical pools on every TP rank)."""
         if self.trivial:
             return int(v)
-        dev = device if device is not None and torch.device(device).type == "cuda" and _INFO.backend == "nccl" \
-            else "cpu"
-        t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+        t = torch.tensor([int(v)], dtype=torch.int64, device=self.ctrl_device(device))
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.pg)
         return int(t.item())
 

@@ -239,3 +239,81 @@ def test_tp_runner_replicated_scheduling():
                     [[5, 17, 99, 3, 250], [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]])
     res = run_ranks(_tp_runner_worker, 2, "qwen2-tiny")
     assert res[0] == ref and res[1] is None
+
+
+class _FakeAR:
+    """Stands in for the one-shot IPC all-reduce on CPU: never takes a message
+    (fits() is False, so RCCL/gloo does the work) but reports a peer timeout
+    from its error word on one rank at a chosen health check."""
+
+    def __init__(self, fail_at):
+        self.fail_at, self.checks, self.resets = fail_at, 0, 0
+
+    def fits(self, t):
+        return False
+
+    def stage_error_check(self):
+        pass
+
+    def raise_if_failed(self):
+        from githubrepostorag_amd.parallel.custom_ar import CommError
+
+        self.checks += 1
+        if self.checks == self.fail_at:
+            raise CommError("injected one-shot all-reduce timeout")
+
+    def reset_error(self):
+        self.resets += 1
+
+
+def _tp_ar_detach_worker(rank, world, cfg_name, bad_rank):
+    """A one-shot all-reduce timeout on ONE rank: every rank must leave the IPC
+    path at the same iteration (group-wide decision in the control all-reduce),
+    drop its captured decode graphs, and keep serving on the process group."""
+    from githubrepostorag_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from githubrepostorag_amd.engine.runner import EngineRunner
+    from githubrepostorag_amd.engine.sequence import SamplingParams
+    from githubrepostorag_amd.engine.tokenizer import ByteBPETokenizer
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import Qwen2Model
+    from githubrepostorag_amd.parallel.comm import make_tp_dp_groups
+
+    cfg = decoder_config(cfg_name)
+    tp, _ = make_tp_dp_groups(world)
+    tp.custom_ar = _FakeAR(fail_at=3 if rank == bad_rank else -1)
+    model = Qwen2Model(cfg, device="cpu", dtype=torch.float32, tp=tp, state_dict=_hf_state_dict(cfg))
+    eng = LLMEngine(model, ByteBPETokenizer(cfg.vocab_size),
+                    EngineConfig(max_num_seqs=4, max_model_len=256, num_blocks=64, use_cuda_graph=False))
+    eng._graphs[("sentinel",)] = object()  # stands for decode graphs that captured the IPC kernel
+    runner = EngineRunner(eng, tp=tp, watchdog_s=0)
+    if rank != 0:
+        runner.join(120)
+        return tp.custom_ar is None, len(eng._graphs), runner.ctrl_stats
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    first = None
+    try:
+        runner.generate([5, 17, 99, 3, 250], sp, timeout=60)
+    except Exception as e:
+        first = type(e).__name__
+    second = runner.generate([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12], sp, timeout=60).token_ids
+    runner.shutdown()
+    return tp.custom_ar is None, len(eng._graphs), runner.ctrl_stats, first, second
+
+
+def test_tp_custom_ar_timeout_detaches_group_wide():
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import Qwen2Model
+
+    cfg = decoder_config("qwen2-tiny")
+    ref = _generate(Qwen2Model(cfg, device="cpu", dtype=torch.float32, state_dict=_hf_state_dict(cfg)),
+                    [[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]])
+    for bad in (1, 0):
+        res = run_ranks(_tp_ar_detach_worker, 2, "qwen2-tiny", bad)
+        lead, fol = res[0], res[1]
+        assert lead[0] and fol[0], res  # both ranks detached
+        assert lead[1] == 0 and fol[1] == 0, res  # both dropped their graphs
+        assert lead[3] in ("CommError", "RuntimeError") and lead[4] == ref[0], res
+        # steady iterations move only the 48-byte header; payloads only with new requests
+        st = lead[2]
+        assert st["iterations"] > 0 and st["payloads"] >= 2
+        assert st["bytes"] - 48 * st["iterations"] < 4096 * st["payloads"]
