@@ -103,14 +103,47 @@ class ShardedIndex:
         return self.table.count()
 
     def _local(self, Q: torch.Tensor, k: int, flt: dict | None = None):
+        """This shard's top-k for every query, with the whole filter applied the way
+        ``VectorTable.search`` applies it: up to four predicates fused in the scan,
+        further ones ANDed into the row bitmap, and host-side checks (unindexed
+        fields; the exact test behind a multi-value field's bloom bit) on an
+        over-fetched candidate list, so no filter is dropped."""
+        from .store import OP_EQ, _and_bitmap
+
         t = self.table
         nq = Q.shape[0]
+        empty = (torch.full((nq, k), float("-inf"), device=Q.device),
+                 torch.full((nq, k), -1, dtype=torch.long, device=Q.device))
         with t.lock:
             pc = t.predicates(flt)
             if pc is None or t.n == 0:
-                return (torch.full((nq, k), float("-inf"), device=Q.device),
-                        torch.full((nq, k), -1, dtype=torch.long, device=Q.device))
-            s, i = t._scan(Q.to(self.device, t.dtype), k, pc[0][:4], t.live, None)
+                return empty
+            preds, checks = pc
+            bitmap = t.live
+            if len(preds) > 4:
+                m = torch.ones(t.n, dtype=torch.bool, device=self.device)
+                for p in preds[4:]:
+                    c = p.column[: t.n]
+                    m &= (c == p.value) if p.op == OP_EQ else ((c & p.value) != 0)
+                bitmap = _and_bitmap(t.live, m)
+                preds = preds[:4]
+            kk = max(k, min(32, k + 8)) if checks else k
+            s, i = t._scan(Q.to(self.device, t.dtype), kk, preds, bitmap, None)
+            t._track_read()
+        if checks:  # exact host checks on the over-fetched rows, then back to [nq, k]
+            sl, il = s.float().cpu().tolist(), i.cpu().tolist()
+            out_s = torch.full((nq, k), float("-inf"))
+            out_i = torch.full((nq, k), -1, dtype=torch.long)
+            for q in range(nq):
+                j = 0
+                for sc, r in zip(sl[q], il[q]):
+                    if r < 0 or j >= k or not t._host_ok(t.rows.get(r)[2], checks):
+                        continue
+                    out_s[q, j], out_i[q, j] = sc, r
+                    j += 1
+            s, i = out_s.to(Q.device), out_i.to(Q.device)
+        elif kk > k:
+            s, i = s[:, :k], i[:, :k]
         return s.float(), self.global_ids(i)
 
     @guarded

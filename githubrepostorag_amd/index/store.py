@@ -271,6 +271,25 @@ class VectorTable:
         self._counts: dict = {}
         # write hook (service/cluster.py mirrors ingest writes to the other replicas): fn(op, args)
         self.on_write = None
+        # searches launch under the lock and read their results back after releasing it; a writer
+        # (which may reallocate or re-sort the device arrays) first waits for every launched search
+        self._readers: list = []
+
+    def _track_read(self) -> None:
+        """Under the lock, after a search's launches: remember its completion event."""
+        if self.device.type != "cuda":
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        if len(self._readers) >= 64:
+            self._readers = [e for e in self._readers if not e.query()]
+        self._readers.append(ev)
+
+    def _drain_readers(self) -> None:
+        """Under the lock, before mutating device arrays: no in-flight search may still read them."""
+        readers, self._readers = self._readers, []
+        for ev in readers:
+            ev.synchronize()
 
     @property
     def ivf(self) -> bool:
@@ -358,6 +377,7 @@ class VectorTable:
         vecs = vecs / vecs.norm(dim=-1, keepdim=True).clamp_min(1e-12)
         metadatas = [dict(m or {}) for m in metadatas]
         with self.lock, side_stream(self.device, wait_caller=vectors.is_cuda):
+            self._drain_readers()
             rows = np.empty(n, dtype=np.int64)
             fresh = []
             for i, rid in enumerate(row_ids):
@@ -404,6 +424,7 @@ class VectorTable:
     @guarded
     def delete(self, row_ids: list[str]) -> int:
         with self.lock, side_stream(self.device):
+            self._drain_readers()
             rows = [self.rows.lookup(r) for r in row_ids]
             rows = np.asarray([r for r in rows if r is not None], dtype=np.int64)
             if rows.size == 0:
@@ -434,6 +455,7 @@ class VectorTable:
         ``provider.register(table)``); host rows are generated on demand.  Returns row0."""
         n = vectors.shape[0]
         with self.lock, side_stream(self.device, wait_caller=vectors.is_cuda):
+            self._drain_readers()
             r0 = self.rows.append_virtual(provider, n)
             if columns is None and hasattr(provider, "columns"):
                 provider.register(self)
@@ -465,6 +487,7 @@ class VectorTable:
         when the table is one shard of a DP index), assign the append
         region, and re-sort every live slot by inverted list (tombstones dropped)."""
         with self.lock, side_stream(self.device):
+            self._drain_readers()
             self._compact_locked(train_iters, sample, seed, group)
 
     def _compact_locked(self, train_iters: int = 10, sample: int = 1 << 18, seed: int = 0, group=None) -> None:
@@ -659,6 +682,7 @@ class VectorTable:
                 q = qvecs.to(self.device, self.dtype)
                 kk = min(32, k + (8 if checks else 0))
                 scores, ids = self._scan(q, kk, preds, bitmap, qpred)
+                self._track_read()
             scores, ids = scores.cpu().tolist(), ids.cpu().tolist()
         out = []
         for qi in range(nq):

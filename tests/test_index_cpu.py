@@ -119,3 +119,13 @@ def test_query_embedding_batcher_coalesces_threads():
     for i in range(len(qs)):
         assert torch.allclose(out[i].float(), ref[i].float(), atol=2e-2)
     emb.close()
+
+
+def test_search_concurrent_with_upsert_and_compaction_cpu():
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location("tig", os.path.join(os.path.dirname(__file__), "test_index_gpu.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod._search_while_writing(torch.device("cpu"), rounds=12)

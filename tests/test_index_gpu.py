@@ -133,3 +133,43 @@ def test_ivf_upsert_delete_compact_snapshot(dev, tmp_path):
 def test_store_honours_index_kind(dev):
     st = VectorStore(64, dev, index_kind="ivf", nlist=16, nprobe=4)
     assert all(t.index_kind == "ivf" for t in st.tables.values())
+
+
+def _search_while_writing(dev, rounds=40):
+    """Searches on a helper thread while the main thread upserts (growing the device arrays)
+    and compacts (re-sorting them in place): every search must still return its anchor row."""
+    import threading
+
+    d = 64
+    g = torch.Generator(device="cpu").manual_seed(5)
+    tab = VectorTable("stress", d, dev, capacity=64, index_kind="ivf", nlist=16, nprobe=16, compact_min=256,
+                      compact_frac=0.05)
+    anchors = torch.nn.functional.normalize(torch.randn(32, d, generator=g), dim=1)
+    tab.upsert([f"a{i}" for i in range(32)], ["anchor"] * 32, anchors.to(dev), [{"repo": "a"}] * 32)
+    errors, stop = [], threading.Event()
+
+    def reader():
+        while not stop.is_set():
+            hits = tab.search(anchors.to(dev), 1)
+            for i, h in enumerate(hits):
+                if not h or h[0].row_id != f"a{i}":
+                    errors.append((i, h[0].row_id if h else None))
+
+    th = threading.Thread(target=reader)
+    th.start()
+    try:
+        for r in range(rounds):
+            noise = torch.nn.functional.normalize(torch.randn(200, d, generator=g), dim=1) * 0.3
+            noise = torch.nn.functional.normalize(noise + torch.randn(1, d, generator=g), dim=1)
+            tab.upsert([f"n{r}_{i}" for i in range(200)], ["noise"] * 200, noise.to(dev), [{"repo": "n"}] * 200)
+            if r % 7 == 6:
+                tab.compact()
+    finally:
+        stop.set()
+        th.join()
+    assert tab.stats["compactions"] > 0
+    assert not errors, errors[:5]
+
+
+def test_search_concurrent_with_upsert_and_compaction(dev):
+    _search_while_writing(dev)
