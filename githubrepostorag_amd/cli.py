@@ -43,10 +43,10 @@ def _settings(args):
     return s
 
 
-def _runtime(args, build_engine=True):
+def _runtime(args, build_engine=True, shard=None):
     from .service.runtime import RAGRuntime
 
-    return RAGRuntime(_settings(args), build_engine=build_engine)
+    return RAGRuntime(_settings(args), build_engine=build_engine, shard=shard)
 
 
 def cmd_serve(args) -> int:
@@ -103,7 +103,8 @@ def _serve_front_door(args, s, replicas: int) -> int:
         v = getattr(args, k, None)
         if v:
             fwd += [f"--{k.replace('_', '-')}", v]
-    procs = spawn_replicas(replicas, hub.address, hub.authkey, fwd, gpus=gpus[:replicas])
+    shards = replicas if s.index_sharding == "shard" else 1
+    procs = spawn_replicas(replicas, hub.address, hub.authkey, fwd, gpus=gpus[:replicas], shards=shards)
     state = APIState(runtime=ClusterRuntimeView(hub, s), queue=hub.queue, events=events, flags=hub.flags,
                      ping_seconds=s.sse_ping_seconds)
     app = create_app(state)
@@ -129,13 +130,17 @@ def cmd_replica(args) -> int:
 
         mod, fn = args.factory.split(":")
         rt = getattr(importlib.import_module(mod), fn)(s)
+        if args.shards > 1 and getattr(rt, "store", None) is not None:
+            from .index.sharded_store import retain_shard
+
+            retain_shard(rt.store, args.rank, args.shards)  # a factory builds full tables: keep this shard
     else:
-        rt = _runtime(args)
+        rt = _runtime(args, shard=(args.rank, args.shards) if args.shards > 1 else None)
         rt.warmup()
     host, port = args.hub.rsplit(":", 1)
     key = bytes.fromhex(os.environ["GRAG_HUB_AUTHKEY"])
     try:
-        return run_replica(rt, (host, int(port)), key, args.rank)
+        return run_replica(rt, (host, int(port)), key, args.rank, shards=args.shards)
     finally:
         if hasattr(rt, "close"):
             rt.close()
@@ -220,6 +225,7 @@ def main(argv=None) -> int:
     common(p)
     p.add_argument("--hub", required=True, help="host:port of the front door's replica hub")
     p.add_argument("--rank", type=int, default=0)
+    p.add_argument("--shards", type=int, default=1, help="this replica holds shard RANK of SHARDS (index sharding)")
     p.add_argument("--factory", default=None, help="module:function(settings) -> runtime (tests)")
     p = sub.add_parser("ingest", help="ingest repositories into the index")
     common(p)

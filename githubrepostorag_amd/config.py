@@ -76,6 +76,9 @@ class Settings:
     device: str = field(default_factory=lambda: _env("DEVICE", "auto"))
     tp: int = field(default_factory=lambda: _int("TP", 1))
     dp: int = field(default_factory=lambda: _int("DP", 1))  # serve: replicas behind one front door
+    # serve --replicas N: "shard" = each replica holds 1/N of every table, searches fan out through the
+    # front door's hub (index/sharded_store.py); "mirror" = full copies, ingest writes broadcast
+    index_sharding: str = field(default_factory=lambda: _env("INDEX_SHARDING", "shard"))
     max_num_seqs: int = field(default_factory=lambda: _int("MAX_NUM_SEQS", 64))
     max_model_len: int = field(default_factory=lambda: _int("MAX_MODEL_LEN", 11712))
     max_num_batched_tokens: int = field(default_factory=lambda: _int("MAX_NUM_BATCHED_TOKENS", 16384))

@@ -699,6 +699,45 @@ class VectorTable:
             out.append(hits)
         return out
 
+    def search_pairs(self, q: torch.Tensor, pairs, k: int, base_filter: dict | None = None) -> list[list[Hit]]:
+        """Graph-traversal lookups (retrieval/graph.py): for each ``(field, value)``
+        pair, the ``k`` rows most similar to the one query ``q`` [1, d] whose
+        ``field`` equals ``value`` (on top of ``base_filter``).  Every indexed pair
+        of a call is ONE launch of the fused score+top-k kernel with per-query
+        predicates (the query repeated, each copy carrying its own ``column ==
+        code`` test); unindexed fields fall back to one filtered search each.
+        Pairs whose value this table has never stored return no rows."""
+        q = q.reshape(1, -1)
+        cols: list[tuple[str, torch.Tensor]] = []
+        col_idx: dict[str, int] = {}
+        sel, vals, slot = [], [], []
+        host_pairs = []
+        out: list[list[Hit]] = [[] for _ in pairs]
+        for j, (f, v) in enumerate(pairs):
+            if f in FILTER_FIELDS:
+                code = self.dicts[f].get(str(v))
+                if code is None:  # value never seen in this table: no row can match
+                    continue
+                if f not in col_idx:
+                    col_idx[f] = len(cols)
+                    cols.append((f, self.columns[f]))
+                sel.append(col_idx[f])
+                vals.append(code)
+                slot.append(j)
+            else:
+                host_pairs.append(j)
+        if slot:
+            Q = q.expand(len(slot), -1).contiguous()
+            dev = self.device
+            qpred = ([c for _, c in cols], torch.tensor(sel, dtype=torch.int32, device=dev),
+                     torch.tensor(vals, dtype=torch.int32, device=dev))
+            for j, hits in zip(slot, self.search(Q, k, base_filter, qpred=qpred)):
+                out[j] = hits
+        for j in host_pairs:  # unindexed edge field: filtered search per value
+            f, v = pairs[j]
+            out[j] = self.search(q, k, dict(base_filter or {}, **{f: v}))[0]
+        return out
+
     # ------------------------------------------------------------------ persistence
     def save(self, path: str | Path) -> None:
         path = Path(path)

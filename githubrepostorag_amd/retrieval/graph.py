@@ -23,7 +23,7 @@ from dataclasses import dataclass, field
 
 import torch
 
-from ..index.store import FILTER_FIELDS, Hit, VectorTable
+from ..index.store import Hit, VectorTable
 from ..utils.gpu_guard import side_stream
 
 
@@ -110,35 +110,10 @@ class GraphRetriever:
         return out[: self.k]
 
     def _adjacent(self, q: torch.Tensor, pairs, base_filter) -> list[list[Hit]]:
-        """All (dst_field, value) lookups of one depth in one fused launch."""
-        tab = self.table
-        cols: list[tuple[str, torch.Tensor]] = []
-        col_idx: dict[str, int] = {}
-        sel, vals, keep = [], [], []
-        host_pairs = []
-        for f, v in pairs:
-            if f in FILTER_FIELDS:
-                code = tab.dicts[f].get(v)
-                if code is None:  # value never seen in this table: no row can match
-                    continue
-                if f not in col_idx:
-                    col_idx[f] = len(cols)
-                    cols.append((f, tab.columns[f]))
-                sel.append(col_idx[f])
-                vals.append(code)
-                keep.append((f, v))
-            else:
-                host_pairs.append((f, v))
-        results: list[list[Hit]] = []
-        if keep:
-            Q = q.expand(len(keep), -1).contiguous()
-            dev = tab.device
-            qpred = ([c for _, c in cols], torch.tensor(sel, dtype=torch.int32, device=dev),
-                     torch.tensor(vals, dtype=torch.int32, device=dev))
-            results = tab.search(Q, self.adjacent_k, base_filter, qpred=qpred)
-        for f, v in host_pairs:  # unindexed edge field: filtered search per value
-            results += tab.search(q, self.adjacent_k, dict(base_filter or {}, **{f: v}))
-        return results
+        """All (dst_field, value) lookups of one depth: one fused launch on a local
+        table (``VectorTable.search_pairs``), one fan-out round on a sharded one
+        (``index/sharded_store.py``)."""
+        return self.table.search_pairs(q, pairs, self.adjacent_k, base_filter)
 
 
 class RetrieverFactory:

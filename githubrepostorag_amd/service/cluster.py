@@ -19,16 +19,27 @@ event.  Every event a replica's worker emits is forwarded and appended to the
 front door's replayable EventLog, so ``GET /rag/jobs/{id}/events`` is one SSE
 endpoint for the whole node; cancels are forwarded to the owning replica; a
 replica that disconnects fails its in-flight jobs (``error`` + ``final``) and
-the hub stops dispatching to it.  Ingest writes (``VectorStore`` upserts made on
-one replica) are broadcast to the others so every replica serves the same
-index (288 GB of HBM holds a full 10M-vector table per GPU, so replicas keep
-full copies and a search never crosses xGMI).
+the hub stops dispatching to it.
+
+The index (INDEX_SHARDING, default ``shard``): each replica holds 1/N of every
+scope table (index/sharded_store.py, rows owned by crc32(row_id) mod N) and
+the hub routes the shard rounds: a replica's search / traversal round is
+fanned out to every other live replica (C4), their per-shard top-k lists are
+routed back to it (C3) and merged there with its own shard's; an ingest write
+goes to the owning replica only.  A replica lost mid-round answers with an
+empty part (its rows are missing from that answer, nothing hangs).
+``INDEX_SHARDING=mirror`` keeps the round-2 mode: full copies, every ingest
+write broadcast to every replica.
 
 Wire messages (pickled tuples over the authenticated socket, our own processes
 only):
   replica -> hub: ("hello", rank, capacity, info) | ("event", job, name, data)
-                  | ("health", info) | ("upsert", table, payload)
+                  | ("health", info) | ("upsert", table, payload)          [mirror]
+                  | ("shard_req", req, scope, op, payload)                 [shard round]
+                  | ("shard_res", origin, req, result) | ("shard_write", owner, scope, op, payload)
   hub -> replica: ("run", job, request) | ("cancel", job) | ("upsert", table, payload) | ("stop",)
+                  | ("shard_plan", req, n_parts) | ("shard_part", req, rank, result)
+                  | ("shard_exec", origin, req, scope, op, payload) | ("shard_apply", scope, op, payload)
 """
 from __future__ import annotations
 
@@ -103,6 +114,11 @@ class ReplicaHub:
         self._loop: asyncio.AbstractEventLoop | None = None
         self._slot_cond: asyncio.Condition | None = None
         self.flags = HubCancelFlags(self)
+        # shard rounds in flight, by the replica that still owes a part: {rank: {(origin, req)}}
+        self._shard_pending: dict[int, set] = {}
+        # jobs the front door timed out whose replica has not sent its final event yet: {job: replica}
+        self._timed_out: dict[str, _Replica] = {}
+        self.timeout_grace = 60.0
         # the front door's queue admits as many jobs as the replicas have slots; the rest wait in FIFO order
         self.queue = JobQueue({"run_rag_job": self.run_rag_job}, max_jobs=256, job_timeout=job_timeout,
                               keep_result=keep_result)
@@ -147,25 +163,65 @@ class ReplicaHub:
                 kind = msg[0]
                 if kind == "event":
                     _, job_id, name, data = msg
+                    if job_id in self._timed_out:  # the client already got error + final
+                        if name == "final":
+                            self._timed_out.pop(job_id, None)
+                            self._finish(job_id)
+                        continue
                     self.events.emit_sync(job_id, name, data)
                     if name == "final":
                         self._finish(job_id)
                 elif kind == "health":
-                    rep.info = msg[1]
-                elif kind == "upsert":  # an ingest on this replica: mirror it on every other replica
+                    rep.info = {**rep.info, **msg[1]}  # hello fields (pid, shard) persist
+                elif kind == "upsert":  # mirror mode: an ingest on this replica, applied on every other one
                     for other in self.live_replicas():
                         if other is not rep:
                             other.send(msg)
+                elif kind == "shard_req":
+                    self._shard_fanout(rep, *msg[1:])
+                elif kind == "shard_res":
+                    _, origin, req, result = msg
+                    with self._lock:
+                        self._shard_pending.get(rep.rank, set()).discard((origin, req))
+                        o = self.replicas.get(origin)
+                    if o is not None:
+                        o.send(("shard_part", req, rep.rank, result))
+                elif kind == "shard_write":
+                    _, owner, scope, op, payload = msg
+                    with self._lock:
+                        o = self.replicas.get(owner)
+                    if o is None or not o.send(("shard_apply", scope, op, payload)):
+                        log.warning("shard write for replica %d dropped: replica not connected", owner)
         except (EOFError, OSError, ConnectionResetError):
             pass
         finally:
             if rep is not None:
                 self._fail_replica(rep, "replica disconnected")
 
+    def _shard_fanout(self, origin: _Replica, req, scope, op, payload) -> None:
+        """C4 of one shard round: every other live replica runs ``op`` on its shard."""
+        targets = [r for r in self.live_replicas() if r is not origin]
+        with self._lock:
+            for t in targets:
+                self._shard_pending.setdefault(t.rank, set()).add((origin.rank, req))
+        origin.send(("shard_plan", req, len(targets)))
+        for t in targets:
+            if not t.send(("shard_exec", origin.rank, req, scope, op, payload)):
+                with self._lock:
+                    self._shard_pending.get(t.rank, set()).discard((origin.rank, req))
+                origin.send(("shard_part", req, t.rank, None))
+
     def _fail_replica(self, rep: _Replica, why: str) -> None:
         with rep.lock:
             was_alive = rep.alive
             rep.alive = False
+        with self._lock:
+            owed = self._shard_pending.pop(rep.rank, set())
+        for origin, req in owed:  # rounds still waiting for this replica's part: answer them empty
+            with self._lock:
+                o = self.replicas.get(origin)
+            if o is not None:
+                o.send(("shard_part", req, rep.rank, None))
         with self._lock:
             if self.replicas.get(rep.rank) is rep:
                 self.replicas.pop(rep.rank, None)
@@ -279,11 +335,27 @@ class ReplicaHub:
             rep.send(("cancel", job_id))
 
     async def _on_timeout(self, job_id: str, req: dict) -> None:
+        """The client gets error + final now; the replica's slot stays taken until the replica
+        reports the (cooperatively) cancelled job's final event, or ``timeout_grace`` passes, so the
+        hub never sends a replica more jobs than it advertised capacity for."""
+        with self._lock:
+            rep = self.owner.get(job_id)
+            if rep is not None:
+                self._timed_out[job_id] = rep
         self.flags.cancel_sync(job_id)
         if not self.events.is_closed(job_id):
             await self.events.emit(job_id, "error", {"message": f"job timed out after {self.queue.job_timeout}s"})
             await self.events.emit(job_id, "final", {"answer": "", "sources": None, "error": True})
-        self._finish(job_id)
+        if rep is None:
+            self._finish(job_id)
+            return
+
+        def _deadline():
+            if self._timed_out.pop(job_id, None) is not None:
+                log.warning("replica %d never finished timed-out job %s; freeing its slot", rep.rank, job_id)
+                self._finish(job_id)
+
+        asyncio.get_running_loop().call_later(self.timeout_grace, _deadline)
 
     def health(self) -> dict:
         reps = sorted(self.live_replicas(), key=lambda r: r.rank)
@@ -328,9 +400,72 @@ class _ForwardingEvents(EventLog):
     emit_threadsafe = emit_sync
 
 
+class HubShardTransport:
+    """A replica's end of the shard rounds routed by the hub (index/sharded_store.py transport)."""
+
+    def __init__(self, send, rank: int):
+        import itertools
+
+        self._send = send
+        self.rank = rank
+        self._ids = itertools.count()
+        self._lock = threading.Lock()
+        self._rounds: dict[int, dict] = {}
+
+    def fanout(self, origin: int, scope: str, op: str, payload, timeout: float = 60.0) -> list:
+        req = next(self._ids)
+        st = {"n": None, "parts": [], "ev": threading.Event()}
+        with self._lock:
+            self._rounds[req] = st
+        try:
+            self._send(("shard_req", req, scope, op, payload))
+            if not st["ev"].wait(timeout):
+                log.warning("shard %s round %d on %s: %d of %s parts after %.0fs", op, req, scope,
+                            len(st["parts"]), st["n"], timeout)
+            return [p for p in st["parts"] if p is not None]
+        finally:
+            with self._lock:
+                self._rounds.pop(req, None)
+
+    def write(self, origin: int, owner: int, scope: str, op: str, payload) -> None:
+        self._send(("shard_write", owner, scope, op, payload))
+
+    def deliver(self, msg) -> None:
+        """Reader thread: a plan or a part of one of this replica's rounds."""
+        kind, req = msg[0], msg[1]
+        with self._lock:
+            st = self._rounds.get(req)
+            if st is None:
+                return
+            if kind == "shard_plan":
+                st["n"] = msg[2]
+            else:
+                st["parts"].append(msg[3])
+            if st["n"] is not None and len(st["parts"]) >= st["n"]:
+                st["ev"].set()
+
+
+def attach_sharded_store(runtime, transport, rank: int, nshards: int):
+    """Serve ``runtime``'s (already shard-local) store as shard ``rank`` of ``nshards``:
+    the agent's retrievers and the ingest writer see the union of all shards."""
+    from ..index.sharded_store import ShardedStore
+    from ..retrieval.graph import RetrieverFactory
+
+    local = runtime.store
+    runtime.local_store = local
+    runtime.store = ShardedStore(local, rank, nshards, transport)
+    runtime.retrievers = RetrieverFactory(runtime.store, runtime.embedder)
+    return local
+
+
 def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | None = None,
-                health_every: float = 5.0) -> int:
-    """Serve jobs from the hub until it says stop or the connection drops (blocking)."""
+                health_every: float = 5.0, shards: int = 1) -> int:
+    """Serve jobs from the hub until it says stop or the connection drops (blocking).
+    ``shards`` > 1: this replica holds shard ``rank`` of a row-sharded index and answers
+    the other replicas' shard rounds (service/cluster.py docstring)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from ..index.sharded_store import execute
     from .worker import RAGWorker
 
     s = runtime.settings
@@ -342,13 +477,38 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
         with send_lock:
             conn.send(msg)
 
+    transport = None
+    local_store = getattr(runtime, "store", None)
+    if shards > 1 and local_store is not None:
+        transport = HubShardTransport(send, rank)
+        local_store = attach_sharded_store(runtime, transport, rank, shards)
+    # other replicas' shard rounds and routed writes run here, off the job loop (GPU search + sync)
+    shard_pool = ThreadPoolExecutor(4, thread_name_prefix="shard-exec")
     events = _ForwardingEvents(send)
     flags = CancelFlags()
     worker = RAGWorker(runtime, events, flags, cap, s.job_timeout_s, s.keep_result_s, s.stream_tokens)
     store = getattr(runtime, "store", None)
-    if store is not None and hasattr(store, "add_listener"):
+    if transport is None and store is not None and hasattr(store, "add_listener"):
         store.add_listener(lambda table, payload: send(("upsert", table, payload)))
-    send(("hello", rank, cap, {"device": str(getattr(runtime, "device", "cpu")), "pid": os.getpid()}))
+    send(("hello", rank, cap, {"device": str(getattr(runtime, "device", "cpu")), "pid": os.getpid(),
+                               "shard": f"{rank}/{shards}" if transport is not None else "full"}))
+
+    def shard_exec(origin, req, scope, op, payload):
+        try:
+            res = execute(local_store, scope, op, payload)
+        except Exception:  # answer the round anyway: the origin must not wait for a failed shard
+            log.exception("shard %s on %s for replica %d failed", op, scope, origin)
+            res = None
+        try:
+            send(("shard_res", origin, req, res))
+        except (OSError, EOFError):
+            pass
+
+    def shard_apply(scope, op, payload):
+        try:
+            execute(local_store, scope, op, payload)
+        except Exception:
+            log.exception("routed shard write (%s on %s) failed", op, scope)
 
     async def main():
         loop = asyncio.get_running_loop()
@@ -357,7 +517,16 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
         def reader():
             try:
                 while True:
-                    loop.call_soon_threadsafe(inbox.put_nowait, conn.recv())
+                    msg = conn.recv()
+                    kind = msg[0]
+                    if kind in ("shard_plan", "shard_part") and transport is not None:
+                        transport.deliver(msg)
+                    elif kind == "shard_exec":
+                        shard_pool.submit(shard_exec, *msg[1:])
+                    elif kind == "shard_apply":
+                        shard_pool.submit(shard_apply, *msg[1:])
+                    else:
+                        loop.call_soon_threadsafe(inbox.put_nowait, msg)
             except (EOFError, OSError):
                 loop.call_soon_threadsafe(inbox.put_nowait, ("stop",))
 
@@ -399,7 +568,8 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
             elif kind == "cancel":
                 flags.cancel_sync(msg[1])
             elif kind == "upsert" and store is not None and hasattr(store, "apply_remote"):
-                store.apply_remote(msg[1], msg[2])
+                # mirror mode: a write (maybe triggering a compaction) must not stall job dispatch / health
+                loop.run_in_executor(shard_pool, store.apply_remote, msg[1], msg[2])
             elif kind == "stop":
                 for t in list(tasks):
                     t.cancel()
@@ -408,6 +578,7 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
     try:
         asyncio.run(main())
     finally:
+        shard_pool.shutdown(wait=False)
         try:
             conn.close()
         except OSError:
@@ -416,7 +587,7 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
 
 
 def spawn_replicas(n: int, address, authkey: bytes, extra_args=(), gpus: list[int] | None = None,
-                   env: dict | None = None) -> list[subprocess.Popen]:
+                   env: dict | None = None, shards: int = 1) -> list[subprocess.Popen]:
     """Start one replica child process per GPU (HIP_VISIBLE_DEVICES pins it; never an exec of this
     process).  The authkey travels in the environment, not on the command line."""
     procs = []
@@ -427,7 +598,7 @@ def spawn_replicas(n: int, address, authkey: bytes, extra_args=(), gpus: list[in
             e["HIP_VISIBLE_DEVICES"] = str(gpus[r])
         e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         cmd = [sys.executable, "-m", "githubrepostorag_amd", "replica", "--hub", f"{address[0]}:{address[1]}",
-               "--rank", str(r), *extra_args]
+               "--rank", str(r), "--shards", str(shards), *extra_args]
         procs.append(subprocess.Popen(cmd, env=e))
     return procs
 
@@ -457,7 +628,8 @@ def demo_runtime(settings):
     emb = Embedder.from_name("encoder-tiny", device="cpu", seed=3)
     store = VectorStore(emb.dim, "cpu")
     texts = ["widgets code", "gadget service", "billing module"]
-    store.table("chunk").upsert(["a", "b", "c"], texts, emb.embed_documents(texts),
+    # row ids split over two shards (crc32 mod 2: widgets -> 1, gadget / billing -> 0)
+    store.table("chunk").upsert(["widgets", "gadget", "billing"], texts, emb.embed_documents(texts),
                                 [{"namespace": "default", "repo": "r", "module": "m", "file_path": f"{x}.py"}
                                  for x in "abc"])
     settings.worker_max_jobs = int(os.environ.get("GRAG_DEMO_SLOTS", settings.worker_max_jobs))

@@ -91,11 +91,15 @@ def _probe_replicas(view, component: str) -> dict:
         return {"status": "UP" if ok else "DOWN",
                 "details": {"endpoint": "replicas", "healthy": len(ok), "replicas": len(reps)}}
     if component == "vector_store":
+        if any(r.get("shard", "full") != "full" for r in reps):  # row-sharded index: every shard's rows
+            return {"status": "UP", "details": {"shards": {r.get("shard"): r.get("tables", {}) for r in reps},
+                                                "replicas": len(reps)}}
         return {"status": "UP", "details": {"tables": reps[0].get("tables", {}), "replicas": len(reps)}}
     if component == "gpu":
         return {"status": "UP", "details": {"devices": [r.get("device") for r in reps]}}
     return {"status": "UP", "details": {"replicas": [{"rank": r["rank"], "inflight": r["inflight"],
-                                                      "capacity": r["capacity"]} for r in reps]}}
+                                                      "capacity": r["capacity"], "shard": r.get("shard", "full")}
+                                                     for r in reps]}}
 
 
 def _probe_gpu() -> dict:

@@ -29,7 +29,8 @@ log = logging.getLogger(__name__)
 
 class RAGRuntime:
     def __init__(self, settings: Settings | None = None, device: str | None = None, llm=None, ingest_llm=None,
-                 embedder: Embedder | None = None, store: VectorStore | None = None, build_engine: bool = True):
+                 embedder: Embedder | None = None, store: VectorStore | None = None, build_engine: bool = True,
+                 shard: tuple[int, int] | None = None):
         self.settings = s = settings or get_settings()
         # TP serving (TP=N under torchrun): one process per GPU, the engine's
         # weights sharded over the TP group, replicated scheduling
@@ -58,6 +59,11 @@ class RAGRuntime:
         if s.embed_batch_window_ms > 0 and hasattr(embedder, "enable_batching"):
             embedder.enable_batching(s.embed_batch_window_ms / 1000.0)
         # store
+        if store is None and shard is not None and shard[1] > 1 and s.index_dir:
+            # replica r of N with a sharded index: its own shard snapshot, or the full one cut down
+            from ..index.sharded_store import load_shard
+
+            store = load_shard(s.index_dir, shard[0], shard[1], self.device, nprobe=s.nprobe)
         if store is None:
             if s.index_dir and (Path(s.index_dir) / "manifest.json").exists():
                 store = VectorStore.load(s.index_dir, self.device, nprobe=s.nprobe)

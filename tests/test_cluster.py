@@ -36,12 +36,12 @@ def _sse(client, job_id, timeout=60.0):
 
 @pytest.fixture()
 def cluster():
-    def make(n=2, delay=0.0, slots=2):
+    def make(n=2, delay=0.0, slots=2, shards=1):
         events = EventLog()
         hub = ReplicaHub(events, job_timeout=60.0)
         env = {"GRAG_DEMO_LLM_DELAY": str(delay), "GRAG_DEMO_SLOTS": str(slots), "CUDA_VISIBLE_DEVICES": "",
                "HIP_VISIBLE_DEVICES": "", "OMP_NUM_THREADS": "1"}
-        procs = spawn_replicas(n, hub.address, hub.authkey, FACTORY, env=env)
+        procs = spawn_replicas(n, hub.address, hub.authkey, FACTORY, env=env, shards=shards)
         s = Settings(index_dir=None, data_dir=None)
         state = APIState(runtime=ClusterRuntimeView(hub, s), queue=hub.queue, events=events, flags=hub.flags,
                          ping_seconds=0.5)
@@ -108,6 +108,26 @@ def test_replica_loss_fails_inflight_jobs(cluster):
     # new work goes to the survivor
     jid = client.post("/rag/jobs", json={"query": "after"}).json()["job_id"]
     assert "Widgets" in _sse(client, jid)[-1][1]["answer"]
+
+
+def test_sharded_replicas_answer_from_every_shard(cluster):
+    """INDEX_SHARDING=shard: each replica keeps its shard of the demo table (widgets on
+    replica 1, gadget + billing on replica 0); every job's retrieval fans out through
+    the hub, so whichever replica runs it, its sources cover rows of both shards."""
+    hub, procs, client = cluster(n=2, delay=0.05, slots=2, shards=2)
+    seen_replicas = set()
+    ids = [client.post("/rag/jobs", json={"query": f"where are widgets and gadgets {i}"}).json()["job_id"]
+           for i in range(4)]
+    for jid in ids:
+        ev = _sse(client, jid)
+        final = ev[-1][1]
+        assert ev[-1][0] == "final" and not final.get("error"), ev[-3:]
+        paths = {s["metadata"]["file_path"] for s in final["sources"]}
+        assert paths == {"a.py", "b.py", "c.py"}, paths
+        seen_replicas.add(hub.queue.results[jid]["result"]["replica"])
+    assert seen_replicas == {0, 1}
+    h = client.get("/health").json()["components"]["vector_index"]["details"]["replicas"]
+    assert sorted(r["shard"] for r in h) == ["0/2", "1/2"]
 
 
 def test_store_write_mirroring():
