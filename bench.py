@@ -77,11 +77,13 @@ def parse():
                     help="Python GIL switch interval (s): the engine thread re-takes the GIL quickly after a GPU wait")
     ap.add_argument("--prefetch", type=int, default=1,
                     help="1: the next group's retrieval overlaps engine steps on a helper thread")
-    ap.add_argument("--agent-jobs", type=int, default=64,
+    ap.add_argument("--agent-jobs", type=int, default=256,
                     help="end-to-end phase: agent-loop jobs through POST /rag/jobs + SSE over real HTTP "
                          "(0 disables); secondary fields e2e_ttft_p50_ms / p90 / agent_jobs_per_s")
     ap.add_argument("--agent-concurrency", type=int, default=64)
-    ap.add_argument("--agent-gen-len", type=int, default=32, help="token cap of every agent LLM call")
+    ap.add_argument("--agent-gen-len", type=int, default=32,
+                    help="token cap of the agent's plan / expand / judge / rewrite calls (JSON or one line)")
+    ap.add_argument("--agent-synth-len", type=int, default=256, help="token cap of the agent's synthesize call")
     ap.add_argument("--quant", default="none", choices=["none", "w4"],
                     help="w4: AWQ-format W4A16 decoder weights (group-128 scales + zero points, the reference's "
                          "precision: helm/values.yaml:67) on the decode GEMMs; reported as its own config line")
@@ -460,15 +462,12 @@ def main():
     # encoder and the 10M-row IVF chunk table (namespace filter fused in the scan)
     agent_res = None
     if args.agent_jobs > 0 and tp == 1:
-        agent_res = agent_phase(args, rank, dev, eng, tok, emb, index, corpus, log)
-        tt = torch.tensor([agent_res["wall_s"]], dtype=torch.float64, device=dev)
-        if world > 1:
-            import torch.distributed as dist
-
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        agent_res["agent_jobs_per_s"] = round(args.agent_jobs * world / float(tt.item()), 3)
-        log(f"agent e2e: {agent_res['agent_jobs_per_s']} jobs/s, e2e TTFT p50 {agent_res['e2e_ttft_p50_ms']} ms "
-            f"p90 {agent_res['e2e_ttft_p90_ms']} ms, errors {agent_res['errors']}")
+        agent_res = agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log)
+        if agent_res is not None:
+            agent_res["agent_jobs_per_s"] = agent_res["jobs_per_s"]
+            log(f"agent e2e: {agent_res['jobs_per_s']} jobs/s ({agent_res.get('steady_jobs_per_s')} steady), "
+                f"e2e TTFT p50 {agent_res['e2e_ttft_p50_ms']} ms p90 {agent_res['e2e_ttft_p90_ms']} ms, "
+                f"errors {agent_res['errors']}")
 
     # ---- ingest phase (reported separately)
     ingest_dps = None
@@ -541,6 +540,7 @@ def main():
             "e2e_ttft_p50_ms": None if agent_res is None else agent_res["e2e_ttft_p50_ms"],
             "e2e_ttft_p90_ms": None if agent_res is None else agent_res["e2e_ttft_p90_ms"],
             "agent_jobs_per_s": None if agent_res is None else agent_res["agent_jobs_per_s"],
+            "agent_steady_jobs_per_s": None if agent_res is None else agent_res.get("steady_jobs_per_s"),
             "agent_e2e": agent_res,
         }
         line = json.dumps(res)
@@ -554,8 +554,32 @@ def main():
         dist.destroy_process_group()
 
 
-def agent_phase(args, rank, dev, eng, tok, emb, index, corpus, log):
-    """POST /rag/jobs -> SSE over real HTTP for ``--agent-jobs`` 3-round agent jobs."""
+def _scope_tables(store, emb, corpus, rank, world, dev):
+    """This rank's shard of the project / package / file summary tables next to the chunk table
+    (synthetic hierarchy rows, utils/synthetic.scope_rows; random unit vectors: the corpus is
+    synthetic), rows owned by crc32(row_id) mod world as the sharded store routes them."""
+    import torch
+
+    from githubrepostorag_amd.index.sharded_store import shard_of
+    from githubrepostorag_amd.utils import synthetic
+
+    for scope in ("repo", "module", "file"):
+        ids, texts, metas = synthetic.scope_rows(corpus, scope)
+        keep = [i for i, r in enumerate(ids) if shard_of(r, world) == rank]
+        g = torch.Generator(device="cpu").manual_seed(4242 + rank * 7 + len(scope))
+        v = torch.nn.functional.normalize(torch.randn(len(keep), emb.dim, generator=g), dim=1)
+        store.table(scope).upsert([ids[i] for i in keep], [texts[i] for i in keep], v.to(dev),
+                                  [metas[i] for i in keep])
+
+
+def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log):
+    """POST /rag/jobs -> SSE over real HTTP: ``--agent-jobs`` agent jobs per GPU at
+    ``--agent-concurrency`` per GPU, over all four scope tables (10M-row chunk table + project /
+    package / file summary tables).  N > 1: one front door on rank 0 (service/cluster.py) over a
+    replica on every rank; each replica holds its shard of every table and every retrieval round
+    fans out through the hub (index/sharded_store.py), as ``serve --replicas N`` runs."""
+    import threading
+
     from githubrepostorag_amd.agent.llm import EngineLLM, MeteredLLM
     from githubrepostorag_amd.config import Settings
     from githubrepostorag_amd.engine.runner import EngineRunner
@@ -567,31 +591,79 @@ def agent_phase(args, rank, dev, eng, tok, emb, index, corpus, log):
 
     conc = args.agent_concurrency
     s = Settings(qwen_model=args.model, embed_model=args.encoder, qwen_max_output=args.agent_gen_len,
-                 worker_max_jobs=conc, max_rag_attempts=3, default_namespace=corpus.namespace, job_timeout_s=1800,
-                 llm_retries=0, stream_tokens=True, index_kind=args.index_kind, nlist=args.nlist, nprobe=args.nprobe,
-                 embed_batch_window_ms=1.0, data_dir=None, seed=rank)
-    store = VectorStore(emb.dim, dev)  # project/package/file tables empty: code questions plan to the chunk scope
+                 synth_max_tokens=args.agent_synth_len, worker_max_jobs=conc, max_rag_attempts=3,
+                 default_namespace=corpus.namespace, job_timeout_s=1800, llm_retries=0, stream_tokens=True,
+                 index_kind=args.index_kind, nlist=args.nlist, nprobe=args.nprobe, embed_batch_window_ms=1.0,
+                 data_dir=None, seed=rank)
+    store = VectorStore(emb.dim, dev)
     store.tables["chunk"] = index.table
+    _scope_tables(store, emb, corpus, rank, world, dev)
     runner = EngineRunner(eng, watchdog_s=600)
     llm = MeteredLLM(EngineLLM(runner, tok, max_tokens=args.agent_gen_len, timeout_s=1800, retries=0))
     rt = RAGRuntime(s, device=str(dev), llm=llm, embedder=emb, store=store, build_engine=False)
     rt.engine, rt.runner = eng, runner
-    app = create_app(APIState(runtime=rt))
     import logging
 
     logging.getLogger("githubrepostorag_amd.agent").setLevel(logging.ERROR)  # random weights: parse fallbacks
-    q0 = 50_000_000 + rank * 1_000_000
-    warm = [synthetic.code_question(q0 + 500_000 + i) for i in range(min(conc, 16))]
-    qs = [synthetic.code_question(q0 + i) for i in range(args.agent_jobs)]
+    n_jobs, n_conc = args.agent_jobs * world, conc * world
+    q0 = 50_000_000
+
+    def mix(i):  # half code questions (code scope), half project overviews (project -> package -> file)
+        return synthetic.code_question(q0 + i) if i % 2 == 0 else synthetic.overview_question(q0 + i, corpus)
+
+    warm = [mix(500_000 + i) for i in range(min(n_conc, 16 * world))]
+    qs = [mix(i) for i in range(n_jobs)]
+    res = None
     try:
-        res = run_e2e(app, qs, conc, warmup=warm)
+        if world == 1:
+            res = run_e2e(create_app(APIState(runtime=rt)), qs, n_conc, warmup=warm)
+        else:
+            import torch.distributed as dist
+
+            from githubrepostorag_amd.service.cluster import ClusterRuntimeView, ReplicaHub, run_replica
+            from githubrepostorag_amd.service.events import EventLog
+
+            hub = None
+            obj = [None]
+            if rank == 0:
+                events = EventLog()
+                hub = ReplicaHub(events, job_timeout=1800.0)
+                obj = [(tuple(hub.address), hub.authkey)]
+            dist.broadcast_object_list(obj, src=0)
+            addr, key = obj[0]
+            th = threading.Thread(target=run_replica, args=(rt, addr, key, rank), kwargs={"shards": world},
+                                  name="bench-replica", daemon=True)
+            th.start()
+            if rank == 0:
+                t0 = time.time()
+                while hub.live_count() < world:
+                    if time.time() - t0 > 300:
+                        raise RuntimeError(f"only {hub.live_count()} of {world} replicas connected")
+                    time.sleep(0.05)
+                state = APIState(runtime=ClusterRuntimeView(hub, s), queue=hub.queue, events=events,
+                                 flags=hub.flags)
+                try:
+                    res = run_e2e(create_app(state), qs, n_conc, warmup=warm)
+                    res["replicas"] = hub.health()["replicas"]
+                finally:
+                    hub.close()  # replicas return from run_replica
+            th.join(timeout=120)
+            dist.barrier()
     finally:
         runner.shutdown()
         emb.close()  # the runtime turned on query-embedding batching for this phase
-    res["concurrency"] = conc
+        st = getattr(rt.store, "close", None)
+        if st is not None and rt.store is not store:
+            st()
+    if res is None:
+        return None
+    res["concurrency"] = n_conc
     res["llm_token_cap"] = args.agent_gen_len
-    res["chunk_table"] = {"rows": index.table.count(), "index": index.table.index_kind,
-                          "searches": index.table.stats["searches"]}
+    res["synthesize_token_cap"] = args.agent_synth_len
+    res["tables"] = {"chunk": {"rows": corpus.n, "index": index.table.index_kind},
+                     **{sc: {"rows_this_shard": store.table(sc).count()} for sc in ("repo", "module", "file")}}
+    res["question_mix"] = "1/2 code (code scope), 1/2 project overview (project -> package -> file)"
+    res["front_door"] = "single process" if world == 1 else f"front door + {world} sharded replicas"
     return res
 
 

@@ -118,8 +118,9 @@ class RunContext:
 
 class GraphAgent:
     def __init__(self, llm, retrievers: dict, namespace: str = "default", max_iters: int = 3,
-                 router_top_k: int = 5, embed_fn=None):
+                 router_top_k: int = 5, embed_fn=None, synth_max_tokens: int | None = None):
         self.llm = llm
+        self.synth_max_tokens = synth_max_tokens
         self.retrievers = retrievers
         self.namespace = namespace
         self.max_iters = max_iters
@@ -333,11 +334,14 @@ class GraphAgent:
         dbg_issue = None
         try:
             kw = {"on_token": ctx.on_answer_token} if ctx.on_answer_token else {}
+            if self.synth_max_tokens:
+                kw["max_tokens"] = self.synth_max_tokens
             text = self._complete(prompts.synthesize(system, q, blocks), ctx, "synthesize", **kw)
             if has_content and len(docs) >= 3 and any(p in text.lower() for p in _CONSERVATIVE):
                 try:
                     retry = self._complete(prompts.synthesize(prompts.SYNTH_RETRY, q, blocks), ctx,
-                                           "synthesize_retry")
+                                           "synthesize_retry",
+                                           **({"max_tokens": self.synth_max_tokens} if self.synth_max_tokens else {}))
                     if not any(p in retry.lower() for p in _CONSERVATIVE[:3]):
                         text = retry
                 except Cancelled:

@@ -52,6 +52,8 @@ class Settings:
     qwen_temperature: float = field(default_factory=lambda: _float("QWEN_TEMPERATURE", 0.7))
     qwen_top_p: float = field(default_factory=lambda: _float("QWEN_TOP_P", 0.9))
     router_top_k: int = field(default_factory=lambda: _int("ROUTER_TOP_K", 5))
+    # token cap of the agent's synthesize call (0: QWEN_MAX_OUTPUT like every other agent call)
+    synth_max_tokens: int = field(default_factory=lambda: _int("SYNTH_MAX_TOKENS", 0))
     default_namespace: str = field(default_factory=lambda: _env("DEFAULT_NAMESPACE", "default"))
     metrics_port: int = field(default_factory=lambda: _int("METRICS_PORT", 9000))
     allow_thinking: bool = field(default_factory=lambda: _bool("ALLOW_THINKING", True))

@@ -112,7 +112,16 @@ def run_e2e(app, questions: list[str], concurrency: int, warmup: list[str] | Non
             loop.close()
     ttft = [(r["first_token"] - r["t0"]) * 1e3 for r in res if r["first_token"] is not None]
     lat = [(r["final"] - r["t0"]) * 1e3 for r in res if r["final"] is not None]
+    # saturation throughput (jobs/s at saturation): completions per second over the middle
+    # half of the finish times, past the ramp-up and before the drain (meaningful with jobs >= 4 x concurrency)
+    fin = sorted(r["final"] for r in res if r["final"] is not None)
+    steady = None
+    if len(fin) >= 8:
+        a, b = len(fin) // 4, (3 * len(fin)) // 4
+        if fin[b] > fin[a]:
+            steady = round((b - a) / (fin[b] - fin[a]), 3)
     return {"jobs": len(res), "wall_s": round(wall, 3), "jobs_per_s": round(len(res) / wall, 3),
+            "steady_jobs_per_s": steady,
             "e2e_ttft_p50_ms": round(statistics.median(ttft), 1) if ttft else None,
             "e2e_ttft_p90_ms": round(_pct(ttft, 0.9), 1) if ttft else None,
             "job_latency_p50_ms": round(statistics.median(lat), 1) if lat else None,

@@ -157,7 +157,8 @@ class RAGRuntime:
         """A fresh agent per job (cheap: it only holds references)."""
         s = self.settings
         return GraphAgent(self.llm, self.retrievers.scope_retrievers(), namespace=s.default_namespace,
-                          max_iters=s.max_rag_attempts, router_top_k=s.router_top_k)
+                          max_iters=s.max_rag_attempts, router_top_k=s.router_top_k,
+                          synth_max_tokens=s.synth_max_tokens or None)
 
     def health(self) -> dict:
         out = {"device": str(self.device), "tables": self.store.counts()}

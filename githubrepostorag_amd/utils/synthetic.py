@@ -200,3 +200,47 @@ def code_question(i: int) -> str:
     r = _rng(20_000_033 + i)
     return (f"Why does {r.choice(_WORDS)}_{r.choice(_WORDS)} raise an exception on retry when the "
             f"{r.choice(_WORDS)} {r.choice(_WORDS)} hits a timeout?")
+
+
+def scope_rows(corpus: SyntheticCorpus, scope: str) -> tuple[list[str], list[str], list[dict]]:
+    """The hierarchy-summary rows (ingest/hierarchy.py's repo / module / file documents) that an
+    ingest of ``corpus``'s chunks would have produced: one REPO OVERVIEW per repo, one MODULE
+    SUMMARY per (repo, module), one FILE SUMMARY per (repo, module, file) — the project /
+    package / file tables the agent's scope retrievers search (reference agent_graph.py:158-176)."""
+    ids, texts, metas = [], [], []
+    langs = _LANGS
+    for rp in range(corpus.n_repos):
+        repo = corpus.repo_name(rp)
+        base = {"namespace": corpus.namespace, "repo": repo}
+        if scope == "repo":
+            r = _rng(corpus.seed * 7919 + rp)
+            ids.append(f"{corpus.prefix}repo-{rp}")
+            texts.append(f"REPO OVERVIEW {repo}: this project handles {words(r, 40)}.")
+            metas.append({**base, "scope": "repo", "doc_type": "repo"})
+            continue
+        for md in range(corpus.n_modules):
+            m = corpus.module_name(md)
+            if scope == "module":
+                r = _rng(corpus.seed * 7919 + rp * 131 + md)
+                ids.append(f"{corpus.prefix}module-{rp}-{md}")
+                texts.append(f"MODULE SUMMARY {repo}/{m}: {words(r, 30)}.")
+                metas.append({**base, "module": m, "scope": "module", "doc_type": "module"})
+                continue
+            for f in range(corpus.fpm):
+                ext = langs[(rp + md + f) % len(langs)][0]
+                fp = f"{m}/{_WORDS[f % len(_WORDS)]}_{f}.{ext}"
+                r = _rng(corpus.seed * 7919 + (rp * 131 + md) * 4099 + f)
+                ids.append(f"{corpus.prefix}file-{rp}-{md}-{f}")
+                texts.append(f"FILE SUMMARY {fp}: {words(r, 20)}.")
+                metas.append({**base, "module": m, "file_path": fp, "scope": "file", "doc_type": "file",
+                              "language": langs[(rp + md + f) % len(langs)][1]})
+    return ids, texts, metas
+
+
+def overview_question(i: int, corpus: SyntheticCorpus) -> str:
+    """A project-level question: the planner falls back to the project scope (no code keywords), and
+    the judge's stage-down walks project -> package -> file (agent_graph.py:346-378)."""
+    r = _rng(30_000_041 + i)
+    repo = corpus.repo_name(r.randrange(corpus.n_repos))
+    return (f"Tell me about the {repo} project: how are its {r.choice(_WORDS)} and {r.choice(_WORDS)} "
+            f"parts organised?")

@@ -11,7 +11,7 @@ from dist_utils import free_port
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TINY = ["--model", "qwen2-tiny", "--encoder", "encoder-tiny", "--index-size", "4000", "--index-kind", "ivf",
         "--nlist", "16", "--nprobe", "4", "--batch", "3", "--prompt-len", "48", "--gen-len", "5",
-        "--ingest-files", "4", "--steps", "2", "--warmup", "1", "--agent-jobs", "8", "--agent-concurrency", "4"]
+        "--ingest-files", "4", "--steps", "2", "--warmup", "1", "--agent-jobs", "8", "--agent-concurrency", "4", "--agent-synth-len", "16"]
 
 
 def _run(cmd, env):
@@ -38,6 +38,10 @@ def test_bench_two_ranks_gloo():
                env)
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 6 and res["config"]["parallelism"] == "dp2"
     assert res["value"] > 0
+    # agent phase through one front door over two sharded replicas (every retrieval fans out over the hub)
+    ae = res["agent_e2e"]
+    assert ae["front_door"] == "front door + 2 sharded replicas" and ae["errors"] == 0 and ae["jobs"] == 16
+    assert sorted(r["shard"] for r in ae["replicas"]) == ["0/2", "1/2"]
 
 
 def test_bench_tensor_parallel_two_ranks_gloo():
