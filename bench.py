@@ -174,20 +174,22 @@ def main():
     if tp > 1:
         # TP groups of consecutive ranks; every rank of a group runs the same
         # arrivals (seeded by its DP rank) and steps its shard of the engine in
-        # lockstep (deterministic scheduler + identical sampling seeds).  The
-        # retrieval runs synchronously (no helper thread) so the world-group
-        # search collectives never interleave with the TP all-reduces.
+        # lockstep (deterministic scheduler + identical sampling seeds).  An
+        # arrival is admitted at the same engine step on every TP rank: its
+        # "retrieval done" flag is agreed over the TP group (MIN) each step.
         from githubrepostorag_amd.parallel.custom_ar import enable_for_group
 
         tp_group, dp_group = comm.make_tp_dp_groups(tp)
         if dev.type == "cuda":
             enable_for_group(tp_group, dev)
         dp_rank, dp_size = rank // tp, world // tp
-        args.prefetch = 0
-        if not args.no_ingest:
-            args.no_ingest = True  # the ingest engine's runner threads are not TP-replicated here
-            if rank == 0:
-                print("[bench] --tp > 1: ingest phase skipped", file=sys.stderr)
+    if world > 1:
+        # the index (C6 k-means, C4 query all-gather, C3 top-k all-to-all) on a communicator of its
+        # own: the prefetch thread's search collectives then never share one with the engine's
+        # TP all-reduces or the main thread's barriers
+        import torch.distributed as dist
+
+        group = comm.Group(list(range(world)), pg=dist.new_group(list(range(world))))
 
     from githubrepostorag_amd.embed.service import Embedder
     from githubrepostorag_amd.engine.llm_engine import EngineConfig, LLMEngine
@@ -324,20 +326,27 @@ def main():
         (decode windows capped so no sequence runs past that target),
         admitting the ``arrival`` future's group as soon as it is ready."""
         t0 = time.perf_counter()
+
+        def ready(fut):  # TP: every rank of the group admits the arrival at the same engine step
+            if tp_group is None or tp_group.trivial:
+                return fut.done()
+            return bool(tp_group.min_int(1 if fut.done() else 0, dev))
+
         while True:
             have = min(len(eng.get(r).output_ids) for r in rids)
             if have >= ntok:
                 break
             cap = ntok - have
-            if arrival is not None and not arrival.done() and args.arrival_cap:
+            arrived = arrival is not None and ready(arrival)
+            if arrival is not None and not arrived and args.arrival_cap:
                 # an arrival's retrieval is in flight: one decode step per replay, so the engine looks
                 # for its prompts every ~step instead of every window (TTFT no longer depends on
                 # whether retrieval beats a multi-step window)
                 cap = 1
-            eng.step(max_window=cap)
-            if arrival is not None and arrival.done():
+            if arrived:
                 admit(arrival.result())
                 arrival = None
+            eng.step(max_window=cap)
         if arrival is not None:
             admit(arrival.result())
         phase["generate"] += time.perf_counter() - t0
@@ -461,8 +470,8 @@ def main():
     # (plan / retrieve / judge / rewrite / synthesize, SSE token streaming) on this engine,
     # encoder and the 10M-row IVF chunk table (namespace filter fused in the scan)
     agent_res = None
-    if args.agent_jobs > 0 and tp == 1:
-        agent_res = agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log)
+    if args.agent_jobs > 0:
+        agent_res = agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_group, dp_size)
         if agent_res is not None:
             agent_res["agent_jobs_per_s"] = agent_res["jobs_per_s"]
             log(f"agent e2e: {agent_res['jobs_per_s']} jobs/s ({agent_res.get('steady_jobs_per_s')} steady), "
@@ -479,15 +488,15 @@ def main():
         if dev.type == "cuda":
             torch.cuda.empty_cache()
         comm.barrier()
-        n_docs, secs, ingest_stages = run_ingest_bench(model, tok, emb, args.ingest_files, seed=rank,
+        n_docs, secs, ingest_stages = run_ingest_bench(model, tok, emb, args.ingest_files, seed=dp_rank,
                                                        max_num_seqs=args.ingest_seqs, use_graph=not args.no_graph,
-                                                       mixed_batches=bool(args.ingest_mixed))
+                                                       mixed_batches=bool(args.ingest_mixed), tp=tp_group)
         tt = torch.tensor([secs], dtype=torch.float64, device=dev)
         if world > 1:
             import torch.distributed as dist
 
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        ingest_dps = n_docs * world / float(tt.item())
+        ingest_dps = n_docs * dp_size / float(tt.item())  # one ingest per DP replica (TP peers share it)
         log(f"ingest: {n_docs} docs/rank in {float(tt.item()):.2f}s")
 
     if rank == 0:
@@ -572,12 +581,15 @@ def _scope_tables(store, emb, corpus, rank, world, dev):
                                   [metas[i] for i in keep])
 
 
-def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log):
+def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_group=None, dp_size=1):
     """POST /rag/jobs -> SSE over real HTTP: ``--agent-jobs`` agent jobs per GPU at
     ``--agent-concurrency`` per GPU, over all four scope tables (10M-row chunk table + project /
     package / file summary tables).  N > 1: one front door on rank 0 (service/cluster.py) over a
     replica on every rank; each replica holds its shard of every table and every retrieval round
-    fans out through the hub (index/sharded_store.py), as ``serve --replicas N`` runs."""
+    fans out through the hub (index/sharded_store.py), as ``serve --replicas N`` runs.  Under TP
+    the group's TP rank 0 runs the jobs (its engine runner leads, the peers follow in lockstep) and
+    every other rank joins as a shard-only replica (capacity 0) that answers the index rounds for
+    its shard of the chunk table."""
     import threading
 
     from githubrepostorag_amd.agent.llm import EngineLLM, MeteredLLM
@@ -598,14 +610,17 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log):
     store = VectorStore(emb.dim, dev)
     store.tables["chunk"] = index.table
     _scope_tables(store, emb, corpus, rank, world, dev)
-    runner = EngineRunner(eng, watchdog_s=600)
-    llm = MeteredLLM(EngineLLM(runner, tok, max_tokens=args.agent_gen_len, timeout_s=1800, retries=0))
+    tp = tp_group if tp_group is not None and not tp_group.trivial else None
+    runner = EngineRunner(eng, watchdog_s=600, tp=tp)
+    leader = runner.leader
+    llm = MeteredLLM(EngineLLM(runner, tok, max_tokens=args.agent_gen_len, timeout_s=1800, retries=0)) \
+        if leader else None
     rt = RAGRuntime(s, device=str(dev), llm=llm, embedder=emb, store=store, build_engine=False)
     rt.engine, rt.runner = eng, runner
     import logging
 
     logging.getLogger("githubrepostorag_amd.agent").setLevel(logging.ERROR)  # random weights: parse fallbacks
-    n_jobs, n_conc = args.agent_jobs * world, conc * world
+    n_jobs, n_conc = args.agent_jobs * dp_size, conc * dp_size
     q0 = 50_000_000
 
     def mix(i):  # half code questions (code scope), half project overviews (project -> package -> file)
@@ -631,7 +646,8 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log):
                 obj = [(tuple(hub.address), hub.authkey)]
             dist.broadcast_object_list(obj, src=0)
             addr, key = obj[0]
-            th = threading.Thread(target=run_replica, args=(rt, addr, key, rank), kwargs={"shards": world},
+            th = threading.Thread(target=run_replica, args=(rt, addr, key, rank),
+                                  kwargs={"shards": world, "capacity": conc if leader else 0},
                                   name="bench-replica", daemon=True)
             th.start()
             if rank == 0:
@@ -648,6 +664,10 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log):
                 finally:
                     hub.close()  # replicas return from run_replica
             th.join(timeout=120)
+            if leader:
+                runner.shutdown()  # TP: stops the followers' lockstep loops
+            else:
+                runner.join(timeout=600)
             dist.barrier()
     finally:
         runner.shutdown()
@@ -663,7 +683,9 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log):
     res["tables"] = {"chunk": {"rows": corpus.n, "index": index.table.index_kind},
                      **{sc: {"rows_this_shard": store.table(sc).count()} for sc in ("repo", "module", "file")}}
     res["question_mix"] = "1/2 code (code scope), 1/2 project overview (project -> package -> file)"
-    res["front_door"] = "single process" if world == 1 else f"front door + {world} sharded replicas"
+    res["front_door"] = "single process" if world == 1 else (
+        f"front door + {world} sharded replicas" if tp is None else
+        f"front door + {dp_size} TP-{tp.size} job replicas + {world - dp_size} shard-only replicas, {world} shards")
     return res
 
 

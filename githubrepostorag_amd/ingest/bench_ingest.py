@@ -28,9 +28,14 @@ from .readers import Document
 
 def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs: int = 256,
                      max_model_len: int = 8192, use_graph: bool = True, summary_tokens: int = 128,
-                     mixed_batches: bool = False) -> tuple[int, float, dict]:
-    """Returns (documents ingested, seconds, per-stage seconds)."""
-    dev = next(model.parameters()).device if hasattr(model, "parameters") else torch.device("cpu")
+                     mixed_batches: bool = False, tp=None) -> tuple[int, float, dict]:
+    """Returns (documents ingested, seconds, per-stage seconds).
+
+    ``tp`` (a tensor-parallel group the model is sharded over): the group's TP
+    rank 0 runs the pipeline and owns the request queue; the other ranks mirror
+    its engine in lockstep (engine/runner.py ``follow``) until it shuts down, and
+    report 0 documents (one ingest per TP group)."""
+    dev = torch.device(getattr(model, "device", "cpu"))
     sizes = tuple(sorted({*EngineConfig.graph_batch_sizes, *range(256, max_num_seqs + 1, 128), max_num_seqs}))
     eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max_num_seqs, max_num_batched_tokens=16384,
                                              max_model_len=max_model_len, use_cuda_graph=use_graph, seed=seed,
@@ -38,7 +43,15 @@ def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs:
                                              graph_batch_sizes=tuple(b for b in sizes if b <= max_num_seqs)))
     if use_graph and dev.type == "cuda":
         eng.warmup_graphs()
-    runner = EngineRunner(eng)
+    tp = tp if tp is not None and not tp.trivial else None
+    runner = EngineRunner(eng, tp=tp)
+    if tp is not None and not runner.leader:
+        t0 = time.perf_counter()
+        runner.join()  # lockstep follower until the leader's runner stops
+        del eng
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        return 0, time.perf_counter() - t0, {"tp_follower": True}
     try:
         llm = EngineLLM(runner, tok, max_tokens=summary_tokens, mode="ingest", timeout_s=1800.0, retries=0)
         store = VectorStore(emb.dim, dev)

@@ -65,7 +65,7 @@ class _Replica:
     def __init__(self, rank: int, conn, capacity: int, info: dict):
         self.rank = rank
         self.conn = conn
-        self.capacity = max(1, int(capacity))
+        self.capacity = max(0, int(capacity))  # 0: a shard-only replica (answers index rounds, runs no jobs)
         self.inflight = 0
         self.alive = True
         self.info = info
@@ -469,7 +469,7 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
     from .worker import RAGWorker
 
     s = runtime.settings
-    cap = capacity or s.worker_max_jobs
+    cap = capacity if capacity is not None else s.worker_max_jobs
     conn = Client(tuple(address) if isinstance(address, list) else address, authkey=authkey)
     send_lock = threading.Lock()
 
@@ -486,7 +486,7 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
     shard_pool = ThreadPoolExecutor(4, thread_name_prefix="shard-exec")
     events = _ForwardingEvents(send)
     flags = CancelFlags()
-    worker = RAGWorker(runtime, events, flags, cap, s.job_timeout_s, s.keep_result_s, s.stream_tokens)
+    worker = RAGWorker(runtime, events, flags, max(1, cap), s.job_timeout_s, s.keep_result_s, s.stream_tokens)
     store = getattr(runtime, "store", None)
     if transport is None and store is not None and hasattr(store, "add_listener"):
         store.add_listener(lambda table, payload: send(("upsert", table, payload)))

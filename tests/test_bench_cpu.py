@@ -46,13 +46,19 @@ def test_bench_two_ranks_gloo():
 
 def test_bench_tensor_parallel_two_ranks_gloo():
     """--tp 2 on two ranks: one TP group serving one DP replica's queries in
-    lockstep (a desync would hang or fail the run), index sharded over both."""
+    lockstep (a desync would hang or fail the run), index sharded over both,
+    retrieval prefetched on a helper thread (arrivals admitted at an agreed step)."""
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
     res = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2",
                 "--tp", "2", *TINY], env)
     assert res["config"]["parallelism"] == "tp2dp1" and res["config"]["global_batch"] == 3
-    assert res["value"] > 0 and res["ingest_docs_per_s"] is None and "TP=2" in res["config"]["model"]
+    assert res["value"] > 0 and "TP=2" in res["config"]["model"]
+    # ingest on the TP group (leader runs the pipeline, the peer mirrors its engine) and the agent
+    # phase (TP leader runs jobs, the peer answers index rounds for its shard as a shard-only replica)
+    assert res["ingest_docs_per_s"] > 0 and res["retrieval_prefetch"] is True
+    ae = res["agent_e2e"]
+    assert ae["errors"] == 0 and ae["jobs"] == 8 and "1 shard-only replicas, 2 shards" in ae["front_door"]
 
 
 def test_bench_self_launch_two_ranks():
