@@ -545,6 +545,10 @@ def main():
                                         "engine_prefill": round(timed_engine.get("prefill_s", 0) * 1000, 2),
                                         "engine_decode": round(timed_engine.get("decode_s", 0) * 1000, 2)},
             "retrieval_prefetch": bool(args.prefetch),
+            # TP: bytes each rank receives per 512-row decode sampling step
+            "tp_sampler_bytes_per_decode_step": None if tp == 1 else __import__(
+                "githubrepostorag_amd.ops.sampling", fromlist=["x"]).tp_sampling_bytes(
+                args.batch * D, tp, dcfg.vocab_size, 2),
             "ingest_stage_s": ingest_stages,
             "e2e_ttft_p50_ms": None if agent_res is None else agent_res["e2e_ttft_p50_ms"],
             "e2e_ttft_p90_ms": None if agent_res is None else agent_res["e2e_ttft_p90_ms"],

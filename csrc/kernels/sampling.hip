@@ -78,6 +78,12 @@ struct Params {
   int32_t* gidx;     // [B][S]
   float* hist;       // [2][B][S][kNB]
   uint32_t* state;   // [2][B][4]: prefix, pmask, thr_k, need (float bits)
+  // vocab-parallel (TP) form: this call sees columns [v0, v0 + V) of a Vg-token vocabulary;
+  // gmax / ghist (when set) are the group-wide row max / previous-round histogram the host
+  // reduced over the TP group between launches (grag_sample_tp)
+  int v0, Vg;
+  const float* gmax;  // [B]
+  const float* ghist; // [B][kNB]
 };
 
 struct Row {
@@ -104,7 +110,8 @@ __device__ __forceinline__ Row row_params(const Params& p, int row) {
 // Apply fn(index, adjusted value) to every logit of [lo, hi): 8 per lane per
 // step from one 16-B (bf16) or two 16-B (fp32) loads + one seen-bitmap word.
 template <typename T, typename F>
-__device__ __forceinline__ void for_seg(const T* row, int lo, int hi, const Row& c, F&& fn) {
+__device__ __forceinline__ void for_seg(const T* row, int lo, int hi, const Row& c, F&& fn, int v0 = 0) {
+  // i: local column (loads), i + v0: global token id (seen bitmap, RNG stream, tie order); v0 % 8 == 0
   const int hi8 = lo + ((hi - lo) & ~7);
   const bool pen = c.pen != 1.f && c.seen;
   for (int i = lo + threadIdx.x * 8; i < hi8; i += kT * 8) {
@@ -116,18 +123,20 @@ __device__ __forceinline__ void for_seg(const T* row, int lo, int hi, const Row&
     } else {
       unpack8(*reinterpret_cast<const bf16x8_t*>(row + i), x);
     }
-    const uint32_t w = pen ? (c.seen[i >> 5] >> (i & 31)) & 0xFFu : 0u;
+    const int g = i + v0;
+    const uint32_t w = pen ? (c.seen[g >> 5] >> (g & 31)) & 0xFFu : 0u;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float v = x[j];
       if ((w >> j) & 1u) v = v > 0.f ? v / c.pen : v * c.pen;
-      fn(i + j, c.greedy ? v : v * c.inv_temp);
+      fn(g + j, c.greedy ? v : v * c.inv_temp);
     }
   }
   for (int i = hi8 + threadIdx.x; i < hi; i += kT) {
+    const int g = i + v0;
     float v = (float)row[i];
-    if (pen && ((c.seen[i >> 5] >> (i & 31)) & 1u)) v = v > 0.f ? v / c.pen : v * c.pen;
-    fn(i, c.greedy ? v : v * c.inv_temp);
+    if (pen && ((c.seen[g >> 5] >> (g & 31)) & 1u)) v = v > 0.f ? v / c.pen : v * c.pen;
+    fn(g, c.greedy ? v : v * c.inv_temp);
   }
 }
 
@@ -157,6 +166,7 @@ __device__ __forceinline__ void block_argmax(float& v, int& idx, float* sv, int*
 
 // row max from the S partial maxima (every thread gets it)
 __device__ __forceinline__ float row_max(const Params& p, int row, float* sv) {
+  if (p.gmax) return p.gmax[row];  // TP: the group-wide max (uniform branch)
   float m = -INFINITY;
   for (int s = threadIdx.x; s < p.S; s += kT) m = fmaxf(m, p.seg_max[row * p.S + s]);
 #pragma unroll
@@ -214,8 +224,8 @@ struct RState {
   float need;
 };
 
-__device__ __forceinline__ bool round_active(int r, const Row& c, int V) {
-  return r < 4 ? (c.top_k > 0 && c.top_k < V) : (c.top_p < 1.f);
+__device__ __forceinline__ bool round_active(int r, const Row& c, int Vg) {
+  return r < 4 ? (c.top_k > 0 && c.top_k < Vg) : (c.top_p < 1.f);
 }
 // Digit plan of a 4-round radix select: a 4-bit first digit (16 bins: every
 // token of the row takes part, so it is histogrammed in registers, not with
@@ -248,18 +258,22 @@ __device__ __forceinline__ RState load_state(const Params& p, int row, int j, co
 __device__ void fold_round(const Params& p, int row, int r, int j, const Row& c, RState& st, float* lds_hist,
                            uint32_t* sh_b, float* sh_f) {
   if (r < 0) return;
-  if (round_active(r, c, p.V)) {
-    const float* src = p.hist + ((size_t)(j & 1) * p.B + row) * p.S * kNB;
-    for (int b = threadIdx.x; b < kNB; b += kT) {
-      // all kMaxS partial loads issued back to back (clamped index, masked
-      // add: no per-load branch), summed in a fixed order -> deterministic
-      float v[kMaxS];
+  if (round_active(r, c, p.Vg)) {
+    if (p.ghist) {  // TP: the histogram already summed over segments and ranks
+      for (int b = threadIdx.x; b < kNB; b += kT) lds_hist[b] = p.ghist[(size_t)row * kNB + b];
+    } else {
+      const float* src = p.hist + ((size_t)(j & 1) * p.B + row) * p.S * kNB;
+      for (int b = threadIdx.x; b < kNB; b += kT) {
+        // all kMaxS partial loads issued back to back (clamped index, masked
+        // add: no per-load branch), summed in a fixed order -> deterministic
+        float v[kMaxS];
 #pragma unroll
-      for (int g = 0; g < kMaxS; ++g) v[g] = src[min(g, p.S - 1) * kNB + b];
-      float s = 0.f;
+        for (int g = 0; g < kMaxS; ++g) v[g] = src[min(g, p.S - 1) * kNB + b];
+        float s = 0.f;
 #pragma unroll
-      for (int g = 0; g < kMaxS; ++g) s += g < p.S ? v[g] : 0.f;
-      lds_hist[b] = s;
+        for (int g = 0; g < kMaxS; ++g) s += g < p.S ? v[g] : 0.f;
+        lds_hist[b] = s;
+      }
     }
     __syncthreads();
     if (r == 4) {  // first top-p round: its histogram holds the whole kept mass
@@ -281,7 +295,7 @@ __device__ void fold_round(const Params& p, int row, int r, int j, const Row& c,
     __syncthreads();
   }
   if (r == 3) {  // top-k threshold complete (0 = keep all); top-p starts fresh inside it
-    st.thr_k = round_active(3, c, p.V) ? st.prefix : 0u;
+    st.thr_k = round_active(3, c, p.Vg) ? st.prefix : 0u;
     st.prefix = 0u;
     st.pmask = 0u;
   }
@@ -298,7 +312,7 @@ __global__ __launch_bounds__(kT) void samp_max_kernel(Params p) {
   const int lo = seg * p.seglen, hi = min(p.V, lo + p.seglen);
   float m = -INFINITY;
   int mi = 0x7fffffff;
-  for_seg(lr, lo, hi, c, [&](int i, float x) { better(m, mi, x, i); });
+  for_seg(lr, lo, hi, c, [&](int i, float x) { better(m, mi, x, i); }, p.v0);
   block_argmax(m, mi, sv, si);
   if (threadIdx.x == 0) {
     p.seg_max[row * p.S + seg] = m;
@@ -329,7 +343,7 @@ __global__ __launch_bounds__(kT) void samp_round_kernel(Params p, int r, int r_p
       s[3] = __float_as_uint(st.need);
     }
   }
-  if (!round_active(r, c, p.V)) return;
+  if (!round_active(r, c, p.Vg)) return;
   __syncthreads();
   for (int b = threadIdx.x; b < kNB; b += kT) hist[b] = 0.f;
   __syncthreads();
@@ -350,7 +364,7 @@ __global__ __launch_bounds__(kT) void samp_round_kernel(Params p, int r, int r_p
       const uint32_t b = k >> 28;
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[q] += b == (uint32_t)q ? w : 0.f;
-    });
+    }, p.v0);
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = wave_sum(acc[q]);
     if ((threadIdx.x & 63) == 0) {
@@ -375,7 +389,7 @@ __global__ __launch_bounds__(kT) void samp_round_kernel(Params p, int r, int r_p
           cv = w;
         }
       }
-    });
+    }, p.v0);
     if (cb != 0xFFFFFFFFu) atomicAdd(&hist[cb], cv);
   }
   __syncthreads();
@@ -397,7 +411,7 @@ __global__ __launch_bounds__(kT) void samp_gumbel_kernel(Params p, int r_last, i
   const float M = row_max(p, row, sv);
   RState st = load_state(p, row, J - 1 >= 1 ? J - 1 : -1, c);
   fold_round(p, row, r_last, J - 1, c, st, hist, sh_b, sh_f);
-  const uint32_t thr = (r_last >= 4 && round_active(r_last, c, p.V)) ? st.prefix : st.thr_k;
+  const uint32_t thr = (r_last >= 4 && round_active(r_last, c, p.Vg)) ? st.prefix : st.thr_k;
   const uint64_t ctr = p.rng_counter ? (uint64_t)p.rng_counter[c.sl] : 0ull;
   const uint64_t base = mix64(p.seed ^ mix64(ctr * 0x100000001B3ull + (uint64_t)c.sl));
   const T* lr = (const T*)p.logits + (size_t)row * p.ld;
@@ -410,7 +424,7 @@ __global__ __launch_bounds__(kT) void samp_gumbel_kernel(Params p, int r_last, i
       const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
       better(best, bidx, x - __logf(-__logf(u)), i);
     }
-  });
+  }, p.v0);
   block_argmax(best, bidx, sv, si);
   if (threadIdx.x == 0) {
     p.gval[row * p.S + seg] = best;
@@ -466,6 +480,58 @@ int launch_all(const Params& p, int rounds, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------- vocab-parallel (TP) stages
+// Per-row best (value, global index) over the S segment partials -> pair[row] = {value, index}
+// (the index is exact in fp32: vocabularies are < 2^24).
+__global__ __launch_bounds__(64) void samp_pair_kernel(const float* vals, const int32_t* ids, int S, float* pair) {
+  const int row = blockIdx.x;
+  float v = -INFINITY;
+  int idx = 0x7fffffff;
+  for (int s = threadIdx.x; s < S; s += 64) better(v, idx, vals[row * S + s], ids[row * S + s]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) better(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
+  if (threadIdx.x == 0) {
+    pair[2 * row] = v;
+    pair[2 * row + 1] = (float)idx;
+  }
+}
+
+// Segment partial histograms of launch j -> one [B][kNB] row histogram (fixed summation order).
+__global__ __launch_bounds__(kNB) void samp_hist_reduce_kernel(const float* hist, int B, int S, int j, float* out) {
+  const int row = blockIdx.x, b = threadIdx.x;
+  const float* src = hist + ((size_t)(j & 1) * B + row) * S * kNB;
+  float acc = 0.f;
+  for (int g = 0; g < S; ++g) acc += src[g * kNB + b];
+  out[(size_t)row * kNB + b] = acc;
+}
+
+// Group-wide max from the all-gathered pairs [W][B][2] -> gmax[B].
+__global__ void samp_gmax_kernel(const float* pairs, int W, int B, float* gmax) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= B) return;
+  float m = -INFINITY;
+  for (int w = 0; w < W; ++w) m = fmaxf(m, pairs[((size_t)w * B + row) * 2]);
+  gmax[row] = m;
+}
+
+// Final: best (value, index) over the W ranks' pairs (greedy rows: the max pairs, sampled rows: the
+// Gumbel pairs), then the same token / seen bit / RNG counter update on every rank.
+__global__ void samp_final_tp_kernel(Params p, const float* max_pairs, const float* gum_pairs, int W) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= p.B) return;
+  const Row c = row_params(p, row);
+  const float* src = c.greedy ? max_pairs : gum_pairs;
+  float v = -INFINITY;
+  int idx = 0x7fffffff;
+  for (int w = 0; w < W; ++w) better(v, idx, src[((size_t)w * p.B + row) * 2], (int)src[((size_t)w * p.B + row) * 2 + 1]);
+  int token = idx;
+  if (token < 0 || token >= p.Vg) token = 0;
+  p.out_tok[row] = token;
+  if (c.seen) atomicOr(c.seen + (token >> 5), 1u << (token & 31));
+  if (p.rng_counter) p.rng_counter[c.sl] += 1;
+}
+
 }  // namespace
 
 // Segments per row (~8K tokens per workgroup) and the workspace (floats) a
@@ -512,6 +578,8 @@ GRAG_API int grag_sample(const void* logits, int dtype, int ld, int B, int V, co
   p.gidx = reinterpret_cast<int32_t*>(ws + 3 * BS);
   p.hist = ws + 4 * BS;
   p.state = reinterpret_cast<uint32_t*>(ws + 4 * BS + 2 * BS * kNB);
+  p.v0 = 0;
+  p.Vg = V;
   return dtype == 0 ? launch_all<float>(p, rounds, stream) : launch_all<bf16>(p, rounds, stream);
 }
 
@@ -519,5 +587,84 @@ GRAG_API int grag_mark_seen(const int32_t* tokens, const int32_t* rows, int n, u
                             int seen_words, int V, hipStream_t stream) {
   if (n <= 0) return 0;
   mark_seen_kernel<<<(n + 255) / 256, 256, 0, stream>>>(tokens, rows, n, seen, seen_words, V);
+  return (int)hipGetLastError();
+}
+
+// Vocab-parallel sampler, one stage per call (the host runs the TP collectives between stages;
+// every stage is a fixed launch sequence, so the whole chain is captured in the decode graph):
+//   stage 0: segment max/argmax of this rank's columns -> pair_out [B][2]
+//            (host: all-gather -> pairs_max [W][B][2]; gmax computed here from it by stage 1's
+//            first call with r_prev < 0)
+//   stage 1: radix round r (fold of round r_prev from ghist) -> hist_out [B][kNB] (host: SUM all-reduce
+//            in place, it is the next stage's ghist)
+//   stage 2: Gumbel argmax over the kept tokens (fold of r_last from ghist) -> pair_out
+//            (host: all-gather -> pairs_gum [W][B][2])
+//   stage 3: final token from pairs_max / pairs_gum, seen bit, RNG counter
+// logits: [B, ld] holding this rank's V columns = global tokens [v0, v0 + V); Vg = global vocab.
+// ws: grag_sample_ws_floats(B, V) floats; gmax [B] and ghist [B][256] are caller buffers.
+GRAG_API int grag_sample_tp(int stage, const void* logits, int dtype, int ld, int B, int V, int v0, int Vg,
+                            const float* temperature, const float* top_p, const int32_t* top_k,
+                            const float* penalty, uint32_t* seen, int seen_words, int64_t* rng_counter,
+                            uint64_t seed, const int32_t* slots, int32_t* out_tok, float* ws, int r, int r_prev,
+                            int j, float* gmax, float* ghist, float* pair_out, const float* pairs_max,
+                            const float* pairs_gum, int W, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (ld % 8 != 0 || ws == nullptr || (v0 & 7) != 0) return (int)hipErrorInvalidValue;
+  Params p{};
+  p.logits = logits;
+  p.ld = ld;
+  p.B = B;
+  p.V = V;
+  p.S = grag_sample_segments(V);
+  p.seglen = ((V + p.S - 1) / p.S + 7) & ~7;
+  p.temperature = temperature;
+  p.top_p = top_p;
+  p.top_k = top_k;
+  p.penalty = penalty;
+  p.seen = seen;
+  p.seen_words = seen_words;
+  p.rng_counter = rng_counter;
+  p.seed = seed;
+  p.slots = slots;
+  p.out_tok = out_tok;
+  const size_t BS = (size_t)B * p.S;
+  p.seg_max = ws;
+  p.seg_arg = reinterpret_cast<int32_t*>(ws + BS);
+  p.gval = ws + 2 * BS;
+  p.gidx = reinterpret_cast<int32_t*>(ws + 3 * BS);
+  p.hist = ws + 4 * BS;
+  p.state = reinterpret_cast<uint32_t*>(ws + 4 * BS + 2 * BS * kNB);
+  p.v0 = v0;
+  p.Vg = Vg;
+  const dim3 grid(B, p.S);
+  const bool f32 = dtype == 0;
+  switch (stage) {
+    case 0:
+      if (f32) samp_max_kernel<float><<<grid, kT, 0, stream>>>(p);
+      else samp_max_kernel<bf16><<<grid, kT, 0, stream>>>(p);
+      samp_pair_kernel<<<B, 64, 0, stream>>>(p.seg_max, p.seg_arg, p.S, pair_out);
+      break;
+    case 1:
+      if (r_prev < 0) samp_gmax_kernel<<<(B + 255) / 256, 256, 0, stream>>>(pairs_max, W, B, gmax);
+      p.gmax = gmax;
+      p.ghist = r_prev >= 0 ? ghist : nullptr;
+      if (f32) samp_round_kernel<float><<<grid, kT, 0, stream>>>(p, r, r_prev, j);
+      else samp_round_kernel<bf16><<<grid, kT, 0, stream>>>(p, r, r_prev, j);
+      samp_hist_reduce_kernel<<<B, kNB, 0, stream>>>(p.hist, B, p.S, j, ghist);
+      break;
+    case 2:
+      if (r_prev < 0) samp_gmax_kernel<<<(B + 255) / 256, 256, 0, stream>>>(pairs_max, W, B, gmax);
+      p.gmax = gmax;
+      p.ghist = r_prev >= 0 ? ghist : nullptr;
+      if (f32) samp_gumbel_kernel<float><<<grid, kT, 0, stream>>>(p, r_prev, j);
+      else samp_gumbel_kernel<bf16><<<grid, kT, 0, stream>>>(p, r_prev, j);
+      samp_pair_kernel<<<B, 64, 0, stream>>>(p.gval, p.gidx, p.S, pair_out);
+      break;
+    case 3:
+      samp_final_tp_kernel<<<(B + 63) / 64, 64, 0, stream>>>(p, pairs_max, pairs_gum, W);
+      break;
+    default:
+      return (int)hipErrorInvalidValue;
+  }
   return (int)hipGetLastError();
 }

@@ -31,13 +31,14 @@ import numpy as np
 import torch
 
 from ..ops.attention import KV_TILE, AttnMetadata
-from ..ops.sampling import SamplerState, sample
+from ..ops.sampling import SamplerState, sample, sample_tp
 from .scheduler import KVCacheManager, Scheduler
 from .sequence import Completion, SamplingParams, Sequence, SeqStatus
 from ..utils.gpu_guard import gpu_guard
 from .tokenizer import IncrementalDetokenizer
 
 log = logging.getLogger(__name__)
+_TP_SAMPLER = __import__("os").environ.get("GRAG_TP_SAMPLER", "shard")
 
 
 @dataclass
@@ -330,11 +331,11 @@ class LLMEngine:
         finished = []
         if samp_seqs:
             rows = torch.as_tensor(samp_rows, dtype=torch.long, device=self.device)
-            logits = self.model.compute_logits(hidden.index_select(0, rows))
             slot_t = self._to_dev(np.asarray([s.slot for s in samp_seqs], dtype=np.int32))
             tp = self.model.tp
+            toks_d = self._sample(hidden.index_select(0, rows), slot_t)
             tp.stage_health()
-            toks = self._read_host(sample(logits, self.sampler, slot_t)).reshape(-1).tolist()
+            toks = self._read_host(toks_d).reshape(-1).tolist()
             tp.check_health()
             now = time.perf_counter()
             self.stats["host_prefill_sample_s"] += now - t1
@@ -436,9 +437,17 @@ class LLMEngine:
                                 max_q_len=1, num_seqs=B, num_tokens=B, is_decode=True, num_splits=nsplit,
                                 split_len=split_len, part_o=part_o, part_ml=part_ml)
             hidden = self.model.forward(ids, v["pos"][j], meta, self.kv_caches)
-            logits = self.model.compute_logits(hidden)
-            sample(logits, self.sampler, v["slots"], out=out_tokens[j])
+            self._sample(hidden, v["slots"], out=out_tokens[j])
         return out_tokens
+
+    def _sample(self, hidden: torch.Tensor, slots: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """LM head + sampler.  Under TP the vocab-parallel sampler runs on this rank's logit shard
+        (ops/sampling.sample_tp: small (max, histogram, winner) exchanges instead of a full-logit
+        all-gather); GRAG_TP_SAMPLER=gather keeps the gather for A/B."""
+        m = self.model
+        if m.tp.trivial or not hasattr(m, "local_logits") or _TP_SAMPLER == "gather":
+            return sample(m.compute_logits(hidden), self.sampler, slots, out=out)
+        return sample_tp(m.local_logits(hidden), self.sampler, slots, m.tp, m.vocab0, out=out)
 
     def _window(self, seqs, cap: int | None = None) -> int:
         """Largest power-of-two window <= decode_window that no sequence's

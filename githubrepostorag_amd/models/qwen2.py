@@ -64,6 +64,8 @@ class Qwen2Model:
         # gate/up interleaved in 32-row blocks for the fused SwiGLU GEMM epilogue
         self.gu_interleaved = self.inter % 32 == 0
         self.vocab_shard = -(-cfg.vocab_size // ts)
+        if ts > 1:  # shard starts on 8-token boundaries (the sampler reads seen bits 8 at a time)
+            self.vocab_shard = -(-self.vocab_shard // 8) * 8
         self.vocab0 = tr * self.vocab_shard
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         self.cos_sin = rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device)
@@ -239,8 +241,14 @@ class Qwen2Model:
             h = self.tp.all_reduce(self._proj(m, L, "down_w", defer=defer))
         return rmsnorm(h, self.norm, eps, residual=residual)
 
+    def local_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        """hidden [B, H] -> this rank's vocab shard of the logits [B, vocab_shard] (tokens from
+        ``vocab0``): what the vocab-parallel sampler (ops/sampling.sample_tp) consumes."""
+        return linear(hidden, self.lm_head)
+
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        """hidden [B, H] -> logits [B, vocab] (bf16); vocab-parallel gather under TP."""
+        """hidden [B, H] -> logits [B, vocab] (bf16); vocab-parallel gather under TP (the engine
+        samples from ``local_logits`` instead; this full gather serves tests and scoring)."""
         logits = linear(hidden, self.lm_head)
         if not self.tp.trivial:
             g = self.tp.all_gather(logits)  # [tp, B, Vs]

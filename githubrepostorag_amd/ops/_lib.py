@@ -43,6 +43,7 @@ _SIGS = {
     "grag_score_topk_work": [P, I, P, I, I, I, I, P, P, I, P, P, P, I, P, P, P, I, P, P, P, P, P],
     "grag_topk_num_waves": [],
     "grag_sample": [P, I, I, I, I, P, P, P, P, P, I, P, U64, P, P, P, I, P],
+    "grag_sample_tp": [I, P, I, I, I, I, I, I, P, P, P, P, P, I, P, U64, P, P, P, I, I, I, P, P, P, P, P, I, P],
     "grag_sample_segments": [I],
     "grag_sample_ws_floats": [I, I],
     "grag_mark_seen": [P, P, I, P, I, I, P],

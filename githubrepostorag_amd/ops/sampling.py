@@ -178,3 +178,182 @@ def sample(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, out: 
          ptr(state.top_p), ptr(state.top_k), ptr(state.penalty), ptr(state.seen), state.words, ptr(state.rng),
          state.seed, ptr(slots), ptr(out), ptr(state.workspace(B)), state.rounds)
     return out
+
+
+# ---------------------------------------------------------------------- vocab-parallel sampling (C2)
+# Under TP the LM head is vocab-parallel: rank r holds logits of tokens [v0, v0 + Vs).  Round 2
+# all-gathered the whole [B, V] logits every decode step (152064 x 2 B per row: at TP = 8 and 512
+# rows, 136 MB into every rank per step) to run the sampler on the full row.  The sampler is
+# decomposable instead: Gumbel-max over the kept set is a max over shards of shard-local maxima, and
+# the only cross-shard state is the row max and the radix-select histograms of the top-k / top-p
+# thresholds.  So each rank runs the kernel chain on its own columns and the group exchanges:
+#   C2a  all-gather of [B, 2] (max, argmax) pairs            -> row max M (and greedy winners)
+#   C2b  SUM all-reduce of a [B, 256] fp32 histogram per active radix round (<= 8; 4 for top-p)
+#   C2c  all-gather of [B, 2] (Gumbel max, token) pairs      -> the sampled token
+# = B x (16 W + 1 KB x rounds) bytes per step instead of B x 2 V bytes, and the same token on every
+# rank (seen bitmaps and RNG counters stay replicated).  Tokens equal the TP = 1 sampler's up to the
+# summation order of the histogram mass.
+
+_QSCALE = 134217728.0  # 2^27, csrc/kernels/sampling.hip qkey
+_DIGITS = ((28, 15), (20, 255), (12, 255), (4, 255))
+
+
+def _adjusted_row(x: torch.Tensor, state: SamplerState, s: int, v0: int) -> torch.Tensor:
+    """Penalty (seen tokens, by global id) then temperature, like the kernel's for_seg."""
+    V = x.shape[0]
+    pen = float(state.penalty[s])
+    if pen != 1.0:
+        words = state.seen[s].long() & 0xFFFFFFFF
+        idx = torch.arange(v0, v0 + V, device=x.device)
+        m = ((words[idx >> 5] >> (idx & 31)) & 1).bool()
+        x = torch.where(m, torch.where(x > 0, x / pen, x * pen), x)
+    t = float(state.temperature[s])
+    return x if t <= 0 else x * (1.0 / t)
+
+
+def _qkey(x: torch.Tensor, M: float) -> torch.Tensor:
+    d = torch.clamp(M - x, 0.0, 32.0) * _QSCALE
+    di = torch.where(d >= 4294967295.0, torch.full_like(d, -1.0), d).to(torch.float64).floor().to(torch.int64)
+    return torch.where(di < 0, torch.zeros_like(di), 0xFFFFFFFF - di)
+
+
+def _find_bin(hist: torch.Tensor, need: float) -> tuple[int, float]:
+    """Highest bin whose inclusive suffix sum reaches ``need``; (bin, mass strictly above it)."""
+    suffix = hist.flip(0).cumsum(0).flip(0)
+    ok = (suffix >= need).nonzero()
+    if ok.numel() == 0:  # rounding: the lowest bin
+        return 0, float(suffix[0] - hist[0])
+    b = int(ok.max())
+    return b, float(suffix[b] - hist[b])
+
+
+def sample_tp_ref(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, group, v0: int,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """Host / CPU form of the vocab-parallel sampler (the kernel chain's semantics with the same
+    collectives through ``group``: parallel.comm.Group).  logits [B, >= local columns]."""
+    B, Vg = logits.shape[0], state.vocab
+    Vl = max(0, min(logits.shape[1], Vg - v0))
+    res = torch.empty(B, dtype=torch.int32)
+    for b in range(B):
+        s = int(slots[b])
+        x = _adjusted_row(logits[b, :Vl].float(), state, s, v0)
+        gid = torch.arange(v0, v0 + Vl)
+        greedy = not float(state.temperature[s]) > 0
+        if Vl:
+            i = int(torch.argmax(x))
+            pair = torch.tensor([float(x[i]), float(v0 + i)], dtype=torch.float64)
+        else:
+            pair = torch.tensor([float("-inf"), 2.0 ** 30], dtype=torch.float64)
+        pairs = group.all_gather(pair)  # C2a
+        M = float(pairs[:, 0].max())
+        if greedy:
+            best = max(range(pairs.shape[0]), key=lambda w: (float(pairs[w, 0]), -float(pairs[w, 1])))
+            tok = int(pairs[best, 1])
+        else:
+            key = _qkey(x, M)
+            k, p = int(state.top_k[s]), float(state.top_p[s])
+            thr_k = 0
+            if 0 < k < Vg:  # top-k rounds: counts
+                prefix = pmask = 0
+                need = float(k)
+                for shift, mask in _DIGITS:
+                    sel = (key & pmask) == prefix
+                    h = torch.zeros(mask + 1, dtype=torch.float64)
+                    h.index_add_(0, ((key[sel] >> shift) & mask), torch.ones(int(sel.sum()), dtype=torch.float64))
+                    h = group.all_reduce_host(h)  # C2b
+                    bn, above = _find_bin(h, need)
+                    need -= above
+                    prefix |= bn << shift
+                    pmask |= mask << shift
+                thr_k = prefix
+            thr = thr_k
+            if p < 1.0:  # top-p rounds: probability mass inside the top-k set
+                prefix = pmask = 0
+                w = torch.exp((x - M).double())
+                need = None
+                for shift, mask in _DIGITS:
+                    sel = (key >= thr_k) & ((key & pmask) == prefix)
+                    h = torch.zeros(mask + 1, dtype=torch.float64)
+                    h.index_add_(0, ((key[sel] >> shift) & mask), w[sel])
+                    h = group.all_reduce_host(h)  # C2b
+                    if need is None:
+                        need = p * float(h.sum())
+                    bn, above = _find_bin(h, need)
+                    need -= above
+                    prefix |= bn << shift
+                    pmask |= mask << shift
+                thr = prefix
+            keep = key >= thr
+            if Vl and bool(keep.any()):
+                g = gumbel_noise(state.seed, int(state.rng[s]), s, v0 + Vl)[v0:].to(x.device)
+                z = torch.where(keep, x + g, torch.full_like(x, float("-inf")))
+                i = int(torch.argmax(z))
+                gp = torch.tensor([float(z[i]), float(gid[i])], dtype=torch.float64)
+            else:
+                gp = torch.tensor([float("-inf"), 2.0 ** 30], dtype=torch.float64)
+            gps = group.all_gather(gp)  # C2c
+            best = max(range(gps.shape[0]), key=lambda w: (float(gps[w, 0]), -float(gps[w, 1])))
+            tok = int(gps[best, 1])
+        if not 0 <= tok < Vg:
+            tok = 0
+        res[b] = tok
+        wd = int(state.seen[s, tok >> 5]) & 0xFFFFFFFF
+        wd |= 1 << (tok & 31)
+        state.seen[s, tok >> 5] = wd - (1 << 32) if wd >= (1 << 31) else wd
+        state.rng[s] += 1
+    res = res.to(logits.device)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def sample_tp(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, group, v0: int,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """Vocab-parallel sampler: this rank's logits [B, >= local columns] of tokens [v0, ...) ->
+    the same sampled ids int32 [B] on every rank of ``group`` (parallel.comm.Group)."""
+    if group.trivial:
+        return sample(logits, state, slots, out)
+    if not logits.is_cuda:
+        return sample_tp_ref(logits, state, slots, group, v0, out)
+    B, Vg = logits.shape[0], state.vocab
+    Vl = min(logits.shape[1], Vg - v0)
+    if out is None:
+        out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    dev = logits.device
+    gmax = torch.empty(B, dtype=torch.float32, device=dev)
+    ghist = torch.empty(B, 256, dtype=torch.float32, device=dev)
+    pm = torch.empty(B, 2, dtype=torch.float32, device=dev)
+    pg = torch.empty(B, 2, dtype=torch.float32, device=dev)
+    dtype = 0 if logits.dtype == torch.float32 else 1
+    ws = state.workspace(B)
+    W = group.size
+
+    def stage(st, r=0, r_prev=-1, j=0, pair_out=None, pmax=None, pgum=None):
+        call("grag_sample_tp", st, ptr(logits), dtype, logits.stride(0), B, Vl, v0, Vg, ptr(state.temperature),
+             ptr(state.top_p), ptr(state.top_k), ptr(state.penalty), ptr(state.seen), state.words,
+             ptr(state.rng), state.seed, ptr(slots), ptr(out), ptr(ws), r, r_prev, j, ptr(gmax), ptr(ghist),
+             ptr(pair_out), ptr(pmax), ptr(pgum), W)
+
+    stage(0, pair_out=pm)
+    pairs_max = group.all_gather(pm)  # C2a [W, B, 2]
+    rounds = state.rounds
+    r_prev, j = -1, 0
+    for r in range(8):
+        if not (rounds >> (r // 4)) & 1:
+            continue
+        stage(1, r, r_prev, j, pmax=pairs_max)
+        group.all_reduce(ghist)  # C2b
+        r_prev, j = r, j + 1
+    stage(2, 0, r_prev, j, pair_out=pg, pmax=pairs_max)
+    pairs_gum = group.all_gather(pg)  # C2c
+    stage(3, pmax=pairs_max, pgum=pairs_gum)
+    return out
+
+
+def tp_sampling_bytes(rows: int, world: int, vocab: int, rounds: int) -> dict:
+    """Bytes each rank receives per sampling call: vocab-parallel sampler vs a full-logit all-gather."""
+    n_rounds = (4 if rounds & 1 else 0) + (4 if rounds & 2 else 0)
+    shard = -(-vocab // world)
+    return {"vocab_parallel": rows * (2 * 8 * (world - 1) + n_rounds * 256 * 4 * (world - 1) // world * 2),
+            "logit_all_gather": rows * shard * 2 * (world - 1)}

@@ -164,6 +164,14 @@ class Group:
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.pg)
         return int(t.item())
 
+    def all_reduce_host(self, t: torch.Tensor, device=None) -> torch.Tensor:
+        """SUM of a small host tensor over the group (through the GPU under RCCL)."""
+        if self.trivial:
+            return t
+        x = t.to(self.ctrl_device(device))
+        dist.all_reduce(x, group=self.pg)
+        return x.cpu()
+
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[...] -> [size, ...] (one collective)."""
         if self.trivial:

@@ -262,7 +262,6 @@ def test_sampler(dev):
     p = torch.softmax(x / 0.7, 0)
     sp, si = p.sort(descending=True)
     nucleus = set(si[: int((sp.cumsum(0) < 0.9).sum()) + 1].tolist())
-    assert int(out[1]) in nucleus or True  # seen-bit of sampled tokens changes later draws; check first draw only
     assert int(out[1]) in nucleus
     # bf16 logits path + seen-bit bookkeeping
     out2 = S.sample(logits.to(torch.bfloat16), st, slots)
@@ -396,3 +395,79 @@ def test_splitk_deferred_in_graph(dev):
     graph.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, eager) and torch.equal(r_g, r)
+
+
+class _ThreadGroup:
+    """W simulated TP ranks as W threads of one process (one GPU): all_gather / all_reduce are host
+    rendezvous over device tensors (each rank's stream synchronised first)."""
+
+    def __init__(self, world, rank, shared):
+        self.size, self.rank, self.trivial, self.sh = world, rank, False, shared
+
+    def _exchange(self, t):
+        import threading  # noqa: F401
+
+        torch.cuda.current_stream().synchronize()
+        self.sh["buf"][self.rank] = t.clone()
+        self.sh["bar"].wait()
+        allt = torch.stack([x.to(t.device) for x in self.sh["buf"]])
+        self.sh["bar"].wait()
+        return allt
+
+    def all_gather(self, t):
+        return self._exchange(t)
+
+    def all_reduce(self, t):
+        t.copy_(self._exchange(t).sum(0))
+        return t
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sampler_vocab_parallel_matches_full(dev, world):
+    """each simulated TP rank samples from its own vocab shard of the logits (max pairs,
+    radix histograms and Gumbel winners exchanged); every rank gets the same token as the full-row
+    sampler on the whole vocabulary (greedy rows exactly, sampled rows up to histogram rounding)."""
+    import copy
+    import threading
+
+    V, B = 152064, 24
+    g = torch.Generator().manual_seed(5)
+    logits = (torch.randn(B, V, generator=g) * 3).to(dev).to(torch.bfloat16)
+    base = S.SamplerState(B, V, dev, seed=77)
+    for i in range(B):
+        base.reset_slot(i, 0.0 if i % 6 == 0 else 0.7, 0.8 if i % 2 else 1.0, 40 if i % 3 == 0 else 0, 1.2,
+                        list(range(i, 3000, 7)), seed=i)
+    slots = torch.arange(B, dtype=torch.int32, device=dev)
+    full_state = copy.deepcopy(base)
+    ref = [S.sample(logits, full_state, slots).cpu() for _ in range(2)]
+    shard = -(-V // world)
+    shard = -(-shard // 8) * 8
+    shared = {"buf": [None] * world, "bar": threading.Barrier(world)}
+    outs, errs = [None] * world, []
+
+    def rank_fn(r):
+        try:
+            st = copy.deepcopy(base)
+            grp = _ThreadGroup(world, r, shared)
+            loc = torch.zeros(B, shard, dtype=logits.dtype, device=dev)
+            n = min(shard, V - r * shard)
+            loc[:, :n] = logits[:, r * shard:r * shard + n]
+            with torch.cuda.stream(torch.cuda.Stream()):
+                outs[r] = [S.sample_tp(loc, st, slots, grp, r * shard).cpu() for _ in range(2)]
+                torch.cuda.current_stream().synchronize()
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+            shared["bar"].abort()
+
+    th = [threading.Thread(target=rank_fn, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for r in range(1, world):
+        assert all(torch.equal(outs[0][k], outs[r][k]) for k in range(2))  # every rank: the same tokens
+    for k in range(2):
+        greedy = torch.arange(B) % 6 == 0
+        assert torch.equal(outs[0][k][greedy], ref[k][greedy])
+        assert int((outs[0][k] == ref[k]).sum()) >= B - 1, (outs[0][k], ref[k])
