@@ -28,6 +28,12 @@ namespace {
 enum { EPI_STORE = 0, EPI_SILU = 1, EPI_PARTIAL = 2 };
 enum { ACT_NONE = 0, ACT_GELU = 1, ACT_GELU_TANH = 3 };
 constexpr int kDepth = 3;   // K-steps in flight (ring of kDepth + 1)
+// Diagnostic builds only (scripts/dev/w4_diag.py, never the shipped library): GRAG_W4_DIAG bit 0 drains
+// every load before each step's barrier (no loads in flight across compute), bit 1 pads the workgroup's LDS
+// to 160 KB (one workgroup per CU); GRAG_W4_ALL_VARIANTS launches the 4/8/12-row-tile variants too.
+#ifndef GRAG_W4_DIAG
+#define GRAG_W4_DIAG 0
+#endif
 constexpr int kGroup = 128; // quantisation group along K
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
@@ -112,7 +118,7 @@ __global__ __launch_bounds__(64 * NWV) void gemm_w4_kernel(WArgs p) {
   constexpr int GA = (MT * 2) / NWV;
   constexpr int GW = 3;  // W dwordx4 + two (s, -z s) dwordx2 per lane per K-step
   static_assert((MT * 2) % NWV == 0, "A pieces must split evenly over the waves");
-  __shared__ __attribute__((aligned(16))) char smem[NST * ABYTES];
+  __shared__ __attribute__((aligned(16))) char smem[(GRAG_W4_DIAG & 2) ? 160 * 1024 : NST * ABYTES];
 
   const int tid = threadIdx.x;
   const int L = tid & 63;
@@ -182,6 +188,7 @@ __global__ __launch_bounds__(64 * NWV) void gemm_w4_kernel(WArgs p) {
   for (int t0 = 0; t0 < nsteps; t0 += NST) {
 #pragma unroll
     for (int u = 0; u < NST; ++u) {
+      if constexpr ((GRAG_W4_DIAG & 1) != 0) wait_w<0>(wv[u], s0[u], s1[u]);
       wait_w<(D - 1) * (GA + GW)>(wv[u], s0[u], s1[u]);
       bar();
       issue(t0 + u + D, (u + D) % NST);
@@ -256,7 +263,11 @@ int launch_v(const WArgs& a, int epi, int act, int nwg, hipStream_t s) {
 // kernel's small register loads and its LDS-DMA A ring, which the 16-tile variant never showed in any test
 // or sweep.  The engine therefore takes the W4 path only at 129..256 rows (16-tile padding) and the bf16
 // decode kernel below that (the same quantised values).
+#ifdef GRAG_W4_ALL_VARIANTS
+GRAG_API int grag_gemm_w4_has(int mt, int nwv) { return nwv == 4 && (mt == 4 || mt == 8 || mt == 12 || mt == 16); }
+#else
 GRAG_API int grag_gemm_w4_has(int mt, int nwv) { return nwv == 4 && mt == 16; }
+#endif
 
 // y = epilogue(x @ dequant(wq)^T) for M <= 16 * mt rows.  wq / sz from ops/quant.py pack_w4 (rows in
 // consumption order: natural, or gate/up 16-row pairs for epi 1 = silu*mul -> out [M, N/2]).  ksplit > 1
@@ -290,6 +301,12 @@ GRAG_API int grag_gemm_w4(const void* A, const void* Wq, const void* sz, const v
   const int nwg = (N / (32 * nwv)) * ksplit;
   const int e = ksplit > 1 ? EPI_PARTIAL : epi;
   int err;
+#ifdef GRAG_W4_ALL_VARIANTS
+  if (mt == 4) err = launch_v<4, 4>(a, e, act, nwg, stream);
+  else if (mt == 8) err = launch_v<8, 4>(a, e, act, nwg, stream);
+  else if (mt == 12) err = launch_v<12, 4>(a, e, act, nwg, stream);
+  else
+#endif
   err = launch_v<16, 4>(a, e, act, nwg, stream);
   if (err || ksplit == 1) return err;
   return grag_splitk_reduce(ws, bias, C, ldc, M, N, ksplit, epi, act, stream);
