@@ -113,7 +113,7 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 
-constexpr int kDepth = 3;  // K-steps of W and A in flight (ring of kDepth + 1)
+constexpr int kDepth = 4;  // K-steps of W and A issued ahead (ring of kDepth + 1 slots)
 
 struct DArgs {
   const bf16* A;
@@ -138,6 +138,7 @@ void gemm_dec_kernel(DArgs p) {
   constexpr int GA = (NPC + NWV - 1) / NWV;    // per wave (the last wave may repeat its final piece)
   constexpr int GW = 2 * NTW;                  // W dwordx4 per lane per K-step
   static_assert(NTW == 2 || NTW == 4, "NTW");
+  static_assert(NST * ABYTES <= 160 * 1024, "LDS ring exceeds 160 KB");
   __shared__ __attribute__((aligned(16))) char smem[NST * ABYTES];
 
   const int tid = threadIdx.x;
@@ -246,20 +247,25 @@ void gemm_dec_kernel(DArgs p) {
     }
   };
 
-  // prologue: steps 0 .. D-1 in flight (nsteps >= NST, checked by the launcher)
+  // prologue: steps 0 .. D-1 in flight
 #pragma unroll
   for (int d = 0; d < D; ++d) issue(d, d, wf[d]);
 
-  // nsteps is a multiple of NST (launcher), so ring slots are compile-time in the unrolled body and no
-  // step is conditional
+  // A K-step's LDS slot is read one barrier interval AFTER the wait that retires its LDS-DMA (cdna guide §5
+  // "Read a staged buffer one phase AFTER the wait that retires it"): iteration t retires step t + 1 and
+  // computes step t.  The round-2 schedule (retire step t, barrier, read step t) is the one that returned
+  // wrong results in gemm_w4.hip's 4/8/12-row variants (root cause there, scripts/dev/w4_diag.py); here it
+  // had passed every test, by placement.  Steps t + 2 .. t + D - 1 stay in flight across compute(t), as
+  // many as before (D is one deeper).
+  wait_w<(D - 1) * (GA + GW)>(wf[0]);
+  bar();
   for (int t0 = 0; t0 < nsteps; t0 += NST) {
 #pragma unroll
     for (int u = 0; u < NST; ++u) {
-      // steps t+1 .. t+D-1 were issued after step t: (D-1)(GA+GW) younger ops
-      wait_w<(D - 1) * (GA + GW)>(wf[u]);
-      bar();  // step t's A pieces visible to every wave; every wave is done with slot (u + D) % NST
+      wait_w<(D - 2) * (GA + GW)>(wf[(u + 1) % NST]);  // retire step t + 1
+      bar();  // every wave is done with slot (u + D) % NST (= step t - 1's); step t + 1 retired everywhere
       issue(t0 + u + D, (u + D) % NST, wf[(u + D) % NST]);
-      compute(u, wf[u]);
+      if (t0 + u < nsteps) compute(u, wf[u]);  // uniform: a split's last round may be partial
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-reads land before the workgroup retires
@@ -350,7 +356,7 @@ GRAG_API int grag_gemm_decode_has(int mt, int nwv, int ntw) {
 // [N / (16 ntw)][K / 64][16 ntw][64] (ops/gemm.py dec_pack), ldw ignored; packed = 2: the same for an
 // interleaved gate/up weight packed in gate/up units (16 gate rows then their 16 up rows; ntw 2).
 // Requirements (checked):
-// K % 256 == 0 (whole ring rounds per split), N % (16 * ntw) == 0 (silu: N % 64 == 0), lda/ldw % 8 == 0,
+// K % 64 == 0, N % (16 * ntw) == 0 (silu: N % 64 == 0), lda/ldw % 8 == 0,
 // ldc % 4 == 0, 16-B aligned A/W.
 GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, void* C, int lda, int ldw, int ldc,
                               int M, int N, int K, int epi, int act, int mt, int nwv, int ntw, int ksplit, int gs,
@@ -375,11 +381,9 @@ GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, vo
   if (act != ACT_NONE && act != ACT_GELU && act != ACT_GELU_TANH) return (int)hipErrorInvalidValue;
   if ((epi == EPI_SILU || keep) && act != ACT_NONE) return (int)hipErrorInvalidValue;
   if (keep && bias != nullptr) return (int)hipErrorInvalidValue;
-  constexpr int NST = kDepth + 1;
   const int kt = K / 64;
-  if (kt % NST != 0) return (int)hipErrorInvalidValue;
   if (ksplit < 1) ksplit = 1;
-  const int kts = ((kt / NST + ksplit - 1) / ksplit) * NST;
+  const int kts = (kt + ksplit - 1) / ksplit;
   ksplit = (kt + kts - 1) / kts;  // effective splits (ops/gemm.py dec_ksplit computes the same)
   if ((ksplit > 1 || keep) && ws == nullptr) return (int)hipErrorInvalidValue;
   if (keep && ksplit == 1) return (int)hipErrorInvalidValue;

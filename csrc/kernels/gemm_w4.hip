@@ -18,6 +18,15 @@
 //     is [16 gate rows | the 16 matching up rows] so silu(g)*u forms in registers (EPI_SILU).
 #include "common.h"
 
+// Diagnostic builds only (scripts/dev/w4_diag.py, never the shipped library): GRAG_W4_DIAG bit 0 drains
+// every load before each step's barrier (no loads in flight across compute), bit 1 pads the workgroup's LDS
+// to 160 KB (one workgroup per CU), bit 2 loads the weights with plain (compiler-visible) loads instead of
+// the inline-asm ring, bit 3 checks every fragment against global memory, bit 4 pads wait states between
+// the dequant and the MFMAs.
+#ifndef GRAG_W4_DIAG
+#define GRAG_W4_DIAG 0
+#endif
+
 using namespace grag;
 
 GRAG_API int grag_splitk_reduce(const void* ws, const void* bias, void* C, int ldc, int M, int N, int S, int epi,
@@ -27,13 +36,8 @@ namespace {
 
 enum { EPI_STORE = 0, EPI_SILU = 1, EPI_PARTIAL = 2 };
 enum { ACT_NONE = 0, ACT_GELU = 1, ACT_GELU_TANH = 3 };
-constexpr int kDepth = 3;   // K-steps in flight (ring of kDepth + 1)
-// Diagnostic builds only (scripts/dev/w4_diag.py, never the shipped library): GRAG_W4_DIAG bit 0 drains
-// every load before each step's barrier (no loads in flight across compute), bit 1 pads the workgroup's LDS
-// to 160 KB (one workgroup per CU); GRAG_W4_ALL_VARIANTS launches the 4/8/12-row-tile variants too.
-#ifndef GRAG_W4_DIAG
-#define GRAG_W4_DIAG 0
-#endif
+constexpr int kDepth = 4;   // K-steps issued ahead (ring of kDepth + 1 slots)
+
 constexpr int kGroup = 128; // quantisation group along K
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
@@ -65,6 +69,12 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 // registers are consumed only after wait_w, which names them
 __device__ __forceinline__ void ldw(u32x4_t& q, f32x2_t& sz0, f32x2_t& sz1, const void* pq, const void* p0,
                                     const void* p1) {
+  if constexpr ((GRAG_W4_DIAG & 4) != 0) {  // diagnostic: plain compiler-visible loads (waits placed by hipcc)
+    q = *reinterpret_cast<const u32x4_t*>(pq);
+    sz0 = *reinterpret_cast<const f32x2_t*>(p0);
+    sz1 = *reinterpret_cast<const f32x2_t*>(p1);
+    return;
+  }
   asm volatile(
       "global_load_dwordx4 %0, %3, off\n\t"
       "global_load_dwordx2 %1, %4, off\n\t"
@@ -76,6 +86,10 @@ __device__ __forceinline__ void ldw(u32x4_t& q, f32x2_t& sz0, f32x2_t& sz1, cons
 
 template <int N>
 __device__ __forceinline__ void wait_w(u32x4_t& q, f32x2_t& a, f32x2_t& b) {
+  if constexpr ((GRAG_W4_DIAG & 4) != 0) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    return;
+  }
   asm volatile("s_waitcnt vmcnt(%3)" : "+v"(q), "+v"(a), "+v"(b) : "n"(N) : "memory");
 }
 
@@ -100,6 +114,12 @@ __device__ __forceinline__ bf16x8_t dequant8(unsigned d, float s, float zs) {
   return pack8(v);
 }
 
+#if (GRAG_W4_DIAG & 8) != 0
+// diagnostic: [0] A-fragment mismatches (LDS vs global), [1] W-word mismatches (ring vs global),
+// [2..5] first A mismatch (step, mt, lane, k-half), [6..8] first W mismatch (step, lane, word)
+__device__ unsigned g_w4_diag[16];
+#endif
+
 struct WArgs {
   const bf16* A;
   const unsigned* Wq;  // [N/32][K/64][64][4] dwords
@@ -118,6 +138,7 @@ __global__ __launch_bounds__(64 * NWV) void gemm_w4_kernel(WArgs p) {
   constexpr int GA = (MT * 2) / NWV;
   constexpr int GW = 3;  // W dwordx4 + two (s, -z s) dwordx2 per lane per K-step
   static_assert((MT * 2) % NWV == 0, "A pieces must split evenly over the waves");
+  static_assert(NST * ABYTES <= 160 * 1024, "LDS ring exceeds 160 KB");
   __shared__ __attribute__((aligned(16))) char smem[(GRAG_W4_DIAG & 2) ? 160 * 1024 : NST * ABYTES];
 
   const int tid = threadIdx.x;
@@ -166,11 +187,42 @@ __global__ __launch_bounds__(64 * NWV) void gemm_w4_kernel(WArgs p) {
   const int sw = (li >> 1) & 7;
   const int aoff0 = li * 128 + ((h4 ^ sw) << 4);
   const int aoff1 = li * 128 + (((4 + h4) ^ sw) << 4);
-  auto compute = [&](int slot) {
-    const bf16x8_t w00 = dequant8(wv[slot][0], s0[slot][0], s0[slot][1]);
-    const bf16x8_t w01 = dequant8(wv[slot][1], s0[slot][0], s0[slot][1]);
-    const bf16x8_t w10 = dequant8(wv[slot][2], s1[slot][0], s1[slot][1]);
-    const bf16x8_t w11 = dequant8(wv[slot][3], s1[slot][0], s1[slot][1]);
+  auto compute = [&](int slot, int step) {
+#if (GRAG_W4_DIAG & 8) != 0
+    {  // every fragment this lane is about to use, against the same bytes read straight from global memory
+      const char* Ad = smem + slot * ABYTES;
+      for (int mt = 0; mt < MT; ++mt) {
+        for (int hh = 0; hh < 2; ++hh) {
+          const bf16x8_t got = *reinterpret_cast<const bf16x8_t*>(Ad + mt * 2048 + (hh ? aoff1 : aoff0));
+          const int row = min(mt * 16 + li, p.M - 1);
+          const bf16x8_t want = *reinterpret_cast<const bf16x8_t*>(p.A + (size_t)row * p.lda +
+                                                                    (size_t)(kb + step) * 64 + (4 * hh + h4) * 8);
+          if (__builtin_bit_cast(u32x4_t, got)[0] != __builtin_bit_cast(u32x4_t, want)[0] ||
+              __builtin_bit_cast(u32x4_t, got)[3] != __builtin_bit_cast(u32x4_t, want)[3]) {
+            if (atomicAdd(&g_w4_diag[0], 1u) == 0u) {
+              g_w4_diag[2] = step; g_w4_diag[3] = mt; g_w4_diag[4] = L; g_w4_diag[5] = hh;
+            }
+          }
+        }
+      }
+      const u32x4_t wwant = *reinterpret_cast<const u32x4_t*>(wq + (size_t)step * 1024);
+      for (int e = 0; e < 4; ++e)
+        if (wv[slot][e] != wwant[e]) {
+          if (atomicAdd(&g_w4_diag[1], 1u) == 0u) { g_w4_diag[6] = step; g_w4_diag[7] = L; g_w4_diag[8] = e; }
+        }
+    }
+#endif
+    bf16x8_t w00 = dequant8(wv[slot][0], s0[slot][0], s0[slot][1]);
+    bf16x8_t w01 = dequant8(wv[slot][1], s0[slot][0], s0[slot][1]);
+    bf16x8_t w10 = dequant8(wv[slot][2], s1[slot][0], s1[slot][1]);
+    bf16x8_t w11 = dequant8(wv[slot][3], s1[slot][0], s1[slot][1]);
+#if (GRAG_W4_DIAG & 16) != 0
+    // diagnostic: pin the dequantised fragments, then 16 wait states, before any MFMA reads them
+    asm volatile("" : "+v"(w00), "+v"(w01), "+v"(w10), "+v"(w11));
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     const char* As = smem + slot * ABYTES;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -185,14 +237,25 @@ __global__ __launch_bounds__(64 * NWV) void gemm_w4_kernel(WArgs p) {
 
 #pragma unroll
   for (int d = 0; d < D; ++d) issue(d, d);
+  // A K-step's LDS slot is READ one barrier interval after the wait that retires its LDS-DMA, never in
+  // the same interval (cdna_hip_programming.md §5 "Read a staged buffer one phase AFTER the wait that
+  // retires it"): iteration t waits for step t + 1 and computes step t.  Round 2 waited for step t and
+  // read it right after one barrier; that passed for some row tilings and builds and returned 1-25 %
+  // wrong results for others (scripts/dev/w4_diag.py: draining every load before the barrier, plain
+  // loads instead of the inline-asm register ring, one workgroup per CU and in-kernel data checks did not
+  // explain it; adding wait states moved which tilings failed): the DMA's LDS write is not ordered for a
+  // same-interval ds_read by the vmcnt + barrier alone.
+  wait_w<(D - 1) * (GA + GW)>(wv[0], s0[0], s1[0]);
+  bar();
   for (int t0 = 0; t0 < nsteps; t0 += NST) {
 #pragma unroll
     for (int u = 0; u < NST; ++u) {
-      if constexpr ((GRAG_W4_DIAG & 1) != 0) wait_w<0>(wv[u], s0[u], s1[u]);
-      wait_w<(D - 1) * (GA + GW)>(wv[u], s0[u], s1[u]);
+      if constexpr ((GRAG_W4_DIAG & 1) != 0) wait_w<0>(wv[(u + 1) % NST], s0[(u + 1) % NST], s1[(u + 1) % NST]);
+      // retire step t + 1 (steps t + 2 .. t + D - 1 stay in flight)
+      wait_w<(D - 2) * (GA + GW)>(wv[(u + 1) % NST], s0[(u + 1) % NST], s1[(u + 1) % NST]);
       bar();
-      issue(t0 + u + D, (u + D) % NST);
-      compute(u);
+      issue(t0 + u + D, (u + D) % NST);  // slot of step t - 1: its readers passed this barrier
+      if (t0 + u < nsteps) compute(u, t0 + u);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -257,17 +320,11 @@ int launch_v(const WArgs& a, int epi, int act, int nwg, hipStream_t s) {
 
 }  // namespace
 
-// Variant: (mt, nwv) = (16, 4) only.  The 4-, 8- and 12-row-tile variants of this kernel were built and
-// measured WRONG on dense operands (1-15 % relative error, varying with the build and run) while exact on
-// one-hot probes (scripts/dev/w4_diag3.py / w4_diag4.py): an unresolved ordering problem between this
-// kernel's small register loads and its LDS-DMA A ring, which the 16-tile variant never showed in any test
-// or sweep.  The engine therefore takes the W4 path only at 129..256 rows (16-tile padding) and the bf16
-// decode kernel below that (the same quantised values).
-#ifdef GRAG_W4_ALL_VARIANTS
+// Variants: (mt, nwv) = (4, 4), (8, 4), (12, 4), (16, 4).  Round 2 shipped (16, 4) only: the others
+// returned 1-15 % wrong results on dense operands.  Root cause (scripts/dev/w4_diag.py, GPU runs in
+// profiles/w4_diag_r3.txt): each K-step's A slot was read in the same barrier interval as the vmcnt wait
+// that retired its LDS-DMA; the ring now retires step t + 1 one interval before step t + 1 is read.
 GRAG_API int grag_gemm_w4_has(int mt, int nwv) { return nwv == 4 && (mt == 4 || mt == 8 || mt == 12 || mt == 16); }
-#else
-GRAG_API int grag_gemm_w4_has(int mt, int nwv) { return nwv == 4 && mt == 16; }
-#endif
 
 // y = epilogue(x @ dequant(wq)^T) for M <= 16 * mt rows.  wq / sz from ops/quant.py pack_w4 (rows in
 // consumption order: natural, or gate/up 16-row pairs for epi 1 = silu*mul -> out [M, N/2]).  ksplit > 1
@@ -282,10 +339,9 @@ GRAG_API int grag_gemm_w4(const void* A, const void* Wq, const void* sz, const v
   if (epi != EPI_STORE && epi != EPI_SILU) return (int)hipErrorInvalidValue;
   if (act != ACT_NONE && act != ACT_GELU && act != ACT_GELU_TANH) return (int)hipErrorInvalidValue;
   if (epi == EPI_SILU && (act != ACT_NONE || ksplit > 1)) return (int)hipErrorInvalidValue;
-  constexpr int NST = kDepth + 1;
   const int kt = K / 64;
   if (ksplit < 1) ksplit = 1;
-  const int kts = ((kt / NST + ksplit - 1) / ksplit) * NST;
+  const int kts = (kt + ksplit - 1) / ksplit;  // any split length: steps past a split's end are not computed
   ksplit = (kt + kts - 1) / kts;
   if (ksplit > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
   WArgs a;
@@ -301,13 +357,10 @@ GRAG_API int grag_gemm_w4(const void* A, const void* Wq, const void* sz, const v
   const int nwg = (N / (32 * nwv)) * ksplit;
   const int e = ksplit > 1 ? EPI_PARTIAL : epi;
   int err;
-#ifdef GRAG_W4_ALL_VARIANTS
   if (mt == 4) err = launch_v<4, 4>(a, e, act, nwg, stream);
   else if (mt == 8) err = launch_v<8, 4>(a, e, act, nwg, stream);
   else if (mt == 12) err = launch_v<12, 4>(a, e, act, nwg, stream);
-  else
-#endif
-  err = launch_v<16, 4>(a, e, act, nwg, stream);
+  else err = launch_v<16, 4>(a, e, act, nwg, stream);
   if (err || ksplit == 1) return err;
   return grag_splitk_reduce(ws, bias, C, ldc, M, N, ksplit, epi, act, stream);
 }

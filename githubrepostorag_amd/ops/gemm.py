@@ -276,7 +276,7 @@ def gemm_silu(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None = N
 
 
 # ---------------------------------------------------------------- decode regime (csrc/kernels/gemm_decode.hip)
-DEC_DEPTH = 3  # K-steps in flight; a K-split covers whole rings of DEC_DEPTH + 1 steps
+DEC_DEPTH = 4  # K-steps issued ahead by the decode kernel (ring of DEC_DEPTH + 1 LDS / register slots)
 _DEC_ON = os.environ.get("GRAG_DECODE_GEMM", "1") != "0"
 # (mt, nwv, ntw) compiled: mt 16-row tiles of M, nwv waves per workgroup, ntw 16-row W tiles per wave
 DEC_VARIANTS = [(4, 4, 2), (4, 5, 2), (8, 4, 2), (8, 5, 2), (12, 5, 2), (12, 8, 2), (16, 4, 2)]
@@ -294,10 +294,9 @@ def dec_variants(M: int) -> list[tuple[int, int, int]]:
 
 
 def dec_ksplit(K: int, ksplit: int) -> int:
-    """Effective K-splits after rounding each split to whole rings (same rule as the launcher)."""
+    """Effective K-splits (same rule as the launcher: ceil(kt / ksplit) K-steps per split)."""
     kt = K // 64
-    nst = DEC_DEPTH + 1
-    kts = -(-(kt // nst) // max(1, ksplit)) * nst
+    kts = -(-kt // max(1, ksplit))
     return -(-kt // kts)
 
 

@@ -28,10 +28,10 @@ import os
 import torch
 
 from ._lib import call, ptr
-from .gemm import ACT_NONE, EPI_SILU, EPI_STORE, WS, _num_cus, dec_ksplit
+from .gemm import ACT_NONE, EPI_SILU, EPI_STORE, WS, _num_cus
 
 GROUP = 128
-W4_VARIANTS = [(16, 4)]  # (mt, nwv) compiled (see csrc/kernels/gemm_w4.hip for why only this one)
+W4_VARIANTS = [(4, 4), (8, 4), (12, 4), (16, 4)]  # (mt, nwv) compiled (csrc/kernels/gemm_w4.hip)
 W4_MIN_M = int(os.environ.get("GRAG_W4_MIN_M", "129"))  # below: the bf16 decode kernel (same values)
 W4_MAX_M = 256
 
@@ -114,6 +114,13 @@ class W4Linear:
         return self.wq.numel() * 4 + self.sz.numel() * 4
 
 
+def w4_ksplit(K: int, ksplit: int) -> int:
+    """Effective K-splits of the W4 kernel (same rule as grag_gemm_w4: ceil(kt / ksplit) steps each)."""
+    kt = K // 64
+    kts = -(-kt // max(1, ksplit))
+    return -(-kt // kts)
+
+
 def plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int, int] | None:
     """(mt, nwv, ksplit): the smallest compiled row tiling for M, about one workgroup per CU; None outside
     the measured range (W4_MIN_M..256 rows, and not the FFN-wide gate/up weight, where the bf16 tile kernel
@@ -127,7 +134,7 @@ def plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int, int] | N
     mt, nwv = min(vs)
     tiles = N // (32 * nwv)
     ncu = _num_cus()
-    ks = 1 if silu or tiles >= ncu else dec_ksplit(K, max(1, ncu // tiles))
+    ks = 1 if silu or tiles >= ncu else w4_ksplit(K, max(1, ncu // tiles))
     return mt, nwv, ks
 
 
@@ -145,7 +152,7 @@ def gemm_w4(x: torch.Tensor, w: W4Linear, bias: torch.Tensor | None = None, act:
             y = (torch.nn.functional.silu(v[:, :, 0]) * v[:, :, 1]).reshape(M, -1)
         return y.to(x.dtype)
     mt, nwv, ks = plan_ or plan(M, w.N, K, w.silu)
-    ks = 1 if w.silu else dec_ksplit(K, ks)
+    ks = 1 if w.silu else w4_ksplit(K, ks)
     if out is None:
         out = torch.empty(M, w.N // 2 if w.silu else w.N, dtype=x.dtype, device=x.device)
     fl = ks * M * w.N if ks > 1 else 0

@@ -5,7 +5,13 @@ tiling enabled and one behaviour changed per copy (GRAG_W4_DIAG bits, see the ke
   d0  as shipped                               (loads in flight across the barrier, LDS sized to the ring)
   d1  every load drained before the barrier    (no in-flight register / LDS-DMA writes during compute)
   d2  LDS padded to 160 KB                     (one workgroup per CU)
-  d3  both
+  d4  weights by plain compiler-visible loads (no inline-asm register ring; hipcc places the waits)
+  d5  d4 + drain before the barrier
+  d8  in-kernel checks: every A fragment read from the LDS ring and every W word from the register ring
+      compared with the same bytes loaded straight from global memory (mismatch counters + first
+      mismatch's step / tile / lane), d12 the same with plain W loads
+  d16 16 wait states between the dequant (VALU writes of the W fragments) and the MFMAs reading them,
+      d17 the same + drain before the barrier
 and (``--run``, on the GPU) times nothing: it runs each copy on dense random operands for every tiling
 and reports the max relative error against the fp32 reference of the same 4-bit weights, several times
 in one process.  Which switch removes the error names the mechanism.
@@ -23,6 +29,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 OUT = os.path.join(ROOT, "scripts", "dev", "_w4diag")  # the .so files travel to the GPU box (build/ does not)
 OBJ = os.path.join(ROOT, "build", "w4diag")
 sys.path.insert(0, ROOT)
+DIAGS = (0, 1, 16, 17)
 
 
 def build():
@@ -34,7 +41,7 @@ def build():
     k = os.path.join(ROOT, "csrc", "kernels")
     tile_o = os.path.join(OBJ, "gemm_tile.o")
     subprocess.run([hipcc, *HIPCC_FLAGS, "-I", k, "-c", os.path.join(k, "gemm_tile.hip"), "-o", tile_o], check=True)
-    for d in range(4):
+    for d in DIAGS:
         o = os.path.join(OBJ, f"w4_d{d}.o")
         subprocess.run([hipcc, *HIPCC_FLAGS, "-I", k, f"-DGRAG_W4_DIAG={d}", "-DGRAG_W4_ALL_VARIANTS", "-c",
                         os.path.join(k, "gemm_w4.hip"), "-o", o], check=True)
@@ -52,7 +59,7 @@ def run(reps: int):
     g = torch.Generator(device="cpu").manual_seed(0)
     shapes = [(64, 3584, 3584), (128, 4608, 3584), (192, 3584, 3584), (256, 3584, 3584)]
     P, I = ctypes.c_void_p, ctypes.c_int
-    for d in range(4):
+    for d in DIAGS:
         lib = ctypes.CDLL(os.path.join(OUT, f"libw4_d{d}.so"), mode=ctypes.RTLD_LOCAL)
         f = lib.grag_gemm_w4
         f.argtypes = [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P]
@@ -67,7 +74,10 @@ def run(reps: int):
                 if 16 * mt < M:
                     continue
                 errs = []
+                diag = None
                 for _ in range(reps):
+                    if d & 8:
+                        lib.grag_w4_diag(None, 1)
                     out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=dev)
                     rc = f(x.data_ptr(), q.wq.data_ptr(), q.sz.data_ptr(), None, out.data_ptr(), x.stride(0),
                            out.stride(0), M, N, K, 0, 0, mt, 4, 1, None, torch.cuda.current_stream().cuda_stream)
@@ -75,8 +85,12 @@ def run(reps: int):
                     assert rc == 0, rc
                     e = ((out.float() - ref).abs().max() / ref.abs().max()).item()
                     errs.append(round(e, 5))
+                    if d & 8:
+                        buf = (ctypes.c_uint * 16)()
+                        lib.grag_w4_diag(buf, 0)
+                        diag = list(buf)[:9]
                 print(json.dumps({"diag": d, "M": M, "N": N, "K": K, "mt": mt, "max_rel_err": max(errs),
-                                  "errs": errs}), flush=True)
+                                  "errs": errs, "checks": diag}), flush=True)
 
 
 if __name__ == "__main__":
