@@ -294,10 +294,13 @@ def dec_variants(M: int) -> list[tuple[int, int, int]]:
 
 
 def dec_ksplit(K: int, ksplit: int) -> int:
-    """Effective K-splits (same rule as the launcher: ceil(kt / ksplit) K-steps per split)."""
+    """Effective K-splits of a requested count: splits of whole 4-step rounds (the rule the decode plans
+    were measured with), then the launcher's own rule (ceil(kt / ks) steps per split) on that count, so the
+    fp32 plane count here always equals the kernel's."""
     kt = K // 64
-    kts = -(-kt // max(1, ksplit))
-    return -(-kt // kts)
+    kts = -(-(kt // 4) // max(1, ksplit)) * 4 if kt >= 4 else kt
+    ks = -(-kt // max(1, kts))
+    return -(-kt // -(-kt // ks))
 
 
 def dec_plan(M: int, N: int, K: int, silu: bool = False) -> tuple | None:

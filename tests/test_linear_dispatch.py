@@ -32,7 +32,7 @@ def test_decode_gemm_plan_rules():
     from githubrepostorag_amd.ops import gemm as G
 
     assert G.dec_plan(96, 4608, 1000) is None             # K % 256
-    assert G.dec_ksplit(3584, 9) == 8                     # 56 K-steps: ceil(56 / 9) = 7 per split -> 8 splits
+    assert G.dec_ksplit(3584, 9) == 7                     # 14 rounds of 4 steps -> 2 rounds per split
     assert G.dec_variants(100) == [(8, 4, 2), (8, 5, 2)]
     assert G.dec_variants(190) == [(12, 5, 2), (12, 8, 2)]
     G_ncu = G._num_cus
