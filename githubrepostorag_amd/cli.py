@@ -43,10 +43,10 @@ def _settings(args):
     return s
 
 
-def _runtime(args, build_engine=True, shard=None):
+def _runtime(args, build_engine=True, shard=None, device=None):
     from .service.runtime import RAGRuntime
 
-    return RAGRuntime(_settings(args), build_engine=build_engine, shard=shard)
+    return RAGRuntime(_settings(args), build_engine=build_engine, shard=shard, device=device)
 
 
 def cmd_serve(args) -> int:
@@ -146,10 +146,95 @@ def cmd_replica(args) -> int:
             rt.close()
 
 
+def _spawn_ingest_ranks(n: int) -> int:
+    """``ingest --dp N`` without a launcher: N rank processes of this command (one per GPU), no exec."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=os.environ.get("MASTER_PORT", str(port)))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, "-m", "githubrepostorag_amd", *sys.argv[1:]], env=env))
+    rc = 0
+    for p in procs:
+        rc = rc or p.wait()
+    return rc
+
+
+def cmd_ingest_dp(args, s) -> int:
+    """Data-parallel ingest: rank r of N ingests repositories r, r + N, ... on its own GPU,
+    then the rows are re-partitioned by owning shard (crc32(row id) mod S) into S shard snapshots
+    ``INDEX_DIR/shard-s-of-S`` that ``serve --replicas S`` loads (index/sharded_store.py).  Ids are content
+    hashes (ingest/writer.py), so no id ranges are exchanged; the only collectives are a count all-gather
+    (for the run manifest) and the barriers between the phases (gloo: nothing here needs the GPU fabric)."""
+    import torch.distributed as dist
+
+    from .index.sharded_store import merge_into, shard_dir, split_store
+    from .index.store import VectorStore
+    from .ingest.controller import IngestController
+    from .parallel import comm
+
+    info = comm.init_distributed(backend="gloo")
+    rank, world = info.rank, info.world_size
+    out = args.save or s.index_dir
+    if not out:
+        raise SystemExit("ingest --dp needs --save or INDEX_DIR (the shard snapshots go there)")
+    shards = args.shards or world
+    if args.repos:
+        comps = [{"repo": r, "namespace": args.namespace} for r in args.repos]
+    elif args.source == "synthetic":
+        comps = [{"repo": f"synthetic-repo-{i}", "namespace": args.namespace} for i in range(max(world, args.n_repos))]
+    else:
+        raise SystemExit("ingest --dp splits a list of repositories: pass --repos (or --source synthetic)")
+    mine = comps[rank::world]
+    import torch
+
+    dev = f"cuda:{info.local_rank}" if torch.cuda.is_available() and s.device != "cpu" else "cpu"
+    rt = _runtime(args, device=dev)
+    ctl = IngestController(rt, extract=not args.no_extract)
+    res = ctl.ingest_many(mine, branch=args.branch, source=args.source, path=args.path,
+                          dev_force_standalone=args.dev_force_standalone or s.dev_force_standalone)
+    counts = [None] * world
+    dist.all_gather_object(counts, {"rank": rank, "repos": [r.get("repo") for r in res],
+                                    "nodes": sum(r.get("nodes_written") or 0 for r in res),
+                                    "documents": sum(r.get("documents") or 0 for r in res)})
+    for s_, part in enumerate(split_store(rt.store, shards)):
+        part.save(os.path.join(out, "parts", str(rank), shard_dir(s_, shards)))
+    rt.close()
+    dist.barrier()
+    for s_ in range(rank, shards, world):  # each shard merged by one rank
+        st = VectorStore(rt.store.dim, dev, rt.store.table_names, index_kind=s.index_kind, nlist=s.nlist,
+                         nprobe=s.nprobe)
+        for r in range(world):
+            merge_into(st, VectorStore.load(os.path.join(out, "parts", str(r), shard_dir(s_, shards)), dev))
+        for t in st.tables.values():
+            if t.ivf:
+                t.compact()
+        st.save(os.path.join(out, shard_dir(s_, shards)))
+        print(json.dumps({"shard": s_, "of": shards, "counts": st.counts()}))
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"ingest_dp": world, "shards": shards, "ranks": counts}))
+        import shutil
+
+        shutil.rmtree(os.path.join(out, "parts"), ignore_errors=True)
+    dist.destroy_process_group()
+    return 0 if all(r.get("ok") for r in res) else 1
+
+
 def cmd_ingest(args) -> int:
     from .ingest.controller import IngestController
 
     s = _settings(args)
+    if args.dp > 1 and "WORLD_SIZE" not in os.environ:
+        return _spawn_ingest_ranks(args.dp)
+    if args.dp > 1:
+        logging.basicConfig(level=s.log_level, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+        return cmd_ingest_dp(args, s)
     logging.basicConfig(level=s.log_level, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     rt = _runtime(args)
     ctl = IngestController(rt, extract=not args.no_extract)
@@ -237,6 +322,9 @@ def main(argv=None) -> int:
     p.add_argument("--dev-force-standalone", action="store_true")
     p.add_argument("--no-extract", action="store_true", help="skip the LLM summary/title/keyword extractors")
     p.add_argument("--save", help="snapshot directory (default INDEX_DIR)")
+    p.add_argument("--dp", type=int, default=1, help="data-parallel ingest over N GPUs (one rank per GPU)")
+    p.add_argument("--shards", type=int, default=0, help="--dp: shard snapshots to write (default N)")
+    p.add_argument("--n-repos", dest="n_repos", type=int, default=2, help="--dp --source synthetic: repositories")
     p = sub.add_parser("ask", help="one RAG query through the agent")
     common(p)
     p.add_argument("query")

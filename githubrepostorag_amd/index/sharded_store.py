@@ -246,3 +246,50 @@ def load_shard(index_dir, rank: int, n: int, device, nprobe: int | None = None) 
         retain_shard(st, rank, n)
         return st
     return None
+
+
+# ---------------------------------------------------------------------- data-parallel ingest (C5)
+def export_rows(table: VectorTable):
+    """Every live real row of a table: (row ids, texts, vectors fp32 [n, d] on the host, metadata)."""
+    with table.lock:
+        items = [(rid, r) for rid, r in table.rows.key_to_row.items() if 0 <= r < table.row_slot.shape[0]
+                 and table.row_slot[r] >= 0]
+        if not items:
+            return [], [], torch.zeros(0, table.dim), []
+        slots = torch.as_tensor(np.asarray([table.row_slot[r] for _, r in items], dtype=np.int64))
+        vecs = table.vectors[slots.to(table.device)].float().cpu()
+        ids, texts, metas = [], [], []
+        for rid, r in items:
+            _, text, md = table.rows.get(r)
+            ids.append(rid)
+            texts.append(text)
+            metas.append(md)
+    return ids, texts, vecs, metas
+
+
+def split_store(store: VectorStore, n: int, owner=shard_of) -> list[VectorStore]:
+    """Partition a store's rows by owning shard into ``n`` host stores (same tables / index kind)."""
+    parts = [VectorStore(store.dim, "cpu", store.table_names, index_kind=store.index_kind) for _ in range(n)]
+    for scope, t in store.tables.items():
+        ids, texts, vecs, metas = export_rows(t)
+        by = {}
+        for i, rid in enumerate(ids):
+            by.setdefault(owner(rid, n), []).append(i)
+        for s, idx in by.items():
+            parts[s].table(scope).upsert([ids[i] for i in idx], [texts[i] for i in idx], vecs[idx],
+                                          [metas[i] for i in idx])
+    for p in parts:
+        p.audit = list(store.audit)
+    return parts
+
+
+def merge_into(dst: VectorStore, src: VectorStore) -> int:
+    """Upsert every row of ``src`` into ``dst`` (idempotent: content-hash row ids); returns rows merged."""
+    n = 0
+    for scope, t in src.tables.items():
+        ids, texts, vecs, metas = export_rows(t)
+        if ids:
+            dst.table(scope).upsert(ids, texts, vecs.to(dst.device), metas)
+            n += len(ids)
+    dst.audit.extend(a for a in src.audit if a not in dst.audit)
+    return n
