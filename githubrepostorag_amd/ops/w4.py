@@ -32,8 +32,7 @@ from .gemm import ACT_NONE, EPI_SILU, EPI_STORE, WS, _num_cus
 
 GROUP = 128
 W4_VARIANTS = [(4, 4), (8, 4), (12, 4), (16, 4)]  # (mt, nwv) compiled (csrc/kernels/gemm_w4.hip)
-W4_MIN_M = int(os.environ.get("GRAG_W4_MIN_M", "129"))  # below: the bf16 decode kernel (same values)
-W4_MAX_M = 256
+W4_MAX_M = 256  # largest compiled row tiling (16 x 16 rows)
 
 
 def quantize(w: torch.Tensor, group: int = GROUP) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
@@ -121,11 +120,10 @@ def w4_ksplit(K: int, ksplit: int) -> int:
     return -(-kt // kts)
 
 
-def plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int, int] | None:
-    """(mt, nwv, ksplit): the smallest compiled row tiling for M, about one workgroup per CU; None outside
-    the measured range (W4_MIN_M..256 rows, and not the FFN-wide gate/up weight, where the bf16 tile kernel
-    measured faster: profiles/gemm_w4_ab_v3.jsonl)."""
-    if M < max(1, W4_MIN_M) or M > W4_MAX_M or (silu and W4_MIN_M > 0):
+def tiling(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int, int] | None:
+    """(mt, nwv, ksplit) the kernel runs M rows with: the smallest compiled row tiling that covers M and
+    about one workgroup per CU (K-split for narrow outputs).  None when no tiling fits."""
+    if M < 1 or M > W4_MAX_M:
         return None
     need = -(-M // 16)
     vs = [v for v in W4_VARIANTS if v[0] >= need and N % (32 * v[1]) == 0]
@@ -136,6 +134,28 @@ def plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int, int] | N
     ncu = _num_cus()
     ks = 1 if silu or tiles >= ncu else w4_ksplit(K, max(1, ncu // tiles))
     return mt, nwv, ks
+
+
+def w4_wins(M: int, N: int, K: int, silu: bool = False) -> bool:
+    """Dispatch rule from the hipGraph-timed A/B of scripts/w4_probe.py --graph (profiles/w4_probe_graph_r3.jsonl:
+    each arm captured as 12 back-to-back launches on cold weight copies, Qwen2-7B shapes, M 1..256):
+      gate/up (SwiGLU, N = 37888): W4 1.55x at M <= 32, 1.13x at 64, loses from 96 on (0.53x at 256);
+      down (deep K = 18944): W4 1.2-1.5x at M <= 64, 1.05-1.1x at 96-128, loses from 192 on;
+      qkv / o (K = N-ish, 26-33 MB bf16): the bf16 decode kernels are at or ahead of W4 everywhere
+      (0.72-1.06x): the 4x fewer weight bytes do not pay below ~40 MB of bf16 weight per launch.
+    GRAG_W4_MIN_M / GRAG_W4_MAX_M (rows) pin the range for every projection instead (tests, sweeps)."""
+    lo, hi = os.environ.get("GRAG_W4_MIN_M"), os.environ.get("GRAG_W4_MAX_M")
+    if lo is not None or hi is not None:
+        return int(lo or 1) <= M <= int(hi or W4_MAX_M)
+    if silu:
+        return M <= 64
+    return K >= 4 * N and M <= 128
+
+
+def plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int, int] | None:
+    """The W4 kernel's tiling for this decode batch when it is the faster path (``w4_wins``), else None
+    (the caller runs the bf16 decode kernel on the dequantised copy of the same weights)."""
+    return tiling(M, N, K, silu) if w4_wins(M, N, K, silu) else None
 
 
 def gemm_w4(x: torch.Tensor, w: W4Linear, bias: torch.Tensor | None = None, act: int = ACT_NONE,
@@ -151,7 +171,7 @@ def gemm_w4(x: torch.Tensor, w: W4Linear, bias: torch.Tensor | None = None, act:
             v = y.view(M, -1, 2, 32)
             y = (torch.nn.functional.silu(v[:, :, 0]) * v[:, :, 1]).reshape(M, -1)
         return y.to(x.dtype)
-    mt, nwv, ks = plan_ or plan(M, w.N, K, w.silu)
+    mt, nwv, ks = plan_ or tiling(M, w.N, K, w.silu)
     ks = 1 if w.silu else w4_ksplit(K, ks)
     if out is None:
         out = torch.empty(M, w.N // 2 if w.silu else w.N, dtype=x.dtype, device=x.device)

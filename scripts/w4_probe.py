@@ -2,7 +2,11 @@
 per batch size and Qwen2-7B projection, interleaved in one process on cold weights (copies rotate past the
 Infinity Cache).  One JSON line per (shape, arm): median us.
 
-usage: python scripts/w4_probe.py [--ms 1,8,16,32,64,96,128,192,256] [--reps 15] [--out f.jsonl]
+usage: python scripts/w4_probe.py [--ms 1,8,16,32,64,96,128,192,256] [--reps 15] [--graph] [--out f.jsonl]
+
+--graph: each arm is captured in a hipGraph of ``--calls`` back-to-back launches (as the decode step is
+served) and timed per launch over replays; without it every launch is timed alone between events, which
+adds the host launch gap to every arm.
 """
 from __future__ import annotations
 
@@ -41,6 +45,8 @@ def main():
     ap.add_argument("--ms", default="1,8,16,32,64,96,128,192,256")
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--calls", type=int, default=12)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     enable_tuned_gemms()
@@ -80,12 +86,28 @@ def main():
                 f(); f()
             torch.cuda.synchronize()
             times = {k: [] for k in arms}
-            for _ in range(args.reps):
+            if args.graph:
+                graphs = {}
+                side = torch.cuda.Stream(dev)
                 for k, f in arms.items():
-                    times[k] += timeit(f, 1)
+                    gr = torch.cuda.CUDAGraph()
+                    with torch.cuda.stream(side):
+                        with torch.cuda.graph(gr, stream=side):
+                            for _ in range(args.calls):
+                                f()
+                    graphs[k] = gr
+                torch.cuda.synchronize()
+                for _ in range(args.reps):
+                    for k, gr in graphs.items():
+                        times[k] += [t / args.calls for t in timeit(gr.replay, 1)]
+                del graphs
+            else:
+                for _ in range(args.reps):
+                    for k, f in arms.items():
+                        times[k] += timeit(f, 1)
             best = min(times, key=lambda k: statistics.median(times[k]))
             for k, ts in times.items():
-                row = {"proj": name, "M": M, "N": N, "K": K, "arm": k, "med_us": round(statistics.median(ts), 1),
+                row = {"proj": name, "M": M, "N": N, "K": K, "arm": k, "graph": args.graph, "med_us": round(statistics.median(ts), 1),
                        "best": k == best}
                 line = json.dumps(row)
                 print(line, flush=True)

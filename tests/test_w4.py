@@ -17,10 +17,17 @@ def _unpack_words(L):
     return nib.view(b, t, 4, 16, 2, 2, 8).permute(0, 4, 3, 1, 5, 2, 6).reshape(L.N, L.K)
 
 
-def test_w4_plan_range():
-    assert W.plan(64, 4608, 3584) is None              # small batches: bf16 decode kernel
-    assert W.plan(192, 37888, 3584, silu=True) is None  # gate/up: bf16 tile kernel measured faster
-    assert W.plan(192, 4608, 3584)[:2] == (12, 4) and W.plan(250, 3584, 3584)[:2] == (16, 4)
+def test_w4_plan_range(monkeypatch):
+    monkeypatch.delenv("GRAG_W4_MIN_M", raising=False)
+    monkeypatch.delenv("GRAG_W4_MAX_M", raising=False)
+    assert W.plan(64, 4608, 3584) is None and W.plan(192, 3584, 3584) is None  # qkv / o: bf16 kernels
+    assert W.plan(32, 37888, 3584, silu=True) == (4, 4, 1)                      # gate/up: W4 up to 64 rows
+    assert W.plan(96, 37888, 3584, silu=True) is None
+    assert W.plan(128, 3584, 18944)[:2] == (8, 4) and W.plan(192, 3584, 18944) is None  # down: up to 128
+    assert W.tiling(192, 4608, 3584)[:2] == (12, 4) and W.tiling(250, 3584, 3584)[:2] == (16, 4)
+    assert W.tiling(1, 4608, 3584) == (4, 4, 7) and W.tiling(300, 4608, 3584) is None
+    monkeypatch.setenv("GRAG_W4_MIN_M", "129")
+    assert W.plan(192, 4608, 3584) is not None and W.plan(64, 3584, 18944) is None
 
 
 def test_pack_roundtrip_and_quant_error():
@@ -139,7 +146,7 @@ def test_gemm_w4_dense_repeat(dev, rep):
     g = torch.Generator(device="cpu").manual_seed(10 + rep)
     L = W.W4Linear.quantize(((torch.rand(N, K, generator=g) * 2 - 1) * 0.5).to(dev))
     x = ((torch.rand(M, K, generator=g) * 2 - 1)).to(torch.bfloat16).to(dev)
-    p = W.plan(M, N, K)
+    p = W.tiling(M, N, K)
     G.WS.reserve(dev, p[2] * M * N)
     ref = x.float().cpu() @ L.dequant(torch.float32).cpu().T
     for _ in range(3):
@@ -151,7 +158,7 @@ def test_gemm_w4_graph_replay(dev):
     M, N, K = 192, 3584, 3584
     L = W.W4Linear.quantize(rnd(N, K, dev=dev, seed=5, scale=0.05))  # (16, 4) tiling
     x = rnd(M, K, dev=dev, scale=0.5)
-    p = W.plan(M, N, K)
+    p = W.tiling(M, N, K)
     G.WS.reserve(dev, p[2] * M * N)
     out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     W.gemm_w4(x, L, out=out)
