@@ -69,6 +69,10 @@ def parse():
     ap.add_argument("--top-k", type=int, default=10)
     ap.add_argument("--ingest-files", type=int, default=192, help="source files in the synthetic repo to ingest")
     ap.add_argument("--no-ingest", action="store_true")
+    ap.add_argument("--ingest-ref-cap-files", type=int, default=32,
+                    help="second ingest pass at the reference's one 2048-token cap for every LLM call "
+                         "(ingest/src/app/llm_init.py:56) over this many files: ingest_docs_per_s_ref_cap (0: skip)")
+    ap.add_argument("--ingest-ref-cap", type=int, default=2048, help="the cap of that pass (tests shrink it)")
     ap.add_argument("--ingest-seqs", type=int, default=256, help="concurrent sequences of the ingest engine")
     ap.add_argument("--ingest-mixed", type=int, default=0,
                     help="1: the ingest engine piggybacks decode tokens on prefill steps (mixed batches)")
@@ -481,6 +485,7 @@ def main():
     # ---- ingest phase (reported separately)
     ingest_dps = None
     ingest_stages = None
+    ingest_ref = None
     if not args.no_ingest and args.ingest_files > 0:
         from githubrepostorag_amd.ingest.bench_ingest import run_ingest_bench
 
@@ -498,6 +503,21 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         ingest_dps = n_docs * dp_size / float(tt.item())  # one ingest per DP replica (TP peers share it)
         log(f"ingest: {n_docs} docs/rank in {float(tt.item()):.2f}s")
+        if args.ingest_ref_cap_files > 0:
+            n2, secs2, st2 = run_ingest_bench(model, tok, emb, args.ingest_ref_cap_files, seed=1000 + dp_rank,
+                                              max_num_seqs=args.ingest_seqs, use_graph=not args.no_graph,
+                                              mixed_batches=bool(args.ingest_mixed), tp=tp_group, token_cap=args.ingest_ref_cap,
+                                              max_model_len=11712)
+            tt2 = torch.tensor([secs2], dtype=torch.float64, device=dev)
+            if world > 1:
+                import torch.distributed as dist
+
+                dist.all_reduce(tt2, op=dist.ReduceOp.MAX)
+            ingest_ref = {"docs_per_s": round(n2 * dp_size / float(tt2.item()), 3), "files": n2,
+                          "seconds": round(float(tt2.item()), 2), "token_cap": args.ingest_ref_cap, "max_model_len": 11712,
+                          "decode_tokens": (st2.get("engine") or {}).get("decode_tokens"),
+                          "llm_calls": st2.get("llm_calls")}
+            log(f"ingest at a {args.ingest_ref_cap}-token cap on every call: {n2} docs/rank in {float(tt2.item()):.2f}s")
 
     if rank == 0:
         res = {
@@ -519,6 +539,7 @@ def main():
                                       "flight (serving runner default: uncapped 8-step windows)")
             if args.arrival_cap else "uncapped decode windows (serving runner default)",
             "ingest_docs_per_s": None if ingest_dps is None else round(ingest_dps, 3),
+            "ingest_docs_per_s_ref_cap": None if ingest_ref is None else ingest_ref["docs_per_s"],
             "config": {
                 "model": f"{args.model} TP={tp} + {args.encoder}, {args.index_size}-vec {args.index_kind} index "
                          f"(nlist={args.nlist}, nprobe={args.nprobe}) sharded dp{world}",
@@ -550,6 +571,7 @@ def main():
                 "githubrepostorag_amd.ops.sampling", fromlist=["x"]).tp_sampling_bytes(
                 args.batch * D, tp, dcfg.vocab_size, 2),
             "ingest_stage_s": ingest_stages,
+            "ingest_ref_cap": ingest_ref,
             "e2e_ttft_p50_ms": None if agent_res is None else agent_res["e2e_ttft_p50_ms"],
             "e2e_ttft_p90_ms": None if agent_res is None else agent_res["e2e_ttft_p90_ms"],
             "agent_jobs_per_s": None if agent_res is None else agent_res["agent_jobs_per_s"],

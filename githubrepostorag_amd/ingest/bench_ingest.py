@@ -28,8 +28,11 @@ from .readers import Document
 
 def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs: int = 256,
                      max_model_len: int = 8192, use_graph: bool = True, summary_tokens: int = 128,
-                     mixed_batches: bool = False, tp=None) -> tuple[int, float, dict]:
+                     mixed_batches: bool = False, tp=None, token_cap: int | None = None) -> tuple[int, float, dict]:
     """Returns (documents ingested, seconds, per-stage seconds).
+
+    ``token_cap``: one generation cap for every LLM call instead of the per-call lengths above (the
+    reference's 2048, ingest/src/app/llm_init.py:56; random weights run every call to the cap).
 
     ``tp`` (a tensor-parallel group the model is sharded over): the group's TP
     rank 0 runs the pipeline and owns the request queue; the other ranks mirror
@@ -53,10 +56,11 @@ def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs:
             torch.cuda.empty_cache()
         return 0, time.perf_counter() - t0, {"tp_follower": True}
     try:
-        llm = EngineLLM(runner, tok, max_tokens=summary_tokens, mode="ingest", timeout_s=1800.0, retries=0)
+        llm = EngineLLM(runner, tok, max_tokens=token_cap or summary_tokens, mode="ingest", timeout_s=3600.0,
+                        retries=0)
         store = VectorStore(emb.dim, dev)
         ctl = IngestController(llm=llm, store=store, embedder=emb, settings=Settings(data_dir=None),
-                               summary_tokens=summary_tokens)
+                               summary_tokens=summary_tokens, token_cap=token_cap)
         _, files = synthetic_repo(seed, n_files, f"bench-repo-{seed}")
         docs = [Document(f["text"], {"file_path": f["file_path"], "file_name": f["file_path"].split("/")[-1]})
                 for f in files]

@@ -108,7 +108,7 @@ def docs_digest(docs) -> str:
 
 class IngestController:
     def __init__(self, runtime=None, *, llm=None, store=None, embedder=None, settings=None, extract: bool = True,
-                 summary_tokens: int | None = None, on_event=None):
+                 summary_tokens: int | None = None, on_event=None, token_cap: int | None = None):
         self.s = settings or (runtime.settings if runtime is not None else get_settings())
         self.llm = llm or runtime.ingest_llm
         self.store = store or runtime.store
@@ -116,9 +116,14 @@ class IngestController:
         self.runtime = runtime
         self.on_event = on_event or (lambda kind, data: None)
         toks = summary_tokens or 256
-        self.extractors = ExtractorPipeline(self.llm, title_nodes=5, summary_tokens=toks, enabled=extract)
-        self.hier = HierarchyBuilder(self.llm, ExtractorPipeline(self.llm, title_nodes=3, summary_tokens=toks,
-                                                                 enabled=extract), summary_tokens=2 * toks)
+        # token_cap: ONE generation cap for every ingest LLM call (summaries, titles, keywords, roll-ups) —
+        # the reference's ingest LLM runs every call with max_new_tokens=2048 (ingest/src/app/llm_init.py:56)
+        caps = dict(keyword_tokens=token_cap, title_tokens=token_cap) if token_cap else {}
+        self.extractors = ExtractorPipeline(self.llm, title_nodes=5, summary_tokens=token_cap or toks,
+                                            enabled=extract, **caps)
+        self.hier = HierarchyBuilder(self.llm, ExtractorPipeline(self.llm, title_nodes=3,
+                                                                 summary_tokens=token_cap or toks, enabled=extract,
+                                                                 **caps), summary_tokens=token_cap or 2 * toks)
         self.writer = VectorWriter(self.store, self.embedder)
         self.splitter = DynamicCodeSplitter()
 

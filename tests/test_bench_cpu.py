@@ -11,7 +11,8 @@ from dist_utils import free_port
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TINY = ["--model", "qwen2-tiny", "--encoder", "encoder-tiny", "--index-size", "4000", "--index-kind", "ivf",
         "--nlist", "16", "--nprobe", "4", "--batch", "3", "--prompt-len", "48", "--gen-len", "5",
-        "--ingest-files", "4", "--steps", "2", "--warmup", "1", "--agent-jobs", "8", "--agent-concurrency", "4", "--agent-synth-len", "16"]
+        "--ingest-files", "4", "--steps", "2", "--warmup", "1", "--agent-jobs", "8", "--agent-concurrency", "4", "--agent-synth-len", "16",
+        "--ingest-ref-cap-files", "0"]
 
 
 def _run(cmd, env):
@@ -24,11 +25,14 @@ def _run(cmd, env):
 
 def test_bench_single_process_cpu():
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    res = _run([sys.executable, "bench.py", "--gpus", "1", *TINY], env)
+    res = _run([sys.executable, "bench.py", "--gpus", "1", *TINY, "--ingest-ref-cap-files", "3", "--ingest-ref-cap",
+                "48"], env)
     assert res["n_gpus"] == 1 and res["steps"] == 2 and res["warmup"] == 1
     assert res["metric"].startswith("RAG queries/sec") and res["value"] > 0 and res["higher_is_better"]
     assert res["scaling"] == "weak" and res["config"]["global_batch"] == 3
     assert res["ingest_docs_per_s"] > 0 and res["p50_ttft_ms"] > 0
+    ref = res["ingest_ref_cap"]  # the one-cap-for-every-call ingest pass (2048 by default)
+    assert res["ingest_docs_per_s_ref_cap"] > 0 and ref["token_cap"] == 48 and ref["files"] == 3
 
 
 def test_bench_two_ranks_gloo():

@@ -9,6 +9,8 @@ from githubrepostorag_amd.engine.tokenizer import ByteBPETokenizer
 from githubrepostorag_amd.models.configs import decoder_config
 from githubrepostorag_amd.models.qwen2 import Qwen2Model
 
+from _logits import greedy_within_tolerance
+
 pytestmark = pytest.mark.gpu
 
 
@@ -34,21 +36,17 @@ def test_graph_vs_eager_identical(setup):
     assert [x.token_ids for x in a] == [x.token_ids for x in b]
 
 
-def test_decode_matches_recompute(setup):
+def test_decode_matches_recompute(setup, dev):
+    """Greedy tokens of the batched engine (prefix cache, hipGraph decode windows, split-KV decode attention)
+    against a prefill recompute of each full prefix: every chosen token's recomputed logit is within bf16
+    noise (2 % of the logit scale) of the recompute's maximum — a logit tolerance, not an agreement rate."""
     model, tok = setup
     sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
     eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=8, max_model_len=2048, num_blocks=1024))
     outs = eng.generate(_prompts(tok), sp)
-    agree = total = 0
-    ref = LLMEngine(model, tok, EngineConfig(max_num_seqs=8, max_model_len=2048, num_blocks=1024,
-                                             enable_prefix_caching=False, use_cuda_graph=False))
     for p, o in zip(_prompts(tok), outs):
-        for j in range(len(o.token_ids)):
-            # one-token generation from the full prefix = prefill-computed argmax
-            r = ref.generate([p + o.token_ids[:j]], SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))
-            agree += int(r[0].token_ids[0] == o.token_ids[j])
-            total += 1
-    assert agree / total >= 0.9, (agree, total)
+        assert len(o.token_ids) == 8
+        greedy_within_tolerance(model, dev, p, o.token_ids)
 
 
 def test_prefix_cache_and_sampling(setup):
@@ -99,15 +97,10 @@ def test_long_context_chunked_prefill_and_split_kv_decode(dev):
                                              num_blocks=4096))
     outs = eng.generate(prompts, sp)
     assert all(len(o.token_ids) == 4 for o in outs)
-    ref = LLMEngine(model, tok, EngineConfig(max_num_seqs=1, max_num_batched_tokens=32768, max_model_len=32768,
-                                             num_blocks=2304, enable_prefix_caching=False, use_cuda_graph=False))
-    agree = total = 0
-    for p, o in zip(prompts, outs):
-        for j in range(len(o.token_ids)):
-            r = ref.generate([p + o.token_ids[:j]], SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))
-            agree += int(r[0].token_ids[0] == o.token_ids[j])
-            total += 1
-    assert agree / total >= 0.75, (agree, total)
+    del eng
+    torch.cuda.empty_cache()
+    for p, o in zip(prompts, outs):  # logit tolerance against one unchunked prefill of the whole prefix
+        greedy_within_tolerance(model, dev, p, o.token_ids)
 
 
 def test_sampler_scratch_outlives_graphs_captured_before_it_grew(setup, dev):
