@@ -29,6 +29,8 @@ using namespace grag;
 namespace {
 
 constexpr int KT = 64;  // keys per tile
+constexpr int kPrefillMaxBlocks = 2048;  // 8-wave prefill: block-table window held in LDS
+constexpr float kRescaleLog2 = 8.f;      // 8-wave prefill: deferred-rescale threshold (log2 units)
 
 struct AttnParams {
   const bf16* q;
@@ -282,7 +284,15 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
 //     uniform test), and the heaviest (latest) q tiles are dispatched first.
 // The math (swapped QK^T, exp2 online softmax, P^T straight from the S^T
 // accumulators) is the 4-wave kernel's.
-template <int D, int RPW>
+//
+// NS = ring stages: 2 issues tile t+1 after the barrier that opens tile t and
+// waits vmcnt(0) at the next tile; 3 keeps two tiles in flight (tile t+2
+// issued at tile t's barrier into the stage tile t-1 was read from — every
+// wave passed that barrier after its last read of t-1) and retires only the
+// oldest with a counted vmcnt(2 PPW), so one DMA round trip hides under two
+// tiles of MFMA work.  The barrier is a raw s_barrier: __syncthreads() would
+// drain the younger tile with a vmcnt(0).
+template <int D, int RPW, int NS>
 __global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
   constexpr int NW = 8;
   constexpr int RB = 2 * D;            // bytes per K/V row
@@ -294,10 +304,12 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
   constexpr int PPW = NP / NW;         // pieces per wave per tensor
   constexpr int RPP = 1024 / RB;       // rows per piece
   constexpr int ROWS = 16 * RPW * NW;  // GQA rows per workgroup
-  constexpr int MAXB = 1024;           // block-table window in LDS (16 K keys at BS 16)
+  constexpr int BS = 16;               // KV block size (launcher falls back to the 4-wave kernel otherwise)
+  constexpr int MAXB = kPrefillMaxBlocks;  // block-table window in LDS (32 K keys)
   static_assert(PPW >= 1 && PPW * NW == NP, "piece split");
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE + MAXB * 4];
-  int* bt_lds = reinterpret_cast<int*>(smem + 2 * 2 * TILE);
+  static_assert(NS == 2 || NS == 3, "ring stages");
+  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * TILE + MAXB * 4];
+  int* bt_lds = reinterpret_cast<int*>(smem + NS * 2 * TILE);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h4 = lane >> 4, li = lane & 15;
@@ -314,11 +326,12 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
   const int last_row = min(row_base + ROWS, nrows) - 1;
   const int kv_hi = p.causal ? min(ctx, ctx - qlen + last_row / G + 1) : ctx;
 
-  const int nb = (kv_hi + p.BS - 1) / p.BS;
-  const bool bt_fast = nb <= MAXB;
+  // the whole block-table window goes to LDS once: the per-tile DMA addresses then come from
+  // ds_reads (lgkmcnt) — a global/flat read there would need a vmcnt wait that drains the K/V
+  // pieces in flight.  The launcher guarantees bt_stride <= MAXB.
+  const int nb = (kv_hi + BS - 1) / BS;
   const int32_t* bt = p.block_tables + (size_t)seq * p.bt_stride;
-  if (bt_fast)
-    for (int i = threadIdx.x; i < nb; i += 64 * NW) bt_lds[i] = bt[i];
+  for (int i = threadIdx.x; i < nb; i += 64 * NW) bt_lds[i] = bt[i];
 
   bf16x8_t qf[RPW][NC];
   int key_lim[RPW];  // this lane's row limit
@@ -339,6 +352,10 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
       else qf[j][c] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
+  // Q fragments and the block-table window landed (a compiler-visible wait: without it hipcc's
+  // waitcnt pass cannot prove the Q loads retired on the loop back-edge and puts a vmcnt(0) in
+  // front of the first MFMA of every tile, which also drains the K/V DMA issued for the next tile)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
   __syncthreads();  // block-table window visible
   // smallest key limit over the wave's rows (its first row), wave-uniform:
   // tiles ending below it need no mask
@@ -354,9 +371,8 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
       const int piece = wave * PPW + i;
       const int row = piece * RPP + lrow;
       const int key = min(kt0 + row, kv_hi - 1);
-      const int bi = key / p.BS;
-      const int blk = bt_fast ? bt_lds[bi] : bt[bi];
-      const size_t off = (((size_t)blk * p.Hkv + kvh) * p.BS + (key % p.BS)) * D;
+      const int blk = bt_lds[key / BS];
+      const size_t off = (((size_t)blk * p.Hkv + kvh) * BS + (key % BS)) * D;
       glds16(p.k + off + ((lch ^ kswz<D>(row)) << 3), kdst + piece * 1024);
       glds16(p.v + off + ((lch ^ vswz<D>(row)) << 3), vdst + piece * 1024);
     }
@@ -373,13 +389,24 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
   }
   const int ntiles = (kv_hi + KT - 1) / KT;
   issue(0, 0);
+  if (NS == 3 && ntiles > 1) issue(KT, 1);
+  int stage = 0;  // t % NS
   for (int t = 0; t < ntiles; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + 1 < ntiles) issue((t + 1) * KT, (t + 1) & 1);
+    if (NS == 3 && t + 1 < ntiles)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");  // tile t+1's pieces stay in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + NS - 1 < ntiles) {
+      const int st = stage == 0 ? NS - 1 : stage - 1;  // (t + NS - 1) % NS: the stage tile t-1 used
+      issue((t + NS - 1) * KT, st);
+    }
     const int kt0 = t * KT;
-    const char* k_lds = smem + (t & 1) * 2 * TILE;
+    const char* k_lds = smem + stage * 2 * TILE;
     const char* v_lds = k_lds + TILE;
+    stage = stage + 1 == NS ? 0 : stage + 1;
 
     // S^T = K Q^T: every K fragment read once, used by all RPW row groups
     f32x4_t s[RPW][4];
@@ -402,34 +429,41 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
     bf16x8_t bp[RPW][2];
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
+      // raw scores: the softmax scale (log2 domain) is folded into the exponent's FMA, and the
+      // row max is taken before scaling (the scale is positive)
       float tmax = -INFINITY;
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float x = s[j][tt][r] * p.scale_log2;
           if (need_mask) {
             const int key = kt0 + 16 * tt + 4 * h4 + r;
-            x = (key >= key_lim[j] || key >= kv_hi) ? -INFINITY : x;
+            s[j][tt][r] = (key >= key_lim[j] || key >= kv_hi) ? -INFINITY : s[j][tt][r];
           }
-          s[j][tt][r] = x;
-          tmax = __builtin_fmaxf(tmax, x);
+          tmax = __builtin_fmaxf(tmax, s[j][tt][r]);
         }
       tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float m_new = __builtin_fmaxf(m[j], tmax);
-      const float m_use = m_new == -INFINITY ? 0.f : m_new;
-      const float alpha = __builtin_amdgcn_exp2f(m[j] - m_use);
-      m[j] = m_new;
-      lsum[j] *= alpha;
+      // deferred rescale (cdna guide §5.5 T13): the running max m (scaled units) moves only when a
+      // row's tile max passes it by more than kRescaleLog2, so p = 2^(s c - m) stays <= 2^8 in fp32 and
+      // the O / l rescale runs on the few tiles where some row of the wave moved (wave-uniform branch;
+      // every lane then takes its exact new max, so O and l always see the same factor)
+      const float m_cand = __builtin_fmaxf(m[j], tmax * p.scale_log2);
+      if (__any(m_cand > m[j] + kRescaleLog2)) {
+        const float m_use = m_cand == -INFINITY ? 0.f : m_cand;
+        const float alpha = __builtin_amdgcn_exp2f(m[j] - m_use);
+        m[j] = m_cand;
+        lsum[j] *= alpha;
 #pragma unroll
-      for (int n = 0; n < ND; ++n) o[j][n] *= alpha;
+        for (int n = 0; n < ND; ++n) o[j][n] *= alpha;
+      }
+      const float nm = m[j] == -INFINITY ? 0.f : -m[j];
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p0 = __builtin_amdgcn_exp2f(s[j][2 * cc][r] - m_use);
-          const float p1 = __builtin_amdgcn_exp2f(s[j][2 * cc + 1][r] - m_use);
+          const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][2 * cc][r], p.scale_log2, nm));
+          const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][2 * cc + 1][r], p.scale_log2, nm));
           lsum[j] += p0 + p1;
           bp[j][cc][r] = f2bits(p0);
           bp[j][cc][4 + r] = f2bits(p1);
@@ -719,9 +753,12 @@ int launch_decode(const AttnParams& prm, int nseq, int tk, hipStream_t stream) {
 }
 
 template <int D>
-int launch_prefill(const AttnParams& prm, int nseq, hipStream_t stream) {
+int launch_prefill(const AttnParams& prm, int nseq, int ns, hipStream_t stream) {
   dim3 grid(nseq * prm.tiles_per_seq, prm.Hkv, 1);
-  attn_prefill_kernel<D, 2><<<grid, 512, 0, stream>>>(prm);
+  if (ns == 3)
+    attn_prefill_kernel<D, 2, 3><<<grid, 512, 0, stream>>>(prm);
+  else
+    attn_prefill_kernel<D, 2, 2><<<grid, 512, 0, stream>>>(prm);
   return (int)hipGetLastError();
 }
 
@@ -732,9 +769,10 @@ int dispatch_nw(const AttnParams& prm, int nseq, int nw, bool paged, hipStream_t
   // CU); nw == 2: the generic kernel with one wave per workgroup (A/B reference)
   if (paged && (nw == 1 || nw == 3) && prm.tiles_per_seq == 1 && prm.G <= 16 && prm.BS % 16 == 0)
     return launch_decode<D>(prm, nseq, nw == 3 ? 32 : 64, stream);
-  if (nw == 5) {
+  if (nw == 5 || nw == 6) {  // 8-wave LDS-DMA prefill: 2-stage (5) / 3-stage (6) K/V ring
     if constexpr (D == 128 || D == 64) {
-      if (paged && prm.num_splits == 1) return launch_prefill<D>(prm, nseq, stream);
+      if (paged && prm.num_splits == 1 && prm.BS == 16 && prm.bt_stride <= kPrefillMaxBlocks)
+        return launch_prefill<D>(prm, nseq, nw == 6 ? 3 : 2, stream);
     }
     return (int)hipErrorInvalidValue;
   }
@@ -761,8 +799,8 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
                                   float scale, int causal, int num_splits, int split_len,
                                   float* part_o, float* part_ml, int nw, hipStream_t stream) {
   if (nseq <= 0) return 0;
-  if (Hq % Hkv != 0 || BS <= 0 || nw < 1 || nw > 5) return (int)hipErrorInvalidValue;
-  if (nw == 5 && num_splits > 1) return (int)hipErrorInvalidValue;
+  if (Hq % Hkv != 0 || BS <= 0 || nw < 1 || nw > 6) return (int)hipErrorInvalidValue;
+  if ((nw == 5 || nw == 6) && num_splits > 1) return (int)hipErrorInvalidValue;
   if (num_splits > 1 && (max_q_len != 1 || !part_o || !part_ml || split_len % KT != 0))
     return (int)hipErrorInvalidValue;
   AttnParams prm{};
@@ -783,7 +821,10 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
   prm.G = Hq / Hkv;
   prm.BS = BS;
   prm.bt_stride = bt_stride;
-  const int rows_per_wg = nw == 5 ? 256 : 16 * (nw == 2 ? 1 : nw);  // nw 5: 8 waves x 2 row groups
+  // 8-wave prefill needs KV blocks of 16 and a block table that fits its LDS window; otherwise
+  // the 4-wave kernel (same math) takes the launch
+  if ((nw == 5 || nw == 6) && !(BS == 16 && bt_stride <= kPrefillMaxBlocks && (D == 128 || D == 64))) nw = 4;
+  const int rows_per_wg = (nw == 5 || nw == 6) ? 256 : 16 * (nw == 2 ? 1 : nw);  // nw 5/6: 8 waves x 2 row groups
   prm.tiles_per_seq = (max_q_len * prm.G + rows_per_wg - 1) / rows_per_wg;
   if (nw == 1 && max_q_len != 1) return (int)hipErrorInvalidValue;
   prm.num_splits = num_splits < 1 ? 1 : num_splits;

@@ -184,20 +184,30 @@ def cmd_ingest_dp(args, s) -> int:
     if not out:
         raise SystemExit("ingest --dp needs --save or INDEX_DIR (the shard snapshots go there)")
     shards = args.shards or world
+    standalone = args.dev_force_standalone or s.dev_force_standalone
     if args.repos:
         comps = [{"repo": r, "namespace": args.namespace} for r in args.repos]
     elif args.source == "synthetic":
         comps = [{"repo": f"synthetic-repo-{i}", "namespace": args.namespace} for i in range(max(world, args.n_repos))]
+    elif args.source == "github" and standalone:
+        # the reference's dev mode (ingest_controller.py:490-542): every repository of the account, each a
+        # standalone component; rank 0 lists them once and the list is broadcast so every rank splits the
+        # same order
+        from .ingest.readers import fetch_repositories
+
+        box = [sorted(fetch_repositories(s.github_user, s.github_token)) if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        comps = [{"repo": r, "namespace": "default", "dev_force_standalone": True} for r in box[0]]
     else:
-        raise SystemExit("ingest --dp splits a list of repositories: pass --repos (or --source synthetic)")
+        raise SystemExit("ingest --dp splits a list of repositories: pass --repos, --source synthetic, or "
+                         "--source github --dev-force-standalone")
     mine = comps[rank::world]
     import torch
 
     dev = f"cuda:{info.local_rank}" if torch.cuda.is_available() and s.device != "cpu" else "cpu"
     rt = _runtime(args, device=dev)
     ctl = IngestController(rt, extract=not args.no_extract)
-    res = ctl.ingest_many(mine, branch=args.branch, source=args.source, path=args.path,
-                          dev_force_standalone=args.dev_force_standalone or s.dev_force_standalone)
+    res = ctl.ingest_many(mine, branch=args.branch, source=args.source, path=args.path)  # components carry the flag
     counts = [None] * world
     dist.all_gather_object(counts, {"rank": rank, "repos": [r.get("repo") for r in res],
                                     "nodes": sum(r.get("nodes_written") or 0 for r in res),

@@ -111,7 +111,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         nw = meta.extra.get("decode_nw", DECODE_NW)
     else:
         nw = meta.extra.get("prefill_nw", PREFILL_NW)
-        if nw == 5 and D not in (64, 128):
+        if nw in (5, 6) and D not in (64, 128):
             nw = 4
     call("grag_paged_attention", ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(out), out.stride(0),
          ptr(meta.block_tables), meta.block_tables.stride(0), ptr(meta.q_start), ptr(meta.ctx_len),

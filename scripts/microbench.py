@@ -102,7 +102,11 @@ def attn_prefill_bench(nseq, L):
         meta.extra = {"prefill_nw": code}
         return A.paged_attention(q, kc, vc, meta, 0.088)
 
-    r = rounds({"prefill_4wave": lambda: run(4), "prefill_8wave_dma": lambda: run(5)}, n=3, iters=10)
+    r = rounds({"prefill_4wave": lambda: run(4), "prefill_8wave_dma": lambda: run(5),
+                "prefill_8wave_dma_3stage": lambda: run(6)}, n=3, iters=10)
+    ref = run(5).float()
+    err = (run(6).float() - ref).abs().max().item()
+    r["prefill_8wave_dma_3stage"]["max_abs_diff_vs_2stage"] = round(err, 5)
     fl = nseq * Hq * L * L / 2 * D * 4 / 1e12
     for k in r:
         r[k]["TFLOPs"] = round(fl / (r[k]["min_us"] * 1e-6), 1)
@@ -160,6 +164,7 @@ if __name__ == "__main__":
     if args.what == "prefill":
         res["prefill_16x1024"] = attn_prefill_bench(16, 1024)
         res["prefill_4x4096"] = attn_prefill_bench(4, 4096)
+        res["prefill_2x11712"] = attn_prefill_bench(2, 11712)  # the reference's --max-model-len
     if args.what in ("all", "elementwise"):
         res["elementwise_T14336"] = elementwise_bench()
     if args.what in ("all", "sampler"):

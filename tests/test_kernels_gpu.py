@@ -137,7 +137,7 @@ def test_paged_prefill(dev, Hq, Hkv, D):
     q, kc, vc, meta = _paged_setup(dev, lens_q, lens_ctx, Hq, Hkv, D)
     scale = 1 / math.sqrt(D)
     ref = A.paged_attention_ref(q, kc, vc, meta, scale).reshape(q.shape[0], -1)
-    for code in (4, 5):  # 4-wave register-staged kernel, 8-wave LDS-DMA kernel
+    for code in (4, 5, 6):  # 4-wave register-staged kernel, 8-wave LDS-DMA kernel (2- / 3-stage ring)
         m = _to(meta, dev)
         m.extra = {"prefill_nw": code}
         out = A.paged_attention(q.to(dev), kc.to(dev), vc.to(dev), m, scale)
@@ -153,7 +153,20 @@ def test_paged_prefill_long_context(dev):
     q, kc, vc, meta = _paged_setup(dev, lens_q, lens_ctx, Hq, Hkv, D, seed=7)
     scale = 1 / math.sqrt(D)
     ref = A.paged_attention_ref(q, kc, vc, meta, scale).reshape(q.shape[0], -1)
-    for code in (4, 5):
+    for code in (4, 5, 6):
+        m = _to(meta, dev)
+        m.extra = {"prefill_nw": code}
+        close(A.paged_attention(q.to(dev), kc.to(dev), vc.to(dev), m, scale), ref, 2e-2)
+
+
+def test_paged_prefill_block_size_fallback(dev):
+    """KV blocks of 32 are outside the 8-wave kernel's compiled block size: the launcher runs the 4-wave
+    kernel for the same request (codes 5/6 must still return the right answer, not an error)."""
+    Hq, Hkv, D = 28, 4, 128
+    q, kc, vc, meta = _paged_setup(dev, [40, 90], [40, 150], Hq, Hkv, D, BS=32, seed=9)
+    scale = 1 / math.sqrt(D)
+    ref = A.paged_attention_ref(q, kc, vc, meta, scale).reshape(q.shape[0], -1)
+    for code in (5, 6):
         m = _to(meta, dev)
         m.extra = {"prefill_nw": code}
         close(A.paged_attention(q.to(dev), kc.to(dev), vc.to(dev), m, scale), ref, 2e-2)
