@@ -620,32 +620,39 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
         s[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[c], s[tt], 0, 0, 0);
       }
     }
+    // raw-score max, scale folded into the exponent's FMA; deferred rescale as in the prefill kernel:
+    // O (held in accumulator registers) is touched only on tiles where some row's max moved by more
+    // than kRescaleLog2
     float tmax = -INFINITY;
+    const bool tail = kt0 + TK > kv_hi;
 #pragma unroll
     for (int tt = 0; tt < NT16; ++tt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = kt0 + 16 * tt + 4 * h4 + r;
-        float x = s[tt][r] * p.scale_log2;
-        if (key >= kv_hi) x = -INFINITY;
-        s[tt][r] = x;
-        tmax = fmaxf(tmax, x);
+        if (tail) {
+          const int key = kt0 + 16 * tt + 4 * h4 + r;
+          s[tt][r] = key >= kv_hi ? -INFINITY : s[tt][r];
+        }
+        tmax = fmaxf(tmax, s[tt][r]);
       }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m, tmax);
-    const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m - m_use);
-    m = m_new;
-    lsum *= alpha;
+    const float m_cand = fmaxf(m, tmax * p.scale_log2);
+    if (__any(m_cand > m + kRescaleLog2)) {
+      const float m_use = m_cand == -INFINITY ? 0.f : m_cand;
+      const float alpha = exp2f(m - m_use);
+      m = m_cand;
+      lsum *= alpha;
 #pragma unroll
-    for (int n = 0; n < ND; ++n) o[n] *= alpha;
+      for (int n = 0; n < ND; ++n) o[n] *= alpha;
+    }
+    const float nm = m == -INFINITY ? 0.f : -m;
     float pr[NT16][4];
 #pragma unroll
     for (int tt = 0; tt < NT16; ++tt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        pr[tt][r] = exp2f(s[tt][r] - m_use);
+        pr[tt][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[tt][r], p.scale_log2, nm));
         lsum += pr[tt][r];
       }
     const int tq = li >> 2, tp = li & 3;

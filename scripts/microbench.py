@@ -156,6 +156,8 @@ if __name__ == "__main__":
     if args.what in ("all", "gemm"):
         for M in (1, 8, 64):
             res.update(gemm_bench(M))
+    if args.what in ("all", "attn", "decode"):
+        res["decode_B512_ctx1100_split256"] = attn_decode_bench(512, 1100, 256)  # the bench's decode step
     if args.what in ("all", "attn"):
         for sl in (256, 512):
             res[f"decode_B64_ctx1152_split{sl}"] = attn_decode_bench(64, 1152, sl)
