@@ -286,15 +286,13 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
 // accumulators) is the 4-wave kernel's.
 //
 // NS = ring stages: 2 issues tile t+1 after the barrier that opens tile t and
-// waits vmcnt(0) at the next tile; 3 keeps two tiles in flight (tile t+2
-// issued at tile t's barrier into the stage tile t-1 was read from — every
-// wave passed that barrier after its last read of t-1) and retires only the
-// oldest with a counted vmcnt(2 PPW), so one DMA round trip hides under two
-// tiles of MFMA work.  The barrier is a raw s_barrier: __syncthreads() would
-// drain the younger tile with a vmcnt(0).
-template <int D, int RPW, int NS>
-__global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
-  constexpr int NW = 8;
+// waits vmcnt(0) at the next tile (one barrier per tile, all 8 waves in step);
+// 3 runs the staggered ping-pong schedule described at its loop (two barrier
+// intervals per tile, waves 4-7 one interval behind).  Barriers are raw
+// s_barrier: __syncthreads() would drain the younger tile with a vmcnt(0).
+template <int D, int RPW, int NS, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void attn_prefill_kernel(AttnParams p) {
+  static_assert(NS == 2 || NW == 8, "the staggered schedule pairs waves w and w + 4 on one SIMD");
   constexpr int RB = 2 * D;            // bytes per K/V row
   constexpr int CPR = D / 8;           // 16-B chunks per row
   constexpr int NC = D / 32;
@@ -388,26 +386,9 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
     for (int n = 0; n < ND; ++n) o[j][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
   const int ntiles = (kv_hi + KT - 1) / KT;
-  issue(0, 0);
-  if (NS == 3 && ntiles > 1) issue(KT, 1);
-  int stage = 0;  // t % NS
-  for (int t = 0; t < ntiles; ++t) {
-    if (NS == 3 && t + 1 < ntiles)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");  // tile t+1's pieces stay in flight
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + NS - 1 < ntiles) {
-      const int st = stage == 0 ? NS - 1 : stage - 1;  // (t + NS - 1) % NS: the stage tile t-1 used
-      issue((t + NS - 1) * KT, st);
-    }
-    const int kt0 = t * KT;
-    const char* k_lds = smem + stage * 2 * TILE;
-    const char* v_lds = k_lds + TILE;
-    stage = stage + 1 == NS ? 0 : stage + 1;
-
+  bf16x8_t bp[RPW][2];
+  // phase A: S^T for tile t from the K image at k_lds, softmax -> P^T fragments bp (rescales O)
+  auto phaseA = [&](const int kt0, const char* k_lds) {
     // S^T = K Q^T: every K fragment read once, used by all RPW row groups
     f32x4_t s[RPW][4];
 #pragma unroll
@@ -426,7 +407,6 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
     }
     // masking is needed only on tiles that reach the wave's diagonal / the context end
     const bool need_mask = kt0 + KT > wave_lim_min;
-    bf16x8_t bp[RPW][2];
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       // raw scores: the softmax scale (log2 domain) is folded into the exponent's FMA, and the
@@ -469,6 +449,9 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
           bp[j][cc][4 + r] = f2bits(p1);
         }
     }
+  };
+  // phase B: O^T += V^T P^T from the V image at v_lds
+  auto phaseB = [&](const char* v_lds) {
     // O^T += V^T P^T: every V^T fragment read once, used by all RPW row groups
     const int tq = li >> 2, tp = li & 3;
 #pragma unroll
@@ -490,6 +473,59 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(AttnParams p) {
 #pragma unroll
         for (int j = 0; j < RPW; ++j) o[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[n], bp[j][cc], o[j][n], 0, 0, 0);
     }
+  };
+  auto bar = [&]() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  issue(0, 0);
+  if constexpr (NS == 2) {
+    for (int t = 0; t < ntiles; ++t) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+      if (t + 1 < ntiles) issue((t + 1) * KT, (t + 1) & 1);
+      const char* k_lds = smem + (t & 1) * 2 * TILE;
+      phaseA(t * KT, k_lds);
+      phaseB(k_lds + TILE);
+    }
+  } else {
+    // Staggered ping-pong over a 3-stage ring (cdna guide "Two waves per SIMD"): waves 4-7 run one
+    // barrier interval behind waves 0-3, and every tile is two intervals, A (QK^T MFMAs + softmax VALU)
+    // then B (PV MFMAs), so on each SIMD one wave's softmax overlaps its partner's MFMAs instead of
+    // both waves stalling the matrix core together.  Leading waves: barrier 2t opens A(t), 2t+1 opens
+    // B(t); lagging waves: 2t+1 and 2t+2.  Tile t+2 is issued after the barrier that opens B(t) into the
+    // stage of tile t-1, whose last reader (the lagging B(t-1)) ended at that barrier.  RAW: a leading
+    // wave retires tile t (vmcnt(2 PPW): t+1 stays in flight) before barrier 2t; a lagging wave retires
+    // everything it issued (vmcnt(0)) before the barrier opening its B, which precedes every first read
+    // of those tiles (the leading A of tile t+1 at barrier 2t+2).
+    const bool lag = wave >= NW / 2;
+    if (ntiles > 1) issue(KT, 1);
+    if (lag) {
+      if (ntiles > 1)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();  // barrier 0: the leading A(0) reads tile 0
+    }
+    int stage = 0;  // t % 3
+    for (int t = 0; t < ntiles; ++t) {
+      if (!lag) {
+        if (t + 1 < ntiles)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      bar();
+      const char* k_lds = smem + stage * 2 * TILE;
+      phaseA(t * KT, k_lds);
+      if (lag) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+      if (t + 2 < ntiles) issue((t + 2) * KT, stage == 0 ? 2 : stage - 1);
+      phaseB(k_lds + TILE);
+      stage = stage == 2 ? 0 : stage + 1;
+    }
+    if (!lag) bar();  // the lagging waves' last B
   }
 
 #pragma unroll
@@ -760,9 +796,9 @@ int launch_decode(const AttnParams& prm, int nseq, int tk, hipStream_t stream) {
 }
 
 template <int D>
-int launch_prefill(const AttnParams& prm, int nseq, int ns, hipStream_t stream) {
+int launch_prefill(const AttnParams& prm, int nseq, int nw, hipStream_t stream) {
   dim3 grid(nseq * prm.tiles_per_seq, prm.Hkv, 1);
-  if (ns == 3)
+  if (nw == 6)
     attn_prefill_kernel<D, 2, 3><<<grid, 512, 0, stream>>>(prm);
   else
     attn_prefill_kernel<D, 2, 2><<<grid, 512, 0, stream>>>(prm);
@@ -776,10 +812,10 @@ int dispatch_nw(const AttnParams& prm, int nseq, int nw, bool paged, hipStream_t
   // CU); nw == 2: the generic kernel with one wave per workgroup (A/B reference)
   if (paged && (nw == 1 || nw == 3) && prm.tiles_per_seq == 1 && prm.G <= 16 && prm.BS % 16 == 0)
     return launch_decode<D>(prm, nseq, nw == 3 ? 32 : 64, stream);
-  if (nw == 5 || nw == 6) {  // 8-wave LDS-DMA prefill: 2-stage (5) / 3-stage (6) K/V ring
+  if (nw == 5 || nw == 6) {  // LDS-DMA prefill: 8 waves, 2-stage (5) / staggered 3-stage (6) ring
     if constexpr (D == 128 || D == 64) {
       if (paged && prm.num_splits == 1 && prm.BS == 16 && prm.bt_stride <= kPrefillMaxBlocks)
-        return launch_prefill<D>(prm, nseq, nw == 6 ? 3 : 2, stream);
+        return launch_prefill<D>(prm, nseq, nw, stream);
     }
     return (int)hipErrorInvalidValue;
   }
@@ -807,7 +843,7 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
                                   float* part_o, float* part_ml, int nw, hipStream_t stream) {
   if (nseq <= 0) return 0;
   if (Hq % Hkv != 0 || BS <= 0 || nw < 1 || nw > 6) return (int)hipErrorInvalidValue;
-  if ((nw == 5 || nw == 6) && num_splits > 1) return (int)hipErrorInvalidValue;
+  if (nw >= 5 && num_splits > 1) return (int)hipErrorInvalidValue;
   if (num_splits > 1 && (max_q_len != 1 || !part_o || !part_ml || split_len % KT != 0))
     return (int)hipErrorInvalidValue;
   AttnParams prm{};
@@ -830,8 +866,8 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
   prm.bt_stride = bt_stride;
   // 8-wave prefill needs KV blocks of 16 and a block table that fits its LDS window; otherwise
   // the 4-wave kernel (same math) takes the launch
-  if ((nw == 5 || nw == 6) && !(BS == 16 && bt_stride <= kPrefillMaxBlocks && (D == 128 || D == 64))) nw = 4;
-  const int rows_per_wg = (nw == 5 || nw == 6) ? 256 : 16 * (nw == 2 ? 1 : nw);  // nw 5/6: 8 waves x 2 row groups
+  if (nw >= 5 && !(BS == 16 && bt_stride <= kPrefillMaxBlocks && (D == 128 || D == 64))) nw = 4;
+  const int rows_per_wg = nw >= 5 ? 256 : 16 * (nw == 2 ? 1 : nw);  // nw 5/6: 256 GQA rows per workgroup
   prm.tiles_per_seq = (max_q_len * prm.G + rows_per_wg - 1) / rows_per_wg;
   if (nw == 1 && max_q_len != 1) return (int)hipErrorInvalidValue;
   prm.num_splits = num_splits < 1 ? 1 : num_splits;

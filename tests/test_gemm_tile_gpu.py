@@ -263,3 +263,27 @@ def test_linear_prefill_dispatch(dev, M, N, K):
     y = linear(x, w, b)
     rows = torch.arange(0, M, 37)
     check(y[rows], ref(x[rows], w, b), K)
+
+
+@pytest.mark.parametrize("M", [320, 448, 512])
+@pytest.mark.parametrize("N,K,silu", [(4608, 3584, False), (3584, 3584, False), (3584, 18944, False),
+                                      (37888, 3584, True), (152064, 3584, False)])
+def test_decode_batch_257_512_rows(dev, M, N, K, silu):
+    """Decode batches of 257-512 live sequences: every Qwen2-7B projection
+    and the vocab-wide LM head (N = 152064) through the production dispatch (linear() / mlp_gate_up(),
+    whichever kernel and schedule it picks at this M: K-split tile plans, tail stream-K, the owned LM-head
+    schedule) against the fp32 reference, on sampled rows."""
+    from githubrepostorag_amd.ops.linear import linear
+
+    x, w = rnd(M, K, dev=dev, scale=0.5, seed=M), rnd(N, K, dev=dev, seed=N % 97, scale=0.05)
+    rows = torch.arange(0, M, 29)
+    if silu:
+        y = G.mlp_gate_up(x, w)
+        r = ref(x[rows], w)
+        v = r.view(len(rows), -1, 2, 32)
+        r = (torch.nn.functional.silu(v[:, :, 0]) * v[:, :, 1]).reshape(len(rows), -1)
+    else:
+        y = linear(x, w)
+        r = ref(x[rows], w)
+    assert y.shape == (M, N // 2 if silu else N)
+    check(y[rows], r, K)

@@ -137,7 +137,7 @@ def test_paged_prefill(dev, Hq, Hkv, D):
     q, kc, vc, meta = _paged_setup(dev, lens_q, lens_ctx, Hq, Hkv, D)
     scale = 1 / math.sqrt(D)
     ref = A.paged_attention_ref(q, kc, vc, meta, scale).reshape(q.shape[0], -1)
-    for code in (4, 5, 6):  # 4-wave register-staged kernel, 8-wave LDS-DMA kernel (2- / 3-stage ring)
+    for code in (4, 5, 6):  # register-staged 4-wave; LDS-DMA 8-wave (2-stage / staggered 3-stage ring)
         m = _to(meta, dev)
         m.extra = {"prefill_nw": code}
         out = A.paged_attention(q.to(dev), kc.to(dev), vc.to(dev), m, scale)
