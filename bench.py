@@ -240,9 +240,13 @@ def main():
         A -= 1
     U = D * A  # groups in flight
     u = args.batch // A  # queries per group
-    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max(args.batch * D, 8), max_num_batched_tokens=16384,
+    live = max(args.batch * D, 8)
+    gsizes = EngineConfig.graph_batch_sizes
+    if live > max(gsizes):  # deeper pipelines: decode graphs up to the live-sequence count, 128-row buckets
+        gsizes = tuple(sorted({*gsizes, *range(max(gsizes) + 128, live + 127, 128)}))
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=live, max_num_batched_tokens=16384,
                                              max_model_len=max_len, use_cuda_graph=not args.no_graph,
-                                             seed=dp_rank))
+                                             seed=dp_rank, graph_batch_sizes=gsizes))
     sp = SamplingParams(max_tokens=args.gen_len, temperature=0.4, top_p=0.8, repetition_penalty=1.2,
                         ignore_eos=True)
     sys_prompt = ("You are a senior developer assistant. Answer using the provided context blocks. "
