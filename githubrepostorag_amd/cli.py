@@ -298,7 +298,7 @@ def cmd_bench(args, rest) -> int:
     return subprocess.call([sys.executable, os.path.join(root, "bench.py"), *rest])
 
 
-def main(argv=None) -> int:
+def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="githubrepostorag_amd", description=__doc__.split("\n\n")[0])
     sub = ap.add_subparsers(dest="cmd", required=True)
 
@@ -345,7 +345,11 @@ def main(argv=None) -> int:
     p = sub.add_parser("config", help="print resolved settings")
     common(p)
     sub.add_parser("bench", help="run bench.py (remaining args are forwarded)", add_help=False)
+    return ap
 
+
+def main(argv=None) -> int:
+    ap = build_parser()
     argv = list(sys.argv[1:] if argv is None else argv)
     if argv and argv[0] == "bench":
         return cmd_bench(None, argv[1:])

@@ -62,3 +62,38 @@ def test_launcher_serves_one_front_door():
     sh = (ROOT / "launch_node.sh").read_text()
     serve = sh.split("serve)")[1].split(";;")[0]
     assert "--replicas" in serve and serve.count("githubrepostorag_amd serve") == 1
+
+
+def test_ingest_job_runs_dp_ingest_into_the_shared_volume():
+    """The ingest Job (reference helm/templates/ingest-job.yaml: one batch run writing the vector store the
+    workers read) is data-parallel over the GPUs it requests and writes the shard snapshots to the volume
+    the API pod's replicas load from: its command parses with the CLI's own parser, --dp equals its GPU
+    limit and the API pod's replica count, and INDEX_DIR lies on the PVC both pods mount."""
+    from githubrepostorag_amd.cli import build_parser
+
+    docs = _docs("rag-mi355x.yaml")
+    job = next(d for d in docs if d["kind"] == "Job")
+    spec = job["spec"]["template"]["spec"]
+    c = spec["containers"][0]
+    cmd = c["command"]
+    assert cmd[:3] == ["python", "-m", "githubrepostorag_amd"]
+    args = build_parser().parse_args(cmd[3:])
+    assert args.cmd == "ingest" and args.source == "github" and args.dev_force_standalone
+    assert args.dp == int(c["resources"]["limits"]["amd.com/gpu"])
+    api = next(d for d in docs if d["kind"] == "Deployment" and d["metadata"]["name"] == "rag-api")
+    acmd = api["spec"]["template"]["spec"]["containers"][0]["command"]
+    assert args.dp == int(acmd[acmd.index("--replicas") + 1])
+    cm = next(d for d in docs if d["kind"] == "ConfigMap")["data"]
+    assert cm.get("INDEX_SHARDING", "shard") == "shard"  # replicas load shard-r-of-N snapshots
+    claim = {v["persistentVolumeClaim"]["claimName"] for v in spec["volumes"] if "persistentVolumeClaim" in v}
+    aspec = api["spec"]["template"]["spec"]
+    assert claim and claim <= {v["persistentVolumeClaim"]["claimName"] for v in aspec.get("volumes", [])
+                               if "persistentVolumeClaim" in v}
+    mounts = [m["mountPath"] for m in c["volumeMounts"]]
+    assert any(cm["INDEX_DIR"].startswith(m) for m in mounts)
+
+
+def test_launcher_ingest_is_data_parallel():
+    sh = (ROOT / "launch_node.sh").read_text()
+    ingest = sh.split("ingest)")[1].split(";;")[0]
+    assert "--dp" in ingest and "HIP_VISIBLE_DEVICES=0" not in ingest
