@@ -56,6 +56,9 @@ __device__ __forceinline__ float gelu_tanh_f(float x) {
   const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
   return 0.5f * x * (2.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u)));
 }
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)(uint16_t)f2bits(lo) | ((uint32_t)(uint16_t)f2bits(hi) << 16);
+}
 template <int ACT>
 __device__ __forceinline__ float act_f(float x) {
   if constexpr (ACT == ACT_GELU) return gelu_erf_f(x);
@@ -265,6 +268,23 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
 
   // ---- epilogue.  acc_qm_qn[mt][nt][r]: row m0 + 128 wr + 64 qm + 16 mt + (L & 15),
   // col n0 + 64 wc + 32 qn + 16 nt + 4 (L >> 4) + r
+  // T21-style widened stores (cdna guide §5.5): a lane holds columns 4g..4g+3 (nt 0) and 16+4g..16+4g+3
+  // (nt 1) of its row, g = L >> 4.  One v_permlane16_swap per dword pair trades nt-1 data of 16-lane row
+  // 0 / 2 for nt-0 data of row 1 / 3, after which each lane holds 8 contiguous columns of one row:
+  // g = 0 -> 0..7, 1 -> 16..23, 2 -> 8..15, 3 -> 24..31 of the wave's 32-column block -- one 16-byte
+  // store instead of two 8-byte ones.  Partners share the row (L & 15), so a row guard keeps both
+  // lanes of every swap active together.
+  const bool wide_ok = ((uintptr_t)p.C & 15) == 0 && (p.ldc & 7) == 0;
+  const int wcol = ((L >> 4) & 1) * 16 + ((L >> 5) & 1) * 8;
+  auto store_row16 = [&](bf16* row_base, uint32_t (&d)[2][2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const auto r = __builtin_amdgcn_permlane16_swap(d[0][h], d[1][h], false, false);
+      d[0][h] = r[0];
+      d[1][h] = r[1];
+    }
+    *reinterpret_cast<u32x4_t*>(row_base + wcol) = u32x4_t{d[0][0], d[0][1], d[1][0], d[1][1]};
+  };
   auto epilogue = [&](int m0, int n0, int split) {
     const int mrow = m0 + wr * 128 + (L & 15);
     const int ncol = n0 + wc * 64 + 4 * (L >> 4);
@@ -280,11 +300,26 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
           bg[nt][r] = (p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
           bu[nt][r] = (p.bias && n + 32 < p.N) ? (float)p.bias[n + 32] : 0.f;
         }
+      // the wave's 32 output columns of this 64-column gate/up block are whole: 16-byte stores
+      const bool wide = wide_ok && 2 * ((n0 + wc * 64) / 2 + 32) <= p.N;
+      const int obase = (n0 + wc * 64) / 2;
       auto emit = [&](const Acc& g, const Acc& u, int qm) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
           const int m = mrow + qm * 64 + mt * 16;
           if (m >= p.M) continue;
+          if (wide) {
+            uint32_t d[2][2];
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+                d[nt][h] = pack_bf16x2(silu_f(g[mt][nt][2 * h] + bg[nt][2 * h]) * (u[mt][nt][2 * h] + bu[nt][2 * h]),
+                                       silu_f(g[mt][nt][2 * h + 1] + bg[nt][2 * h + 1]) *
+                                           (u[mt][nt][2 * h + 1] + bu[nt][2 * h + 1]));
+            store_row16(C + (size_t)m * p.ldc + obase, d);
+            continue;
+          }
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
             const int oc = ocol + nt * 16;
@@ -310,10 +345,25 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
             bv[qn][nt][r] = (EPI == EPI_STORE && p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
           }
       auto emit = [&](const Acc& acc, int qm, int qn) {
+        const int nbase = n0 + wc * 64 + qn * 32;
+        const bool wide = EPI == EPI_STORE && wide_ok && nbase + 32 <= p.N;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
           const int m = mrow + qm * 64 + mt * 16;
           if (m >= p.M) continue;
+          if constexpr (EPI == EPI_STORE) {
+            if (wide) {
+              uint32_t d[2][2];
+#pragma unroll
+              for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                  d[nt][h] = pack_bf16x2(act_f<ACT>(acc[mt][nt][2 * h] + bv[qn][nt][2 * h]),
+                                         act_f<ACT>(acc[mt][nt][2 * h + 1] + bv[qn][nt][2 * h + 1]));
+              store_row16((bf16*)p.C + (size_t)m * p.ldc + nbase, d);
+              continue;
+            }
+          }
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
             const int n = ncol + qn * 32 + nt * 16;

@@ -113,6 +113,9 @@ def main():
     ap.add_argument("--out", default="githubrepostorag_amd/tuning/gemm_prefill_gfx950.json")
     ap.add_argument("--log", default=None)
     ap.add_argument("--from-log", default=None, help="rebuild --out from an earlier sweep's --log, no GPU")
+    ap.add_argument("--labels", default=None, help="only these shape labels (e.g. qkv,o)")
+    ap.add_argument("--merge", action="store_true",
+                    help="update only the swept (N, K, silu) keys of the existing --out table, keep the rest")
     args = ap.parse_args()
     if args.from_log:
         write_table(args.out, table_from_log(args.from_log), args.mstep)
@@ -125,6 +128,8 @@ def main():
     t_start = time.time()
     for model in args.models.split(","):
         for label, N, K, silu in SHAPES[model]:
+            if args.labels and label not in args.labels.split(","):
+                continue
             key = f"{N},{K},{int(silu)}"
             ws = [((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(2)]
             xfull = (torch.rand(args.mmax, K, device=dev) * 2 - 1).to(torch.bfloat16)
@@ -187,7 +192,15 @@ def main():
             times[f"{model}/{label}"] = trow
             del ws, xfull
             torch.cuda.empty_cache()
-    write_table(args.out, table, args.mstep, {"sweep_s": round(time.time() - t_start, 1)})
+    extra = {"sweep_s": round(time.time() - t_start, 1)}
+    if args.merge and os.path.exists(args.out):
+        old = json.load(open(args.out))
+        merged = dict(old["table"])
+        merged.update(table)
+        extra = {k: v for k, v in old.items() if k not in ("arch", "note", "mstep", "table")}
+        extra["resweep"] = f"{sorted(table)} re-swept ({round(time.time() - t_start, 1)} s)"
+        table = merged
+    write_table(args.out, table, args.mstep, extra)
 
 if __name__ == "__main__":
     main()
