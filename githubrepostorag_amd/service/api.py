@@ -16,6 +16,7 @@ endpoint, all served in-process:
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import json
 import logging
 import time
@@ -49,8 +50,14 @@ class APIState:
 
 def create_app(state: APIState | None = None, runtime_factory=None) -> FastAPI:
     state = state or APIState()
+
+    @contextlib.asynccontextmanager
+    async def lifespan(_app):
+        await _startup()
+        yield
+
     app = FastAPI(title="RAG API Service", description="MI355X-native code RAG (in-process GPU engine)",
-                  version="2.0.0")
+                  version="2.0.0", lifespan=lifespan)
     app.state.api = state
     app.add_middleware(CORSMiddleware, allow_origins=["*"], allow_credentials=True, allow_methods=["*"],
                        allow_headers=["*"])
@@ -66,8 +73,7 @@ def create_app(state: APIState | None = None, runtime_factory=None) -> FastAPI:
         M.REQUEST_LATENCY.labels(**labels).observe(time.perf_counter() - start)
         return response
 
-    @app.on_event("startup")
-    async def _startup():
+    async def _startup():  # runtime (built off the event loop), job worker, queue
         _get_app_start_time()
         if state.runtime is None and runtime_factory is not None:
             loop = asyncio.get_running_loop()
