@@ -560,11 +560,27 @@ GRAG_API int grag_splitk_reduce(const void* ws, const void* bias, void* C, int l
 //               workgroups share the last (tiles - dp) tiles, dp = (tiles / sk_grid - 1) * sk_grid
 //               (all tiles when tiles < sk_grid); ws >= 2 * sk_grid * 65536 floats, cnt >= tiles
 //               zero-initialised words (each reset by its tile's last arriver);
-//   ksplit == 1, sk_grid < 0: the same with dp = (tiles / |sk_grid|) * |sk_grid| (only the partial
-//               last round is streamed; shares down to a quarter tile);
+//   ksplit == 1, sk_grid < 0: every full round of the device's CUs is data-parallel, dp =
+//               (tiles / ncu) * ncu, and |sk_grid| stream-K workgroups share the partial last round
+//               (|sk_grid| = ncu: one per CU; fewer for a thin remainder; shares down to a quarter tile);
 //   otherwise every tile is one workgroup.
 // Requirements (checked): K % 64 == 0, every split >= 2 K-tiles, lda/ldw % 8 == 0,
 // N % 8 == 0 (silu: N % 64 == 0), ldc % 8 == 0, 16-B aligned pointers.
+namespace {
+// compute units of the current device (cached per device; a host query, legal during graph capture)
+int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+}  // namespace
+
 GRAG_API int grag_gemm_tile(const void* A, const void* W, const void* bias, void* C, int lda, int ldw, int ldc,
                             int M, int N, int K, int epi, int act, int ksplit, int sk_grid, void* ws, void* cnt,
                             hipStream_t stream) {
@@ -606,10 +622,11 @@ GRAG_API int grag_gemm_tile(const void* A, const void* W, const void* bias, void
   // sk_grid < 0: every full round is data-parallel and only the remainder is streamed over |sk_grid|
   // workgroups (shares >= a quarter tile: <= 5 parts per tile, the last arriver folds <= 4 slabs)
   const int skg = sk_grid < 0 ? -sk_grid : sk_grid;
-  if (ksplit == 1 && skg > 0 && tiles % skg != 0) {
+  const int ncu = device_cus();
+  if (ksplit == 1 && skg > 0 && tiles % (sk_grid < 0 ? ncu : skg) != 0) {
     if (ws == nullptr || cnt == nullptr) return (int)hipErrorInvalidValue;
     const long rounds = tiles / skg;
-    a.dp_tiles = sk_grid < 0 ? (int)(rounds * skg) : rounds >= 1 ? (int)((rounds - 1) * skg) : 0;
+    a.dp_tiles = sk_grid < 0 ? (int)((tiles / ncu) * ncu) : rounds >= 1 ? (int)((rounds - 1) * skg) : 0;
     a.sk_grid = skg;
     const long min_share = sk_grid < 0 ? (kt + 3) / 4 : (kt + 1) / 2;
     if ((tiles - a.dp_tiles) * kt < (long)skg * min_share) return (int)hipErrorInvalidValue;

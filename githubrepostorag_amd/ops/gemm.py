@@ -116,10 +116,11 @@ def sk_ok(M: int, N: int, K: int, ksplit: int, sk: int) -> bool:
         return kts >= 2 and (ksplit - 1) * kts < kt and kt - (ksplit - 1) * kts >= 2
     tiles = -(-M // 256) * -(-N // 256)
     skg = abs(sk)
-    if skg == 0 or tiles % skg == 0:
+    ncu = _num_cus()
+    if skg == 0 or tiles % (ncu if sk < 0 else skg) == 0:
         return True
     rounds = tiles // skg
-    dp = rounds * skg if sk < 0 else (rounds - 1) * skg if rounds >= 1 else 0
+    dp = (tiles // ncu) * ncu if sk < 0 else (rounds - 1) * skg if rounds >= 1 else 0
     return (tiles - dp) * kt >= skg * ((kt + 3) // 4 if sk < 0 else (kt + 1) // 2)
 
 

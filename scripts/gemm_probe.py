@@ -41,8 +41,10 @@ def schedules(M, N, K, silu):
     for ks in (2, 3, 4, 5, 6, 7, 8, 9, 12, 16):
         if G.sk_ok(M, N, K, ks, 0) and ks <= kt // 2:
             out.append((ks, 0))
-    for sk in (ncu, -ncu, ncu // 2, -ncu // 2, 192, -192):
-        if G.sk_ok(M, N, K, 1, sk):
+    tiles = -(-M // 256) * -(-N // 256)
+    tail = tiles % ncu
+    for sk in (ncu, -ncu, ncu // 2, -ncu // 2, 192, -192, -tail, -2 * tail, -4 * tail):
+        if sk and abs(sk) <= ncu and G.sk_ok(M, N, K, 1, sk):
             out.append((1, sk))
     return list(dict.fromkeys(out))
 

@@ -65,6 +65,15 @@ def own_arms(M, N, K):
     kt = K // 64
     if tiles > ncu and tiles % ncu and (tiles % ncu) * kt >= ncu * ((kt + 3) // 4):
         arms.add((1, -ncu))
+    # tail-only stream-K over a smaller grid: the last partial round's tiles shared by g workgroups
+    # (g = 1x / 2x / 4x the leftover tiles, capped by the launcher's quarter-tile rule), so a thin
+    # last round (e.g. 10 tiles after two full rounds) costs a fraction of a round instead of a round
+    tail = tiles % ncu
+    if tiles > ncu and tail:
+        for f in (1, 2, 4):
+            g = min(ncu, tail * f, (tail * kt) // ((kt + 3) // 4))
+            if g >= 2 and G.sk_ok(M, N, K, 1, -g):
+                arms.add((1, -g))
     return sorted(arms)
 
 

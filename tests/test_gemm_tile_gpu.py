@@ -108,8 +108,10 @@ def test_gemm_graph_replay(dev):
 
 @pytest.mark.parametrize("M,N,K,sk", [(512, 1536, 512, 16), (512, 1536, 512, 20), (2560, 1024, 384, 16),
                                       (4096, 4608, 1024, 256), (192, 37888, 1024, 256),
-                                      # sk < 0: whole rounds data-parallel, only the remainder streamed
-                                      (512, 1536, 512, -20), (2560, 1024, 384, -16), (1280, 4608, 1024, -64)])
+                                      # sk < 0: every full round of the CUs data-parallel, |sk| workgroups
+                                      # stream the rest (fewer tiles than CUs: all of them are streamed)
+                                      (512, 1536, 512, -20), (2560, 1024, 384, -16), (1280, 4608, 1024, -64),
+                                      (4352, 4096, 512, -40), (4352, 4096, 512, -16)])
 def test_gemm_stream_k(dev, M, N, K, sk):
     x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
     y = G.gemm(x, w, b, ksplit=1, sk=sk)
