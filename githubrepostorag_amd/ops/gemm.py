@@ -147,8 +147,10 @@ def prefill_plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int] 
     1131 us at 7040; owned 650-770 us across the range), so the library is taken only where it won at
     both buckets around M; otherwise the owned schedule measured at the bucket at or above M (re-checked
     against the launcher rule at this M).  SwiGLU shapes are always owned (the library needs a separate
-    SiLU*mul pass: owned won all 63 buckets on Qwen2-7B / 1.5B).  Unmeasured shapes: None (library) for
-    plain GEMMs, ``plan`` for SwiGLU."""
+    SiLU*mul pass: owned won all 63 buckets on Qwen2-7B / 1.5B).  Of the two buckets around M, the one on M's
+    own row-tile grid is preferred (its schedule was measured on the identical tile count), and a tail-only
+    stream-K grid is re-derived for M's own remainder (``_tail_grid``).  Unmeasured shapes: None (library)
+    for plain GEMMs, ``plan`` for SwiGLU."""
     t = _prefill_table().get((N, K, int(silu)))
     if t is None:
         return plan(M, N, K) if silu else None
@@ -160,8 +162,28 @@ def prefill_plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int] 
     won = [r for r in cand if r[2] is not None and (silu or r[2] < r[1])]  # SwiGLU: owned at every bucket
     if not won:
         return plan(M, N, K) if silu else None
+    # a bucket with M's own row-tile count ran on the identical tile grid: its schedule transfers as is
+    same = [r for r in won if -(-r[0] // 256) == -(-M // 256)]
+    if same:
+        won = same
     ks, sk = won[0][3], won[0][4]
+    if ks == 1 and sk < 0:
+        sk = _tail_grid(won[0][0], M, N, sk)
     return (ks, sk) if sk_ok(M, N, K, ks, sk) else (1, 0)
+
+
+def _tail_grid(Mb: int, M: int, N: int, sk: int) -> int:
+    """A tail-only stream-K grid measured at bucket Mb, re-derived for M: the sweep's grids are 1x / 2x / 4x
+    the tiles left after the full CU rounds (or one per CU), so keep that ratio to M's own remainder (0: no
+    remainder, whole tiles)."""
+    ncu = _num_cus()
+    tn = -(-N // 256)
+    tail_b, tail = (-(-Mb // 256) * tn) % ncu, (-(-M // 256) * tn) % ncu
+    if tail == 0:
+        return 0
+    if -sk >= ncu or tail_b == 0:
+        return -ncu
+    return -min(ncu, max(1, round(-sk * tail / tail_b)))
 
 
 PREFILL_MIN_M = 257  # above one 256-row tile: the prefill regime (decode batches use plan())
