@@ -607,6 +607,17 @@ class LLMEngine:
             reason = "length"
         elif s.total_len >= self.cfg.max_model_len:
             reason = "length"
+        if s.on_token is None and not p.stop:
+            # nobody reads the text before the end (no stream consumer, no stop strings): detokenize once
+            # at finish instead of per token (~2 us x 512 rows of host time per decode step)
+            if reason is not None:
+                ids = s.output_ids[:-1] if reason == "stop" and tok in self._eos else s.output_ids
+                s.text = self._detok_all(ids)
+                s.finish_reason = reason
+                s.finish_time = now
+                self.sched.finish(s)
+                return True
+            return False
         if s.detok is None:
             s.detok = IncrementalDetokenizer(self.tok)
         delta = ""
@@ -628,6 +639,13 @@ class LLMEngine:
             self.sched.finish(s)
         self._notify(s, delta, reason is not None)
         return reason is not None
+
+    def _detok_all(self, ids) -> str:
+        """The text IncrementalDetokenizer would have produced for ``ids`` (same bytes, same decoder)."""
+        tb = getattr(self.tok, "token_bytes", None)
+        if tb is None:
+            return "".join(self.tok.decode([t]) for t in ids)
+        return b"".join(tb(t) for t in ids).decode("utf-8", errors="replace")
 
     def _notify(self, s: Sequence, delta, finished: bool) -> None:
         if s.on_token is not None:

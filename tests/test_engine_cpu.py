@@ -225,3 +225,30 @@ def test_complete_many_wave_matches_single_calls(model, tok):
         assert all(not m.error for m in many)
     finally:
         runner.shutdown()
+
+
+def test_lazy_detokenization_matches_streaming_text():
+    """Requests without a token callback or stop strings are detokenized once at finish (host time per
+    decode step); the text must equal what the per-token incremental decoder produces for the same ids."""
+    from githubrepostorag_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from githubrepostorag_amd.engine.sequence import SamplingParams
+    from githubrepostorag_amd.engine.tokenizer import ByteBPETokenizer
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import Qwen2Model
+
+    cfg = decoder_config("qwen2-tiny")
+    model = Qwen2Model(cfg, device="cpu", seed=0)
+    tok = ByteBPETokenizer(cfg.vocab_size)
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_model_len=256, num_blocks=64))
+    prompts = [tok.encode("def retry(policy): " * n) for n in (1, 3)]
+    sp = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
+    lazy = eng.generate(prompts, sp)
+    seen = []
+    streamed = [eng.add_request(p, sp, on_token=lambda s, d, f: seen.append(d)) for p in prompts]
+    while eng.has_unfinished():
+        eng.step()
+    for rid, a in zip(streamed, lazy):
+        b = eng.completion(eng.pop(rid))
+        assert b.token_ids == a.token_ids and b.text == a.text and b.text
+        assert a.text == eng._detok_all(a.token_ids)
+    assert seen  # the streamed requests went through the per-token path
