@@ -76,6 +76,12 @@ def parse():
     ap.add_argument("--ingest-seqs", type=int, default=256, help="concurrent sequences of the ingest engine")
     ap.add_argument("--ingest-mixed", type=int, default=0,
                     help="1: the ingest engine piggybacks decode tokens on prefill steps (mixed batches)")
+    ap.add_argument("--mixed", type=int, default=0,
+                    help="1: stall-free batching in the serving engine: every prefill step also carries one decode "
+                         "token of every decode-ready sequence (decode rows run in the prefill GEMMs)")
+    ap.add_argument("--max-batched-tokens", type=int, default=16384,
+                    help="prefill token budget per engine step (smaller: arrivals prefilled in chunks over "
+                         "several mixed steps)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--switch-interval", type=float, default=0.0,
                     help="Python GIL switch interval (s): the engine thread re-takes the GIL quickly after a GPU wait")
@@ -244,7 +250,8 @@ def main():
     gsizes = EngineConfig.graph_batch_sizes
     if live > max(gsizes):  # deeper pipelines: decode graphs up to the live-sequence count, 128-row buckets
         gsizes = tuple(sorted({*gsizes, *range(max(gsizes) + 128, live + 127, 128)}))
-    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=live, max_num_batched_tokens=16384,
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=live, max_num_batched_tokens=args.max_batched_tokens,
+                                             mixed_batches=bool(args.mixed),
                                              max_model_len=max_len, use_cuda_graph=not args.no_graph,
                                              seed=dp_rank, graph_batch_sizes=gsizes))
     sp = SamplingParams(max_tokens=args.gen_len, temperature=0.4, top_p=0.8, repetition_penalty=1.2,
@@ -549,6 +556,8 @@ def main():
                          f"(nlist={args.nlist}, nprobe={args.nprobe}) sharded dp{world}",
                 "global_batch": args.batch * dp_size,
                 "inflight_batches": D,
+                "mixed_batches": bool(args.mixed),
+                "max_batched_tokens": args.max_batched_tokens,
                 "arrival_groups": A,
                 "concurrent_seqs": args.batch * D * dp_size,
                 "seq_len": args.prompt_len,

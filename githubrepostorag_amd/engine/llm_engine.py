@@ -274,6 +274,10 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ prefill
     def _run_prefill(self, items) -> list[Sequence]:
+        n_pref = next((i for i, (s, a, b) in enumerate(items) if b - a == 1 and s.output_ids and a == s.total_len - 1),
+                      len(items))
+        if 0 < n_pref < len(items):
+            return self._run_mixed(items[:n_pref], [s for s, _, _ in items[n_pref:]])
         t0 = time.perf_counter()
         seqs = [s for s, _, _ in items]
         ids, pos, slots, q_start, ctx = [], [], [], [0], []
@@ -347,6 +351,107 @@ class LLMEngine:
         if n_dec:
             self.stats["decode_tokens"] += n_dec
             self.stats["mixed_steps"] += 1
+        self.stats["prefill_s"] += time.perf_counter() - t0
+        return finished
+
+    def _run_mixed(self, pitems, dseqs) -> list[Sequence]:
+        """One step of prefill chunks plus one decode token for every decode-ready sequence (stall-free
+        batching): the decode rows ride in the prefill step's GEMMs (M = prefill tokens + decode rows,
+        run at the prefill schedule's MFMA rate instead of a separate weight-streaming decode step) and
+        their attention runs on the split-KV decode kernel.  Inputs go up as one packed int32 buffer: the
+        prefill part built per chunk, the decode part from the per-slot block table (_decode_inputs)."""
+        t0 = time.perf_counter()
+        bs = self.cfg.block_size
+        n_pref, n_dec = len(pitems), len(dseqs)
+        ids, pos, slots, q_start, ctx = [], [], [], [0], []
+        for s, a, b in pitems:
+            ids.append(np.asarray(s.all_ids[a:b], dtype=np.int32))
+            pos.append(np.arange(a, b, dtype=np.int32))
+            slots.append(self._slots_of(s, a, b))
+            q_start.append(q_start[-1] + (b - a))
+            ctx.append(b)
+        Tp = q_start[-1]
+        T = Tp + n_dec
+        pseqs = [s for s, _, _ in pitems]
+        wp = max(len(s.blocks) for s in pseqs)
+        max_ctx = max(s.total_len for s in dseqs)
+        wd = -(-max_ctx // bs)
+        dec = self._decode_inputs(dseqs, n_dec, wd, 1)
+        o = 0
+        d_ids = dec[o:o + n_dec]; o += n_dec
+        d_pos = dec[o:o + n_dec]; o += n_dec
+        d_slot = dec[o:o + n_dec]; o += n_dec
+        d_ctx = dec[o:o + n_dec]; o += n_dec
+        d_samp = dec[o:o + n_dec]; o += n_dec
+        o += n_dec + 1  # q_start 0..n_dec
+        d_bt = dec[o:]
+        # rows to sample: the last token of every prefill chunk that completes its prompt, then every decode row
+        done = [i for i, (s, a, b) in enumerate(pitems) if b == s.total_len]
+        samp_rows = np.concatenate([np.asarray([q_start[i + 1] - 1 for i in done], dtype=np.int32),
+                                    np.arange(Tp, T, dtype=np.int32)])
+        samp_slots = np.concatenate([np.asarray([pseqs[i].slot for i in done], dtype=np.int32), d_samp])
+        packed = np.concatenate([
+            *ids, d_ids, *pos, d_pos, *slots, d_slot,                       # [T] x 3
+            np.asarray(q_start, dtype=np.int32), np.asarray(ctx, dtype=np.int32),
+            self._block_table(pseqs, wp).reshape(-1),                       # prefill chunks
+            np.arange(n_dec + 1, dtype=np.int32), d_ctx, d_bt,              # decode rows
+            samp_rows, samp_slots])
+        dev = self._to_dev(packed)
+        th = time.perf_counter()
+        self.stats["host_prefill_prep_s"] += th - t0
+        o = 0
+        t_ids = dev[o:o + T]; o += T
+        t_pos = dev[o:o + T]; o += T
+        t_slot = dev[o:o + T]; o += T
+        p_qs = dev[o:o + n_pref + 1]; o += n_pref + 1
+        p_ctx = dev[o:o + n_pref]; o += n_pref
+        p_bt = dev[o:o + n_pref * wp].view(n_pref, wp); o += n_pref * wp
+        q_qs = dev[o:o + n_dec + 1]; o += n_dec + 1
+        q_ctx = dev[o:o + n_dec]; o += n_dec
+        q_bt = dev[o:o + n_dec * wd].view(n_dec, wd); o += n_dec * wd
+        ns = len(samp_rows)
+        t_rows = dev[o:o + ns]; o += ns
+        t_samp = dev[o:o + ns]
+        split_len = _split_len_for(n_dec)
+        nsplit = max(1, -(-max_ctx // split_len))
+        hq, dh = self.model.hq, self.model.head_dim
+        meta = AttnMetadata(q_start=p_qs, ctx_len=p_ctx, block_tables=p_bt, slot_mapping=t_slot,
+                            max_q_len=max(b - a for _, a, b in pitems), num_seqs=n_pref, num_tokens=Tp)
+        meta.extra["decode_rows"] = (Tp, AttnMetadata(
+            q_start=q_qs, ctx_len=q_ctx, block_tables=q_bt, slot_mapping=t_slot[Tp:], max_q_len=1, num_seqs=n_dec,
+            num_tokens=n_dec, is_decode=True, num_splits=nsplit, split_len=split_len,
+            part_o=self._part_o[: nsplit * n_dec * hq * dh] if self.on_gpu else None,
+            part_ml=self._part_ml[: nsplit * n_dec * hq * 2] if self.on_gpu else None))
+        hidden = self.model.forward(t_ids, t_pos, meta, self.kv_caches)
+        toks_d = self._sample(hidden.index_select(0, t_rows), t_samp)
+        t1 = time.perf_counter()
+        self.stats["host_prefill_launch_s"] += t1 - th
+        tp = self.model.tp
+        tp.stage_health()
+        toks = self._read_host(toks_d).reshape(-1).tolist()
+        tp.check_health()
+        now = time.perf_counter()
+        self.stats["host_prefill_sample_s"] += now - t1
+        finished = []
+        for s, a, b in pitems:
+            s.num_computed = b
+            self.kv.register_full_blocks(s)
+        k = 0
+        for i in done:
+            s = pseqs[i]
+            if self._append(s, int(toks[k]), now):
+                finished.append(s)
+            k += 1
+        for s in dseqs:
+            if s.finish_reason is None and s.status == SeqStatus.RUNNING:
+                s.num_computed = s.total_len
+                if self._append(s, int(toks[k]), now):
+                    finished.append(s)
+            k += 1
+        self.stats["host_prefill_post_s"] += time.perf_counter() - now
+        self.stats["prefill_tokens"] += Tp
+        self.stats["decode_tokens"] += n_dec
+        self.stats["mixed_steps"] += 1
         self.stats["prefill_s"] += time.perf_counter() - t0
         return finished
 

@@ -89,8 +89,6 @@ def paged_attention_ref(q, k_cache, v_cache, meta: AttnMetadata, scale: float, c
 def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMetadata,
                     scale: float, causal: bool = True, out: torch.Tensor | None = None) -> torch.Tensor:
     """q [T, Hq, D] (token-major) -> out [T, Hq*D]."""
-    if not q.is_cuda:
-        return paged_attention_ref(q, k_cache, v_cache, meta, scale, causal).reshape(q.shape[0], -1)
     dec = meta.extra.get("decode_rows")
     if dec is not None:  # mixed step: prefill rows [0, Tp) + one-token decode rows [Tp, T)
         Tp, dmeta = dec
@@ -101,6 +99,12 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                              num_tokens=Tp)
         paged_attention(q[:Tp], k_cache, v_cache, pmeta, scale, causal, out=out[:Tp])
         paged_attention(q[Tp:], k_cache, v_cache, dmeta, scale, causal, out=out[Tp:])
+        return out
+    if not q.is_cuda:
+        ref = paged_attention_ref(q, k_cache, v_cache, meta, scale, causal).reshape(q.shape[0], -1)
+        if out is None:
+            return ref
+        out.copy_(ref)
         return out
     T, Hq, D = q.shape
     Hkv, BS = k_cache.shape[1], k_cache.shape[2]

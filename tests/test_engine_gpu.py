@@ -129,3 +129,25 @@ def test_sampler_scratch_outlives_graphs_captured_before_it_grew(setup, dev):
     a = eng.generate(_prompts(tok), sp)
     b = LLMEngine(model, tok, EngineConfig(use_cuda_graph=False, **cfg)).generate(_prompts(tok), sp)
     assert [x.token_ids for x in a] == [x.token_ids for x in b]
+
+
+def test_mixed_steps_match_separate_steps(setup, dev):
+    """Stall-free batching (decode rows riding in prefill steps, their attention on the split-KV decode kernel,
+    inputs from the per-slot block table) against separate prefill / hipGraph decode steps: every greedy token
+    of the mixed engine passes the same logit-tolerance check against a prefill recompute."""
+    model, tok = setup
+    sp = SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True)
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=8, max_model_len=2048, num_blocks=1024,
+                                             max_num_batched_tokens=64, mixed_batches=True))
+    prompts = _prompts(tok)
+    ids = [eng.add_request(prompts[0], sp)]
+    for p in prompts[1:]:  # later arrivals prefill in 64-token chunks while the earlier ones decode
+        eng.step()
+        ids.append(eng.add_request(p, sp))
+    while eng.has_unfinished():
+        eng.step()
+    assert eng.stats["mixed_steps"] > 0
+    for p, r in zip(prompts, ids):
+        out = eng.get(r).output_ids
+        assert len(out) == 10
+        greedy_within_tolerance(model, dev, p, out)
