@@ -350,8 +350,11 @@ def main():
         while True:
             have = min(len(eng.get(r).output_ids) for r in rids)
             if have >= ntok:
-                break
-            cap = ntok - have
+                # stall-free batching: the sub-step also finishes its arrivals' prefill (chunks ride with one
+                # decode token of every live sequence), so every sub-step does one group's prefill work
+                if not (args.mixed and (arrival is not None or eng.has_pending_prefill())):
+                    break
+            cap = max(1, ntok - have)
             arrived = arrival is not None and ready(arrival)
             if arrival is not None and not arrived and args.arrival_cap:
                 # an arrival's retrieval is in flight: one decode step per replay, so the engine looks

@@ -451,28 +451,41 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
       const bool is_last = flag[0] != 0u;
       __syncthreads();  // every wave has read the flag before the next segment's DMA reuses the LDS
       if (!is_last) continue;
-      // fixed-order sum (((s_first + s_first+1) + ...) + s_last); this part's own from registers
-      for (int c = first; c <= last; ++c) {
-        if (c == j) continue;
-        const float* src = p.slab + (size_t)slot_of(c, ts) * 65536 + tid * 4;
-        // 8 loads in flight per quadrant, then the adds (one vmcnt per quadrant, not per chunk)
-        auto fold = [&](Acc& acc, int q0) {
+      // fixed-order sum (((s_first + s_first+1) + ...) + s_last) whichever part arrives last (bitwise
+      // reproducible for any part count: the running sum is built in part order, this part's own term
+      // taken from its registers at its position); 8 loads in flight per quadrant and part
+      auto fold = [&](Acc& acc, int q0) {
+        f32x4_t s[8];
+        for (int c = first; c <= last; ++c) {
+          if (c == j) {
+            if (c == first) {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) s[i] = acc[i >> 1][i & 1];
+            } else {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) s[i] += acc[i >> 1][i & 1];
+            }
+            continue;
+          }
+          const float* src = p.slab + (size_t)slot_of(c, ts) * 65536 + tid * 4;
           f32x4_t t[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) t[i] = *reinterpret_cast<const f32x4_t*>(src + (q0 + i) * kThreads * 4);
-          if (c < j) {  // parts before this one are summed first: fold them left of the registers
+          if (c == first) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) acc[i >> 1][i & 1] = t[i] + acc[i >> 1][i & 1];
+            for (int i = 0; i < 8; ++i) s[i] = t[i];
           } else {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) acc[i >> 1][i & 1] += t[i];
+            for (int i = 0; i < 8; ++i) s[i] += t[i];
           }
-        };
-        fold(acc00, 0);
-        fold(acc01, 8);
-        fold(acc11, 16);
-        fold(acc10, 24);
-      }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i >> 1][i & 1] = s[i];
+      };
+      fold(acc00, 0);
+      fold(acc01, 8);
+      fold(acc11, 16);
+      fold(acc10, 24);
     }
     epilogue(m0, n0, split);
   }

@@ -176,6 +176,11 @@ class LLMEngine:
     def has_unfinished(self) -> bool:
         return self.sched.has_work()
 
+    def has_pending_prefill(self) -> bool:
+        """Admitted or waiting requests whose prompt is not fully prefilled yet."""
+        sch = self.sched
+        return bool(sch.waiting) or any(s.is_prefill for s in sch.running)
+
     def get(self, req_id: str) -> Sequence | None:
         return self._seqs.get(req_id)
 

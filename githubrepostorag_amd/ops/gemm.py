@@ -181,6 +181,8 @@ def _tail_grid(Mb: int, M: int, N: int, sk: int) -> int:
     tail_b, tail = (-(-Mb // 256) * tn) % ncu, (-(-M // 256) * tn) % ncu
     if tail == 0:
         return 0
+    if tail_b and -sk > tail_b and -sk % tail_b == 0:  # K-aligned split: s parts per leftover tile
+        return -(-sk // tail_b) * tail
     if -sk >= ncu or tail_b == 0:
         return -ncu
     return -min(ncu, max(1, round(-sk * tail / tail_b)))

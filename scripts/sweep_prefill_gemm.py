@@ -74,6 +74,13 @@ def own_arms(M, N, K):
             g = min(ncu, tail * f, (tail * kt) // ((kt + 3) // 4))
             if g >= 2 and G.sk_ok(M, N, K, 1, -g):
                 arms.add((1, -g))
+        # K-aligned tail splits: every leftover tile cut into s equal K parts (s x tail workgroups, more than
+        # one per CU allowed): the parts of a round start at the same K offsets (L2 reuse, unlike a grid
+        # that straddles tiles) and the tail costs ceil(s tail / CUs) / s of a round
+        for s_ in (2, 3, 4):
+            g = tail * s_
+            if g > ncu // 2 and G.sk_ok(M, N, K, 1, -g):
+                arms.add((1, -g))
     return sorted(arms)
 
 

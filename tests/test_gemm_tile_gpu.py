@@ -111,7 +111,11 @@ def test_gemm_graph_replay(dev):
                                       # sk < 0: every full round of the CUs data-parallel, |sk| workgroups
                                       # stream the rest (fewer tiles than CUs: all of them are streamed)
                                       (512, 1536, 512, -20), (2560, 1024, 384, -16), (1280, 4608, 1024, -64),
-                                      (4352, 4096, 512, -40), (4352, 4096, 512, -16)])
+                                      (4352, 4096, 512, -40), (4352, 4096, 512, -16),
+                                      # K-aligned tail splits with more stream-K workgroups than CUs: 392 tiles
+                                      # = 256 + 136, every leftover tile in 3 K parts (408 workgroups); 90 tiles
+                                      # in 3 parts (270)
+                                      (7040, 3584, 2048, -408), (1280, 4608, 1024, -270)])
 def test_gemm_stream_k(dev, M, N, K, sk):
     x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
     y = G.gemm(x, w, b, ksplit=1, sk=sk)
@@ -120,7 +124,7 @@ def test_gemm_stream_k(dev, M, N, K, sk):
     assert torch.equal(y, y2), "stream-K fixup must be bitwise reproducible"
 
 
-@pytest.mark.parametrize("M,I,sk", [(192, 4096, 48), (768, 2048, -20)])
+@pytest.mark.parametrize("M,I,sk", [(192, 4096, 48), (768, 2048, -20), (768, 2048, -192)])
 def test_gemm_silu_stream_k(dev, M, I, sk):
     K = 1024  # (192, 48): 32 tiles over 48 stream-K workgroups, every tile split; (768, -20): 8-tile remainder
     x = rnd(M, K, dev=dev, scale=0.3)
