@@ -28,17 +28,38 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // One block per token.  Work units (16 B each):
 //   [0, (Hq+Hkv)*D/16)           rotary units: 8 pairs (i..i+7, i+D/2..i+D/2+7)
 //   [.., + Hkv*D/8)              v copy units
+// PL: the projection arrives as S fp32 split-K planes [S][T][ld] (ops/gemm.py SplitKPartial): the reduce is
+// folded in here (sum in plane order, rounded to bf16 exactly as grag_splitk_reduce would store it).
+template <bool PL>
 __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
     const bf16* __restrict__ qkv, int ld, const bf16* __restrict__ bias,
     const int32_t* __restrict__ positions, const float* __restrict__ cos_sin,
     const int32_t* __restrict__ slot_mapping, bf16* __restrict__ q_out, bf16* __restrict__ k_cache,
-    bf16* __restrict__ v_cache, int Hq, int Hkv, int D, int BS) {
+    bf16* __restrict__ v_cache, int Hq, int Hkv, int D, int BS, const float* __restrict__ planes, int S,
+    size_t plane) {
   const int t = blockIdx.x;
+  const float* prow = PL ? planes + (size_t)t * ld : nullptr;
+  // 8 consecutive projection outputs of this token as bf16-rounded floats
+  auto load8 = [&](int col, float* x) {
+    if constexpr (PL) {
+      f32x4_t a = *reinterpret_cast<const f32x4_t*>(prow + col), b = *reinterpret_cast<const f32x4_t*>(prow + col + 4);
+      for (int s = 1; s < S; ++s) {
+        a += *reinterpret_cast<const f32x4_t*>(prow + s * plane + col);
+        b += *reinterpret_cast<const f32x4_t*>(prow + s * plane + col + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[j] = bits2f(f2bits(a[j]));
+        x[j + 4] = bits2f(f2bits(b[j]));
+      }
+    } else {
+      unpack8(*reinterpret_cast<const bf16x8_t*>(qkv + (size_t)t * ld + col), x);
+    }
+  };
   const int half = D >> 1;
   const int upp = half >> 3;  // rotary units per head
   const int n_rot = (Hq + Hkv) * upp;
   const int n_v = Hkv * (D >> 3);
-  const bf16* row = qkv + (size_t)t * ld;
   const int pos = positions[t];
   const int slot = slot_mapping ? slot_mapping[t] : -1;
   // cos_sin == nullptr: no rotary (absolute-position decoders, GPT-2) — the
@@ -52,8 +73,8 @@ __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
       const int i0 = (u % upp) * 8;
       const int col = head * D + i0;
       float x1[8], x2[8];
-      unpack8(*reinterpret_cast<const bf16x8_t*>(row + col), x1);
-      unpack8(*reinterpret_cast<const bf16x8_t*>(row + col + half), x2);
+      load8(col, x1);
+      load8(col + half, x2);
       if (bias) {
         float b1[8], b2[8];
         unpack8(*reinterpret_cast<const bf16x8_t*>(bias + col), b1);
@@ -95,14 +116,19 @@ __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
       const int vh = vu / (D >> 3);
       const int i0 = (vu % (D >> 3)) * 8;
       const int col = (Hq + Hkv + vh) * D + i0;
-      bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(row + col);
-      if (bias) {
-        float a[8], b[8];
-        unpack8(v, a);
-        unpack8(*reinterpret_cast<const bf16x8_t*>(bias + col), b);
+      bf16x8_t v;
+      if (bias || PL) {
+        float a[8];
+        load8(col, a);
+        if (bias) {
+          float b[8];
+          unpack8(*reinterpret_cast<const bf16x8_t*>(bias + col), b);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] += b[j];
+          for (int j = 0; j < 8; ++j) a[j] += b[j];
+        }
         v = pack8(a);
+      } else {
+        v = *reinterpret_cast<const bf16x8_t*>(qkv + (size_t)t * ld + col);
       }
       *reinterpret_cast<bf16x8_t*>(v_cache + (((size_t)blk * Hkv + vh) * BS + off) * D + i0) = v;
     }
@@ -248,9 +274,24 @@ GRAG_API int grag_qkv_rope_kvstore(const void* qkv, int ld, const void* bias,
                                    hipStream_t stream) {
   if (T <= 0) return 0;
   if (D % 16 != 0 || ld % 8 != 0) return (int)hipErrorInvalidValue;
-  qkv_rope_kernel<<<T, kThreads, 0, stream>>>((const bf16*)qkv, ld, (const bf16*)bias, positions,
-                                              cos_sin, slot_mapping, (bf16*)q_out,
-                                              (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, D, BS);
+  qkv_rope_kernel<false><<<T, kThreads, 0, stream>>>((const bf16*)qkv, ld, (const bf16*)bias, positions,
+                                                     cos_sin, slot_mapping, (bf16*)q_out,
+                                                     (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, D, BS, nullptr, 1, 0);
+  return (int)hipGetLastError();
+}
+
+// Same from the S fp32 split-K planes [S][T][N] of the projection (N = (Hq + 2 Hkv) D): the split-K reduce of
+// a deferred qkv projection (ops/gemm.py SplitKPartial) folded into this pass.
+GRAG_API int grag_qkv_rope_kvstore_planes(const float* planes, int S, int N, const void* bias,
+                                          const int32_t* positions, const float* cos_sin,
+                                          const int32_t* slot_mapping, void* q_out, void* k_cache,
+                                          void* v_cache, int T, int Hq, int Hkv, int D, int BS,
+                                          hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (D % 16 != 0 || N % 8 != 0 || S < 1 || N != (Hq + 2 * Hkv) * D) return (int)hipErrorInvalidValue;
+  qkv_rope_kernel<true><<<T, kThreads, 0, stream>>>(nullptr, N, (const bf16*)bias, positions, cos_sin,
+                                                    slot_mapping, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache,
+                                                    Hq, Hkv, D, BS, planes, S, (size_t)T * N);
   return (int)hipGetLastError();
 }
 

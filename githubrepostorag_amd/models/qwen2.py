@@ -188,7 +188,7 @@ class Qwen2Model:
             if W4.plan(x.shape[0], q.N, q.K, q.silu) is not None and W4.capture_ok(x.device, x.shape[0], q):
                 return W4.gemm_w4(x, q, bias)
         w = getattr(L, name)
-        if defer and bias is None:  # o / down feeding residual add + RMSNorm: split-K reduce folded into the norm
+        if defer and bias is None:  # o / down (residual add + RMSNorm) and qkv (RoPE pass) fold the split-K reduce
             return linear_deferred(x, w)
         if name == "gu_w":
             return mlp_gate_up(x, w) if self.gu_interleaved else silu_mul(linear(x, w))
@@ -231,7 +231,7 @@ class Qwen2Model:
                 x = rmsnorm(h, L.in_norm, eps)
             else:
                 x = rmsnorm(h, L.in_norm, eps, residual=residual)
-            qkv = self._proj(x, L, "qkv_w")
+            qkv = self._proj(x, L, "qkv_w", defer=True)  # a K-split's reduce folds into the RoPE pass
             q = qkv_rope_kvstore(qkv, L.qkv_b, positions, self.cos_sin, meta.slot_mapping, kc, vc,
                                  self.hq, self.hkv, self.head_dim)
             a = paged_attention(q, kc, vc, meta, self.scale, causal=True)

@@ -34,6 +34,7 @@ _SIGS = {
     "grag_bert_embed_ln": [P, P, P, P, P, P, P, P, P, I, I, F, P],
     "grag_embed_gather": [P, P, P, I, I, P],
     "grag_qkv_rope_kvstore": [P, I, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "grag_qkv_rope_kvstore_planes": [P, I, I, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "grag_silu_mul": [P, P, I, I, P],
     "grag_bias_act": [P, P, P, I, I, I, P],
     "grag_pool_l2norm": [P, P, P, P, P, I, I, I, I, I, P],

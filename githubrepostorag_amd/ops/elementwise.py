@@ -49,7 +49,20 @@ def qkv_rope_kvstore_ref(qkv, bias, positions, cos_sin, slot_mapping, k_cache, v
 def qkv_rope_kvstore(qkv, bias, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D):
     """Split packed QKV [T, (Hq+2Hkv)*D], add bias, apply NeoX RoPE to q/k
     (skipped when ``cos_sin`` is None), return q [T, Hq, D] and scatter k/v
-    into the paged caches [blocks, Hkv, BS, D]."""
+    into the paged caches [blocks, Hkv, BS, D].  ``qkv`` may be the deferred fp32 split-K planes of the
+    projection (ops/gemm.py SplitKPartial): the kernel then folds the split-K reduce into this pass."""
+    from .gemm import SplitKPartial
+
+    if isinstance(qkv, SplitKPartial):
+        if not qkv.device.type == "cuda":
+            qkv = qkv.materialize()
+        else:
+            T = qkv.M
+            q = torch.empty(T, Hq, D, dtype=qkv.dtype, device=qkv.device)
+            call("grag_qkv_rope_kvstore_planes", ptr(qkv.planes), qkv.S, qkv.N, ptr(bias), ptr(positions),
+                 ptr(cos_sin), ptr(slot_mapping), ptr(q), ptr(k_cache), ptr(v_cache), T, Hq, Hkv, D,
+                 k_cache.shape[2])
+            return q
     if not qkv.is_cuda:
         return qkv_rope_kvstore_ref(qkv, bias, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
     T = qkv.shape[0]

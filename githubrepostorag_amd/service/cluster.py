@@ -603,6 +603,25 @@ def spawn_replicas(n: int, address, authkey: bytes, extra_args=(), gpus: list[in
     return procs
 
 
+def gpu_demo_runtime(settings):
+    """A GPU replica runtime on the product path: the real in-process engine (QWEN_MODEL, e.g. the
+    qwen2-small config with random weights: hipGraph decode, paged KV, fused sampler), a tiny encoder and
+    the GPU vector store over the demo chunks.  For the front door's GPU test (tests/test_cluster_gpu.py)
+    and GPU rehearsals of ``serve --replicas`` without checkpoints."""
+    from ..embed.service import Embedder
+    from ..index.store import VectorStore
+    from .runtime import RAGRuntime
+
+    dev = "cuda"
+    emb = Embedder.from_name("encoder-tiny", device=dev, seed=3)
+    store = VectorStore(emb.dim, dev)
+    texts = ["widgets code", "gadget service", "billing module"]
+    store.table("chunk").upsert(["widgets", "gadget", "billing"], texts, emb.embed_documents(texts),
+                                [{"namespace": "default", "repo": "r", "module": "m", "file_path": f"{x}.py"}
+                                 for x in "abc"])
+    return RAGRuntime(settings, device=dev, embedder=emb, store=store)
+
+
 def demo_runtime(settings):
     """A CPU replica runtime with a scripted LLM and a tiny encoder over three chunks (tests, and a
     GPU-less rehearsal of ``serve --replicas``: ``replica --factory

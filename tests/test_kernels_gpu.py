@@ -82,6 +82,31 @@ def test_qkv_rope_kvstore(dev):
     close(vc, vr, 1e-2)
 
 
+@pytest.mark.parametrize("T", [48, 190, 512])
+def test_qkv_rope_kvstore_from_splitk_planes(dev, T):
+    """Qwen2-7B qkv at decode batches as deferred K-split planes (reduce folded into the RoPE / KV-store pass)
+    against the unfused path (split-K reduce to bf16, then RoPE): identical q / K / V bits."""
+    from githubrepostorag_amd.ops import gemm as G
+    from githubrepostorag_amd.ops.linear import linear, linear_deferred
+
+    Hq, Hkv, D, BS, NB, K = 28, 4, 128, 16, 64, 3584
+    N = (Hq + 2 * Hkv) * D
+    x = rnd(T, K, dev=dev, scale=0.5)
+    w = rnd(N, K, dev=dev, scale=0.05, seed=1)
+    bias = rnd(N, dev=dev, seed=2)
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int32).to(dev)
+    cs = E.rope_cos_sin(4096, D, 1e6, dev)
+    slots = torch.randperm(NB * BS)[:T].to(torch.int32).to(dev)
+    part = linear_deferred(x, w)
+    assert isinstance(part, G.SplitKPartial) and part.S > 1, G.deferred_plan(T, N, K)
+    caches = [(torch.zeros(NB, Hkv, BS, D, dtype=torch.bfloat16, device=dev),
+               torch.zeros(NB, Hkv, BS, D, dtype=torch.bfloat16, device=dev)) for _ in range(2)]
+    q1 = E.qkv_rope_kvstore(part, bias, pos, cs, slots, *caches[0], Hq, Hkv, D)
+    q2 = E.qkv_rope_kvstore(linear(x, w), bias, pos, cs, slots, *caches[1], Hq, Hkv, D)
+    assert torch.equal(q1, q2)
+    assert torch.equal(caches[0][0], caches[1][0]) and torch.equal(caches[0][1], caches[1][1])
+
+
 def test_silu_mul_bias_act(dev):
     gu = rnd(17, 2 * 1024, dev=dev)
     close(E.silu_mul(gu), E.silu_mul(gu.cpu()), 2e-2)
