@@ -212,7 +212,9 @@ def main():
     if args.merge and os.path.exists(args.out):
         old = json.load(open(args.out))
         merged = dict(old["table"])
-        merged.update(table)
+        for key, rows in table.items():  # rows below the sweep's range (decode-batch rows) are kept
+            lo = min(r[0] for r in rows)
+            merged[key] = sorted([r for r in merged.get(key, []) if r[0] < lo] + rows)
         extra = {k: v for k, v in old.items() if k not in ("arch", "note", "mstep", "table")}
         extra["resweep"] = f"{sorted(table)} re-swept ({round(time.time() - t_start, 1)} s)"
         table = merged
