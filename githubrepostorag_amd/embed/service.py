@@ -11,7 +11,7 @@ import threading
 import torch
 
 from ..engine.tokenizer import WordPieceTokenizer
-from ..utils.gpu_guard import gpu_guard, gpu_shared, side_stream
+from ..utils.gpu_guard import gpu_guard, gpu_shared, set_device_of, side_stream
 from ..models.configs import EncoderConfig, encoder_config
 from ..models.encoder import BertEncoder, EncoderGraphs
 
@@ -142,7 +142,7 @@ class _QueryBatcher:
         import time
 
         if self.emb.encoder.device.type == "cuda":
-            torch.cuda.set_device(self.emb.encoder.device)
+            set_device_of(self.emb.encoder.device)
         while not self._stop:
             first = self.q.get()
             if first is None:

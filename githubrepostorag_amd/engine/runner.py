@@ -33,6 +33,7 @@ import time
 
 import torch
 
+from ..utils.gpu_guard import set_device_of
 from .llm_engine import LLMEngine
 from .sequence import Completion, SamplingParams
 
@@ -236,7 +237,7 @@ class EngineRunner:
         """Follower loop of a TP rank: mirror the leader's request stream and
         step in lockstep until the leader stops."""
         if self.engine.on_gpu:
-            torch.cuda.set_device(self.engine.device)
+            set_device_of(self.engine.device)
 
         def drop(seq, delta, finished):
             if finished:
@@ -286,7 +287,7 @@ class EngineRunner:
 
     def _loop(self):
         if self.engine.on_gpu:
-            torch.cuda.set_device(self.engine.device)
+            set_device_of(self.engine.device)
         while True:
             with self._cv:
                 while (not self._stop and not self._pending and not self._aborts

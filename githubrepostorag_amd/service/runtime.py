@@ -46,6 +46,8 @@ class RAGRuntime:
             self.tp_group, self.dp_group = comm.make_tp_dp_groups(s.tp)
             enable_for_group(self.tp_group, device or s.resolved_device())
         self.device = torch.device(device or s.resolved_device())
+        if self.device.type == "cuda" and self.device.index is None:  # threads pin it with set_device
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.started = time.time()
         dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
         # encoder

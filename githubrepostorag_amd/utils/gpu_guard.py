@@ -167,3 +167,10 @@ def side_stream(device, wait_caller: bool = False, join: str = "sync"):
         prev.wait_stream(s)
     else:
         s.synchronize()
+
+
+def set_device_of(dev) -> None:
+    """torch.cuda.set_device for a device that may carry no index ("cuda" means the current device)."""
+    d = torch.device(dev)
+    if d.type == "cuda":
+        torch.cuda.set_device(d.index if d.index is not None else torch.cuda.current_device())
