@@ -62,8 +62,16 @@ class EngineConfig:
 
 
 def _split_len_for(batch: int) -> int:
-    # decode split-KV plan (microbench, 32-key LDS-DMA tiles: B64 ctx1152 split256
-    # 36.7 us < split512 38.0 us; small batches need more splits to fill the CUs)
+    """Keys per split-KV part of the decode attention (flash-decoding) for a batch size.  Small batches
+    need splits to put enough waves on the CUs (B64 ctx1152: split 256 36.7 us < split 512 38.0 us); from
+    ~200 live sequences (x 4 KV heads) the batch alone fills the chip, and long parts win by dropping the
+    combine pass and the partial round trip: B512 ctx1100 251 -> 233 / 225 / 210 us at parts of 512 /
+    1024 / 2048 keys, B256 ctx1100 125 -> 105 us at 2048 (profiles/mb_decode_splits_r3.json).  The part
+    length still caps one wave's keys, so a long sequence among short ones is split."""
+    if batch >= 384:
+        return 32 * KV_TILE
+    if batch >= 192:
+        return 16 * KV_TILE
     if batch >= 8:
         return 4 * KV_TILE
     return 2 * KV_TILE

@@ -156,6 +156,12 @@ if __name__ == "__main__":
     if args.what in ("all", "gemm"):
         for M in (1, 8, 64):
             res.update(gemm_bench(M))
+    if args.what == "decode_splits":  # split-KV plan at the bench's 512-row step: fewer splits, no combine
+        for sl in (256, 512, 1024, 2048):
+            res[f"decode_B512_ctx1100_split{sl}"] = attn_decode_bench(512, 1100, sl)
+        for sl in (256, 2048):
+            res[f"decode_B256_ctx1100_split{sl}"] = attn_decode_bench(256, 1100, sl)
+            res[f"decode_B128_ctx2048_split{sl}"] = attn_decode_bench(128, 2048, sl)
     if args.what in ("all", "attn", "decode"):
         res["decode_B512_ctx1100_split256"] = attn_decode_bench(512, 1100, 256)  # the bench's decode step
     if args.what in ("all", "attn"):
