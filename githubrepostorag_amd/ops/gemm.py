@@ -131,8 +131,10 @@ PREFILL_TABLE = Path(__file__).resolve().parents[1] / "tuning" / "gemm_prefill_g
 def _prefill_table() -> dict:
     if _PREFILL["table"] is None:
         t = {}
-        if os.environ.get("GRAG_PREFILL_TABLE", "1") != "0" and PREFILL_TABLE.exists():
-            for k, rows in json.loads(PREFILL_TABLE.read_text())["table"].items():
+        env = os.environ.get("GRAG_PREFILL_TABLE", "1")  # "0": no table; a path: that table (A/B runs)
+        path = Path(env) if env not in ("0", "1") else PREFILL_TABLE
+        if env != "0" and path.exists():
+            for k, rows in json.loads(path.read_text())["table"].items():
                 t[tuple(map(int, k.split(",")))] = ([r[0] for r in rows], rows)
         _PREFILL["table"] = t
     return _PREFILL["table"]
@@ -159,7 +161,9 @@ def prefill_plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int] 
     cand = [rows[min(i, len(rows) - 1)]]
     if 0 < i < len(rows) and ms[i] != M:
         cand.append(rows[i - 1])
-    won = [r for r in cand if r[2] is not None and (silu or r[2] < r[1])]  # SwiGLU: owned at every bucket
+    # SwiGLU: owned at every bucket; plain GEMMs: owned unless the library was clearly faster (OWN_SLACK:
+    # near-ties, within box-to-box spread, go to the owned kernel)
+    won = [r for r in cand if r[2] is not None and (silu or r[2] < r[1] * OWN_SLACK)]
     if not won:
         return plan(M, N, K) if silu else None
     # a bucket with M's own row-tile count ran on the identical tile grid: its schedule transfers as is
@@ -188,6 +192,7 @@ def _tail_grid(Mb: int, M: int, N: int, sk: int) -> int:
     return -min(ncu, max(1, round(-sk * tail / tail_b)))
 
 
+OWN_SLACK = float(os.environ.get("GRAG_OWN_SLACK", "1.03"))
 PREFILL_MIN_M = 257  # above one 256-row tile: the prefill regime (decode batches use plan())
 
 

@@ -18,6 +18,7 @@ latency-bound sections off the engine's stream.
 from __future__ import annotations
 
 import contextlib
+import os
 import functools
 import threading
 
@@ -124,7 +125,8 @@ def _thread_stream(device: torch.device) -> torch.cuda.Stream:
     s = streams.get(device.index)
     if s is None:  # high priority: latency-bound retrieval preempts bulk engine work
         lo, hi = torch.cuda.Stream.priority_range()
-        s = streams[device.index] = torch.cuda.Stream(device=device, priority=min(lo, hi))
+        prio = min(lo, hi) if os.environ.get("GRAG_SIDE_PRIORITY", "high") == "high" else 0
+        s = streams[device.index] = torch.cuda.Stream(device=device, priority=prio)
     return s
 
 
