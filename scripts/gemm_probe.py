@@ -46,6 +46,9 @@ def schedules(M, N, K, silu):
     for sk in (ncu, -ncu, ncu // 2, -ncu // 2, 192, -192, -tail, -2 * tail, -4 * tail):
         if sk and abs(sk) <= ncu and G.sk_ok(M, N, K, 1, sk):
             out.append((1, sk))
+    for s_ in (2, 3, 4):  # K-aligned tail splits, more stream-K workgroups than CUs allowed
+        if tail and G.sk_ok(M, N, K, 1, -s_ * tail):
+            out.append((1, -s_ * tail))
     return list(dict.fromkeys(out))
 
 
@@ -65,7 +68,7 @@ def main():
         M, N, K = int(parts[0]), int(parts[1]), int(parts[2])
         silu = len(parts) > 3 and parts[3] == "silu"
         wbytes = N * K * 2
-        ncopy = max(1, min(8, (600 << 20) // wbytes + 1))
+        ncopy = max(1, min(32, (600 << 20) // wbytes + 1))  # > the 256 MB MALL: cold weights, as in decode
         ws = [(torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16) * 0.05 for _ in range(ncopy)]
         x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
         it = {"i": 0}
