@@ -621,21 +621,53 @@ class LLMEngine:
             self.model.tp.check_health()
         now = time.perf_counter()
         finished = []
-        live = list(seqs)
-        for j in range(K):
-            nxt = []
-            for i, s in enumerate(seqs):
-                if s.finish_reason is not None or s.status != SeqStatus.RUNNING:
-                    continue
+        # fast path for sequences nobody watches per token (no stream consumer, no stop strings / ids) and
+        # no EOS stop in this window: the window's tokens are appended in one extend, and only the token
+        # that ends the sequence goes through _append (finish + detokenize)
+        cols = toks[:K, :n].T.tolist()
+        eos, mml = self._eos, self.cfg.max_model_len
+        slow = []
+        ntok = 0
+        for i, s in enumerate(seqs):
+            p = s.params
+            c = cols[i]
+            if (s.on_token is not None or p.stop or p.stop_token_ids
+                    or (not p.ignore_eos and eos and not eos.isdisjoint(c))):
+                slow.append(i)
+                continue
+            out = s.output_ids
+            room = min(K, p.max_tokens - len(out), mml - len(s.prompt_ids) - len(out))
+            if room <= 0:
+                slow.append(i)
+                continue
+            if s.first_token_time is None:
+                s.first_token_time = now
+            if room < K or room == p.max_tokens - len(out) or room == mml - len(s.prompt_ids) - len(out):
+                out.extend(c[:room - 1])  # the last token of the sequence finishes it through _append
                 s.num_computed = s.total_len
-                if self._append(s, int(toks[j, i]), now):
+                if self._append(s, c[room - 1], now):
                     finished.append(s)
-                else:
-                    nxt.append(s)
-            self.stats["decode_tokens"] += len(live)
-            live = nxt
-            if not live:
-                break
+            else:
+                out.extend(c)
+                s.num_computed = s.total_len - 1
+            ntok += room
+        self.stats["decode_tokens"] += ntok
+        if slow:
+            live = [seqs[i] for i in slow]
+            for j in range(K):
+                nxt = []
+                for s, i in zip(live, slow):
+                    if s.finish_reason is not None or s.status != SeqStatus.RUNNING:
+                        continue
+                    s.num_computed = s.total_len
+                    if self._append(s, int(toks[j, i]), now):
+                        finished.append(s)
+                    else:
+                        nxt.append((s, i))
+                self.stats["decode_tokens"] += len(live)
+                if not nxt:
+                    break
+                live, slow = [s for s, _ in nxt], [i for _, i in nxt]
         self.stats["decode_steps"] += K
         self.stats["decode_s"] += now - t0
         self.stats["host_decode_post_s"] += time.perf_counter() - now

@@ -126,6 +126,9 @@ class Scheduler:
         self.max_model_len = max_model_len
         self.waiting: collections.deque[Sequence] = collections.deque()
         self.running: list[Sequence] = []
+        # running sequences admitted with prompt tokens still to prefill (admission order): the chunked-prefill
+        # pass walks these instead of every running sequence (a 512-row decode step has none)
+        self.prefilling: list[Sequence] = []
         self.free_slots = list(range(max_num_seqs - 1, -1, -1))
         self.lock = threading.Lock()
         self.num_preemptions = 0
@@ -165,6 +168,8 @@ class Scheduler:
         return bool(self.waiting or self.running)
 
     def _finish(self, seq: Sequence) -> None:
+        if seq in self.prefilling:
+            self.prefilling.remove(seq)
         self.kv.free(seq)
         if seq.slot >= 0:
             self.free_slots.append(seq.slot)
@@ -204,6 +209,8 @@ class Scheduler:
             return False
         v = max(victims, key=lambda s: s.arrival)
         self.running.remove(v)
+        if v in self.prefilling:
+            self.prefilling.remove(v)
         self.kv.free(v)
         self.free_slots.append(v.slot)
         v.slot = -1
@@ -219,8 +226,10 @@ class Scheduler:
         with self.lock:
             budget = self.max_num_batched_tokens
             items = []
-            # continue partially prefilled running sequences
-            for seq in self.running:
+            # continue partially prefilled running sequences (the ones whose prompt is done drop out here)
+            if self.prefilling:
+                self.prefilling = [q for q in self.prefilling if q.status == SeqStatus.RUNNING and q.is_prefill]
+            for seq in self.prefilling:
                 if budget <= 0:
                     break
                 out_ids = seq.output_ids
@@ -259,6 +268,7 @@ class Scheduler:
                 seq.slot = self.free_slots.pop()
                 seq.status = SeqStatus.RUNNING
                 self.running.append(seq)
+                self.prefilling.append(seq)
                 admitted.append(("admitted", seq))
                 items.append((seq, seq.num_computed, seq.num_computed + n))
                 budget -= n
@@ -283,10 +293,22 @@ class Scheduler:
                     if len(items) > n_pref:
                         return "mixed", items
                 return "prefill", items
-            # decode every running sequence (one new token each)
+            # decode every running sequence (one new token each).  Fast path: every sequence already holds
+            # the blocks for its next token (the engine reserves a decode window ahead) -> no preemption
+            bs = self.kv.block_size
+            out = []
+            for seq in self.running:
+                out_ids = seq.output_ids
+                L = len(seq.prompt_ids) + len(out_ids)
+                if seq.num_computed < L - (1 if out_ids else 0):
+                    continue
+                if len(seq.blocks) * bs < L:
+                    break
+                out.append((seq, L - 1, L))
+            else:
+                return ("decode", out) if out else (None, [])
             out = []
             preempted = False
-            bs = self.kv.block_size
             running = SeqStatus.RUNNING
             for seq in list(self.running):
                 if seq.status != running:  # preempted earlier in this loop
