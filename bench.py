@@ -59,10 +59,10 @@ def parse():
     ap.add_argument("--nlist", type=int, default=4096)
     ap.add_argument("--nprobe", type=int, default=32)
     ap.add_argument("--batch", type=int, default=64, help="queries per GPU per step")
-    ap.add_argument("--inflight", type=int, default=8,
-                    help="batches' worth of queries in flight (1 = closed batch).  Default 8 = 512 live sequences "
-                         "(the largest decode graph); steady-state sweep: 3 -> 59.8, 4 -> 62.6, 6 -> 61.9, "
-                         "8 -> 67.1 queries/s, p50 TTFT 88 ms at 4-8 (profiles/sweep_inflight_r2.txt)")
+    ap.add_argument("--inflight", type=int, default=16,
+                    help="batches' worth of queries in flight (1 = closed batch).  Default 16 = 1024 live sequences; "
+                         "same-box sweep (profiles/sweep_inflight_r3b.txt): D 8 -> 69.0-69.3, 12 -> 71.4-71.9, "
+                         "16 -> 71.9-72.4 queries/s at the same p50 TTFT (86-87 ms)")
     ap.add_argument("--arrival-groups", type=int, default=8, help="queries of a step arrive in this many groups")
     ap.add_argument("--prompt-len", type=int, default=1024)
     ap.add_argument("--gen-len", type=int, default=128)
