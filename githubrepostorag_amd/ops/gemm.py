@@ -192,7 +192,7 @@ def _tail_grid(Mb: int, M: int, N: int, sk: int) -> int:
     return -min(ncu, max(1, round(-sk * tail / tail_b)))
 
 
-OWN_SLACK = float(os.environ.get("GRAG_OWN_SLACK", "1.03"))
+OWN_SLACK = float(os.environ.get("GRAG_OWN_SLACK", "1.06"))  # beyond the 3-5 % box-to-box spread
 PREFILL_MIN_M = 257  # above one 256-row tile: the prefill regime (decode batches use plan())
 
 
