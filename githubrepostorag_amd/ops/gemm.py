@@ -163,7 +163,7 @@ def prefill_plan(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int] 
         cand.append(rows[i - 1])
     # SwiGLU: owned at every bucket; plain GEMMs: owned unless the library was clearly faster (OWN_SLACK:
     # near-ties, within box-to-box spread, go to the owned kernel)
-    won = [r for r in cand if r[2] is not None and (silu or r[2] < r[1] * OWN_SLACK)]
+    won = [r for r in cand if r[2] is not None and (silu or r[1] is None or r[2] < r[1] * OWN_SLACK)]
     if not won:
         return plan(M, N, K) if silu else None
     # a bucket with M's own row-tile count ran on the identical tile grid: its schedule transfers as is
