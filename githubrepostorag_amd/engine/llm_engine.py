@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from ..ops.attention import KV_TILE, AttnMetadata
-from ..ops.sampling import SamplerState, sample, sample_tp
+from ..ops.sampling import SamplerState, reset_slots, sample, sample_tp
 from .scheduler import KVCacheManager, Scheduler
 from .sequence import Completion, SamplingParams, Sequence, SeqStatus
 from ..utils.gpu_guard import gpu_guard
@@ -235,9 +235,10 @@ class LLMEngine:
             s.finish_time = time.perf_counter()
             self._notify(s, None, True)
             finished.append(s)
-        for s in getattr(self.sched, "last_admitted", []):
-            self.sampler.reset_slot(s.slot, s.params.temperature, s.params.top_p, s.params.top_k,
-                                    s.params.repetition_penalty, s.all_ids, seed=s.params.seed)
+        adm = getattr(self.sched, "last_admitted", [])
+        if adm:
+            reset_slots(self.sampler, [(s.slot, s.params.temperature, s.params.top_p, s.params.top_k,
+                                        s.params.repetition_penalty, s.all_ids, s.params.seed) for s in adm])
         self.stats["host_sched_s"] += time.perf_counter() - th
         if not items:
             return finished

@@ -67,6 +67,39 @@ class SamplerState:
             mark_seen(self, toks, torch.full_like(toks, slot))
 
 
+def reset_slots(state: SamplerState, entries) -> None:
+    """``SamplerState.reset_slot`` for every sequence admitted in one engine step, batched: one upload of the
+    sampling parameters, one index_copy per field, one seen-bit clear and one seen-bit scatter over all the
+    prompts (a per-sequence reset costs about eight small launches each).
+    entries: (slot, temperature, top_p, top_k, penalty, prompt_ids, seed) per sequence, distinct slots."""
+    if len(entries) <= 1 or not state.temperature.is_cuda:
+        for e in entries:
+            state.reset_slot(*e)
+        return
+    dev = state.device
+    fl = torch.tensor([[float(e[1]), float(e[2]), float(e[4])] for e in entries], dtype=torch.float32)
+    it = torch.tensor([[e[0], int(e[3]), int(e[6]) if e[6] is not None else 0] for e in entries], dtype=torch.int64)
+    fl, it = fl.to(dev), it.to(dev)
+    idx = it[:, 0]
+    state.temperature.index_copy_(0, idx, fl[:, 0])
+    state.top_p.index_copy_(0, idx, fl[:, 1])
+    state.penalty.index_copy_(0, idx, fl[:, 2])
+    state.top_k.index_copy_(0, idx, it[:, 1].to(torch.int32))
+    state.rng.index_copy_(0, idx, it[:, 2])
+    state.seen.index_fill_(0, idx, 0)
+    toks, sl = [], []
+    for slot, temperature, top_p, top_k, penalty, prompt_ids, _ in entries:
+        sampled = temperature > 0
+        state._uses_topk[slot] = sampled and 0 < int(top_k) < state.vocab
+        state._uses_topp[slot] = sampled and float(top_p) < 1.0
+        if penalty != 1.0 and len(prompt_ids):
+            toks.extend(prompt_ids)
+            sl.extend([slot] * len(prompt_ids))
+    if toks:
+        t = torch.tensor([toks, sl], dtype=torch.int32).to(dev)
+        mark_seen(state, t[0], t[1])
+
+
 def mark_seen(state: SamplerState, tokens: torch.Tensor, slots: torch.Tensor) -> None:
     if not tokens.is_cuda:
         t = tokens.long()

@@ -509,3 +509,23 @@ def test_sampler_vocab_parallel_matches_full(dev, world):
         greedy = torch.arange(B) % 6 == 0
         assert torch.equal(outs[0][k][greedy], ref[k][greedy])
         assert int((outs[0][k] == ref[k]).sum()) >= B - 1, (outs[0][k], ref[k])
+
+
+def test_sampler_reset_slots_batched_matches_per_slot(dev):
+    """The engine's batched admission reset (one upload + index_copy per field + one seen-bit scatter) leaves
+    the same sampler state as one reset_slot per sequence."""
+    from githubrepostorag_amd.ops.sampling import SamplerState, reset_slots
+
+    V = 152064
+    entries = [(3, 0.4, 0.8, 0, 1.2, list(range(100, 1124)), None), (7, 0.0, 1.0, 50, 1.0, [5, 6], 11),
+               (0, 0.7, 0.9, 40, 1.1, [1, 2, 3, 152063], 5)]
+    a, b = SamplerState(8, V, dev, seed=1), SamplerState(8, V, dev, seed=1)
+    for s in (a, b):  # dirty state from a previous occupant
+        s.seen.fill_(-1)
+        s.temperature.fill_(9.0)
+    reset_slots(a, entries)
+    for e in entries:
+        b.reset_slot(*e)
+    for name in ("temperature", "top_p", "top_k", "penalty", "rng", "seen"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert a._uses_topk == b._uses_topk and a._uses_topp == b._uses_topp
