@@ -630,6 +630,8 @@ class LLMEngine:
         slow = []
         ntok = 0
         for i, s in enumerate(seqs):
+            if s.finish_reason is not None or s.status != SeqStatus.RUNNING:
+                continue
             p = s.params
             c = cols[i]
             if (s.on_token is not None or p.stop or p.stop_token_ids
