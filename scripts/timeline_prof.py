@@ -28,15 +28,23 @@ def main():
     ap.add_argument("--last-ms", type=float, default=2400.0)
     ap.add_argument("--gap-us", type=float, default=30.0)
     ap.add_argument("--top", type=int, default=10)
+    ap.add_argument("--marker", default=None,
+                    help="kernel-name substring of a marker launched at the start and the end of the window "
+                         "(bench.py GRAG_TRACE_MARK=1: a float64 fill); overrides --last-ms")
     a = ap.parse_args()
     ev = []
     with open(a.trace) as f:
         for r in csv.DictReader(f):
             ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     ev.sort()
-    t_end = max(e[1] for e in ev)
-    t0 = t_end - int(a.last_ms * 1e6)
-    ev = [e for e in ev if e[0] >= t0]
+    marks = [e for e in ev if a.marker and a.marker in e[2]]
+    if len(marks) >= 2:
+        t0, t_end = marks[0][1], marks[-1][0]
+        ev = [e for e in ev if e[0] >= t0 and e[1] <= t_end and a.marker not in e[2]]
+    else:
+        t_end = max(e[1] for e in ev)
+        t0 = t_end - int(a.last_ms * 1e6)
+        ev = [e for e in ev if e[0] >= t0]
     busy = 0
     cur_s, cur_e = ev[0][0], ev[0][1]
     gaps = []
@@ -52,7 +60,7 @@ def main():
             cur_e = max(cur_e, e)
         prev_name = n if e >= cur_e else prev_name
     busy += cur_e - cur_s
-    wall = t_end - ev[0][0]
+    wall = (t_end - t0) if len(marks) >= 2 else (t_end - ev[0][0])
     print(f"window {wall / 1e6:.1f} ms, kernels {len(ev)}, GPU busy {busy / 1e6:.1f} ms "
           f"({100 * busy / wall:.1f} %), idle {(wall - busy) / 1e6:.1f} ms")
     for lo, hi in ((0, 5), (5, 30), (30, 200), (200, 2000), (2000, 1e12)):
