@@ -301,10 +301,16 @@ class LLMEngine:
             slots.append(self._slots_of(s, a, b))
             q_start.append(q_start[-1] + (b - a))
             ctx.append(b)
+        # rows to sample: the last token of every chunk that completes its prompt.  Uploaded with the step's
+        # inputs: a separate pageable upload after the forward is a synchronous copy queued behind it, which
+        # held the host until the forward finished and left the GPU idle while the LM head and sampler launched
+        samp = [i for i, (s, a, b) in enumerate(items) if b == s.total_len]
         width = max(len(s.blocks) for s in seqs)
         packed = np.concatenate([np.concatenate(ids), np.concatenate(pos), np.concatenate(slots),
                                  np.asarray(q_start, dtype=np.int32), np.asarray(ctx, dtype=np.int32),
-                                 self._block_table(seqs, width).reshape(-1)])
+                                 self._block_table(seqs, width).reshape(-1),
+                                 np.asarray([q_start[i + 1] - 1 for i in samp], dtype=np.int32),
+                                 np.asarray([items[i][0].slot for i in samp], dtype=np.int32)])
         dev = self._to_dev(packed)
         th = time.perf_counter()
         self.stats["host_prefill_prep_s"] += th - t0
@@ -315,56 +321,33 @@ class LLMEngine:
         d_slot = dev[o:o + T]; o += T
         d_qs = dev[o:o + n + 1]; o += n + 1
         d_ctx = dev[o:o + n]; o += n
-        d_bt = dev[o:o + n * width].view(n, width)
+        d_bt = dev[o:o + n * width].view(n, width); o += n * width
+        d_rows = dev[o:o + len(samp)]; o += len(samp)
+        d_samp_slots = dev[o:o + len(samp)]
         meta = AttnMetadata(q_start=d_qs, ctx_len=d_ctx, block_tables=d_bt, slot_mapping=d_slot,
                             max_q_len=max(b - a for _, a, b in items), num_seqs=n, num_tokens=T)
-        # mixed step: trailing one-token decode rows (scheduler.schedule); on the
-        # GPU their attention runs on the split-KV decode kernel
-        n_pref = next((i for i, (s, a, b) in enumerate(items) if b - a == 1 and s.output_ids and a == s.total_len - 1),
-                      n)
-        n_dec = n - n_pref
-        if n_dec and n_pref and self.on_gpu:
-            Tp = q_start[n_pref]
-            split_len = _split_len_for(n_dec)
-            nsplit = max(1, -(-max(ctx[n_pref:]) // split_len))
-            hq, dh = self.model.hq, self.model.head_dim
-            meta.extra["decode_rows"] = (Tp, AttnMetadata(
-                q_start=d_qs[n_pref:] - Tp, ctx_len=d_ctx[n_pref:], block_tables=d_bt[n_pref:],
-                slot_mapping=d_slot[Tp:], max_q_len=1, num_seqs=n_dec, num_tokens=n_dec, is_decode=True,
-                num_splits=nsplit, split_len=split_len, part_o=self._part_o[: nsplit * n_dec * hq * dh],
-                part_ml=self._part_ml[: nsplit * n_dec * hq * 2]))
-            meta.num_seqs, meta.num_tokens = n_pref, Tp
-            meta.max_q_len = max(b - a for _, a, b in items[:n_pref])
         hidden = self.model.forward(d_ids, d_pos, meta, self.kv_caches)
+        tp = self.model.tp
+        if samp:  # LM head + sampler queued right behind the forward
+            toks_d = self._sample(hidden.index_select(0, d_rows), d_samp_slots)
+            tp.stage_health()
         t1 = time.perf_counter()
         self.stats["host_prefill_launch_s"] += t1 - th
-        # sample for sequences whose prompt is now complete (first token) and for decode rows (next token)
-        samp_rows, samp_seqs = [], []
-        for i, (s, a, b) in enumerate(items):
+        for s, a, b in items:  # host bookkeeping while the GPU runs
             s.num_computed = b
             self.kv.register_full_blocks(s)
-            if b == s.total_len:
-                samp_rows.append(q_start[i + 1] - 1)
-                samp_seqs.append(s)
         finished = []
-        if samp_seqs:
-            rows = torch.as_tensor(samp_rows, dtype=torch.long, device=self.device)
-            slot_t = self._to_dev(np.asarray([s.slot for s in samp_seqs], dtype=np.int32))
-            tp = self.model.tp
-            toks_d = self._sample(hidden.index_select(0, rows), slot_t)
-            tp.stage_health()
+        if samp:
             toks = self._read_host(toks_d).reshape(-1).tolist()
             tp.check_health()
             now = time.perf_counter()
             self.stats["host_prefill_sample_s"] += now - t1
-            for s, t in zip(samp_seqs, toks):
+            for i, t in zip(samp, toks):
+                s = items[i][0]
                 if self._append(s, int(t), now):
                     finished.append(s)
             self.stats["host_prefill_post_s"] += time.perf_counter() - now
-        self.stats["prefill_tokens"] += T - n_dec
-        if n_dec:
-            self.stats["decode_tokens"] += n_dec
-            self.stats["mixed_steps"] += 1
+        self.stats["prefill_tokens"] += T
         self.stats["prefill_s"] += time.perf_counter() - t0
         return finished
 

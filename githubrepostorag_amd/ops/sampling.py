@@ -79,7 +79,7 @@ def reset_slots(state: SamplerState, entries) -> None:
     dev = state.device
     fl = torch.tensor([[float(e[1]), float(e[2]), float(e[4])] for e in entries], dtype=torch.float32)
     it = torch.tensor([[e[0], int(e[3]), int(e[6]) if e[6] is not None else 0] for e in entries], dtype=torch.int64)
-    fl, it = fl.to(dev), it.to(dev)
+    fl, it = fl.pin_memory().to(dev, non_blocking=True), it.pin_memory().to(dev, non_blocking=True)
     idx = it[:, 0]
     state.temperature.index_copy_(0, idx, fl[:, 0])
     state.top_p.index_copy_(0, idx, fl[:, 1])
@@ -96,7 +96,7 @@ def reset_slots(state: SamplerState, entries) -> None:
             toks.extend(prompt_ids)
             sl.extend([slot] * len(prompt_ids))
     if toks:
-        t = torch.tensor([toks, sl], dtype=torch.int32).to(dev)
+        t = torch.tensor([toks, sl], dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
         mark_seen(state, t[0], t[1])
 
 
