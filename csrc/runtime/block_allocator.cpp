@@ -116,6 +116,29 @@ uint64_t grag_hash_block(uint64_t parent, const int32_t* toks, int n) {
   return h ? h : 1;
 }
 
+// Chained hashes of `nblocks` consecutive full blocks of `bs` tokens (one call for a prompt's blocks).
+void grag_hash_blocks(uint64_t parent, const int32_t* toks, int nblocks, int bs, uint64_t* out) {
+  for (int b = 0; b < nblocks; ++b) {
+    parent = grag_hash_block(parent, toks + (size_t)b * bs, bs);
+    out[b] = parent;
+  }
+}
+
+// grag_alloc_register for n (block, hash) pairs under one lock.
+void grag_alloc_register_many(void* a, const int32_t* blocks, const uint64_t* hashes, int n) {
+  auto* al = static_cast<Allocator*>(a);
+  std::lock_guard<std::mutex> g(al->mu);
+  for (int i = 0; i < n; ++i) {
+    const int block = blocks[i];
+    const uint64_t h = hashes[i];
+    if (block < 0 || block >= al->num_blocks || h == 0) continue;
+    if (al->by_hash.count(h)) continue;
+    if (al->hash_of[block]) continue;
+    al->hash_of[block] = h;
+    al->by_hash[h] = block;
+  }
+}
+
 // Look up the longest cached prefix of `ntok` tokens. Fills out[] with the
 // reused block ids (refcount taken) and returns how many full blocks matched.
 int grag_alloc_match_prefix(void* a, const int32_t* toks, int ntok, int32_t* out, uint64_t* hashes_out) {

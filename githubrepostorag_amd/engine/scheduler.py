@@ -96,16 +96,18 @@ class KVCacheManager:
         if not self.prefix_caching:
             return
         full = min(seq.num_computed, len(seq.prompt_ids)) // self.block_size
-        if len(seq.block_hashes) >= full:
+        have = len(seq.block_hashes)
+        if have >= full:
             return
-        ids = seq.prompt_ids
+        bs = self.block_size
         parent = seq.block_hashes[-1] if seq.block_hashes else 0
-        for b in range(len(seq.block_hashes), full):
-            chunk = np.asarray(ids[b * self.block_size:(b + 1) * self.block_size], dtype=np.int32)
-            h = int(rt().grag_hash_block(parent, chunk.ctypes.data, self.block_size))
-            rt().grag_alloc_register(self._h, seq.blocks[b], h)
-            seq.block_hashes.append(h)
-            parent = h
+        n = full - have  # one hashing call and one registration call for all the newly full blocks
+        toks = np.asarray(seq.prompt_ids[have * bs:full * bs], dtype=np.int32)
+        hashes = np.empty(n, dtype=np.uint64)
+        rt().grag_hash_blocks(parent, toks.ctypes.data, n, bs, hashes.ctypes.data)
+        blocks = np.asarray(seq.blocks[have:full], dtype=np.int32)
+        rt().grag_alloc_register_many(self._h, blocks.ctypes.data, hashes.ctypes.data, n)
+        seq.block_hashes.extend(int(h) for h in hashes)
 
     def free(self, seq: Sequence) -> None:
         if seq.blocks:
@@ -158,10 +160,9 @@ class Scheduler:
                 seq.prefix_sig = 0
             else:
                 toks = np.asarray(seq.prompt_ids[:n], dtype=np.int32)
-                h = 0
-                for b in range(self.SIG_BLOCKS):
-                    h = int(rt().grag_hash_block(h, toks[b * bs:].ctypes.data, bs))
-                seq.prefix_sig = h
+                hs = np.empty(self.SIG_BLOCKS, dtype=np.uint64)
+                rt().grag_hash_blocks(0, toks.ctypes.data, self.SIG_BLOCKS, bs, hs.ctypes.data)
+                seq.prefix_sig = int(hs[-1])
         return seq.prefix_sig
 
     def has_work(self) -> bool:
