@@ -485,10 +485,13 @@ class LLMEngine:
             # object changed, and the batch is one row gather
             tab, owner, have = self._slot_block_table()
             tw = tab.shape[1]
-            for s in seqs:
+            rows_l, ids_l, len_l = [0] * n, [0] * n, [0] * n  # one pass over the rows (1024-row steps)
+            for i, s in enumerate(seqs):
                 r = s.slot
                 b = s.blocks
-                nb = min(len(b), tw)
+                nb = len(b)
+                if nb > tw:
+                    nb = tw
                 h = have[r]
                 if owner[r] is not b or h > nb:
                     tab[r, :nb] = b[:nb]
@@ -497,11 +500,16 @@ class LLMEngine:
                 elif h < nb:
                     tab[r, h:nb] = b[h:nb]
                     have[r] = nb
-            rows = np.fromiter((s.slot for s in seqs), dtype=np.int64, count=n)
+                out = s.output_ids
+                pr = s.prompt_ids
+                rows_l[i] = r
+                ids_l[i] = out[-1] if out else pr[-1]
+                len_l[i] = len(pr) + len(out)
+            rows = np.asarray(rows_l, dtype=np.int64)
             bt[:n] = tab[rows, :width] if width <= tw else np.pad(tab[rows], ((0, 0), (0, width - tw)))
-            ids[:n] = [self._last_id(s) for s in seqs]
-            sl[:n] = [s.slot for s in seqs]
-            L = np.fromiter((s.total_len for s in seqs), dtype=np.int64, count=n)
+            ids[:n] = ids_l
+            sl[:n] = rows_l
+            L = np.asarray(len_l, dtype=np.int64)
             p = L[None, :] - 1 + np.arange(K, dtype=np.int64)[:, None]  # [K, n]
             pos[:, :n] = p
             ctx[:, :n] = p + 1
