@@ -67,6 +67,15 @@ with torch.inference_mode():
     for _ in range(3):
         g.replay()
     torch.cuda.synchronize()
+    import time as _t
+    host = []
+    for _ in range(10):  # host cost of one replay call (hipGraphLaunch), GPU idle before it
+        torch.cuda.synchronize()
+        h0 = _t.perf_counter()
+        g.replay()
+        host.append((_t.perf_counter() - h0) * 1e3)
+    torch.cuda.synchronize()
+    print(f"graph replay host call: median {sorted(host)[len(host) // 2]:.3f} ms (min {min(host):.3f})")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(a.reps):
