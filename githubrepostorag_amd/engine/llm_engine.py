@@ -620,8 +620,9 @@ class LLMEngine:
         eos, mml = self._eos, self.cfg.max_model_len
         slow = []
         ntok = 0
+        running = SeqStatus.RUNNING
         for i, s in enumerate(seqs):
-            if s.finish_reason is not None or s.status != SeqStatus.RUNNING:
+            if s.finish_reason is not None or s.status is not running:
                 continue
             p = s.params
             c = cols[i]
@@ -630,21 +631,26 @@ class LLMEngine:
                 slow.append(i)
                 continue
             out = s.output_ids
-            room = min(K, p.max_tokens - len(out), mml - len(s.prompt_ids) - len(out))
-            if room <= 0:
+            lo = len(out)
+            L = len(s.prompt_ids) + lo
+            left = p.max_tokens - lo  # tokens until max_tokens / max_model_len end the sequence
+            if mml - L < left:
+                left = mml - L
+            if left <= 0:
                 slow.append(i)
                 continue
             if s.first_token_time is None:
                 s.first_token_time = now
-            if room < K or room == p.max_tokens - len(out) or room == mml - len(s.prompt_ids) - len(out):
-                out.extend(c[:room - 1])  # the last token of the sequence finishes it through _append
-                s.num_computed = s.total_len
-                if self._append(s, c[room - 1], now):
+            if left <= K:  # the window's token `left` ends the sequence: it goes through _append
+                out.extend(c[:left - 1])
+                s.num_computed = L + left - 1
+                if self._append(s, c[left - 1], now):
                     finished.append(s)
+                ntok += left
             else:
                 out.extend(c)
-                s.num_computed = s.total_len - 1
-            ntok += room
+                s.num_computed = L + K - 1
+                ntok += K
         self.stats["decode_tokens"] += ntok
         if slow:
             live = [seqs[i] for i in slow]
