@@ -1,6 +1,7 @@
 """Fused sampler op + persistent per-slot sampler state."""
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from ._lib import call, lib, ptr
@@ -87,16 +88,21 @@ def reset_slots(state: SamplerState, entries) -> None:
     state.top_k.index_copy_(0, idx, it[:, 1].to(torch.int32))
     state.rng.index_copy_(0, idx, it[:, 2])
     state.seen.index_fill_(0, idx, 0)
-    toks, sl = [], []
+    toks, sl, cnt = [], [], []
     for slot, temperature, top_p, top_k, penalty, prompt_ids, _ in entries:
         sampled = temperature > 0
         state._uses_topk[slot] = sampled and 0 < int(top_k) < state.vocab
         state._uses_topp[slot] = sampled and float(top_p) < 1.0
         if penalty != 1.0 and len(prompt_ids):
-            toks.extend(prompt_ids)
-            sl.extend([slot] * len(prompt_ids))
+            toks.append(np.asarray(prompt_ids, dtype=np.int32))
+            sl.append(slot)
+            cnt.append(len(prompt_ids))
     if toks:
-        t = torch.tensor([toks, sl], dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
+        # packed with numpy: a [2, N] list -> torch.tensor costs ~3x more at N = 8K prompt tokens
+        packed = np.empty((2, sum(cnt)), dtype=np.int32)
+        packed[0] = np.concatenate(toks)
+        packed[1] = np.repeat(np.asarray(sl, dtype=np.int32), cnt)
+        t = torch.from_numpy(packed).pin_memory().to(dev, non_blocking=True)
         mark_seen(state, t[0], t[1])
 
 
