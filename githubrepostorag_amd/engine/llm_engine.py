@@ -563,6 +563,8 @@ class LLMEngine:
         """Largest power-of-two window <= decode_window that no sequence's
         max_tokens / max_model_len cuts short and whose KV blocks fit."""
         K = max(1, self.cfg.decode_window if cap is None else min(cap, self.cfg.decode_window))
+        if K == 1:  # nothing to cut short (a 1-step window is what the scheduler already reserved for)
+            return 1
         for s in seqs:
             K = min(K, s.params.max_tokens - len(s.output_ids), self.cfg.max_model_len - s.total_len)
         K = max(1, K)
@@ -581,7 +583,7 @@ class LLMEngine:
         # replicated scheduling makes every TP rank pick, capture and replay the same graph in lockstep
         use_graph = self.on_gpu and self.cfg.use_cuda_graph and n <= max(self.cfg.graph_batch_sizes)
         K = self._window(seqs, max_window) if use_graph else 1
-        max_ctx = max(s.total_len for s in seqs) + K - 1
+        max_ctx = max(len(s.prompt_ids) + len(s.output_ids) for s in seqs) + K - 1
         if use_graph:
             width = self.max_blocks_per_seq
             B = next(b for b in self.cfg.graph_batch_sizes if b >= n)
