@@ -294,16 +294,19 @@ class Scheduler:
                     if len(items) > n_pref:
                         return "mixed", items
                 return "prefill", items
-            # decode every running sequence (one new token each).  Fast path: every sequence already holds
-            # the blocks for its next token (the engine reserves a decode window ahead) -> no preemption
+            # decode every running sequence (one new token each).  Fast path: every sequence holds, or can
+            # take from the free list, the blocks for its next token -> no preemption (at 1-step windows about
+            # 1/16 of the rows cross a block boundary every step; ensure is idempotent, so the slow path
+            # below redoes the whole batch if the free list runs dry)
             bs = self.kv.block_size
+            ensure = self.kv.ensure
             out = []
             for seq in self.running:
                 out_ids = seq.output_ids
                 L = len(seq.prompt_ids) + len(out_ids)
                 if seq.num_computed < L - (1 if out_ids else 0):
                     continue
-                if len(seq.blocks) * bs < L:
+                if len(seq.blocks) * bs < L and not ensure(seq, L):
                     break
                 out.append((seq, L - 1, L))
             else:
