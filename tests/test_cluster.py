@@ -79,6 +79,11 @@ def test_front_door_dispatches_over_replicas(cluster):
         assert "Widgets are handled" in final["answer"]
         pids.add(final["answer"].split("pid ")[1].rstrip(")."))
     assert len(pids) == 2, "both replicas must have served jobs"
+    # the SSE "final" event is forwarded from the replica before the hub's queue task resumes and records
+    # the job result: wait for the bookkeeping instead of reading it in the same instant
+    deadline = time.time() + 10
+    while time.time() < deadline and any("result" not in hub.queue.results.get(j, {}) for j in ids):
+        time.sleep(0.05)
     assert sum(hub.queue.results[j]["result"]["replica"] in (0, 1) for j in ids) == 6
     r = client.get("/health")
     assert r.status_code == 200 and r.json()["status"] == "UP", r.json()

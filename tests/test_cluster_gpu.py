@@ -57,6 +57,9 @@ def test_front_door_over_gpu_replicas():
             final = ev[-1][1]
             assert not final.get("error"), final
             assert isinstance(final.get("answer"), str)
+            deadline = time.time() + 10  # the hub records the result just after the forwarded "final" event
+            while time.time() < deadline and "result" not in hub.queue.results.get(jid, {}):
+                time.sleep(0.05)
             replicas.add(hub.queue.results[jid]["result"]["replica"])
         assert replicas == {0, 1}, "both GPU replicas must have served jobs"
         h = client.get("/health").json()
