@@ -609,7 +609,7 @@ GRAG_API int grag_sample_tp(int stage, const void* logits, int dtype, int ld, in
                             int j, float* gmax, float* ghist, float* pair_out, const float* pairs_max,
                             const float* pairs_gum, int W, hipStream_t stream) {
   if (B <= 0) return 0;
-  if (ld % 8 != 0 || ws == nullptr || (v0 & 7) != 0) return (int)hipErrorInvalidValue;
+  if (ld % 8 != 0 || ws == nullptr || (v0 & 7) != 0 || V < 0) return (int)hipErrorInvalidValue;
   Params p{};
   p.logits = logits;
   p.ld = ld;

@@ -19,15 +19,25 @@ each replica keeps 1/N of every scope table and every read fans out:
                             so ingest on any replica writes each row once.
 
 The local shard's search runs while the remote ones are in flight.  The
-transport is pluggable: ``service/cluster.py`` routes rounds through the
-front door's replica hub (authenticated local sockets, replica loss turns
-into an empty partial, never a hang); ``LocalShardTransport`` wires N stores
-in one process (tests, rehearsals).  Merged results equal a flat store's up to
-score ties (tests/test_sharded_store.py)."""
+transport is pluggable: ``service/mesh.py`` (the serving default) runs every
+round replica-to-replica over direct authenticated sockets with coalesced
+requests and acknowledged writes; ``service/cluster.py`` HubShardTransport
+relays rounds through the front door's hub (``GRAG_SHARD_TRANSPORT=hub``);
+``LocalShardTransport`` wires N stores in one process (tests, rehearsals).
+Merged results equal a flat store's up to score ties
+(tests/test_sharded_store.py).
+
+A round that did not hear from every shard is DEGRADED (its answer lacks the
+missing shards' rows): it is counted in the table's stats, the
+``rag_index_degraded_rounds_total`` metric and the calling thread's
+``round_health()`` record, which the worker reports in the job's
+``retrieval`` event (``degraded``, ``missing_shards``)."""
 from __future__ import annotations
 
 import concurrent.futures as cf
+import contextlib
 import logging
+import threading
 import zlib
 
 import numpy as np
@@ -85,6 +95,32 @@ def merge_hits(parts: list[list[list[Hit]]], k: int) -> list[list[Hit]]:
     return out
 
 
+# ---------------------------------------------------------------------- round health
+_TLS = threading.local()
+
+
+@contextlib.contextmanager
+def round_health():
+    """Collect the shard rounds the CALLING thread runs inside the block:
+    ``{"rounds", "degraded_rounds", "missing_shards"}`` (a job's agent runs on one thread)."""
+    rec = {"rounds": 0, "degraded_rounds": 0, "missing_shards": set()}
+    prev = getattr(_TLS, "rec", None)
+    _TLS.rec = rec
+    try:
+        yield rec
+    finally:
+        _TLS.rec = prev
+
+
+def _note_round(missing) -> None:
+    rec = getattr(_TLS, "rec", None)
+    if rec is not None:
+        rec["rounds"] += 1
+        if missing:
+            rec["degraded_rounds"] += 1
+            rec["missing_shards"].update(missing)
+
+
 # ---------------------------------------------------------------------- transports
 class LocalShardTransport:
     """N shards in one process: a round calls ``execute`` on every other shard's
@@ -99,8 +135,8 @@ class LocalShardTransport:
     def fanout(self, origin: int, scope: str, op: str, payload, timeout: float = 60.0) -> list:
         return [execute(st, scope, op, payload) for r, st in sorted(self.stores.items()) if r != origin]
 
-    def write(self, origin: int, owner: int, scope: str, op: str, payload) -> None:
-        execute(self.stores[owner], scope, op, payload)
+    def write(self, origin: int, owner: int, scope: str, op: str, payload):
+        return execute(self.stores[owner], scope, op, payload)
 
 
 # ---------------------------------------------------------------------- facade
@@ -112,7 +148,7 @@ class ShardedTable:
                  timeout: float = 60.0):
         self.local, self.scope, self.rank, self.nshards = local, scope, rank, nshards
         self.transport, self.owner, self.timeout = transport, owner, timeout
-        self.stats = {"rounds": 0, "remote_parts": 0}
+        self.stats = {"rounds": 0, "remote_parts": 0, "degraded_rounds": 0}
         self._pool = cf.ThreadPoolExecutor(32, thread_name_prefix=f"shard-{scope}")  # rounds wait on replies
 
     # attributes the retrievers / health read straight from the local shard
@@ -125,11 +161,20 @@ class ShardedTable:
         mine = local_fn()
         try:
             remote = fut.result(self.timeout + 5.0)
+            missing = list(getattr(remote, "missing", ()))
         except Exception:
             log.exception("sharded %s round on %s failed; answering from the local shard", op, self.scope)
-            remote = []
+            remote, missing = [], [r for r in range(self.nshards) if r != self.rank]
         self.stats["rounds"] += 1
         self.stats["remote_parts"] += len(remote)
+        if missing:
+            # recall dropped by len(missing)/N for this answer: visible, never silent
+            self.stats["degraded_rounds"] += 1
+            from ..service import metrics as M
+
+            M.INDEX_DEGRADED_ROUNDS.labels(table=self.scope).inc()
+            log.warning("sharded %s round on %s: no answer from shard(s) %s (degraded)", op, self.scope, missing)
+        _note_round(missing)
         return mine, remote
 
     def search(self, qvecs: torch.Tensor, k: int, flt: dict | None = None, qpred=None) -> list[list[Hit]]:
@@ -168,7 +213,9 @@ class ShardedTable:
                 new += self.local.upsert(ids, tx, vectors.index_select(0, sel), md)
             else:
                 v = vectors.index_select(0, sel).detach().float().cpu().numpy()
-                self.transport.write(self.rank, o, self.scope, "upsert", (ids, tx, v, md))
+                # acknowledged transports (mesh, local) return the owner's count or raise
+                r = self.transport.write(self.rank, o, self.scope, "upsert", (ids, tx, v, md))
+                new += int(r) if isinstance(r, int) else 0
         return new
 
     def delete(self, row_ids) -> int:
@@ -179,7 +226,8 @@ class ShardedTable:
             if o == self.rank:
                 n += self.local.delete(ids)
             else:
-                self.transport.write(self.rank, o, self.scope, "delete", ids)
+                r = self.transport.write(self.rank, o, self.scope, "delete", ids)
+                n += int(r) if isinstance(r, int) else 0
         return n
 
     def close(self) -> None:

@@ -679,6 +679,11 @@ class VectorTable:
                     extra = m
                     preds = preds[:4]
                 bitmap = self.live if extra is None else _and_bitmap(self.live, extra)
+                if qpred is not None and qpred[0] and isinstance(qpred[0][0], str):
+                    # per-query predicates by column NAME (search_pairs): the column tensors are taken
+                    # here, under the lock, so a concurrent upsert's _grow cannot swap them between the
+                    # lookup and the scan (a stale, shorter column read up to the new self.n)
+                    qpred = ([self.columns[f] for f in qpred[0]], qpred[1], qpred[2])
                 q = qvecs.to(self.device, self.dtype)
                 kk = min(32, k + (8 if checks else 0))
                 scores, ids = self._scan(q, kk, preds, bitmap, qpred)
@@ -708,28 +713,31 @@ class VectorTable:
         code`` test); unindexed fields fall back to one filtered search each.
         Pairs whose value this table has never stored return no rows."""
         q = q.reshape(1, -1)
-        cols: list[tuple[str, torch.Tensor]] = []
+        cols: list[str] = []
         col_idx: dict[str, int] = {}
         sel, vals, slot = [], [], []
         host_pairs = []
         out: list[list[Hit]] = [[] for _ in pairs]
-        for j, (f, v) in enumerate(pairs):
-            if f in FILTER_FIELDS:
-                code = self.dicts[f].get(str(v))
-                if code is None:  # value never seen in this table: no row can match
-                    continue
-                if f not in col_idx:
-                    col_idx[f] = len(cols)
-                    cols.append((f, self.columns[f]))
-                sel.append(col_idx[f])
-                vals.append(code)
-                slot.append(j)
-            else:
-                host_pairs.append(j)
+        with self.lock:  # codes are stable once assigned; read them consistently with the columns' state
+            for j, (f, v) in enumerate(pairs):
+                if f in FILTER_FIELDS:
+                    code = self.dicts[f].get(str(v))
+                    if code is None:  # value never seen in this table: no row can match
+                        continue
+                    if f not in col_idx:
+                        col_idx[f] = len(cols)
+                        cols.append(f)
+                    sel.append(col_idx[f])
+                    vals.append(code)
+                    slot.append(j)
+                else:
+                    host_pairs.append(j)
         if slot:
             Q = q.expand(len(slot), -1).contiguous()
             dev = self.device
-            qpred = ([c for _, c in cols], torch.tensor(sel, dtype=torch.int32, device=dev),
+            # columns by name: search() takes the tensors under the table lock (a concurrent upsert may
+            # grow and replace them until then)
+            qpred = (cols, torch.tensor(sel, dtype=torch.int32, device=dev),
                      torch.tensor(vals, dtype=torch.int32, device=dev))
             for j, hits in zip(slot, self.search(Q, k, base_filter, qpred=qpred)):
                 out[j] = hits

@@ -356,7 +356,9 @@ def sample_tp(logits: torch.Tensor, state: SamplerState, slots: torch.Tensor, gr
     if not logits.is_cuda:
         return sample_tp_ref(logits, state, slots, group, v0, out)
     B, Vg = logits.shape[0], state.vocab
-    Vl = min(logits.shape[1], Vg - v0)
+    # a rank whose (8-aligned) vocab shard starts past the vocabulary holds no real columns: V = 0 makes
+    # the kernel emit (-inf, sentinel) pairs and empty histograms for it
+    Vl = max(0, min(logits.shape[1], Vg - v0))
     if out is None:
         out = torch.empty(B, dtype=torch.int32, device=logits.device)
     dev = logits.device

@@ -22,22 +22,26 @@ replica that disconnects fails its in-flight jobs (``error`` + ``final``) and
 the hub stops dispatching to it.
 
 The index (INDEX_SHARDING, default ``shard``): each replica holds 1/N of every
-scope table (index/sharded_store.py, rows owned by crc32(row_id) mod N) and
-the hub routes the shard rounds: a replica's search / traversal round is
-fanned out to every other live replica (C4), their per-shard top-k lists are
-routed back to it (C3) and merged there with its own shard's; an ingest write
-goes to the owning replica only.  A replica lost mid-round answers with an
-empty part (its rows are missing from that answer, nothing hangs).
+scope table (index/sharded_store.py, rows owned by crc32(row_id) mod N).  A
+replica's search / traversal round goes straight to every other replica over
+the peer mesh (service/mesh.py; C4), their per-shard top-k lists come back on
+the same connections (C3) and are merged there with its own shard's; an
+ingest write goes to the owning replica only and is acknowledged.  The hub
+only distributes the peer table (``("peers", {rank: address})``) when
+membership changes.  ``GRAG_SHARD_TRANSPORT=hub`` keeps the round-3 relay
+through the hub.  A replica lost mid-round is reported as a missing shard
+(``degraded`` retrieval; nothing hangs).
 ``INDEX_SHARDING=mirror`` keeps the round-2 mode: full copies, every ingest
 write broadcast to every replica.
 
 Wire messages (pickled tuples over the authenticated socket, our own processes
 only):
-  replica -> hub: ("hello", rank, capacity, info) | ("event", job, name, data)
+  replica -> hub: ("hello", rank, capacity, info{..., mesh: address}) | ("event", job, name, data)
                   | ("health", info) | ("upsert", table, payload)          [mirror]
                   | ("shard_req", req, scope, op, payload)                 [shard round]
                   | ("shard_res", origin, req, result) | ("shard_write", owner, scope, op, payload)
   hub -> replica: ("run", job, request) | ("cancel", job) | ("upsert", table, payload) | ("stop",)
+                  | ("peers", {rank: mesh address})                        [mesh membership]
                   | ("shard_plan", req, n_parts) | ("shard_part", req, rank, result)
                   | ("shard_exec", origin, req, scope, op, payload) | ("shard_apply", scope, op, payload)
 """
@@ -119,8 +123,9 @@ class ReplicaHub:
         # jobs the front door timed out whose replica has not sent its final event yet: {job: replica}
         self._timed_out: dict[str, _Replica] = {}
         self.timeout_grace = 60.0
-        # the front door's queue admits as many jobs as the replicas have slots; the rest wait in FIFO order
-        self.queue = JobQueue({"run_rag_job": self.run_rag_job}, max_jobs=256, job_timeout=job_timeout,
+        # the front door's queue admits as many jobs as the replicas have slots (it grows with every
+        # replica that connects: set_max_jobs in _admit_capacity); the rest wait in FIFO order
+        self.queue = JobQueue({"run_rag_job": self.run_rag_job}, max_jobs=16, job_timeout=job_timeout,
                               keep_result=keep_result)
         self.queue.ctx["on_timeout"] = self._on_timeout
         self._closed = False
@@ -157,6 +162,8 @@ class ReplicaHub:
                 self._fail_replica(old, "replica re-registered")
             log.info("replica %d connected (capacity %d)", rep.rank, rep.capacity)
             M.CLUSTER_REPLICAS.set(self.live_count())
+            self._broadcast_peers()  # before any job reaches the new replica (same connection, in order)
+            self._admit_capacity()
             self._notify_slots()
             while True:
                 msg = conn.recv()
@@ -234,7 +241,24 @@ class ReplicaHub:
                 self.events.emit_sync(j, "final", {"answer": "", "sources": None, "error": True})
             self._finish(j)
         M.CLUSTER_REPLICAS.set(self.live_count())
+        if was_alive:
+            self._broadcast_peers()
         self._notify_slots()
+
+    def _broadcast_peers(self) -> None:
+        """Mesh membership: every live replica learns every live replica's mesh address."""
+        live = self.live_replicas()
+        peers = {r.rank: tuple(r.info["mesh"]) for r in live if r.info.get("mesh")}
+        for r in live:
+            if r.info.get("mesh"):
+                r.send(("peers", peers))
+
+    def _admit_capacity(self) -> None:
+        """The front door's queue runs as many jobs at once as the replicas have slots (never fewer
+        than it ever had: a reconnecting replica finds its consumers there)."""
+        cap = self.capacity()
+        if cap > self.queue.max_jobs:
+            self.queue.set_max_jobs(cap)
 
     # ------------------------------------------------------------------ scheduling
     def live_replicas(self) -> list[_Replica]:
@@ -414,7 +438,7 @@ class HubShardTransport:
 
     def fanout(self, origin: int, scope: str, op: str, payload, timeout: float = 60.0) -> list:
         req = next(self._ids)
-        st = {"n": None, "parts": [], "ev": threading.Event()}
+        st = {"n": None, "parts": {}, "ev": threading.Event()}
         with self._lock:
             self._rounds[req] = st
         try:
@@ -422,7 +446,12 @@ class HubShardTransport:
             if not st["ev"].wait(timeout):
                 log.warning("shard %s round %d on %s: %d of %s parts after %.0fs", op, req, scope,
                             len(st["parts"]), st["n"], timeout)
-            return [p for p in st["parts"] if p is not None]
+            with self._lock:
+                parts = dict(st["parts"])
+            from .mesh import Parts
+
+            return Parts([p for p in parts.values() if p is not None],
+                         missing=[r for r, p in parts.items() if p is None])
         finally:
             with self._lock:
                 self._rounds.pop(req, None)
@@ -439,8 +468,9 @@ class HubShardTransport:
                 return
             if kind == "shard_plan":
                 st["n"] = msg[2]
-            else:
-                st["parts"].append(msg[3])
+            else:  # keyed by the answering rank: a duplicate (e.g. an empty answer from the hub's
+                # failed-send path AND its replica-lost path) cannot complete the round early
+                st["parts"].setdefault(int(msg[2]), msg[3])
             if st["n"] is not None and len(st["parts"]) >= st["n"]:
                 st["ev"].set()
 
@@ -478,10 +508,18 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
             conn.send(msg)
 
     transport = None
+    mesh = None
     local_store = getattr(runtime, "store", None)
     if shards > 1 and local_store is not None:
-        transport = HubShardTransport(send, rank)
+        if os.environ.get("GRAG_SHARD_TRANSPORT", "mesh") == "hub":
+            transport = HubShardTransport(send, rank)
+        else:  # replica-to-replica rounds (service/mesh.py); the hub only tells us who the peers are
+            from .mesh import PeerMesh
+
+            transport = mesh = PeerMesh(rank, shards, authkey, host=os.environ.get("GRAG_MESH_HOST", "127.0.0.1"))
         local_store = attach_sharded_store(runtime, transport, rank, shards)
+        if mesh is not None:
+            mesh.store = local_store
     # other replicas' shard rounds and routed writes run here, off the job loop (GPU search + sync)
     shard_pool = ThreadPoolExecutor(4, thread_name_prefix="shard-exec")
     events = _ForwardingEvents(send)
@@ -491,7 +529,8 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
     if transport is None and store is not None and hasattr(store, "add_listener"):
         store.add_listener(lambda table, payload: send(("upsert", table, payload)))
     send(("hello", rank, cap, {"device": str(getattr(runtime, "device", "cpu")), "pid": os.getpid(),
-                               "shard": f"{rank}/{shards}" if transport is not None else "full"}))
+                               "shard": f"{rank}/{shards}" if transport is not None else "full",
+                               **({"mesh": tuple(mesh.address)} if mesh is not None else {})}))
 
     def shard_exec(origin, req, scope, op, payload):
         try:
@@ -519,7 +558,9 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
                 while True:
                     msg = conn.recv()
                     kind = msg[0]
-                    if kind in ("shard_plan", "shard_part") and transport is not None:
+                    if kind == "peers" and mesh is not None:
+                        mesh.set_peers(msg[1])
+                    elif kind in ("shard_plan", "shard_part") and isinstance(transport, HubShardTransport):
                         transport.deliver(msg)
                     elif kind == "shard_exec":
                         shard_pool.submit(shard_exec, *msg[1:])
@@ -579,6 +620,8 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
         asyncio.run(main())
     finally:
         shard_pool.shutdown(wait=False)
+        if mesh is not None:
+            mesh.close()
         try:
             conn.close()
         except OSError:

@@ -81,3 +81,7 @@ CLUSTER_INFLIGHT = Gauge("grag_cluster_replica_inflight_jobs", "Jobs running on 
                          registry=REGISTRY)
 CLUSTER_DISPATCH = Counter("grag_cluster_dispatched_jobs_total", "Jobs dispatched to a replica", ["replica"],
                            registry=REGISTRY)
+# sharded index rounds (index/sharded_store.py, service/mesh.py)
+INDEX_DEGRADED_ROUNDS = Counter("rag_index_degraded_rounds_total",
+                                "Sharded retrieval rounds answered without every shard (recall dropped)", ["table"],
+                                registry=REGISTRY)

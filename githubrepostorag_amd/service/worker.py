@@ -21,6 +21,7 @@ import time
 import uuid
 
 from ..agent.graph_agent import Cancelled
+from ..index.sharded_store import round_health
 from . import metrics as M
 from ..utils.tracing import Trace
 from .events import CancelFlags, EventLog
@@ -45,8 +46,26 @@ class JobQueue:
     async def start(self) -> None:
         if self._q is not None:
             return
+        self._loop = asyncio.get_running_loop()
         self._q = asyncio.Queue()
         self._tasks = [asyncio.create_task(self._consume(i)) for i in range(self.max_jobs)]
+
+    def set_max_jobs(self, n: int) -> None:
+        """Raise the concurrency bound (thread-safe; e.g. the front door's queue follows the sum of its
+        replicas' slots).  Consumers are only added: a smaller bound leaves the extra ones idle-waiting
+        on the queue, and the hub's job function waits for a replica slot anyway."""
+        self.max_jobs = max(1, int(n))
+        loop = getattr(self, "_loop", None)
+        if loop is None or self._q is None:
+            return
+        try:
+            loop.call_soon_threadsafe(self._grow)
+        except RuntimeError:  # loop closed
+            pass
+
+    def _grow(self) -> None:
+        while self._q is not None and len(self._tasks) < self.max_jobs:
+            self._tasks.append(asyncio.create_task(self._consume(len(self._tasks))))
 
     async def stop(self) -> None:
         for t in self._tasks:
@@ -137,20 +156,27 @@ class RAGWorker:
             t_rag = time.perf_counter()
             trace = Trace(job_id, observer=M.observe_span)
             trace.add("queue_wait", queue_wait)
-            result = await loop.run_in_executor(
-                self.executor,
-                lambda: agent.run(query, namespace=namespace, progress_cb=progress,
-                                  cancel_check=lambda: self.flags.is_cancelled_sync(job_id),
-                                  force_level=forced, on_answer_token=on_token if self.stream_tokens else None,
-                                  trace=trace, repo=req.get("repo_name") or None,
-                                  top_k=req.get("top_k") or None))
+            def run_agent():
+                # the job's shard rounds run on this thread: record whether any lost a shard
+                with round_health() as health:
+                    res = agent.run(query, namespace=namespace, progress_cb=progress,
+                                    cancel_check=lambda: self.flags.is_cancelled_sync(job_id),
+                                    force_level=forced, on_answer_token=on_token if self.stream_tokens else None,
+                                    trace=trace, repo=req.get("repo_name") or None,
+                                    top_k=req.get("top_k") or None)
+                return res, health
+
+            result, health = await loop.run_in_executor(self.executor, run_agent)
             M.WORKER_RETRIEVAL_DURATION.observe(time.perf_counter() - t_rag)
             sources = result.get("sources") or []
             debug = result.get("debug") or {}
-            await self.events.emit(job_id, "retrieval", {"attempt": 0, "scope": result.get("scope", ""),
-                                                         "sources_found": len(sources),
-                                                         "turns": debug.get("turns", []),
-                                                         "final_ctx_blocks": debug.get("final_ctx_blocks", 0)})
+            retrieval = {"attempt": 0, "scope": result.get("scope", ""), "sources_found": len(sources),
+                         "turns": debug.get("turns", []), "final_ctx_blocks": debug.get("final_ctx_blocks", 0)}
+            if health["rounds"]:  # sharded index: were all shards heard in every round?
+                retrieval.update(degraded=health["degraded_rounds"] > 0, shard_rounds=health["rounds"],
+                                 degraded_rounds=health["degraded_rounds"],
+                                 missing_shards=sorted(health["missing_shards"]))
+            await self.events.emit(job_id, "retrieval", retrieval)
             await self.events.emit(job_id, "timing", {"job_s": round(time.perf_counter() - t_job, 4),
                                                       "agent_s": round(time.perf_counter() - t_rag, 4),
                                                       "trace_id": trace.trace_id, "totals_ms": trace.totals(),

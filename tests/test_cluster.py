@@ -135,6 +135,47 @@ def test_sharded_replicas_answer_from_every_shard(cluster):
     assert sorted(r["shard"] for r in h) == ["0/2", "1/2"]
 
 
+def test_sharded_replicas_over_hub_relay(cluster, monkeypatch):
+    """GRAG_SHARD_TRANSPORT=hub keeps the round-3 relay through the front door's hub."""
+    monkeypatch.setenv("GRAG_SHARD_TRANSPORT", "hub")
+    hub, procs, client = cluster(n=2, delay=0.0, slots=2, shards=2)
+    ev = _sse(client, client.post("/rag/jobs", json={"query": "widgets and gadgets"}).json()["job_id"])
+    final = ev[-1][1]
+    assert {s["metadata"]["file_path"] for s in final["sources"]} == {"a.py", "b.py", "c.py"}
+    ret = next(d for e, d in ev if e == "retrieval")
+    assert ret["degraded"] is False and ret["shard_rounds"] > 0
+
+
+def test_lost_shard_marks_retrieval_degraded(cluster):
+    """A job whose rounds could not reach every shard says so in its retrieval event (recall down by
+    1/N), instead of silently answering from the shards that did answer."""
+    hub, procs, client = cluster(n=2, delay=0.0, slots=2, shards=2)
+    ev = _sse(client, client.post("/rag/jobs", json={"query": "widgets"}).json()["job_id"])
+    assert next(d for e, d in ev if e == "retrieval")["degraded"] is False
+    procs[1].kill()
+    t0 = time.time()
+    while hub.live_count() > 1:
+        assert time.time() - t0 < 30
+        time.sleep(0.05)
+    ev = _sse(client, client.post("/rag/jobs", json={"query": "widgets again"}).json()["job_id"])
+    ret = next(d for e, d in ev if e == "retrieval")
+    assert ret["degraded"] is True and ret["missing_shards"] == [1], ret
+    final = ev[-1][1]
+    assert {s["metadata"]["file_path"] for s in final["sources"]} <= {"b.py", "c.py"}  # shard 0's rows only
+
+
+def test_front_door_admits_the_replicas_capacity(cluster):
+    """The hub's queue runs as many jobs at once as its replicas have slots (round 3 capped it at 256,
+    so 8 replicas x 64 slots left half the posted jobs waiting at the door)."""
+    hub, procs, client = cluster(n=2, delay=0.0, slots=300)
+    t0 = time.time()
+    while hub.queue.max_jobs < 600 or len(hub.queue._tasks) < 600:
+        assert time.time() - t0 < 10, (hub.queue.max_jobs, len(hub.queue._tasks))
+        client.get("/health")  # any request keeps the app loop turning
+        time.sleep(0.05)
+    assert hub.capacity() == 600
+
+
 def test_store_write_mirroring():
     a, b = VectorStore(8, "cpu"), VectorStore(8, "cpu")
     sent = []

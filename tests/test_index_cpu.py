@@ -129,3 +129,13 @@ def test_search_concurrent_with_upsert_and_compaction_cpu():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     mod._search_while_writing(torch.device("cpu"), rounds=12)
+
+
+def test_search_pairs_concurrent_with_growing_upsert_cpu():
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location("tig", os.path.join(os.path.dirname(__file__), "test_index_gpu.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod._pairs_while_writing(torch.device("cpu"), rounds=12)

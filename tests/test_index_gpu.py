@@ -173,3 +173,44 @@ def _search_while_writing(dev, rounds=40):
 
 def test_search_concurrent_with_upsert_and_compaction(dev):
     _search_while_writing(dev)
+
+
+def _pairs_while_writing(dev, rounds=40):
+    """Graph-traversal lookups (search_pairs: per-query column predicates) on a helper thread
+    while the main thread upserts rows with NEW filter values (growing the rows, the columns and
+    the dictionaries): every lookup must return its anchor row and only rows of its pair."""
+    import threading
+
+    d = 64
+    g = torch.Generator(device="cpu").manual_seed(6)
+    tab = VectorTable("stress_pairs", d, dev, capacity=64)
+    anchors = torch.nn.functional.normalize(torch.randn(8, d, generator=g), dim=1)
+    tab.upsert([f"a{i}" for i in range(8)], ["anchor"] * 8, anchors.to(dev),
+               [{"repo": f"r{i}", "module": f"m{i % 2}"} for i in range(8)])
+    errors, stop = [], threading.Event()
+
+    def reader():
+        while not stop.is_set():
+            for i in range(8):
+                pairs = [("repo", f"r{i}"), ("module", f"m{i % 2}")]
+                out = tab.search_pairs(anchors[i].to(dev), pairs, 3)
+                if not out[0] or out[0][0].row_id != f"a{i}" or any(h.metadata["repo"] != f"r{i}" for h in out[0]):
+                    errors.append((i, [h.row_id for h in out[0]]))
+                if any(h.metadata["module"] != f"m{i % 2}" for h in out[1]):
+                    errors.append((i, "module", [h.row_id for h in out[1]]))
+
+    th = threading.Thread(target=reader)
+    th.start()
+    try:
+        for r in range(rounds):
+            noise = torch.nn.functional.normalize(torch.randn(150, d, generator=g), dim=1)
+            tab.upsert([f"n{r}_{i}" for i in range(150)], ["noise"] * 150, noise.to(dev),
+                       [{"repo": f"new{r}_{i % 5}", "module": f"nm{r}"} for i in range(150)])
+    finally:
+        stop.set()
+        th.join()
+    assert not errors, errors[:5]
+
+
+def test_search_pairs_concurrent_with_growing_upsert(dev):
+    _pairs_while_writing(dev)

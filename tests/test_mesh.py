@@ -1,0 +1,128 @@
+"""Replica-to-replica shard mesh (service/mesh.py): N PeerMesh endpoints over real
+authenticated sockets in one process.  Sharded searches and traversal lookups
+equal a flat store's, routed writes are acknowledged by their owner, concurrent
+rounds coalesce into fewer messages and stacked launches, and a round that loses
+a shard is reported as degraded (never a silent partial answer).
+Reference: one shared ANN store per worker
+(rag_worker/src/worker/services/graph_rag_retrievers.py:68-80)."""
+import secrets
+import threading
+import time
+
+import pytest
+import torch
+
+from githubrepostorag_amd.index.sharded_store import ShardedStore, round_health, shard_of
+from githubrepostorag_amd.index.store import VectorStore
+from githubrepostorag_amd.service.mesh import PeerMesh, ShardWriteError
+
+D = 32
+
+
+def _rows(n, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    ids = [f"row{i}" for i in range(n)]
+    texts = [f"text {i}" for i in range(n)]
+    vecs = torch.nn.functional.normalize(torch.randn(n, D, generator=g), dim=1)
+    metas = [{"namespace": "default", "repo": f"r{i % 5}", "module": f"m{i % 7}", "file_path": f"m{i % 7}/f{i % 11}.py"}
+             for i in range(n)]
+    return ids, texts, vecs, metas
+
+
+@pytest.fixture()
+def mesh3():
+    key = secrets.token_bytes(16)
+    n = 3
+    locs = [VectorStore(D, "cpu") for _ in range(n)]
+    meshes = [PeerMesh(r, n, key, store=locs[r]) for r in range(n)]
+    peers = {r: m.address for r, m in enumerate(meshes)}
+    for m in meshes:
+        m.set_peers(peers)
+    facades = [ShardedStore(locs[r], r, n, meshes[r]) for r in range(n)]
+    yield locs, meshes, facades
+    for f in facades:
+        f.close()
+    for m in meshes:
+        m.close()
+
+
+def test_mesh_writes_acked_on_owner_and_search_matches_flat(mesh3):
+    locs, meshes, facades = mesh3
+    ids, texts, vecs, metas = _rows(240)
+    flat = VectorStore(D, "cpu")
+    flat.table("chunk").upsert(ids, texts, vecs, metas)
+    new = facades[1].table("chunk").upsert(ids, texts, vecs, metas)  # ingest on replica 1: routed + acked
+    assert new == 240, new  # every owner acknowledged its rows
+    for r, loc in enumerate(locs):
+        keys = list(loc.table("chunk").rows.key_to_row)
+        assert keys and all(shard_of(k, 3) == r for k in keys)
+    g = torch.Generator().manual_seed(9)
+    Q = torch.nn.functional.normalize(torch.randn(5, D, generator=g), dim=1)
+    for flt in (None, {"repo": "r2"}, {"module": "m3", "namespace": "default"}, {"repo": "missing"}):
+        ref = [[h.row_id for h in hs] for hs in flat.table("chunk").search(Q, 7, flt)]
+        for fac in facades:
+            with round_health() as h:
+                got = [[h_.row_id for h_ in hs] for hs in fac.table("chunk").search(Q, 7, flt)]
+            assert got == ref, flt
+            assert h["rounds"] == 1 and h["degraded_rounds"] == 0
+    # traversal lookups (search_pairs) across shards
+    pairs = [("repo", "r1"), ("module", "m4"), ("file_path", "m2/f3.py")]
+    ref = [[x.row_id for x in hs] for hs in flat.table("chunk").search_pairs(Q[0], pairs, 4)]
+    got = [[x.row_id for x in hs] for hs in facades[2].table("chunk").search_pairs(Q[0], pairs, 4)]
+    assert got == ref
+    assert facades[0].table("chunk").delete(["row1", "row2", "row3", "row4"]) == 4
+    assert facades[2].table("chunk").count() == 236
+
+
+def test_mesh_coalesces_concurrent_rounds(mesh3):
+    locs, meshes, facades = mesh3
+    ids, texts, vecs, metas = _rows(300, seed=1)
+    facades[0].table("chunk").upsert(ids, texts, vecs, metas)
+    g = torch.Generator().manual_seed(3)
+    Q = torch.nn.functional.normalize(torch.randn(64, D, generator=g), dim=1)
+    ref = [[h.row_id for h in hs] for hs in facades[0].table("chunk").search(Q, 5, {"namespace": "default"})]
+    out, errs = [None] * 64, []
+
+    def job(i):
+        try:
+            out[i] = [h.row_id for h in facades[0].table("chunk").search(Q[i:i + 1], 5, {"namespace": "default"})[0]]
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    served0 = [m.stats["served_msgs"] for m in meshes]
+    reqs0 = [m.stats["served_reqs"] for m in meshes]
+    ths = [threading.Thread(target=job, args=(i,)) for i in range(64)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs and out == ref
+    msgs = sum(m.stats["served_msgs"] for m in meshes[1:]) - sum(served0[1:])
+    reqs = sum(m.stats["served_reqs"] for m in meshes[1:]) - sum(reqs0[1:])
+    assert reqs == 128  # 64 rounds x 2 remote shards
+    assert msgs < reqs, (msgs, reqs)  # concurrent rounds shared messages
+    assert sum(m.stats["stacked_searches"] for m in meshes[1:]) > 0  # ... and stacked launches
+
+
+def test_mesh_lost_shard_is_degraded_and_writes_fail_loudly(mesh3):
+    locs, meshes, facades = mesh3
+    ids, texts, vecs, metas = _rows(90, seed=2)
+    facades[0].table("chunk").upsert(ids, texts, vecs, metas)
+    meshes[2].close()  # shard 2's replica goes away
+    time.sleep(0.1)
+    q = vecs[:2]
+    with round_health() as h:
+        hits = facades[0].table("chunk").search(q, 5)
+    assert h["degraded_rounds"] == 1 and h["missing_shards"] == {2}
+    assert all(shard_of(x.row_id, 3) != 2 for hs in hits for x in hs)
+    assert facades[0].table("chunk").stats["degraded_rounds"] == 1
+    # a write owned by the lost shard raises instead of vanishing
+    owned2 = [i for i in ids if shard_of(i, 3) == 2][:1]
+    j = ids.index(owned2[0])
+    with pytest.raises(ShardWriteError):
+        facades[0].table("chunk").upsert(owned2, [texts[j]], vecs[j:j + 1], [metas[j]])
+    # the hub's next peer table drops the shard: rounds still report it missing (recall is down)
+    meshes[0].set_peers({1: meshes[1].address})
+    with round_health() as h:
+        facades[0].table("chunk").search(q, 5)
+    assert h["missing_shards"] == {2}
