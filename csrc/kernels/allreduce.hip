@@ -21,6 +21,14 @@
 // signals call k+1 after its kernel k (which read slot k & 1) has finished.
 // The peer pointers are a by-value kernel argument, so the launch is
 // hipGraph-capturable; in-place (out == x) is allowed.
+//
+// The same protocol serves the TP sampler's small exchanges (SURVEY §2.8 C2:
+// per-rank (max, id) pairs, 256-bin histograms, Gumbel winners): OP_SUM_F32
+// sums fp32 vectors (rank order, bit-identical on every rank) and OP_GATHER
+// concatenates every rank's bytes (out = [W][n]).  All three ops of one
+// communicator share its epochs, so they may be mixed in any order as long as
+// every rank issues the same sequence — the engine's lockstep TP decode does,
+// and a decode graph then holds no RCCL call at all.
 #include "common.h"
 
 #include <cstring>
@@ -38,6 +46,10 @@ struct Peers {
   unsigned* flags[kMaxRanks];
 };
 
+enum { OP_SUM_BF16 = 0, OP_SUM_F32 = 1, OP_GATHER = 2 };
+typedef float f32x4v_t __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4v_t __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ void st_release_sys(unsigned* p, unsigned v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -45,7 +57,8 @@ __device__ __forceinline__ unsigned ld_acquire_sys(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <int W>
+// n8: 16-byte vectors per rank (8 bf16 / 4 fp32 / 16 raw bytes); slot_elems in bf16 units.
+template <int W, int OP>
 __global__ __launch_bounds__(kThreads) void ar_oneshot_kernel(Peers peers, int rank, const bf16* __restrict__ x,
                                                               bf16* out, long n8, long slot_elems,
                                                               unsigned* __restrict__ epochs, unsigned* err,
@@ -86,17 +99,33 @@ __global__ __launch_bounds__(kThreads) void ar_oneshot_kernel(Peers peers, int r
   __syncthreads();
   if (s_fail) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: peers' slot data, not stale L1 lines
-  bf16x8_t* ov = reinterpret_cast<bf16x8_t*>(out);
-  for (long i = v0 + threadIdx.x; i < v1; i += kThreads) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (OP == OP_SUM_BF16) {
+    bf16x8_t* ov = reinterpret_cast<bf16x8_t*>(out);
+    for (long i = v0 + threadIdx.x; i < v1; i += kThreads) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < W; ++r) {
-      float v[8];
-      unpack8(reinterpret_cast<const bf16x8_t*>(peers.data[r] + off)[i], v);
+      for (int r = 0; r < W; ++r) {
+        float v[8];
+        unpack8(reinterpret_cast<const bf16x8_t*>(peers.data[r] + off)[i], v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+        for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      }
+      ov[i] = pack8(acc);
     }
-    ov[i] = pack8(acc);
+  } else if constexpr (OP == OP_SUM_F32) {
+    f32x4v_t* ov = reinterpret_cast<f32x4v_t*>(out);
+    for (long i = v0 + threadIdx.x; i < v1; i += kThreads) {
+      f32x4v_t acc = reinterpret_cast<const f32x4v_t*>(peers.data[0] + off)[i];
+#pragma unroll
+      for (int r = 1; r < W; ++r) acc += reinterpret_cast<const f32x4v_t*>(peers.data[r] + off)[i];
+      ov[i] = acc;
+    }
+  } else {  // OP_GATHER: out[r][i] = rank r's vector i
+    u32x4v_t* ov = reinterpret_cast<u32x4v_t*>(out);
+    for (long i = v0 + threadIdx.x; i < v1; i += kThreads) {
+#pragma unroll
+      for (int r = 0; r < W; ++r) ov[r * n8 + i] = reinterpret_cast<const u32x4v_t*>(peers.data[r] + off)[i];
+    }
   }
 }
 
@@ -129,33 +158,62 @@ GRAG_API int grag_ar_open_handle(const void* handle /* 64 bytes */, void** ptr) 
 }
 GRAG_API int grag_ar_close_handle(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
 
+namespace {
+template <int OP>
+int launch_oneshot(void* const* regions, int W, int rank, const void* x, void* out, long n16, long slot_bytes,
+                   void* epochs, void* err, int grid, long spin_max, hipStream_t stream);
+}  // namespace
+
 // regions: host array of W region base pointers (own + opened peers), rank order.
 // n: elements (bf16, multiple of 8, <= slot_bytes / 2); grid: fixed per communicator (<= kMaxBlocks).
 GRAG_API int grag_ar_oneshot(void* const* regions, int W, int rank, const void* x, void* out, long n,
                              long slot_bytes, void* epochs, void* err, int grid, long spin_max,
                              hipStream_t stream) {
-  if (W < 1 || W > kMaxRanks || rank < 0 || rank >= W || grid < 1 || grid > kMaxBlocks) return (int)hipErrorInvalidValue;
   if (n % 8 != 0 || n * 2 > slot_bytes) return (int)hipErrorInvalidValue;
+  return launch_oneshot<OP_SUM_BF16>(regions, W, rank, x, out, n / 8, slot_bytes, epochs, err, grid, spin_max, stream);
+}
+
+// op 1: fp32 sum of `nbytes` per rank (out may alias x); op 2: gather, out = W x nbytes (rank order, no alias).
+// nbytes: multiple of 16, <= slot_bytes.  Same communicator (regions / epochs / grid) as grag_ar_oneshot.
+GRAG_API int grag_ar_oneshot_op(void* const* regions, int W, int rank, int op, const void* x, void* out, long nbytes,
+                                long slot_bytes, void* epochs, void* err, int grid, long spin_max,
+                                hipStream_t stream) {
+  if (nbytes % 16 != 0 || nbytes > slot_bytes || nbytes < 0) return (int)hipErrorInvalidValue;
+  if (op == OP_SUM_F32)
+    return launch_oneshot<OP_SUM_F32>(regions, W, rank, x, out, nbytes / 16, slot_bytes, epochs, err, grid, spin_max,
+                                      stream);
+  if (op == OP_GATHER)
+    return launch_oneshot<OP_GATHER>(regions, W, rank, x, out, nbytes / 16, slot_bytes, epochs, err, grid, spin_max,
+                                     stream);
+  return (int)hipErrorInvalidValue;
+}
+
+namespace {
+template <int OP>
+int launch_oneshot(void* const* regions, int W, int rank, const void* x, void* out, long n16, long slot_bytes,
+                   void* epochs, void* err, int grid, long spin_max, hipStream_t stream) {
+  if (W < 1 || W > kMaxRanks || rank < 0 || rank >= W || grid < 1 || grid > kMaxBlocks) return (int)hipErrorInvalidValue;
   Peers p{};
   const long doff = grag_ar_data_offset();
   for (int r = 0; r < W; ++r) {
     p.flags[r] = reinterpret_cast<unsigned*>(regions[r]);
     p.data[r] = reinterpret_cast<const bf16*>(reinterpret_cast<char*>(regions[r]) + doff);
   }
-  const long n8 = n / 8, slot_elems = slot_bytes / 2;
+  const long n8 = n16, slot_elems = slot_bytes / 2;
   auto go = [&](auto kern) {
     kern<<<grid, kThreads, 0, stream>>>(p, rank, (const bf16*)x, (bf16*)out, n8, slot_elems, (unsigned*)epochs,
                                         (unsigned*)err, spin_max);
   };
   switch (W) {
-    case 1: go(ar_oneshot_kernel<1>); break;
-    case 2: go(ar_oneshot_kernel<2>); break;
-    case 3: go(ar_oneshot_kernel<3>); break;
-    case 4: go(ar_oneshot_kernel<4>); break;
-    case 5: go(ar_oneshot_kernel<5>); break;
-    case 6: go(ar_oneshot_kernel<6>); break;
-    case 7: go(ar_oneshot_kernel<7>); break;
-    default: go(ar_oneshot_kernel<8>); break;
+    case 1: go(ar_oneshot_kernel<1, OP>); break;
+    case 2: go(ar_oneshot_kernel<2, OP>); break;
+    case 3: go(ar_oneshot_kernel<3, OP>); break;
+    case 4: go(ar_oneshot_kernel<4, OP>); break;
+    case 5: go(ar_oneshot_kernel<5, OP>); break;
+    case 6: go(ar_oneshot_kernel<6, OP>); break;
+    case 7: go(ar_oneshot_kernel<7, OP>); break;
+    default: go(ar_oneshot_kernel<8, OP>); break;
   }
   return (int)hipGetLastError();
 }
+}  // namespace

@@ -124,6 +124,27 @@ class EngineLLM:
         return SamplingParams(max_tokens=int(mt), stop=list(kw.get("stop") or self.stop),
                               ignore_eos=bool(kw.get("ignore_eos", False)), **d)
 
+    def fit(self, ids: list[int], max_tokens: int) -> list[int]:
+        """Prompt ids that fit the engine's max_model_len with room to generate: an over-long prompt loses
+        the MIDDLE of its text (the agent's prompts are system + question, then the retrieved context
+        blocks, then the answer cue; ingest prompts are an instruction, then the material) — the head and
+        the answer cue / chat-template tail are kept.  Counted in grag_llm_prompt_truncations_total."""
+        eng = getattr(self.runner, "engine", None)
+        mml = getattr(getattr(eng, "cfg", None), "max_model_len", None)
+        if not mml:
+            return ids
+        reserve = max(1, min(int(max_tokens), max(16, mml // 8)))
+        budget = mml - reserve
+        if len(ids) <= budget:
+            return ids
+        tail = min(64, budget // 4)
+        log.warning("prompt of %d tokens cut to %d (max_model_len %d, %d reserved to generate): middle "
+                    "context dropped", len(ids), budget, mml, reserve)
+        from ..service import metrics as M
+
+        M.PROMPT_TRUNCATIONS.inc()
+        return ids[:budget - tail] + ids[len(ids) - tail:]
+
     def _post(self, prompt: str, out: str) -> str:
         if self.mode == "ingest":
             return sanitize(out) or "No response generated"
@@ -136,8 +157,9 @@ class EngineLLM:
         caller's thread, and submitted to the engine together — no thread per call, no tokenising on
         the engine thread — then awaited; failed items are retried as one smaller wave."""
         sp = self.params(**kw)
-        ids = [self.tok.encode(self.tok.apply_chat_template(self._messages(p), True,
-                                                             None if self.allow_thinking else False))
+        ids = [self.fit(self.tok.encode(self.tok.apply_chat_template(self._messages(p), True,
+                                                                     None if self.allow_thinking else False)),
+                        sp.max_tokens)
                for p in prompt_list]
         out: list[CompletionResponse | None] = [None] * len(prompt_list)
         todo = list(range(len(prompt_list)))
@@ -162,6 +184,7 @@ class EngineLLM:
         text = self.tok.apply_chat_template(self._messages(prompt), True,
                                             None if self.allow_thinking else False)
         sp = self.params(**kw)
+        text = self.fit(self.tok.encode(text), sp.max_tokens)  # token ids, within max_model_len
         cancel_check = kw.get("cancel_check")
         err = None
         for attempt in range(self.retries + 1):

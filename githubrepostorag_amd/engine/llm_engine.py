@@ -41,6 +41,15 @@ log = logging.getLogger(__name__)
 _TP_SAMPLER = __import__("os").environ.get("GRAG_TP_SAMPLER", "shard")
 
 
+class PromptTooLongError(ValueError):
+    """A prompt that leaves no room for one generated token within max_model_len."""
+
+    def __init__(self, n_prompt: int, max_model_len: int):
+        super().__init__(f"This model's maximum context length is {max_model_len} tokens. However, your prompt has "
+                         f"{n_prompt} tokens. Please reduce the length of the messages.")
+        self.n_prompt, self.max_model_len = n_prompt, max_model_len
+
+
 @dataclass
 class EngineConfig:
     max_num_seqs: int = 64
@@ -167,8 +176,11 @@ class LLMEngine:
         ids = self.tok.encode(prompt) if isinstance(prompt, str) else list(prompt)
         if not ids:
             ids = [self.tok.pad_token_id] if hasattr(self.tok, "pad_token_id") else [0]
-        if len(ids) >= self.cfg.max_model_len:  # keep the tail (most recent context) like a sliding truncation
-            ids = ids[-(self.cfg.max_model_len - 1):]
+        if len(ids) >= self.cfg.max_model_len:
+            # rejected like vLLM's server does (helm/templates/qwen-deployment.yaml:30-31 --max-model-len):
+            # never cut silently here.  Callers that own the prompt's structure fit it first (agent/llm.py
+            # EngineLLM keeps the head and the answer cue); the OpenAI endpoints answer HTTP 400.
+            raise PromptTooLongError(len(ids), self.cfg.max_model_len)
         req_id = req_id or uuid.uuid4().hex
         seq = Sequence(req_id, ids, params, on_token=on_token)
         with self._lock:

@@ -104,13 +104,17 @@ class Group:
     custom_ar = None  # parallel.custom_ar.IpcAllReduce: one-shot xGMI all-reduce for small messages
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
-        """C1: small bf16 messages (decode [B, hidden]) take the one-shot IPC
-        all-reduce when attached; everything else goes to RCCL / gloo."""
+        """C1: small bf16 messages (decode [B, hidden]) and small fp32 ones (the
+        TP sampler's histograms) take the one-shot IPC all-reduce when attached;
+        everything else goes to RCCL / gloo."""
         if not self.trivial:
             ar = self.custom_ar
-            if ar is not None and ar.fits(t):
-                return ar.all_reduce(t)
-            dist.all_reduce(t, group=self.pg)
+            if ar is not None:
+                if ar.fits(t):
+                    return ar.all_reduce(t)
+                if t.dtype == torch.float32 and ar.fits_bytes(t):
+                    return ar.all_reduce_f32(t)
+            _gloo_staged(lambda x: dist.all_reduce(x, group=self.pg), t)
         return t
 
     def stage_health(self) -> None:
@@ -176,9 +180,26 @@ class Group:
         """[...] -> [size, ...] (one collective)."""
         if self.trivial:
             return t.unsqueeze(0)
+        ar = self.custom_ar
+        if ar is not None and t.is_cuda:  # C2 small exchanges: one-shot IPC gather (capturable)
+            src = t.contiguous()
+            nb = src.numel() * src.element_size()
+            if nb % 16 == 0 and ar.fits_bytes(src):
+                return ar.all_gather(src)
+            nbp = -(-nb // 16) * 16
+            if 0 < nbp <= ar.slot_bytes:  # odd sizes (e.g. [1, 2] fp32): padded to 16-byte vectors
+                pad = torch.zeros(nbp, dtype=torch.uint8, device=t.device)
+                pad[:nb] = src.view(-1).view(torch.uint8)
+                g = ar.all_gather(pad)[:, :nb].contiguous()
+                return g.view(t.dtype).view(self.size, *t.shape)
         # flat concatenated form: the only layout both RCCL and gloo accept
+        src = t.contiguous().view(-1)
+        if _INFO.backend == "gloo" and src.is_cuda:  # shared-GPU rehearsal: gloo works on host tensors
+            out = torch.empty(self.size * src.numel(), dtype=t.dtype)
+            dist.all_gather_into_tensor(out, src.cpu(), group=self.pg)
+            return out.to(t.device).view(self.size, *t.shape)
         out = torch.empty(self.size * t.numel(), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous().view(-1), group=self.pg)
+        dist.all_gather_into_tensor(out, src, group=self.pg)
         return out.view(self.size, *t.shape)
 
     def all_gather_topk(self, scores: torch.Tensor, ids: torch.Tensor, k: int):
@@ -202,14 +223,30 @@ class Group:
         the result came from local rank i (one all_to_all_single)."""
         if self.trivial:
             return t
+        if _INFO.backend == "gloo" and t.is_cuda:  # shared-GPU rehearsal: gloo works on host tensors
+            h = t.contiguous().cpu()
+            out = torch.empty_like(h)
+            dist.all_to_all_single(out.view(-1), h.view(-1), group=self.pg)
+            return out.to(t.device)
         out = torch.empty_like(t)
         dist.all_to_all_single(out.view(-1), t.contiguous().view(-1), group=self.pg)
         return out
 
     def broadcast(self, t: torch.Tensor, src_local: int = 0) -> torch.Tensor:
         if not self.trivial:
-            dist.broadcast(t, src=self.ranks[src_local], group=self.pg)
+            _gloo_staged(lambda x: dist.broadcast(x, src=self.ranks[src_local], group=self.pg), t)
         return t
+
+
+def _gloo_staged(op, t: torch.Tensor) -> None:
+    """Run an in-place collective ``op`` on ``t``; under gloo a GPU tensor goes through a host copy
+    (the shared-GPU rehearsal: several ranks on one card, where RCCL refuses duplicate devices)."""
+    if _INFO.backend == "gloo" and t.is_cuda:
+        h = t.cpu()
+        op(h)
+        t.copy_(h)
+    else:
+        op(t)
 
 
 def world_group() -> Group:

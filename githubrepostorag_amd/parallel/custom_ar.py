@@ -35,7 +35,9 @@ _SIGS = {
     "grag_ar_free": ([P], I), "grag_ar_get_handle": ([P, P], I), "grag_ar_handle_size": ([], I),
     "grag_ar_open_handle": ([P, P], I), "grag_ar_close_handle": ([P], I),
     "grag_ar_oneshot": ([P, I, I, P, P, L, L, P, P, I, L, P], I),
+    "grag_ar_oneshot_op": ([P, I, I, I, P, P, L, L, P, P, I, L, P], I),
 }
+OP_SUM_F32, OP_GATHER = 1, 2
 MAX_RANKS = 8
 
 
@@ -131,6 +133,33 @@ class IpcAllReduce:
         check(rc, "grag_ar_oneshot")
         return out
 
+    def fits_bytes(self, t: torch.Tensor) -> bool:
+        nb = t.numel() * t.element_size()
+        return t.is_cuda and t.is_contiguous() and nb % 16 == 0 and 0 < nb <= self.slot_bytes
+
+    def all_reduce_f32(self, t: torch.Tensor, stream=None) -> torch.Tensor:
+        """fp32 sum over ranks, in place (rank-order accumulation: bit-identical on every rank)."""
+        if t.dtype != torch.float32 or not self.fits_bytes(t):
+            raise ValueError("tensor does not fit the one-shot fp32 all-reduce")
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        rc = _fn("grag_ar_oneshot_op")(self._arr, self.W, self.rank, OP_SUM_F32, ptr(t), ptr(t),
+                                       t.numel() * 4, self.slot_bytes, ptr(self.epochs), ptr(self.err), self.grid,
+                                       self.spin_max, s.cuda_stream)
+        check(rc, "grag_ar_oneshot_op(sum_f32)")
+        return t
+
+    def all_gather(self, t: torch.Tensor, stream=None) -> torch.Tensor:
+        """[...] -> [W, ...] (rank order), any dtype; the bytes per rank a multiple of 16."""
+        if not self.fits_bytes(t):
+            raise ValueError("tensor does not fit the one-shot all-gather")
+        out = torch.empty((self.W, *t.shape), dtype=t.dtype, device=t.device)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        rc = _fn("grag_ar_oneshot_op")(self._arr, self.W, self.rank, OP_GATHER, ptr(t), ptr(out),
+                                       t.numel() * t.element_size(), self.slot_bytes, ptr(self.epochs),
+                                       ptr(self.err), self.grid, self.spin_max, s.cuda_stream)
+        check(rc, "grag_ar_oneshot_op(gather)")
+        return out
+
     def failed(self) -> bool:
         return bool(self.err.item())
 
@@ -173,11 +202,19 @@ def enable_for_group(group, device) -> IpcAllReduce | None:
         ar = IpcAllReduce.create(group.pg, group.rank, group.size, dev)
         g = torch.Generator(device=dev).manual_seed(1234 + group.rank)
         x = torch.randn(4096, generator=g, device=dev).to(torch.bfloat16)
-        ref = x.float().clone()
+        cdev = group.ctrl_device(dev)  # RCCL: on the GPU; gloo (shared-GPU rehearsal): on the host
+        ref = x.float().to(cdev)
         dist.all_reduce(ref, group=group.pg)
         got = ar.all_reduce(x.clone())
-        ok = torch.tensor([0 if ar.failed() or not torch.allclose(got.float(), ref, atol=0.1, rtol=0.02) else 1],
-                          device=dev)
+        # the sampler's exchanges: fp32 sum and all-gather over the same communicator
+        y = torch.arange(64, dtype=torch.float32, device=dev) + group.rank
+        ys = ar.all_reduce_f32(y.clone())
+        yg = ar.all_gather(y)
+        want_s = sum(torch.arange(64, dtype=torch.float32) + r for r in range(group.size))
+        good = (not ar.failed() and torch.allclose(got.float().cpu(), ref.cpu(), atol=0.1, rtol=0.02)
+                and torch.equal(ys.cpu(), want_s)
+                and all(torch.equal(yg[r].cpu(), torch.arange(64, dtype=torch.float32) + r) for r in range(group.size)))
+        ok = torch.tensor([1 if good else 0], device=cdev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group.pg)
         if int(ok.item()) != 1:
             log.warning("one-shot all-reduce self-check failed; staying on RCCL")

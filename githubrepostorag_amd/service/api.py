@@ -162,6 +162,16 @@ def create_app(state: APIState | None = None, runtime_factory=None) -> FastAPI:
 
     async def _generate(rt, text, sp, stream: bool, model: str, chat: bool):
         loop = asyncio.get_running_loop()
+        # vLLM's contract (reference server flags, helm/templates/qwen-deployment.yaml:30-31): a prompt that
+        # does not fit max_model_len is a 400, never a silently shortened prompt
+        ids = rt.tokenizer.encode(text)
+        eng = getattr(rt.runner, "engine", None)
+        mml = getattr(getattr(eng, "cfg", None), "max_model_len", None)
+        if mml and len(ids) >= mml:
+            from ..engine.llm_engine import PromptTooLongError
+
+            raise HTTPException(400, str(PromptTooLongError(len(ids), mml)))
+        text = ids
         rid = f"{'chatcmpl' if chat else 'cmpl'}-{uuid.uuid4().hex}"
         created = int(time.time())
         if not stream:

@@ -85,3 +85,6 @@ CLUSTER_DISPATCH = Counter("grag_cluster_dispatched_jobs_total", "Jobs dispatche
 INDEX_DEGRADED_ROUNDS = Counter("rag_index_degraded_rounds_total",
                                 "Sharded retrieval rounds answered without every shard (recall dropped)", ["table"],
                                 registry=REGISTRY)
+PROMPT_TRUNCATIONS = Counter("grag_llm_prompt_truncations_total",
+                             "Agent / ingest prompts whose middle context was cut to fit max_model_len",
+                             registry=REGISTRY)

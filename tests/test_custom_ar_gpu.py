@@ -53,6 +53,44 @@ def test_oneshot_simulated_ranks(dev, W):
             c.close()
 
 
+def test_oneshot_f32_sum_and_gather_simulated_ranks(dev):
+    """The TP sampler's exchanges on the same communicator as the bf16 all-reduce: fp32 sums
+    (histograms) bit-identical on every rank, and all-gathers in rank order, mixed in one epoch
+    sequence (what one TP decode step issues)."""
+    from githubrepostorag_amd.parallel.custom_ar import IpcAllReduce
+
+    W = 2
+    comms = IpcAllReduce.simulated(W, dev, slot_bytes=1 << 20, grid=32)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(W)]
+    g = torch.Generator(device="cpu").manual_seed(11)
+    try:
+        for it in range(12):
+            B = [1, 2, 7, 64, 512, 3][it % 6]
+            hs = [torch.rand(B, 256, generator=g).to(dev) for _ in range(W)]
+            ps = [torch.randn(B, 4, generator=g).to(dev) for _ in range(W)]  # 16 B per row: gather-able
+            xs = [torch.randn(B * 3584, generator=g).to(torch.bfloat16).to(dev) for _ in range(W)]
+            h_out = [h.clone() for h in hs]
+            x_out = [x.clone() for x in xs]
+            p_out = [None] * W
+            torch.cuda.synchronize()
+            for r in range(W):
+                with torch.cuda.stream(streams[r]):
+                    comms[r].all_reduce(x_out[r], stream=streams[r])
+                    comms[r].all_reduce_f32(h_out[r], stream=streams[r])
+                    p_out[r] = comms[r].all_gather(ps[r], stream=streams[r])
+            torch.cuda.synchronize()
+            href = hs[0].double() + hs[1].double()
+            for r in range(W):
+                assert not comms[r].failed(), f"rank {r} timed out waiting for peers"
+                assert torch.allclose(h_out[r].double(), href, atol=1e-6)
+                assert torch.equal(h_out[r], h_out[0])
+                assert torch.equal(p_out[r], torch.stack(ps))
+                assert torch.equal(x_out[r], x_out[0])
+    finally:
+        for c in comms:
+            c.close()
+
+
 def _hip():
     return ctypes.CDLL("libamdhip64.so")
 

@@ -252,3 +252,44 @@ def test_lazy_detokenization_matches_streaming_text():
         assert b.token_ids == a.token_ids and b.text == a.text and b.text
         assert a.text == eng._detok_all(a.token_ids)
     assert seen  # the streamed requests went through the per-token path
+
+
+def test_over_long_prompt_rejected_by_engine_and_fitted_by_agent_llm(model, tok):
+    """The prompt-length contract (vLLM --max-model-len, helm/templates/qwen-deployment.yaml:30-31): the
+    engine rejects a prompt that leaves no room to generate instead of silently keeping its tail; the
+    agent / ingest client cuts the MIDDLE (retrieved context) and keeps the head (system prompt +
+    question) and the answer cue; the OpenAI endpoint answers 400."""
+    from fastapi.testclient import TestClient
+
+    from githubrepostorag_amd.agent.llm import EngineLLM
+    from githubrepostorag_amd.config import Settings
+    from githubrepostorag_amd.engine.llm_engine import PromptTooLongError
+    from githubrepostorag_amd.engine.runner import EngineRunner
+    from githubrepostorag_amd.service.api import APIState, create_app
+
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_model_len=128, num_blocks=64, use_cuda_graph=False))
+    with pytest.raises(PromptTooLongError):
+        eng.add_request(list(range(1, 200)), GREEDY)
+    runner = EngineRunner(eng)
+    try:
+        llm = EngineLLM(runner, tok, max_tokens=8, mode="worker", timeout_s=60.0)
+        ids = list(range(1, 300))
+        fitted = llm.fit(ids, 8)
+        assert len(fitted) <= 120 and fitted[:40] == ids[:40] and fitted[-20:] == ids[-20:]
+        assert llm.fit(ids[:50], 8) == ids[:50]
+        prompt = "SYSTEM RULES. Question: where are widgets?\n\nContext:\n" + "block text " * 400 + "\n\nAnswer:"
+        r = llm.complete(prompt, temperature=0.0)
+        assert not r.error and isinstance(r.text, str)
+
+        class RT:  # the OpenAI endpoint over this runner
+            settings = Settings(index_dir=None, data_dir=None, job_timeout_s=30.0)
+            tokenizer = tok
+
+        RT.runner = runner
+        with TestClient(create_app(APIState(runtime=RT()))) as client:
+            bad = client.post("/v1/completions", json={"prompt": "x " * 400, "max_tokens": 4})
+            assert bad.status_code == 400 and "maximum context length is 128" in bad.json()["detail"]
+            ok = client.post("/v1/completions", json={"prompt": "hello", "max_tokens": 4, "temperature": 0})
+            assert ok.status_code == 200 and ok.json()["choices"][0]["finish_reason"] in ("length", "stop")
+    finally:
+        runner.shutdown()
