@@ -44,8 +44,29 @@ import sys
 import time
 
 
+# BASELINE.json configs as flag presets (explicit flags still win: the preset only fills defaults).
+#   c1  plumbing floor, no GPU: tiny synthetic corpus, MiniLM-L6 encoder on CPU, brute-force (flat) cosine,
+#       GPT-2-small greedy answers (reference default encoder: rag_shared/config.py:24)
+#   c2  Qwen2-1.5B + bge-base, 1M-vector brute-force cosine-GEMM index, one MI355X bf16
+#   c3  Qwen2-7B TP=1 + bge-large, 10M-vector IVF sharded DP=N (the headline; the flag defaults)
+#   c4  Qwen2-72B TP=8 + 100M-vector index, concurrent ingest + query (needs the 8-GPU node)
+#   c5  3-round refinement loop on Qwen2-7B: the agent phase is the measured workload (jobs/s, SSE TTFT)
+PRESETS = {
+    "c1": dict(model="gpt2", encoder="all-minilm-l6-v2", index_kind="flat", index_size=20_000, batch=8,
+               prompt_len=256, gen_len=32, inflight=2, arrival_groups=2, greedy=1, cpu=1, ingest_files=8,
+               ingest_ref_cap_files=0, ingest_seqs=16, agent_jobs=16, agent_concurrency=4, agent_synth_len=32,
+               agent_gen_len=16, steps=2, warmup=1),
+    "c2": dict(model="qwen2-1.5b", encoder="bge-base-en-v1.5", index_kind="flat", index_size=1_000_000),
+    "c3": dict(),
+    "c4": dict(model="qwen2-72b", tp=8, index_size=100_000_000, nlist=16384, nprobe=64),
+    "c5": dict(agent_jobs=512, agent_concurrency=256, agent_synth_len=256),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", default=None, choices=sorted(PRESETS),
+                    help="a BASELINE.json config (c1..c5, see PRESETS); explicit flags override its values")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
@@ -107,8 +128,29 @@ def parse():
                     help="1: the harness caps the decode window to one step while an arrival's retrieval is in "
                          "flight (an admission policy of this bench loop; the serving runner's equivalent, "
                          "GRAG_ARRIVAL_WINDOW, is off by default).  Reported as ttft_admission_policy")
+    ap.add_argument("--greedy", type=int, default=0,
+                    help="1: greedy answers (temperature 0; BASELINE config 1) instead of the reference worker's "
+                         "temperature 0.4 / top_p 0.8 / repetition_penalty 1.2")
+    ap.add_argument("--cpu", type=int, default=0, help="1: run on the host even if a GPU is visible (config 1)")
+    ap.add_argument("--kv-cache-gb", type=float, default=None,
+                    help="KV pool of the serving engine in GiB (default: half the free HBM); several ranks "
+                         "sharing one GPU (a rehearsal) split the card with it")
+    ap.add_argument("--ingest-kv-gb", type=float, default=None, help="KV pool of the ingest engine in GiB")
+    ap.add_argument("--agent-sweep", default="",
+                    help="comma list of agent concurrencies (per GPU) to sweep after the agent phase: "
+                         "agent_saturation in the JSON (jobs/s and SSE first-token p50 at each)")
+    ap.add_argument("--serving-steps", type=int, default=-1,
+                    help="timed steps of the same workload through the SERVING loop (engine/runner.py "
+                         "EngineRunner thread, arrivals submitted from the retrieval thread under the runner's "
+                         "admission hint): serving_runner in the JSON.  -1: --steps; 0: skip")
     ap.add_argument("--out", default=None)
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.preset:
+        explicit = {a.split("=", 1)[0].lstrip("-").replace("-", "_") for a in sys.argv[1:] if a.startswith("--")}
+        for k, v in PRESETS[args.preset].items():
+            if k not in explicit:
+                setattr(args, k, v)
+    return args
 
 
 def _free_port() -> int:
@@ -170,6 +212,9 @@ def main():
         sys.exit(spawn_ranks(args.gpus))
     if args.switch_interval > 0:
         sys.setswitchinterval(args.switch_interval)
+    if args.cpu:  # before torch initialises HIP: this process never touches a GPU
+        os.environ["HIP_VISIBLE_DEVICES"] = ""
+        os.environ["CUDA_VISIBLE_DEVICES"] = ""
     import torch
 
     from githubrepostorag_amd.parallel import comm
@@ -208,8 +253,8 @@ def main():
     from githubrepostorag_amd.engine.sequence import SamplingParams
     from githubrepostorag_amd.engine.tokenizer import load_tokenizer
     from githubrepostorag_amd.index.sharded import ShardedIndex
+    from githubrepostorag_amd.models import build_decoder
     from githubrepostorag_amd.models.configs import decoder_config
-    from githubrepostorag_amd.models.qwen2 import Qwen2Model
     from githubrepostorag_amd.utils import synthetic
 
     def log(*a):
@@ -218,7 +263,10 @@ def main():
 
     t_setup = time.perf_counter()
     dcfg = decoder_config(args.model)
-    model = Qwen2Model(dcfg, device=dev, seed=1, tp=tp_group)
+    model = build_decoder(dcfg, device=dev, seed=1, tp=tp_group,  # Qwen2 or GPT-2 by the config's arch
+                          **({} if dev.type == "cuda" else {"dtype": torch.float32}))
+    if args.quant == "w4" and not hasattr(model, "quantize_w4"):
+        raise SystemExit(f"--quant w4 needs a Qwen2 decoder, not {dcfg.arch}")
     w4_bytes = model.quantize_w4() if args.quant == "w4" else 0
     if w4_bytes:
         log(f"W4A16 decode weights: {w4_bytes / 1e9:.2f} GB packed (+ bf16 copy of the same values for prefill)")
@@ -242,6 +290,7 @@ def main():
     max_len = args.prompt_len + args.gen_len + 64
     if args.agent_jobs > 0:  # the agent phase's synthesize prompts carry 5 context blocks
         max_len = max(max_len, 4096)
+    max_len = min(max_len, dcfg.max_position)  # GPT-2: 1024 positions
     D = max(1, min(args.inflight, args.gen_len))
     A = max(1, min(args.arrival_groups, args.batch, max(1, args.gen_len // D)))
     while args.batch % A:
@@ -253,11 +302,12 @@ def main():
     if live > max(gsizes):  # deeper pipelines: decode graphs up to the live-sequence count, 128-row buckets
         gsizes = tuple(sorted({*gsizes, *range(max(gsizes) + 128, live + 127, 128)}))
     eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=live, max_num_batched_tokens=args.max_batched_tokens,
-                                             mixed_batches=bool(args.mixed),
+                                             mixed_batches=bool(args.mixed), kv_cache_gb=args.kv_cache_gb,
                                              max_model_len=max_len, use_cuda_graph=not args.no_graph,
                                              seed=dp_rank, graph_batch_sizes=gsizes))
-    sp = SamplingParams(max_tokens=args.gen_len, temperature=0.4, top_p=0.8, repetition_penalty=1.2,
-                        ignore_eos=True)
+    sp = (SamplingParams(max_tokens=args.gen_len, temperature=0.0, ignore_eos=True) if args.greedy else
+          SamplingParams(max_tokens=args.gen_len, temperature=0.4, top_p=0.8, repetition_penalty=1.2,
+                         ignore_eos=True))
     sys_prompt = ("You are a senior developer assistant. Answer using the provided context blocks. "
                   "Cite blocks as [1], [2]. If the specific information needed is not in the context, "
                   "say so clearly and suggest looking in specific repos/modules that might contain the answer.")
@@ -485,6 +535,13 @@ def main():
             eng.pop(r)
     log(f"serving: {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms, {ms_step:.1f} ms/step")
     eng_stats = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()}
+
+    # ---- the same workload through the serving loop (reported next to the harness numbers)
+    serving_res = None
+    n_srv = args.steps if args.serving_steps < 0 else args.serving_steps
+    if n_srv > 0 and tp == 1 and pool is not None:
+        serving_res = serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, n_srv, dev, dp_size, group,
+                                           world, log)
     if pool is not None:
         pool.shutdown(wait=True)
     log("per-step phases (ms, timed steps): " + ", ".join(f"{k}={v / args.steps * 1000:.1f}"
@@ -518,7 +575,9 @@ def main():
         comm.barrier()
         n_docs, secs, ingest_stages = run_ingest_bench(model, tok, emb, args.ingest_files, seed=dp_rank,
                                                        max_num_seqs=args.ingest_seqs, use_graph=not args.no_graph,
-                                                       mixed_batches=bool(args.ingest_mixed), tp=tp_group)
+                                                       mixed_batches=bool(args.ingest_mixed), tp=tp_group,
+                                                       kv_cache_gb=args.ingest_kv_gb,
+                                                       max_model_len=min(8192, dcfg.max_position))
         tt = torch.tensor([secs], dtype=torch.float64, device=dev)
         if world > 1:
             import torch.distributed as dist
@@ -530,7 +589,7 @@ def main():
             n2, secs2, st2 = run_ingest_bench(model, tok, emb, args.ingest_ref_cap_files, seed=1000 + dp_rank,
                                               max_num_seqs=args.ingest_seqs, use_graph=not args.no_graph,
                                               mixed_batches=bool(args.ingest_mixed), tp=tp_group, token_cap=args.ingest_ref_cap,
-                                              max_model_len=11712)
+                                              max_model_len=min(11712, dcfg.max_position), kv_cache_gb=args.ingest_kv_gb)
             tt2 = torch.tensor([secs2], dtype=torch.float64, device=dev)
             if world > 1:
                 import torch.distributed as dist
@@ -564,8 +623,11 @@ def main():
             "ingest_docs_per_s": None if ingest_dps is None else round(ingest_dps, 3),
             "ingest_docs_per_s_ref_cap": None if ingest_ref is None else ingest_ref["docs_per_s"],
             "config": {
+                "preset": args.preset or "c3",
                 "model": f"{args.model} TP={tp} + {args.encoder}, {args.index_size}-vec {args.index_kind} index "
                          f"(nlist={args.nlist}, nprobe={args.nprobe}) sharded dp{world}",
+                "sampling": "greedy" if args.greedy else "temperature 0.4, top_p 0.8, repetition_penalty 1.2",
+                "device": dev.type,
                 "global_batch": args.batch * dp_size,
                 "inflight_batches": D,
                 "mixed_batches": bool(args.mixed),
@@ -595,12 +657,14 @@ def main():
             "tp_sampler_bytes_per_decode_step": None if tp == 1 else __import__(
                 "githubrepostorag_amd.ops.sampling", fromlist=["x"]).tp_sampling_bytes(
                 args.batch * D, tp, dcfg.vocab_size, 2),
+            "serving_runner": serving_res,
             "ingest_stage_s": ingest_stages,
             "ingest_ref_cap": ingest_ref,
             "e2e_ttft_p50_ms": None if agent_res is None else agent_res["e2e_ttft_p50_ms"],
             "e2e_ttft_p90_ms": None if agent_res is None else agent_res["e2e_ttft_p90_ms"],
             "agent_jobs_per_s": None if agent_res is None else agent_res["agent_jobs_per_s"],
             "agent_steady_jobs_per_s": None if agent_res is None else agent_res.get("steady_jobs_per_s"),
+            "agent_saturation": None if agent_res is None else agent_res.get("agent_saturation"),
             "agent_e2e": agent_res,
         }
         line = json.dumps(res)
@@ -612,6 +676,85 @@ def main():
         import torch.distributed as dist
 
         dist.destroy_process_group()
+
+
+def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, dp_size, group, world, log):
+    """The headline workload through the product's serving loop: the engine steps on its own
+    EngineRunner thread (engine/runner.py, as ``serve`` runs it) and this thread only submits and waits.
+    Each group's retrieval runs on the helper thread inside ``runner.arrival()`` (the admission hint:
+    decode replays go one step at a time until its prompts are submitted), then its prompts are submitted
+    from that thread, as a server's request threads do.  Same arrival pipeline as the harness (U groups
+    of u queries in flight, staggered by S tokens); one step = A arrivals, A oldest groups complete.
+    Returns qps / p50 TTFT next to the harness's (submission -> first token)."""
+    import collections
+
+    import torch
+
+    from githubrepostorag_amd.engine.runner import EngineRunner
+    from githubrepostorag_amd.parallel import comm
+
+    runner = EngineRunner(eng, watchdog_s=0)
+    inflight = collections.deque()
+
+    def arrive():
+        with runner.arrival():
+            prompts, t_sub, _ = prepare()
+            hs = [runner.submit(p, sp) for p in prompts]
+        return hs, t_sub
+
+    def ntok(h):
+        s_ = eng.get(h.req_id)
+        return args.gen_len if s_ is None else len(s_.output_ids)
+
+    def sub_step():
+        fut = pool.submit(arrive)
+        hs, t_sub = inflight.popleft()
+        for h in hs:
+            h.wait(600)
+        inflight.append(fut.result())
+        return [h.result.first_token_at - t_sub for h in hs]
+
+    try:
+        for k in range(U - 1):  # fill, staggered like the harness
+            inflight.append(arrive())
+            d = max(1, round((k + 1) * S) - round(k * S))
+            t0 = time.perf_counter()
+            while min(ntok(h) for h in inflight[-1][0]) < 1 + d and time.perf_counter() - t0 < 120:
+                time.sleep(0.0005)
+        inflight.append(arrive())
+        for _ in range(max(1, args.warmup) * A):
+            sub_step()
+        comm.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        ttfts = []
+        for _ in range(steps * A):
+            ttfts += sub_step()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        comm.barrier()
+        elapsed = time.perf_counter() - t_start
+        for hs, _ in inflight:  # drain (untimed)
+            for h in hs:
+                h.wait(600)
+    finally:
+        runner.shutdown()
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    allt = [ttfts]
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        allt = group.all_gather(torch.tensor(ttfts, dtype=torch.float64, device=dev)).cpu().tolist()
+    elapsed = float(t.item())
+    qps = args.batch * steps * dp_size / elapsed
+    p50 = statistics.median([x for r in allt for x in r]) * 1000.0
+    log(f"serving loop (EngineRunner + admission hint): {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms")
+    return {"value": round(qps, 3), "p50_ttft_ms": round(p50, 2), "steps": steps,
+            "ms_per_step": round(elapsed / steps * 1000.0, 2),
+            "loop": "engine/runner.py EngineRunner thread; arrivals submitted from the retrieval thread under "
+                    "runner.arrival() (1-step decode replays while a retrieval is in flight)"}
 
 
 def _scope_tables(store, emb, corpus, rank, world, dev):
@@ -653,8 +796,10 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_gr
     from githubrepostorag_amd.utils import synthetic
 
     conc = args.agent_concurrency
+    levels = [int(x) for x in args.agent_sweep.split(",") if x.strip()]
+    slots = max([conc, *levels])  # a replica's job slots: the largest concurrency it will be driven at
     s = Settings(qwen_model=args.model, embed_model=args.encoder, qwen_max_output=args.agent_gen_len,
-                 synth_max_tokens=args.agent_synth_len, worker_max_jobs=conc, max_rag_attempts=3,
+                 synth_max_tokens=args.agent_synth_len, worker_max_jobs=slots, max_rag_attempts=3,
                  default_namespace=corpus.namespace, job_timeout_s=1800, llm_retries=0, stream_tokens=True,
                  index_kind=args.index_kind, nlist=args.nlist, nprobe=args.nprobe, embed_batch_window_ms=1.0,
                  data_dir=None, seed=rank)
@@ -679,10 +824,15 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_gr
 
     warm = [mix(500_000 + i) for i in range(min(n_conc, 16 * world))]
     qs = [mix(i) for i in range(n_jobs)]
+    # saturation sweep: 2 x concurrency jobs per level (>= 64), fresh questions for each
+    sweep = []
+    for j, c in enumerate(levels):
+        n = max(64, 2 * c) * dp_size
+        sweep.append(([mix(10_000_000 * (j + 1) + i) for i in range(n)], c * dp_size))
     res = None
     try:
         if world == 1:
-            res = run_e2e(create_app(APIState(runtime=rt)), qs, n_conc, warmup=warm)
+            res = run_e2e(create_app(APIState(runtime=rt)), qs, n_conc, warmup=warm, sweep=sweep)
         else:
             import torch.distributed as dist
 
@@ -698,7 +848,7 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_gr
             dist.broadcast_object_list(obj, src=0)
             addr, key = obj[0]
             th = threading.Thread(target=run_replica, args=(rt, addr, key, rank),
-                                  kwargs={"shards": world, "capacity": conc if leader else 0},
+                                  kwargs={"shards": world, "capacity": slots if leader else 0},
                                   name="bench-replica", daemon=True)
             th.start()
             if rank == 0:
@@ -710,7 +860,7 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_gr
                 state = APIState(runtime=ClusterRuntimeView(hub, s), queue=hub.queue, events=events,
                                  flags=hub.flags)
                 try:
-                    res = run_e2e(create_app(state), qs, n_conc, warmup=warm)
+                    res = run_e2e(create_app(state), qs, n_conc, warmup=warm, sweep=sweep)
                     res["replicas"] = hub.health()["replicas"]
                 finally:
                     hub.close()  # replicas return from run_replica

@@ -26,6 +26,7 @@ returns, the engine is marked healthy again.
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 import threading
@@ -92,6 +93,7 @@ class EngineRunner:
         self._step_t0: float | None = None
         self._step_failed: BaseException | None = None  # TP: reported in the next control all-reduce
         self._ar_failed = False
+        self._expecting = 0  # admission hints in flight (arrival())
         self.ctrl_stats = {"iterations": 0, "bytes": 0, "payloads": 0}
         self._thread = threading.Thread(target=self._loop if self.leader else self.follow, name="grag-engine",
                                         daemon=True)
@@ -115,7 +117,25 @@ class EngineRunner:
             self._cv.notify()
         return h
 
+    @contextlib.contextmanager
+    def arrival(self):
+        """Admission hint: the caller will submit a prompt at the end of this block (a RAG query between
+        its retrieval and its generation).  While any hint is open, decode replays run ONE step each, so
+        the prompt's prefill starts about one decode step after it is submitted instead of after a whole
+        multi-step window — the serving-loop form of the headline bench's admission policy (bench.py
+        ``--arrival-cap``).  Under TP the leader's window is broadcast, so followers replay alike."""
+        with self._cv:
+            self._expecting += 1
+        try:
+            yield self
+        finally:
+            with self._cv:
+                self._expecting -= 1
+                self._cv.notify()
+
     def _window(self) -> int | None:
+        if self._expecting > 0:
+            return 1
         if self.ARRIVAL_WINDOW <= 0:
             return None
         return self.ARRIVAL_WINDOW if time.monotonic() - self._last_submit < self.ARRIVAL_RECENT_S else None

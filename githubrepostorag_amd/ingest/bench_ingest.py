@@ -28,7 +28,8 @@ from .readers import Document
 
 def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs: int = 256,
                      max_model_len: int = 8192, use_graph: bool = True, summary_tokens: int = 128,
-                     mixed_batches: bool = False, tp=None, token_cap: int | None = None) -> tuple[int, float, dict]:
+                     mixed_batches: bool = False, tp=None, token_cap: int | None = None,
+                     kv_cache_gb: float | None = None) -> tuple[int, float, dict]:
     """Returns (documents ingested, seconds, per-stage seconds).
 
     ``token_cap``: one generation cap for every LLM call instead of the per-call lengths above (the
@@ -42,7 +43,7 @@ def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs:
     sizes = tuple(sorted({*EngineConfig.graph_batch_sizes, *range(256, max_num_seqs + 1, 128), max_num_seqs}))
     eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max_num_seqs, max_num_batched_tokens=16384,
                                              max_model_len=max_model_len, use_cuda_graph=use_graph, seed=seed,
-                                             mixed_batches=mixed_batches,
+                                             mixed_batches=mixed_batches, kv_cache_gb=kv_cache_gb,
                                              graph_batch_sizes=tuple(b for b in sizes if b <= max_num_seqs)))
     if use_graph and dev.type == "cuda":
         eng.warmup_graphs()

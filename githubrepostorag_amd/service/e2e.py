@@ -98,8 +98,10 @@ def _pct(xs: list[float], p: float) -> float | None:
 
 
 def run_e2e(app, questions: list[str], concurrency: int, warmup: list[str] | None = None,
-            timeout_s: float = 1800.0) -> dict:
-    """Serve ``app`` on localhost and push ``questions`` through the HTTP API."""
+            timeout_s: float = 1800.0, sweep: list[tuple[list[str], int]] | None = None) -> dict:
+    """Serve ``app`` on localhost and push ``questions`` through the HTTP API at ``concurrency``.
+    ``sweep``: further (questions, concurrency) runs on the same server, one after the other (a
+    saturation curve); their summaries go to ``agent_saturation``."""
     with ServerThread(app) as srv:
         loop = asyncio.new_event_loop()
         try:
@@ -108,8 +110,20 @@ def run_e2e(app, questions: list[str], concurrency: int, warmup: list[str] | Non
             t0 = time.perf_counter()
             res = loop.run_until_complete(_drive(srv.url, questions, concurrency, timeout_s))
             wall = time.perf_counter() - t0
+            curve = []
+            for qs, conc in sweep or []:
+                t1 = time.perf_counter()
+                r = loop.run_until_complete(_drive(srv.url, qs, conc, timeout_s))
+                curve.append(dict(concurrency=conc, **_summary(r, time.perf_counter() - t1)))
         finally:
             loop.close()
+    out = _summary(res, wall)
+    if sweep:
+        out["agent_saturation"] = curve
+    return out
+
+
+def _summary(res: list[dict], wall: float) -> dict:
     ttft = [(r["first_token"] - r["t0"]) * 1e3 for r in res if r["first_token"] is not None]
     lat = [(r["final"] - r["t0"]) * 1e3 for r in res if r["final"] is not None]
     # saturation throughput (jobs/s at saturation): completions per second over the middle

@@ -1,0 +1,58 @@
+#!/bin/bash
+# One parametrised GPU session runner (replaces round 3's per-session scripts/gpu_r3*.sh).
+#
+#   TAG=r4a bash scripts/gpu_run.sh STEP [STEP ...]
+#
+# Steps (each under its own time limit, logs in gpurun_out/<TAG>_<step>.log):
+#   tests[=SEL]      pytest -m gpu over SEL (default: tests)              (600 s)
+#   smoke            __graft_entry__.smoke()                              (300 s)
+#   bench[=ARGS]     python bench.py ARGS (',' separates args)            (900 s)
+#   preset=cN        python bench.py --preset cN (BASELINE config N)      (900 s)
+#   dp2              shared-GPU DP rehearsal: bench --gpus 2, gloo, both ranks on cuda:0
+#   tp2              shared-GPU TP rehearsal: bench --gpus 2 --tp 2 (IPC all-reduce + vocab-parallel
+#                    sampler in the decode graphs, lockstep ingest and agent)
+#   sweep=ARGS       bench with --agent-sweep (agent saturation curve)
+#   prof             rocprofv3 --kernel-trace --stats over a 2-step bench (scripts/profile_bench.sh)
+#
+# A step that exits 0 or 1 (a clean Python failure) lets the next one run; a fault, abort, segfault or
+# time limit (124 / 134 / 137 / 139) ends the session there (no more GPU work after a GPU fault).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+mkdir -p gpurun_out
+TAG=${TAG:-run}
+worst=0
+
+run() {  # run LIMIT NAME CMD...
+  local lim=$1 name=$2
+  shift 2
+  local log="gpurun_out/${TAG}_${name}.log"
+  echo "== $name: $*"
+  timeout -k 10 "$lim" "$@" > "$log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  grep -E '^\{' "$log" | cut -c1-900 || true
+  grep -E "passed|failed|error|serving|agent e2e|ingest:|smoke ok|Traceback" "$log" | tail -6 || true
+  [ $rc -ne 0 ] && tail -25 "$log"
+  [ $rc -gt $worst ] && worst=$rc
+  case $rc in 0|1|2) return 0 ;; *) echo "== stopping: $name ended with $rc"; exit $rc ;; esac
+}
+
+REH="--steps 2 --warmup 1 --kv-cache-gb 48 --ingest-kv-gb 24 --ingest-files 48 --ingest-ref-cap-files 0 --agent-jobs 64"
+for step in "$@"; do
+  key=${step%%=*}
+  val=""
+  [[ "$step" == *=* ]] && val=${step#*=}
+  case $key in
+    tests) run 600 "tests" python -u -m pytest ${val:-tests} -m gpu -x -q --timeout 240 --timeout-method thread ;;
+    smoke) run 300 smoke python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run 900 bench python -u bench.py ${val//,/ } ;;
+    preset) run 900 "preset_$val" python -u bench.py --preset "$val" --out "gpurun_out/${TAG}_preset_$val.json" ;;
+    dp2) run 900 dp2 env GRAG_DIST_BACKEND=gloo python -u bench.py --gpus 2 $REH ${val//,/ } ;;
+    tp2) run 900 tp2 env GRAG_DIST_BACKEND=gloo python -u bench.py --gpus 2 --tp 2 $REH ${val//,/ } ;;
+    sweep) run 1100 sweep python -u bench.py --no-ingest --agent-sweep "${val:-64,256,512,1024}" --steps 2 --warmup 1 ;;
+    prof) run 700 prof bash scripts/profile_bench.sh ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+exit $worst
