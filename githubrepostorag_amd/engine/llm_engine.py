@@ -34,7 +34,7 @@ from ..ops.attention import KV_TILE, AttnMetadata
 from ..ops.sampling import SamplerState, reset_slots, sample, sample_tp
 from .scheduler import KVCacheManager, Scheduler
 from .sequence import Completion, SamplingParams, Sequence, SeqStatus
-from ..utils.gpu_guard import gpu_guard
+from ..utils.gpu_guard import gpu_guard, no_gc
 from .tokenizer import IncrementalDetokenizer
 
 log = logging.getLogger(__name__)
@@ -719,7 +719,7 @@ class LLMEngine:
         graph = torch.cuda.CUDAGraph()
         # thread_local: API / retrieval threads keep launching (and syncing) on
         # their own streams while the engine thread captures
-        with torch.cuda.graph(graph, pool=self._graph_pool, capture_error_mode="thread_local"):
+        with no_gc(), torch.cuda.graph(graph, pool=self._graph_pool, capture_error_mode="thread_local"):
             self._decode_forward(v, B, nsplit, split_len, out, K)
         torch.cuda.synchronize()
         self.sampler.rng.copy_(rng_save)

@@ -23,6 +23,7 @@ from ..ops.elementwise import ACT_GELU, POOL_CLS, POOL_MEAN, bias_act, pool_l2no
 from ..ops import gemm as _tile
 from ..ops.linear import linear
 from ..ops.norm import bert_embed_ln, layernorm
+from ..utils.gpu_guard import no_gc
 from .configs import EncoderConfig
 
 
@@ -207,7 +208,7 @@ class EncoderGraphs:
             self.enc.forward(ids, pos, starts, lens, L, want_bf16=True)  # eager warm-up sizes workspaces
             s.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
+            with no_gc(), torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
                 outf, outb = self.enc.forward(ids, pos, starts, lens, L, want_bf16=True)
         cur.wait_stream(s)
         self.stats["captures"] += 1

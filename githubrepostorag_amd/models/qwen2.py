@@ -25,6 +25,7 @@ the FFN and the vocab are sharded per rank; two all-reduces per layer.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -35,6 +36,8 @@ from ..ops.linear import linear, linear_deferred
 from ..ops.norm import embed_gather, rmsnorm
 from ..parallel.comm import Group
 from .configs import DecoderConfig
+
+FFN_PAD = int(os.environ.get("GRAG_FFN_PAD", "64"))  # per-rank FFN width granule (models/qwen2.py Qwen2Model)
 
 
 class _Layer:
@@ -60,7 +63,12 @@ class Qwen2Model:
             self.kv_head0 = tr // (ts // cfg.num_kv_heads)
         self.head_dim = cfg.head_dim
         assert cfg.intermediate_size % ts == 0
-        self.inter = cfg.intermediate_size // ts
+        # the per-rank FFN width, zero-padded up to a multiple of FFN_PAD (default 64) so every MLP GEMM
+        # takes the owned kernels (K % 64): Qwen2-72B at TP=8 has 29568 / 8 = 3696 -> 3712.  The padded
+        # gate/up rows and down_proj columns are zero, so silu(0) * 0 adds nothing: outputs are unchanged.
+        self.inter_real = cfg.intermediate_size // ts
+        pad = max(1, FFN_PAD)
+        self.inter = -(-self.inter_real // pad) * pad
         # gate/up interleaved in 32-row blocks for the fused SwiGLU GEMM epilogue
         self.gu_interleaved = self.inter % 32 == 0
         self.vocab_shard = -(-cfg.vocab_size // ts)
@@ -100,8 +108,14 @@ class Qwen2Model:
             L.qkv_b = self._rand(g, qkv_rows, std=std) if cfg.qkv_bias else None
             L.o_w = self._rand(g, H, self.hq * D, std=std)
             L.post_norm = torch.ones(H, dtype=self.dtype, device=dev)
-            L.gu_w = self._rand(g, 2 * self.inter, H, std=std)
-            L.down_w = self._rand(g, H, self.inter, std=std)
+            if self.inter == self.inter_real:
+                L.gu_w = self._rand(g, 2 * self.inter, H, std=std)
+                L.down_w = self._rand(g, H, self.inter, std=std)
+            else:
+                wg, wu = self._pad_ffn(self._rand(g, self.inter_real, H, std=std)), \
+                    self._pad_ffn(self._rand(g, self.inter_real, H, std=std))
+                L.gu_w = interleave_gate_up(wg, wu) if self.gu_interleaved else torch.cat([wg, wu], 0).contiguous()
+                L.down_w = self._pad_ffn(self._rand(g, H, self.inter_real, std=std), dim=1)
             self.layers.append(L)
         self.norm = torch.ones(H, dtype=self.dtype, device=dev)
         if cfg.tie_word_embeddings:
@@ -109,6 +123,15 @@ class Qwen2Model:
         else:
             self.lm_head = self._pad_rows(self._rand(g, min(self.vocab_shard, cfg.vocab_size - self.vocab0), H,
                                                      std=std))
+
+    def _pad_ffn(self, t: torch.Tensor, dim: int = 0) -> torch.Tensor:
+        """Zero-pad an FFN weight from the real per-rank width to ``self.inter`` along ``dim``."""
+        extra = self.inter - t.shape[dim]
+        if extra <= 0:
+            return t.contiguous()
+        shape = list(t.shape)
+        shape[dim] = extra
+        return torch.cat([t, torch.zeros(shape, dtype=t.dtype, device=t.device)], dim).contiguous()
 
     def _pad_rows(self, t: torch.Tensor) -> torch.Tensor:
         # equal-sized vocab shards so the TP all-gather of logits is one collective
@@ -128,7 +151,7 @@ class Qwen2Model:
 
         q0, q1 = self.tp.rank * self.hq * D, (self.tp.rank + 1) * self.hq * D
         k0, k1 = self.kv_head0 * D, (self.kv_head0 + self.hkv) * D
-        i0, i1 = self.tp.rank * self.inter, (self.tp.rank + 1) * self.inter
+        i0, i1 = self.tp.rank * self.inter_real, (self.tp.rank + 1) * self.inter_real
         self.embed = get("model.embed_tokens.weight")
         self.layers = []
         for i in range(cfg.num_layers):
@@ -144,9 +167,10 @@ class Qwen2Model:
                 L.qkv_b = None
             L.o_w = get(p + "self_attn.o_proj.weight")[:, q0:q1].contiguous()
             L.post_norm = get(p + "post_attention_layernorm.weight")
-            wg, wu = get(p + "mlp.gate_proj.weight")[i0:i1], get(p + "mlp.up_proj.weight")[i0:i1]
+            wg = self._pad_ffn(get(p + "mlp.gate_proj.weight")[i0:i1])
+            wu = self._pad_ffn(get(p + "mlp.up_proj.weight")[i0:i1])
             L.gu_w = interleave_gate_up(wg, wu) if self.gu_interleaved else torch.cat([wg, wu], 0).contiguous()
-            L.down_w = get(p + "mlp.down_proj.weight")[:, i0:i1].contiguous()
+            L.down_w = self._pad_ffn(get(p + "mlp.down_proj.weight")[:, i0:i1], dim=1)
             self.layers.append(L)
         self.norm = get("model.norm.weight")
         head = self.embed if cfg.tie_word_embeddings or "lm_head.weight" not in sd else get("lm_head.weight")

@@ -259,6 +259,42 @@ def gemm_splitk(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
     return y.to(x.dtype)
 
 
+def kernel_for(M: int, N: int, K: int, tile_ok: bool = True, dev: torch.device | None = None) -> str:
+    """The kernel linear() runs a bf16 [M, K] x [N, K]^T projection on: "decode" / "tile" / "tile_prefill"
+    (owned MFMA kernels of ops/gemm.py), "skinny" / "stream" (owned weight-streaming kernels here),
+    "splitk" (K-sliced library bmm) or "library" (hipBLASLt).  ``tile_ok``: the operands meet
+    ops/gemm.supported (alignment, K % 64).  ``dev``: check that a hipGraph capture in progress can use
+    the split-K / stream-K workspaces (None: plan as in steady state, workspaces ready)."""
+    capturing = dev is not None and torch.cuda.is_current_stream_capturing()
+    if tile_ok:
+        if TILE_MIN_M <= M and _tile.dec_plan(M, N, K) is not None and (
+                dev is None or _tile.dec_capture_ok(dev, M, N, K)):
+            return "decode"
+        if use_tile(M, N, K) and (dev is None or _tile.capture_ok(dev, M, N, K)):
+            return "tile"
+        if M >= _tile.PREFILL_MIN_M and _tile.prefill_plan(M, N, K) is not None and (
+                dev is None or _tile.capture_ok(dev, M, N, K)):
+            return "tile_prefill"
+    if splitk_parts(M, N, K):
+        return "splitk"
+    stream_ready = not capturing or _WS.ready(dev, M, N, K)
+    choice = measured_choice(M, N, K)
+    if choice == "library":
+        return "library"
+    if choice == "skinny" and K % 64 == 0:
+        return "skinny"
+    if choice == "stream" and K % 16 == 0 and N % 4 == 0 and stream_ready:
+        return "stream"
+    if K % 64 == 0 and use_skinny(M, N, K):
+        return "skinny"
+    if K % 16 == 0 and N % 4 == 0 and use_stream(M, N, K) and stream_ready:
+        return "stream"
+    return "library"
+
+
+OWNED_KINDS = ("decode", "tile", "tile_prefill", "skinny", "stream")
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
     """y = x @ w.T (+ b); w is [out, in] (K-contiguous, TN GEMM)."""
     if not x.is_cuda:
@@ -272,30 +308,19 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> t
             and x.stride(1) == 1 and w.stride(1) == 1):
         M, K = x.shape
         N = w.shape[0]
-        if (TILE_MIN_M <= M and _tile.supported(x, w) and _tile.dec_plan(M, N, K) is not None
-                and _tile.dec_capture_ok(x.device, M, N, K)):
+        kind = kernel_for(M, N, K, _tile.supported(x, w), x.device)
+        if kind == "decode":
             return _tile.gemm_decode(x, w, b)
-        if use_tile(M, N, K) and _tile.supported(x, w) and _tile.capture_ok(x.device, M, N, K):
+        if kind == "tile":
             return _tile.gemm(x, w, b)
-        if M >= _tile.PREFILL_MIN_M and _tile.supported(x, w):
+        if kind == "tile_prefill":
             p = _tile.prefill_plan(M, N, K)
-            if p is not None and _tile.capture_ok(x.device, M, N, K):
-                return _tile.gemm(x, w, b, ksplit=p[0], sk=p[1])
-        parts = splitk_parts(M, N, K)
-        if parts:
-            return gemm_splitk(x, w, b, parts)
-        choice = measured_choice(M, N, K)
-        if choice == "library":
-            return torch.nn.functional.linear(x, w, b)
-        if choice == "skinny" and K % 64 == 0:
+            return _tile.gemm(x, w, b, ksplit=p[0], sk=p[1])
+        if kind == "splitk":
+            return gemm_splitk(x, w, b, splitk_parts(M, N, K))
+        if kind == "skinny":
             return gemm_skinny(x, w, b)
-        if (choice == "stream" and K % 16 == 0 and N % 4 == 0
-                and (not torch.cuda.is_current_stream_capturing() or _WS.ready(x.device, M, N, K))):
-            return gemm_stream(x, w, b)
-        if K % 64 == 0 and use_skinny(M, N, K):
-            return gemm_skinny(x, w, b)
-        if (K % 16 == 0 and N % 4 == 0 and use_stream(M, N, K)
-                and (not torch.cuda.is_current_stream_capturing() or _WS.ready(x.device, M, N, K))):
+        if kind == "stream":
             return gemm_stream(x, w, b)
     return torch.nn.functional.linear(x, w, b)
 

@@ -569,7 +569,10 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
                     else:
                         loop.call_soon_threadsafe(inbox.put_nowait, msg)
             except (EOFError, OSError):
-                loop.call_soon_threadsafe(inbox.put_nowait, ("stop",))
+                try:
+                    loop.call_soon_threadsafe(inbox.put_nowait, ("stop",))
+                except RuntimeError:  # the replica loop already returned (the hub said stop)
+                    pass
 
         threading.Thread(target=reader, name="replica-reader", daemon=True).start()
         tasks = set()

@@ -69,7 +69,7 @@ async def _drive(url: str, questions: list[str], concurrency: int, timeout_s: fl
                 r.raise_for_status()
                 jid = r.json()["job_id"]
                 first = final = None
-                err = False
+                err = degraded = False
                 ntok = 0
                 async with client.stream("GET", f"/rag/jobs/{jid}/events") as resp:
                     async for line in resp.aiter_lines():
@@ -81,11 +81,14 @@ async def _drive(url: str, questions: list[str], concurrency: int, timeout_s: fl
                             ntok += 1
                             if first is None:
                                 first = now
+                        elif ev.get("event") == "retrieval":  # sharded index: a round missed a shard
+                            degraded = bool((ev.get("data") or {}).get("degraded"))
                         elif ev.get("event") == "final":
                             final = now
                             err = bool((ev.get("data") or {}).get("error"))
                             break
-                return {"t0": t0, "first_token": first, "final": final, "error": err, "tokens": ntok}
+                return {"t0": t0, "first_token": first, "final": final, "error": err, "tokens": ntok,
+                        "degraded": degraded}
 
         return await asyncio.gather(*[one(q) for q in questions])
 
@@ -139,5 +142,6 @@ def _summary(res: list[dict], wall: float) -> dict:
             "e2e_ttft_p50_ms": round(statistics.median(ttft), 1) if ttft else None,
             "e2e_ttft_p90_ms": round(_pct(ttft, 0.9), 1) if ttft else None,
             "job_latency_p50_ms": round(statistics.median(lat), 1) if lat else None,
-            "errors": sum(r["error"] for r in res), "mean_tokens_streamed": round(
+            "errors": sum(r["error"] for r in res), "degraded_jobs": sum(r.get("degraded", False) for r in res),
+            "mean_tokens_streamed": round(
                 statistics.mean(r["tokens"] for r in res), 1) if res else 0}

@@ -176,3 +176,19 @@ def set_device_of(dev) -> None:
     d = torch.device(dev)
     if d.type == "cuda":
         torch.cuda.set_device(d.index if d.index is not None else torch.cuda.current_device())
+
+
+@contextlib.contextmanager
+def no_gc():
+    """Cyclic GC off for the block (a hipGraph capture): a collection that runs in the capturing thread
+    can free an OLD graph (e.g. a dropped engine's), and destroying a graph while a stream captures is
+    an illegal call that aborts the process from the graph's destructor.  Collection resumes after."""
+    import gc
+
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()

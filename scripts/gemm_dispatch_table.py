@@ -20,6 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--models", default="qwen2-7b,qwen2-1.5b")
 ap.add_argument("--out", default="githubrepostorag_amd/tuning/gemm_dispatch_gfx950.json")
 ap.add_argument("--M", default="1,2,4,8,16,24,32,48,64,96,128")
+ap.add_argument("--merge", action="store_true", help="update the measured (N, K) rows of --out, keep the rest")
 a = ap.parse_args()
 L.enable_tuned_gemms()
 dev = torch.device("cuda")
@@ -55,11 +56,19 @@ def time_fn(fn, reps=20, rounds=5):
 
 
 shapes = set()
-for name in a.models.split(","):
+for spec in a.models.split(","):  # "model" or "model:tp" (per-rank shapes of a TP-sharded Qwen2)
+    name, _, tp = spec.partition(":")
+    tp = int(tp or 1)
     c = decoder_config(name)
-    H, I, D = c.hidden_size, c.intermediate_size, c.head_dim
-    shapes |= {((c.num_heads + 2 * c.num_kv_heads) * D, H), (H, c.num_heads * D), (2 * I, H), (H, I),
-               (c.vocab_size, H)}
+    H, D = c.hidden_size, c.head_dim
+    hq, hkv = c.num_heads // tp, max(1, c.num_kv_heads // tp)
+    from githubrepostorag_amd.models.qwen2 import FFN_PAD  # noqa: E402
+
+    I = -(-(c.intermediate_size // tp) // FFN_PAD) * FFN_PAD if tp > 1 else c.intermediate_size
+    vocab = -(-c.vocab_size // tp)
+    shapes |= {((hq + 2 * hkv) * D, H), (H, hq * D), (H, I), (-(-vocab // 8) * 8 if tp > 1 else vocab, H)}
+    if tp == 1:
+        shapes.add((2 * I, H))  # gate/up at TP>1 runs the fused SwiGLU kernels (ops/gemm.py mlp_gate_up)
 for N, K in sorted(shapes):
     ncopy = max(2, min(12, (1 << 30) // (N * K * 2) + 1))
     ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02 for _ in range(ncopy)]
@@ -88,6 +97,10 @@ for N, K in sorted(shapes):
     table[f"{N},{K}"] = rows
     del ws
 os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+if a.merge and os.path.exists(a.out):
+    old = json.load(open(a.out))
+    table = {**old.get("table", {}), **table}
+    report = {**old.get("times_us", {}), **report}
 with open(a.out, "w") as f:
     json.dump({"arch": "gfx950", "note": "fastest decode GEMM per (N,K) and batch bucket M; see scripts/"
                "gemm_dispatch_table.py", "table": table, "times_us": report}, f, indent=1)

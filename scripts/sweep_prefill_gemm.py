@@ -39,7 +39,27 @@ SHAPES = {
                    ("down", 1536, 8960, False)],
     "bge-large": [("qkv", 3072, 1024, False), ("o", 1024, 1024, False), ("ffn1", 4096, 1024, False),
                   ("ffn2", 1024, 4096, False)],
+    "bge-base": [("qkv", 2304, 768, False), ("o", 768, 768, False), ("ffn1", 3072, 768, False),
+                 ("ffn2", 768, 3072, False)],
 }
+
+
+def _tp_shapes(model: str, tp: int):
+    """Per-rank projection shapes of a TP-sharded Qwen2 (models/qwen2.py: q heads / TP, kv heads / TP or
+    one replicated, FFN zero-padded to a multiple of 64)."""
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import FFN_PAD
+
+    c = decoder_config(model)
+    hq, hkv, D, H = c.num_heads // tp, max(1, c.num_kv_heads // tp), c.head_dim, c.hidden_size
+    inter = -(-(c.intermediate_size // tp) // FFN_PAD) * FFN_PAD
+    return [("qkv", (hq + 2 * hkv) * D, H, False), ("o", H, hq * D, False), ("gate_up", 2 * inter, H, True),
+            ("down", H, inter, False)]
+
+
+# BASELINE config 4 (Qwen2-72B TP=8) and Qwen2-7B at TP 2 / 4 (28 heads: TP 8 does not divide them)
+for _m, _tp in (("qwen2-72b", 8), ("qwen2-7b", 2), ("qwen2-7b", 4)):
+    SHAPES[f"{_m}-tp{_tp}"] = _tp_shapes(_m, _tp)
 
 
 def med_us(fn, reps):

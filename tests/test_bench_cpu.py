@@ -75,3 +75,24 @@ def test_bench_self_launch_two_ranks():
     res = _run([sys.executable, "bench.py", "--gpus", "2", *TINY], env)
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 6 and res["config"]["parallelism"] == "dp2"
     assert res["value"] > 0 and "ttft_admission_policy" in res
+
+
+def test_bench_self_launch_eight_ranks():
+    """The driver's 8-GPU command form, rehearsed on the host: ``python bench.py --gpus 8`` spawns 8 rank
+    processes (gloo), shards the index 8 ways, runs the agent phase through ONE front door over 8 sharded
+    replicas (every retrieval round fans out replica-to-replica over the shard mesh) and reports the
+    whole-job aggregate with no job errors and no degraded (shard-missing) retrieval."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               GRAG_DIST_BACKEND="gloo")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    args = list(TINY)
+    args[args.index("--agent-jobs") + 1] = "4"  # per GPU: 32 jobs over the 8 replicas
+    args[args.index("--ingest-files") + 1] = "2"
+    res = _run([sys.executable, "bench.py", "--gpus", "8", *args, "--serving-steps", "0"], env)
+    assert res["n_gpus"] == 8 and res["config"]["parallelism"] == "dp8" and res["config"]["global_batch"] == 24
+    assert res["value"] > 0 and res["ingest_docs_per_s"] > 0
+    ae = res["agent_e2e"]
+    assert ae["front_door"] == "front door + 8 sharded replicas" and ae["errors"] == 0 and ae["jobs"] == 32
+    assert ae["degraded_jobs"] == 0
+    assert sorted(r["shard"] for r in ae["replicas"]) == [f"{r}/8" for r in range(8)]

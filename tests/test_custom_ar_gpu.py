@@ -25,12 +25,24 @@ pytestmark = pytest.mark.gpu
 # 3 streams already sharing one (the 3rd rank then serialised behind another
 # and, by design, timed out with the err flag instead of hanging).  Real ranks
 # are separate processes on separate GPUs.
+_STREAMS = []
+
+
+def _rank_streams(dev, W):
+    """The simulated ranks' streams, created ONCE for the module: every new stream is mapped onto one of
+    the process's few hardware queues, and two rank streams that share a queue serialise (the waiting
+    rank's kernel then spins against a peer queued behind it and, by design, times out)."""
+    while len(_STREAMS) < W:
+        _STREAMS.append(torch.cuda.Stream(device=dev))
+    return _STREAMS[:W]
+
+
 @pytest.mark.parametrize("W", [2])
 def test_oneshot_simulated_ranks(dev, W):
     from githubrepostorag_amd.parallel.custom_ar import IpcAllReduce
 
     comms = IpcAllReduce.simulated(W, dev, slot_bytes=1 << 20, grid=32)
-    streams = [torch.cuda.Stream(device=dev) for _ in range(W)]
+    streams = _rank_streams(dev, W)
     g = torch.Generator(device="cpu").manual_seed(W)
     try:
         for it, n in enumerate([8, 4096, 3584 * 7, 3584 * 64, 8 * 1000] * 4):  # epochs cycle both slots
@@ -60,8 +72,8 @@ def test_oneshot_f32_sum_and_gather_simulated_ranks(dev):
     from githubrepostorag_amd.parallel.custom_ar import IpcAllReduce
 
     W = 2
-    comms = IpcAllReduce.simulated(W, dev, slot_bytes=1 << 20, grid=32)
-    streams = [torch.cuda.Stream(device=dev) for _ in range(W)]
+    comms = IpcAllReduce.simulated(W, dev, slot_bytes=4 << 20, grid=32)
+    streams = _rank_streams(dev, W)
     g = torch.Generator(device="cpu").manual_seed(11)
     try:
         for it in range(12):

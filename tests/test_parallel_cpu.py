@@ -317,3 +317,34 @@ def test_tp_custom_ar_timeout_detaches_group_wide():
         st = lead[2]
         assert st["iterations"] > 0 and st["payloads"] >= 2
         assert st["bytes"] - 48 * st["iterations"] < 4096 * st["payloads"]
+
+
+def _tp_pad_worker(rank, world, cfg_name, inter):
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import Qwen2Model
+    from githubrepostorag_amd.parallel.comm import make_tp_dp_groups
+
+    cfg = decoder_config(cfg_name, intermediate_size=inter)
+    tp, _ = make_tp_dp_groups(world)
+    model = Qwen2Model(cfg, device="cpu", dtype=torch.float32, tp=tp, state_dict=_hf_state_dict(cfg))
+    prompts = [[5, 17, 99, 3, 250], [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]]
+    return _generate(model, prompts), model.inter_real, model.inter
+
+
+def test_tp_ffn_zero_padding_matches_unpadded(monkeypatch):
+    """Config 4's per-rank FFN width (Qwen2-72B TP=8: 29568 / 8 = 3696) is not a multiple of 64; the
+    model zero-pads it (3712) so every MLP GEMM runs on the owned kernels.  Padded TP=2 ranks (176 -> 192
+    here) must generate exactly what an unpadded single-rank model does."""
+    import githubrepostorag_amd.models.qwen2 as q2
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import Qwen2Model
+
+    cfg = decoder_config("qwen2-tiny", intermediate_size=352)
+    monkeypatch.setattr(q2, "FFN_PAD", 1)
+    ref_model = Qwen2Model(cfg, device="cpu", dtype=torch.float32, state_dict=_hf_state_dict(cfg))
+    assert ref_model.inter == 352
+    ref = _generate(ref_model, [[5, 17, 99, 3, 250], [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]])
+    res = run_ranks(_tp_pad_worker, 2, "qwen2-tiny", 352)
+    for toks, real, padded in res:
+        assert (real, padded) == (176, 192)
+        assert toks == ref
