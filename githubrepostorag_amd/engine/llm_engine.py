@@ -131,7 +131,10 @@ class LLMEngine:
                       # host-side time by section (the GPU idles whenever one of these outlasts the queued work)
                       "host_sched_s": 0.0, "host_prefill_prep_s": 0.0, "host_prefill_launch_s": 0.0,
                       "host_prefill_sample_s": 0.0, "host_prefill_post_s": 0.0, "host_decode_prep_s": 0.0,
-                      "host_decode_post_s": 0.0}
+                      "host_decode_post_s": 0.0, "capture_s": 0.0}
+        # optional per-step timeline (a list; None = off): (t_start, kind, rows, tokens, seconds) per step,
+        # kind "prefill" / "decode" / "mixed" / "capture" — the ingest critical-path trace reads it
+        self.trace: list | None = None
         self._eos = set(getattr(tokenizer, "eos_token_ids", set()))
         self._lock = threading.RLock()
         max_split = -(-cfg.max_model_len // KV_TILE)
@@ -255,10 +258,15 @@ class LLMEngine:
         if not items:
             return finished
         self.stats["steps"] += 1
+        t0 = time.perf_counter() if self.trace is not None else 0.0
+        tok0 = self.stats["prefill_tokens"] + self.stats["decode_tokens"]
         if kind in ("prefill", "mixed"):
             finished += self._run_prefill(items)
         else:
             finished += self._run_decode([s for s, _, _ in items], max_window)
+        if self.trace is not None:
+            self.trace.append((t0, kind, len(items), self.stats["prefill_tokens"] + self.stats["decode_tokens"] - tok0,
+                               time.perf_counter() - t0))
         return finished
 
     # ------------------------------------------------------------------ helpers
@@ -698,8 +706,15 @@ class LLMEngine:
             self._graph_pool = torch.cuda.graph_pool_handle()
 
     def _capture(self, B, nsplit, split_len, K=1) -> _DecodeGraph:
-        with gpu_guard():  # no other thread may sync / allocate while the capture is open
-            return self._capture_locked(B, nsplit, split_len, K)
+        t0 = time.perf_counter()
+        try:
+            with gpu_guard():  # no other thread may sync / allocate while the capture is open
+                return self._capture_locked(B, nsplit, split_len, K)
+        finally:
+            dt = time.perf_counter() - t0
+            self.stats["capture_s"] += dt
+            if self.trace is not None:
+                self.trace.append((t0, "capture", B, K, dt))
 
     def _capture_locked(self, B, nsplit, split_len, K=1) -> _DecodeGraph:
         self._ensure_static()

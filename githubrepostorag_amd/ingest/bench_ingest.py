@@ -67,6 +67,7 @@ def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs:
                 for f in files]
         if dev.type == "cuda":
             torch.cuda.synchronize()
+        eng.trace = []  # per-step timeline for the critical-path summary below
         t0 = time.perf_counter()
         res = ctl.ingest_component(repo=f"bench-repo-{seed}", namespace="bench", documents=docs, force=True)
         if dev.type == "cuda":
@@ -76,9 +77,47 @@ def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs:
         st["engine"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()
                         if isinstance(v, (int, float))}
         st["llm_calls"] = ctl.extractors.wave.calls + ctl.hier.wave.calls + ctl.hier.extract.wave.calls
+        st["timeline"] = critical_path(eng.trace, t0, dt)
+        eng.trace = None
         return res["documents"], dt, st
     finally:
         runner.shutdown()
         del eng
         if dev.type == "cuda":
             torch.cuda.empty_cache()
+
+
+def critical_path(trace: list, t0: float, total: float, bucket: float = 1.0) -> dict:
+    """Where the ingest wall time went, from the engine's per-step trace (engine/llm_engine.py ``trace``):
+    totals per step kind, the engine-idle remainder (host work, waits between dependent waves), and a
+    per-``bucket`` timeline of prefill / decode / capture seconds and mean decode rows — the decode-step
+    count is the length of the dependent generation chain (file -> module -> repo summaries -> extractors)."""
+    tot = {"prefill_s": 0.0, "decode_s": 0.0, "capture_s": 0.0, "prefill_tokens": 0, "decode_steps": 0,
+           "decode_tokens": 0}
+    nb = max(1, int(total / bucket) + 1)
+    tl = [{"t": round(i * bucket, 1), "prefill_s": 0.0, "decode_s": 0.0, "capture_s": 0.0, "rows": 0, "steps": 0}
+          for i in range(nb)]
+    for ts, kind, rows, toks, sec in trace:
+        b = tl[min(nb - 1, max(0, int((ts - t0) / bucket)))]
+        if kind == "capture":
+            tot["capture_s"] += sec
+            b["capture_s"] += sec
+        elif kind == "decode":
+            tot["decode_s"] += sec
+            tot["decode_steps"] += 1
+            tot["decode_tokens"] += toks
+            b["decode_s"] += sec
+            b["rows"] += rows
+            b["steps"] += 1
+        else:
+            tot["prefill_s"] += sec
+            tot["prefill_tokens"] += toks
+            b["prefill_s"] += sec
+    busy = tot["prefill_s"] + tot["decode_s"]  # decode_s includes captures made inside a decode step
+    out = {k: round(v, 3) if isinstance(v, float) else v for k, v in tot.items()}
+    out["engine_idle_s"] = round(max(0.0, total - busy), 3)
+    out["mean_decode_step_ms"] = round(1000 * tot["decode_s"] / max(1, tot["decode_steps"]), 2)
+    out["buckets"] = [{"t": b["t"], "prefill_s": round(b["prefill_s"], 2), "decode_s": round(b["decode_s"], 2),
+                       "capture_s": round(b["capture_s"], 2),
+                       "mean_rows": round(b["rows"] / b["steps"], 1) if b["steps"] else 0} for b in tl]
+    return out
