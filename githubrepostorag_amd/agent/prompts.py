@@ -129,6 +129,15 @@ def file_summary(path: str) -> str:
             "Avoid boilerplate; keep it under ~200–300 words.")
 
 
+def file_summary_prompt(path: str, content: str) -> str:
+    """The FILE SUMMARY roll-up call (hierarchy_summary_service.py:32-38: instruction + "\n\n" + the file's
+    chunks) with the same instruction and content, the content FIRST and in the extractors' section form:
+    a single-chunk file's prompt then starts with exactly the token prefix of that chunk's summary / title
+    / keyword prompts (``summary_extract``), so the engine's prefix cache computes the file text once for
+    all four calls (content first so ingest prompts share a KV prefix)."""
+    return f"Here is the content of the section:\n{content}\n\n{file_summary(path)}"
+
+
 def module_summary(module: str, repo: str) -> str:
     # hierarchy_summary_service.py:112-116
     return (f"MODULE SUMMARY for '{module}' in repo {repo}.\n"

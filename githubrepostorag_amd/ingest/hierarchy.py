@@ -60,7 +60,7 @@ class HierarchyBuilder:
                            kind: str) -> list[Node]:
         files = [(fp, ns) for fp, ns in group_nodes_by_file(code_nodes).items() if fp]
         concat = ["\n\n".join(n.get_content() for n in ns)[:25000] for _, ns in files]
-        texts = self.wave.map([prompts.file_summary(fp) + "\n\n" + c for (fp, _), c in zip(files, concat)],
+        texts = self.wave.map([prompts.file_summary_prompt(fp, c) for (fp, _), c in zip(files, concat)],
                               max_tokens=self.summary_tokens, priority=ROLLUP_PRIORITY)
         docs = []
         for (fp, ns), t in zip(files, texts):
@@ -107,7 +107,7 @@ class HierarchyBuilder:
         def one_module(item):
             m, fps = item
             concat = ["\n\n".join(n.get_content() for n in nodes_of[fp])[:25000] for fp in fps]
-            texts = self.wave.map([prompts.file_summary(fp) + "\n\n" + c for fp, c in zip(fps, concat)],
+            texts = self.wave.map([prompts.file_summary_prompt(fp, c) for fp, c in zip(fps, concat)],
                                   max_tokens=self.summary_tokens, priority=ROLLUP_PRIORITY)
             with lock:
                 done_files[0] = max(done_files[0], time.perf_counter() - t0)
