@@ -140,7 +140,8 @@ def cmd_replica(args) -> int:
     host, port = args.hub.rsplit(":", 1)
     key = bytes.fromhex(os.environ["GRAG_HUB_AUTHKEY"])
     try:
-        return run_replica(rt, (host, int(port)), key, args.rank, shards=args.shards)
+        return run_replica(rt, (host, int(port)), key, args.rank, shards=args.shards,
+                           health_every=float(os.environ.get("GRAG_HEALTH_EVERY", "5")))
     finally:
         if hasattr(rt, "close"):
             rt.close()

@@ -586,6 +586,8 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
                 last_h = time.time()
                 try:
                     h = runtime.health() if hasattr(runtime, "health") else {}
+                    if mesh is not None:
+                        h = {**h, "mesh_stats": mesh.round_stats()}
                     send(("health", {"device": str(getattr(runtime, "device", "cpu")), **h}))
                 except Exception:  # pragma: no cover
                     pass
@@ -697,6 +699,16 @@ def demo_runtime(settings):
     store.table("chunk").upsert(["widgets", "gadget", "billing"], texts, emb.embed_documents(texts),
                                 [{"namespace": "default", "repo": "r", "module": "m", "file_path": f"{x}.py"}
                                  for x in "abc"])
+    extra = int(os.environ.get("GRAG_DEMO_ROWS", "0"))  # load tests: a larger synthetic table per scope
+    if extra:
+        import torch
+
+        g = torch.Generator().manual_seed(11)
+        for scope in ("chunk", "file", "module", "repo"):
+            v = torch.nn.functional.normalize(torch.randn(extra, emb.dim, generator=g), dim=1)
+            store.table(scope).upsert([f"{scope}-{i}" for i in range(extra)], [f"{scope} text {i}" for i in range(extra)],
+                                      v, [{"namespace": "default", "repo": f"r{i % 7}", "module": f"m{i % 23}",
+                                           "file_path": f"m{i % 23}/f{i % 97}.py"} for i in range(extra)])
     settings.worker_max_jobs = int(os.environ.get("GRAG_DEMO_SLOTS", settings.worker_max_jobs))
     return RAGRuntime(settings, device="cpu", llm=ScriptedLLM(router), embedder=emb, store=store,
                       build_engine=False)

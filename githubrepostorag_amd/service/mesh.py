@@ -35,6 +35,7 @@ Wire (pickled tuples over multiprocessing.connection, our own processes only):
 """
 from __future__ import annotations
 
+import collections
 import itertools
 import logging
 import queue
@@ -171,6 +172,8 @@ class PeerMesh:
         self._closed = False
         self._served: set = set()  # accepted connections (closed with the mesh: peers see EOF, not a hang)
         self.stats = {"rounds": 0, "degraded_rounds": 0, "served_msgs": 0, "served_reqs": 0, "stacked_searches": 0}
+        self._lat = collections.deque(maxlen=8192)  # seconds per round (fan-out -> last part)
+        self._t_first = None
         threading.Thread(target=self._accept_loop, name="mesh-accept", daemon=True).start()
 
     # ------------------------------------------------------------------ membership
@@ -217,7 +220,8 @@ class PeerMesh:
                 missing.append(r)
                 continue
             waits.append((r, ln.submit(next(self._ids), scope, op, payload)))
-        deadline = time.monotonic() + timeout
+        t_round = time.monotonic()
+        deadline = t_round + timeout
         parts = []
         for r, p in waits:
             if p.ev.wait(max(0.0, deadline - time.monotonic())) and p.ok:
@@ -227,9 +231,25 @@ class PeerMesh:
                     log.warning("mesh: shard %d failed %s on %s: %s", r, op, scope, p.res)
                 missing.append(r)
         self.stats["rounds"] += 1
+        now = time.monotonic()
+        self._lat.append(now - t_round)
+        if self._t_first is None:
+            self._t_first = t_round
         if missing:
             self.stats["degraded_rounds"] += 1
         return Parts(parts, missing)
+
+    def round_stats(self) -> dict:
+        """Rounds this replica originated: count, degraded count, latency p50 / p99 (ms) over the last 8192,
+        rounds/s since the first; plus what it served for its peers (messages, requests, stacked launches)."""
+        lat = sorted(self._lat)
+        out = dict(self.stats)
+        if lat:
+            out["p50_ms"] = round(1000 * lat[len(lat) // 2], 3)
+            out["p99_ms"] = round(1000 * lat[min(len(lat) - 1, int(0.99 * len(lat)))], 3)
+            span = time.monotonic() - self._t_first
+            out["rounds_per_s"] = round(self.stats["rounds"] / span, 2) if span > 0 else None
+        return out
 
     def write(self, origin: int, owner: int, scope: str, op: str, payload, timeout: float = 120.0):
         """A routed upsert / delete, acknowledged by the owner (returns its applied count)."""

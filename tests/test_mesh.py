@@ -126,3 +126,22 @@ def test_mesh_lost_shard_is_degraded_and_writes_fail_loudly(mesh3):
     with round_health() as h:
         facades[0].table("chunk").search(q, 5)
     assert h["missing_shards"] == {2}
+
+
+def test_front_door_mesh_load_small():
+    """scripts/mesh_load.py at a CPU-tier size: 4 sharded replica processes behind one front door, 96
+    concurrent agent jobs over real HTTP; every retrieval round goes replica-to-replica, none loses a
+    shard, and the replicas report their round latencies (p50 / p99) and rounds/s."""
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "mesh_load", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
+                                  "mesh_load.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    res = mod.run(replicas=4, jobs=96, concurrency=96, rows=500, delay=0.0, slots=32)
+    assert res["errors"] == 0 and res["degraded_jobs"] == 0 and res["jobs"] == 96
+    assert res["shard_rounds"] > 96 and res["round_p99_ms_max"] > 0
+    assert all(r.get("rounds", 0) > 0 and r.get("degraded_rounds", 1) == 0 for r in res["per_replica"])
+    assert res["served_reqs"] >= res["shard_rounds"] * 3  # each round asked all 3 other shards
