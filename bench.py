@@ -684,12 +684,15 @@ def main():
 
 def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, dp_size, group, world, log):
     """The headline workload through the product's serving loop: the engine steps on its own
-    EngineRunner thread (engine/runner.py, as ``serve`` runs it) and this thread only submits and waits.
-    Each group's retrieval runs on the helper thread inside ``runner.arrival()`` (the admission hint:
-    decode replays go one step at a time until its prompts are submitted), then its prompts are submitted
-    from that thread, as a server's request threads do.  Same arrival pipeline as the harness (U groups
-    of u queries in flight, staggered by S tokens); one step = A arrivals, A oldest groups complete.
-    Returns qps / p50 TTFT next to the harness's (submission -> first token)."""
+    EngineRunner thread (engine/runner.py, as ``serve`` runs it); this thread only submits and waits.
+    Closed loop at the harness's concurrency: U groups of u queries in flight (staggered by S tokens, as
+    the harness fills its pipeline); whenever the oldest group completes, a new group arrives: its
+    retrieval (embed + search + prompt) runs on the helper thread inside ``runner.arrival()`` (the
+    admission hint: decode replays go one step at a time until its prompts are submitted) and its prompts
+    are submitted from that thread, as a server's request threads do.  The engine itself runs free (up to
+    8-step replays when no arrival is pending): nothing caps its windows to the pipeline as the harness
+    does.  Timed: ``steps`` x A completions; qps = completed queries / wall time, p50 TTFT = submission ->
+    first token.  ``steady_state_decode_ratio`` ~ 1.0 shows the window was steady state."""
     import collections
 
     import torch
@@ -698,7 +701,7 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
     from githubrepostorag_amd.parallel import comm
 
     runner = EngineRunner(eng, watchdog_s=0)
-    inflight = collections.deque()
+    inflight = collections.deque()  # oldest first: (handles, t_sub) or a Future of one
 
     def arrive():
         with runner.arrival():
@@ -712,24 +715,26 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
         s_ = eng.get(h.req_id)
         return 0 if s_ is None else len(s_.output_ids)
 
-    def sub_step():
-        fut = pool.submit(arrive)
-        hs, t_sub = inflight.popleft()
+    def complete_one():
+        """Wait for the oldest group, replace it with a new arrival; its queries' TTFTs (s)."""
+        g = inflight.popleft()
+        hs, t_sub = g.result() if hasattr(g, "result") else g
         for h in hs:
             h.wait(600)
-        inflight.append(fut.result())
+        inflight.append(pool.submit(arrive))
         return [h.result.first_token_at - t_sub for h in hs]
 
     try:
-        for k in range(U - 1):  # fill, staggered like the harness
+        with runner.arrival():  # fill with 1-step decode replays: the stagger lands exactly
+            for k in range(U - 1):
+                inflight.append(arrive())
+                d = max(1, round((k + 1) * S) - round(k * S))
+                t0 = time.perf_counter()
+                while min(ntok(h) for h in inflight[-1][0]) < 1 + d and time.perf_counter() - t0 < 120:
+                    time.sleep(0.0002)
             inflight.append(arrive())
-            d = max(1, round((k + 1) * S) - round(k * S))
-            t0 = time.perf_counter()
-            while min(ntok(h) for h in inflight[-1][0]) < 1 + d and time.perf_counter() - t0 < 120:
-                time.sleep(0.0005)
-        inflight.append(arrive())
         for _ in range(max(1, args.warmup) * A):
-            sub_step()
+            complete_one()
         comm.barrier()
         if dev.type == "cuda":
             torch.cuda.synchronize()
@@ -737,13 +742,14 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
         dec0 = eng.stats["decode_tokens"]
         ttfts = []
         for _ in range(steps * A):
-            ttfts += sub_step()
+            ttfts += complete_one()
         dec1 = eng.stats["decode_tokens"]
         if dev.type == "cuda":
             torch.cuda.synchronize()
         comm.barrier()
         elapsed = time.perf_counter() - t_start
-        for hs, _ in inflight:  # drain (untimed)
+        for g in inflight:  # drain (untimed)
+            hs, _ = g.result() if hasattr(g, "result") else g
             for h in hs:
                 h.wait(600)
     finally:
@@ -764,8 +770,9 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
             # decode tokens the engine produced in the timed window / what the completed queries needed:
             # ~1.0 when the window was the pipeline's steady state (no backlog built or drained in it)
             "steady_state_decode_ratio": round((dec1 - dec0) / max(1, args.batch * steps * (args.gen_len - 1)), 3),
-            "loop": "engine/runner.py EngineRunner thread; arrivals submitted from the retrieval thread under "
-                    "runner.arrival() (1-step decode replays while a retrieval is in flight)"}
+            "loop": "engine/runner.py EngineRunner thread, closed loop at the harness's concurrency; arrivals "
+                    "submitted from the retrieval thread under runner.arrival() (1-step decode replays while a "
+                    "retrieval is in flight, up to 8-step replays otherwise)"}
 
 
 def _scope_tables(store, emb, corpus, rank, world, dev):
