@@ -746,17 +746,30 @@ class LLMEngine:
         return g
 
     @torch.inference_mode()
-    def warmup_graphs(self, batch_sizes=None, max_ctx: int = 2048, windows=(1,)) -> int:
+    def warmup_graphs(self, batch_sizes=None, max_ctx=2048, windows=(1,), params: SamplingParams | None = None) -> int:
         """Capture the decode graphs a workload will replay ahead of time
         (batch buckets x decode windows K, split plan of ``max_ctx``) so no
         capture lands inside a latency-sensitive step.  Keyed on the
         sampler's current launch chain: call it once requests with the
         serving sampling parameters have been admitted.  Returns the number
-        of graphs captured."""
+        of graphs captured.  ``max_ctx`` may be a list (one split plan per context length).  ``params``:
+        capture for the sampler launch chain these sampling parameters select (top-k / top-p rounds)
+        instead of the live slots' (e.g. an ingest engine warmed before its first request)."""
         if not (self.on_gpu and self.cfg.use_cuda_graph):
             return 0
-        with self._on_stream():
-            return self._warmup_graphs(batch_sizes, max_ctx, windows)
+        prev = self.sampler.rounds_override
+        if params is not None:
+            sampled = params.temperature > 0
+            self.sampler.rounds_override = ((1 if sampled and 0 < params.top_k < self.sampler.vocab else 0)
+                                            | (2 if sampled and params.top_p < 1.0 else 0))
+        try:
+            with self._on_stream():
+                n = 0
+                for mc in (max_ctx if isinstance(max_ctx, (list, tuple)) else [max_ctx]):
+                    n += self._warmup_graphs(batch_sizes, mc, windows)
+                return n
+        finally:
+            self.sampler.rounds_override = prev
 
     def _warmup_graphs(self, batch_sizes, max_ctx, windows) -> int:
         n = 0

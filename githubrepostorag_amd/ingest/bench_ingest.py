@@ -12,6 +12,7 @@ have for these prompts (code summary 128, keywords 64, title 32, roll-ups
 """
 from __future__ import annotations
 
+import logging
 import time
 
 import torch
@@ -19,11 +20,14 @@ import torch
 from ..agent.llm import EngineLLM
 from ..config import Settings
 from ..engine.llm_engine import EngineConfig, LLMEngine
+from ..engine.sequence import SamplingParams
 from ..engine.runner import EngineRunner
 from ..index.store import VectorStore
 from ..utils.synthetic import synthetic_repo
 from .controller import IngestController
 from .readers import Document
+
+log = logging.getLogger(__name__)
 
 
 def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs: int = 256,
@@ -46,7 +50,14 @@ def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs:
                                              mixed_batches=mixed_batches, kv_cache_gb=kv_cache_gb,
                                              graph_batch_sizes=tuple(b for b in sizes if b <= max_num_seqs)))
     if use_graph and dev.type == "cuda":
-        eng.warmup_graphs()
+        # the decode graphs the ingest will replay, captured before timing: every batch bucket x decode
+        # window x the split plans of short / medium / long contexts, for the ingest sampling chain (top-p)
+        ctxs = sorted({c for c in (2048, 4096, max_model_len) if c <= max_model_len})
+        t_w = time.perf_counter()
+        n_w = eng.warmup_graphs(max_ctx=ctxs, windows=(1, 2, 4, 8),
+                                params=SamplingParams(temperature=EngineLLM.INGEST["temperature"],
+                                                      top_p=EngineLLM.INGEST["top_p"]))
+        log.info("ingest engine: %d decode graphs captured in %.1fs", n_w, time.perf_counter() - t_w)
     tp = tp if tp is not None and not tp.trivial else None
     runner = EngineRunner(eng, tp=tp)
     if tp is not None and not runner.leader:

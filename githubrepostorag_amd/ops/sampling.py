@@ -31,8 +31,12 @@ class SamplerState:
         self._uses_topk = [False] * max_slots
         self._uses_topp = [False] * max_slots
 
+    rounds_override: int | None = None  # graph warm-up: capture for the rounds a workload WILL use
+
     @property
     def rounds(self) -> int:
+        if self.rounds_override is not None:
+            return self.rounds_override
         return (1 if any(self._uses_topk) else 0) | (2 if any(self._uses_topp) else 0)
 
     def workspace(self, rows: int) -> torch.Tensor:
