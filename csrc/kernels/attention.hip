@@ -556,9 +556,18 @@ __global__ __launch_bounds__(64 * NW) void attn_prefill_kernel(AttnParams p) {
 // comes through the scalar cache, so no vector load sits between two tiles.
 // Tile t+1 is issued before tile t is computed and retired with a counted
 // vmcnt, keeping 32 KiB per wave in flight under the MFMA/softmax work.
-template <int D, int TK>
+//
+// NS > 2 stages (round 4): NS - 1 tiles stay in flight while one is computed.
+// The ring is what bounds the bytes in flight per CU: with 32-key tiles a
+// 2-stage ring (32 KiB per wave, 5 waves per CU) keeps 5 x 16 KiB = 80 KiB
+// in flight, a 4-stage ring (64 KiB per wave, 2 waves per CU) 2 x 48 KiB =
+// 96 KiB, and 512 resident waves divide the (sequence x kv-head) grid of
+// power-of-two batches into whole rounds (2 048 / 4 096 waves at 512 / 1024
+// live sequences) where 1 280 resident waves leave a 0.2-0.6 partial round.
+template <int D, int TK, int NS = 2>
 __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
   static_assert(TK == 32 || TK == 64, "keys per tile");
+  static_assert(NS >= 2 && NS <= 4, "ring stages");
   constexpr int NT16 = TK / 16, NCC = TK / 32;
   constexpr int RB = 2 * D;
   constexpr int CPR = D / 8;
@@ -567,7 +576,8 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
   constexpr int TILE = TK * RB;      // bytes per K (or V) tile
   constexpr int NI = TILE / 1024;    // LDS-DMA instructions per tile per tensor
   constexpr int RPI = 1024 / RB;     // rows per instruction
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+  static_assert((NS - 1) * 2 * NI <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * TILE];
 
   const int lane = threadIdx.x;
   const int h4 = lane >> 4, li = lane & 15;
@@ -632,16 +642,19 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
 #pragma unroll
   for (int n = 0; n < ND; ++n) o[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int ntiles = (kv_hi - kv_lo + TK - 1) / TK;
-  issue(kv_lo, 0);
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < ntiles) issue(kv_lo + t * TK, t);
   for (int t = 0; t < ntiles; ++t) {
-    const int stage = t & 1;
+    const int stage = t % NS;
     const int kt0 = kv_lo + t * TK;
-    if (t + 1 < ntiles) {
-      issue(kt0 + TK, stage ^ 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (t + NS - 1 < ntiles) issue(kt0 + (NS - 1) * TK, (t + NS - 1) % NS);
+    // retire tile t: the tiles issued after it may stay in flight (counted, in issue order)
+    const int after = min(NS - 1, ntiles - 1 - t);
+    if (after >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * 2 * NI) : "memory");
+    else if (after == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * 2 * NI) : "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const char* k_lds = smem + stage * 2 * TILE;
     const char* v_lds = k_lds + TILE;
     f32x4_t s[NT16];
@@ -779,12 +792,16 @@ int launch(const AttnParams& prm, int nseq, hipStream_t stream) {
 }
 
 template <int D>
-int launch_decode(const AttnParams& prm, int nseq, int tk, hipStream_t stream) {
+int launch_decode(const AttnParams& prm, int nseq, int tk, int ns, hipStream_t stream) {
   dim3 grid(nseq, prm.Hkv, prm.num_splits);
-  if (tk == 32)
-    paged_decode_kernel<D, 32><<<grid, 64, 0, stream>>>(prm);
+  if (tk == 32 && ns == 4)
+    paged_decode_kernel<D, 32, 4><<<grid, 64, 0, stream>>>(prm);
+  else if (tk == 32 && ns == 3)
+    paged_decode_kernel<D, 32, 3><<<grid, 64, 0, stream>>>(prm);
+  else if (tk == 32)
+    paged_decode_kernel<D, 32, 2><<<grid, 64, 0, stream>>>(prm);
   else
-    paged_decode_kernel<D, 64><<<grid, 64, 0, stream>>>(prm);
+    paged_decode_kernel<D, 64, 2><<<grid, 64, 0, stream>>>(prm);
   int err = (int)hipGetLastError();
   if (err) return err;
   if (prm.num_splits > 1) {
@@ -810,8 +827,10 @@ int dispatch_nw(const AttnParams& prm, int nseq, int nw, bool paged, hipStream_t
   // nw == 1 / 3 with q_len == 1: LDS-DMA pipelined decode kernel with 64- / 32-key
   // tiles (32-key tiles halve the LDS ring so more single-wave workgroups share a
   // CU); nw == 2: the generic kernel with one wave per workgroup (A/B reference)
-  if (paged && (nw == 1 || nw == 3) && prm.tiles_per_seq == 1 && prm.G <= 16 && prm.BS % 16 == 0)
-    return launch_decode<D>(prm, nseq, nw == 3 ? 32 : 64, stream);
+  // nw == 7 / 8: 32-key tiles in a 4- / 3-stage ring
+  if (paged && (nw == 1 || nw == 3 || nw == 7 || nw == 8) && prm.tiles_per_seq == 1 && prm.G <= 16 &&
+      prm.BS % 16 == 0)
+    return launch_decode<D>(prm, nseq, nw == 1 ? 64 : 32, nw == 7 ? 4 : nw == 8 ? 3 : 2, stream);
   if (nw == 5 || nw == 6) {  // LDS-DMA prefill: 8 waves, 2-stage (5) / staggered 3-stage (6) ring
     if constexpr (D == 128 || D == 64) {
       if (paged && prm.num_splits == 1 && prm.BS == 16 && prm.bt_stride <= kPrefillMaxBlocks)
@@ -819,7 +838,7 @@ int dispatch_nw(const AttnParams& prm, int nseq, int nw, bool paged, hipStream_t
     }
     return (int)hipErrorInvalidValue;
   }
-  if (nw == 3) nw = 1;
+  if (nw == 3 || nw == 7 || nw == 8) nw = 1;
   if (nw == 2) nw = 1;
   if (paged) {
     return nw == 1 ? launch<D, 1, true>(prm, nseq, stream) : launch<D, 4, true>(prm, nseq, stream);

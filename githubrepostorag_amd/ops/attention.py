@@ -13,7 +13,11 @@ KV_TILE = 64  # keys per kernel tile; split lengths must be multiples of this
 # decode kernel variant: 64-key tiles (nw code 1) or 32-key tiles (nw code 3,
 # half the LDS ring -> more single-wave workgroups per CU)
 # (scripts/microbench.py, B=64 ctx=1152: 64-key 42.3 us -> 32-key 36.7 us)
-DECODE_NW = {64: 1, 32: 3}[int(os.environ.get("GRAG_DECODE_TK", "32"))]
+# GRAG_DECODE_STAGES: LDS ring depth of the 32-key kernel (2: nw 3; 3: nw 8; 4: nw 7 — NS - 1 tiles in flight
+# per wave; csrc/kernels/attention.hip paged_decode_kernel)
+_DEC_STAGES = int(os.environ.get("GRAG_DECODE_STAGES", "2"))
+DECODE_NW = {64: 1, 32: {2: 3, 3: 8, 4: 7}[_DEC_STAGES]}[int(os.environ.get("GRAG_DECODE_TK", "32"))]
+DECODE_RING_NW = {2: 3, 3: 8, 4: 7}  # stages -> nw code (microbench / A/B)
 # prefill kernel: 8-wave LDS-DMA variant (nw code 5, head_dim 64/128) or the
 # 4-wave register-staged kernel (nw code 4); GRAG_PREFILL_ATTN=v1 selects the latter
 PREFILL_NW = 4 if os.environ.get("GRAG_PREFILL_ATTN", "v2") == "v1" else 5

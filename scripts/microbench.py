@@ -76,10 +76,12 @@ def attn_decode_bench(B, ctx, split_len):
                           part_o=torch.empty(ns * B * Hq * D, device=dev), part_ml=torch.empty(ns * B * Hq * 2, device=dev))
     import copy
 
-    m32 = copy.copy(meta)
-    m32.extra = {"decode_nw": 3}
-    r = rounds({f"paged_decode_split{split_len}": lambda: A.paged_attention(q, kc, vc, meta, 0.088),
-                f"paged_decode_tk32_split{split_len}": lambda: A.paged_attention(q, kc, vc, m32, 0.088)})
+    arms = {}
+    for name, code in (("tk64", 1), ("tk32", 3), ("tk32_ns3", 8), ("tk32_ns4", 7)):
+        mm = copy.copy(meta)
+        mm.extra = {"decode_nw": code}
+        arms[f"paged_decode_{name}_split{split_len}"] = (lambda mm=mm: A.paged_attention(q, kc, vc, mm, 0.088))
+    r = rounds(arms)
     gb = B * ctx * Hkv * D * 2 * 2 / 1e9
     for k in r:
         r[k]["TB_s"] = round(gb / (r[k]["min_us"] * 1e-6) / 1e3, 2)
@@ -162,6 +164,10 @@ if __name__ == "__main__":
         for sl in (256, 2048):
             res[f"decode_B256_ctx1100_split{sl}"] = attn_decode_bench(256, 1100, sl)
             res[f"decode_B128_ctx2048_split{sl}"] = attn_decode_bench(128, 2048, sl)
+    if args.what == "decode_ring":  # LDS ring depth of the 32-key decode kernel at the bench's / ingest's shapes
+        for B, ctx, sl in ((512, 1100, 2048), (1024, 1100, 2048), (256, 1100, 1024), (64, 1152, 256),
+                           (176, 3000, 1024), (16, 6000, 256), (1, 4096, 64)):
+            res[f"decode_B{B}_ctx{ctx}_split{sl}"] = attn_decode_bench(B, ctx, sl)
     if args.what in ("all", "attn", "decode"):
         res["decode_B512_ctx1100_split256"] = attn_decode_bench(512, 1100, 256)  # the bench's decode step
     if args.what in ("all", "attn"):
