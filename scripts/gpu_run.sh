@@ -13,6 +13,7 @@
 #                    sampler in the decode graphs, lockstep ingest and agent)
 #   sweep=ARGS       bench with --agent-sweep (agent saturation curve)
 #   prof             rocprofv3 --kernel-trace --stats over a 2-step bench (scripts/profile_bench.sh)
+#   mb=WHAT          scripts/microbench.py --what WHAT (json in gpurun_out/<TAG>_mb_WHAT.json)
 #
 # A step that exits 0 or 1 (a clean Python failure) lets the next one run; a fault, abort, segfault or
 # time limit (124 / 134 / 137 / 139) ends the session there (no more GPU work after a GPU fault).
@@ -52,6 +53,7 @@ for step in "$@"; do
     tp2) run 900 tp2 env GRAG_DIST_BACKEND=gloo python -u bench.py --gpus 2 --tp 2 $REH ${val//,/ } ;;
     sweep) run 1100 sweep python -u bench.py --no-ingest --agent-sweep "${val:-64,256,512,1024}" --steps 2 --warmup 1 ;;
     prof) run 700 prof bash scripts/profile_bench.sh ;;
+    mb) run 400 "mb_$val" python -u scripts/microbench.py --what "$val" --out "gpurun_out/${TAG}_mb_$val.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -153,6 +153,7 @@ def sampler_bench(B):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="all")
+    ap.add_argument("--out", default=None, help="also write the JSON here")
     args = ap.parse_args()
     res = {}
     if args.what in ("all", "gemm"):
@@ -184,3 +185,6 @@ if __name__ == "__main__":
     if args.what in ("all", "sampler"):
         res["sampler_B64"] = sampler_bench(64)
     print(json.dumps(res, indent=1))
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)
