@@ -617,7 +617,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if args.quant == "none" else "w4a16 (AWQ format, group 128) decode / bf16 prefill",
+            "dtype": ("fp32" if dev.type != "cuda" else "bf16") if args.quant == "none" else
+                     "w4a16 (AWQ format, group 128) decode / bf16 prefill",
             "data": "synthetic (random-init weights, clustered synthetic vectors, generated chunk texts/questions)",
             "p50_ttft_ms": round(p50, 2),
             # p50_ttft_ms is measured under this bench loop's admission policy, not the serving runner's default
