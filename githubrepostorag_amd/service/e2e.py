@@ -9,6 +9,12 @@ httpx client drives N concurrent jobs exactly as the UI does
             (reference: the first visible output is the final event,
             rag_worker/src/worker/worker.py:170, qwen_llm.py:149-151)
   jobs/s  = completed jobs / wall time of the run
+
+The client runs in a child process by default (``client_process``): like the
+reference's browser it is not part of the server, and hundreds of SSE streams
+parsed in the server's interpreter would compete with the engine thread for
+its GIL.  ``python -m githubrepostorag_amd.service.e2e --url U --questions F
+--concurrency C --out O`` is that child.
 """
 from __future__ import annotations
 
@@ -100,26 +106,56 @@ def _pct(xs: list[float], p: float) -> float | None:
     return xs[min(len(xs) - 1, int(round(p * (len(xs) - 1))))]
 
 
+def _drive_child(url: str, questions: list[str], concurrency: int, timeout_s: float) -> tuple[list[dict], float]:
+    """_drive in a child process (no torch, no GPU): (per-job records with times relative to its start,
+    wall seconds)."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        qf, of = os.path.join(d, "q.json"), os.path.join(d, "out.json")
+        with open(qf, "w") as f:
+            json.dump(questions, f)
+        env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        r = subprocess.run([sys.executable, "-m", "githubrepostorag_amd.service.e2e", "--url", url, "--questions", qf,
+                            "--concurrency", str(concurrency), "--timeout", str(timeout_s), "--out", of],
+                           env=env, timeout=timeout_s + 60)
+        if r.returncode != 0:
+            raise RuntimeError(f"e2e client exited with {r.returncode}")
+        with open(of) as f:
+            out = json.load(f)
+    return out["records"], out["wall_s"]
+
+
 def run_e2e(app, questions: list[str], concurrency: int, warmup: list[str] | None = None,
-            timeout_s: float = 1800.0, sweep: list[tuple[list[str], int]] | None = None) -> dict:
+            timeout_s: float = 1800.0, sweep: list[tuple[list[str], int]] | None = None,
+            client_process: bool = True) -> dict:
     """Serve ``app`` on localhost and push ``questions`` through the HTTP API at ``concurrency``.
     ``sweep``: further (questions, concurrency) runs on the same server, one after the other (a
     saturation curve); their summaries go to ``agent_saturation``."""
     with ServerThread(app) as srv:
-        loop = asyncio.new_event_loop()
+        loop = None if client_process else asyncio.new_event_loop()
+
+        def drive(qs, conc):
+            if client_process:
+                return _drive_child(srv.url, qs, conc, timeout_s)
+            t0 = time.perf_counter()
+            r = loop.run_until_complete(_drive(srv.url, qs, conc, timeout_s))
+            return r, time.perf_counter() - t0
+
         try:
             if warmup:
-                loop.run_until_complete(_drive(srv.url, warmup, concurrency, timeout_s))
-            t0 = time.perf_counter()
-            res = loop.run_until_complete(_drive(srv.url, questions, concurrency, timeout_s))
-            wall = time.perf_counter() - t0
+                drive(warmup, concurrency)
+            res, wall = drive(questions, concurrency)
             curve = []
             for qs, conc in sweep or []:
-                t1 = time.perf_counter()
-                r = loop.run_until_complete(_drive(srv.url, qs, conc, timeout_s))
-                curve.append(dict(concurrency=conc, **_summary(r, time.perf_counter() - t1)))
+                r, w = drive(qs, conc)
+                curve.append(dict(concurrency=conc, **_summary(r, w)))
         finally:
-            loop.close()
+            if loop is not None:
+                loop.close()
     out = _summary(res, wall)
     if sweep:
         out["agent_saturation"] = curve
@@ -145,3 +181,27 @@ def _summary(res: list[dict], wall: float) -> dict:
             "errors": sum(r["error"] for r in res), "degraded_jobs": sum(r.get("degraded", False) for r in res),
             "mean_tokens_streamed": round(
                 statistics.mean(r["tokens"] for r in res), 1) if res else 0}
+
+
+def _main() -> int:
+    import argparse
+
+    ap = argparse.ArgumentParser(description="e2e client: drive POST /rag/jobs + SSE at a concurrency")
+    ap.add_argument("--url", required=True)
+    ap.add_argument("--questions", required=True, help="JSON list of questions")
+    ap.add_argument("--concurrency", type=int, required=True)
+    ap.add_argument("--timeout", type=float, default=1800.0)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    with open(a.questions) as f:
+        qs = json.load(f)
+    t0 = time.perf_counter()
+    res = asyncio.run(_drive(a.url, qs, a.concurrency, a.timeout))
+    wall = time.perf_counter() - t0
+    with open(a.out, "w") as f:
+        json.dump({"records": res, "wall_s": wall}, f)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(_main())
