@@ -861,8 +861,8 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
                                   float scale, int causal, int num_splits, int split_len,
                                   float* part_o, float* part_ml, int nw, hipStream_t stream) {
   if (nseq <= 0) return 0;
-  if (Hq % Hkv != 0 || BS <= 0 || nw < 1 || nw > 6) return (int)hipErrorInvalidValue;
-  if (nw >= 5 && num_splits > 1) return (int)hipErrorInvalidValue;
+  if (Hq % Hkv != 0 || BS <= 0 || nw < 1 || nw > 8) return (int)hipErrorInvalidValue;
+  if ((nw == 5 || nw == 6) && num_splits > 1) return (int)hipErrorInvalidValue;
   if (num_splits > 1 && (max_q_len != 1 || !part_o || !part_ml || split_len % KT != 0))
     return (int)hipErrorInvalidValue;
   AttnParams prm{};
