@@ -166,6 +166,19 @@ class EngineRunner:
                 **self.engine.stats, **self.engine.kv.stats()}
 
     # ------------------------------------------------------------------ loop
+    def _complete(self, finished) -> None:
+        """Hand the results of the requests that finished in a step to their handles (the callback-free
+        ones; streamed requests complete through their token callback)."""
+        for seq in finished or ():
+            if seq.on_token is not None:
+                continue
+            h = self._handles.pop(seq.req_id, None)
+            if h is None:
+                continue
+            self.engine.pop(seq.req_id)
+            h.result = self.engine.completion(seq)
+            h.done.set()
+
     def _on_token_wrapper(self, user_cb):
         def cb(seq, delta, finished):
             if user_cb is not None and delta:
@@ -335,7 +348,11 @@ class EngineRunner:
                 continue
             for rid, prompt, params, cb in pending:
                 try:
-                    self.engine.add_request(prompt, params, req_id=rid, on_token=self._on_token_wrapper(cb))
+                    # a request nobody streams gets no per-token callback: the engine keeps it on its decode
+                    # fast path (tokens appended per window, detokenised once at the end) and the handle is
+                    # completed from the step's finished list below
+                    self.engine.add_request(prompt, params, req_id=rid,
+                                            on_token=None if cb is None else self._on_token_wrapper(cb))
                 except Exception as e:  # bad request: fail just this handle
                     h = self._handles.pop(rid, None)
                     if h is not None:
@@ -347,7 +364,7 @@ class EngineRunner:
             self._step_t0 = time.monotonic()
             err = None
             try:
-                self.engine.step(max_window=win)
+                self._complete(self.engine.step(max_window=win))
             except Exception as e:  # engine fault: fail every in-flight request, keep serving
                 log.exception("engine step failed")
                 err = e

@@ -18,6 +18,18 @@ KV_TILE = 64  # keys per kernel tile; split lengths must be multiples of this
 _DEC_STAGES = int(os.environ.get("GRAG_DECODE_STAGES", "2"))
 DECODE_NW = {64: 1, 32: {2: 3, 3: 8, 4: 7}[_DEC_STAGES]}[int(os.environ.get("GRAG_DECODE_TK", "32"))]
 DECODE_RING_NW = {2: 3, 3: 8, 4: 7}  # stages -> nw code (microbench / A/B)
+_DEC_AUTO = "GRAG_DECODE_STAGES" not in os.environ and os.environ.get("GRAG_DECODE_TK", "32") == "32"
+
+
+def decode_variant(nsplit: int, split_len: int) -> int:
+    """Decode kernel per split plan (profiles/mb_decode_ring_r4.json, 32-key tiles): long-context decode
+    (split-KV parts covering > 2048 keys: ingest's 3-6K-token prompts) keeps two tiles in flight per wave
+    in a 3-stage ring (B176 ctx3000: 238.8 -> 207.8 us, B16 ctx6000: 53.5 -> 50.1 us); the serving
+    batches (one part of ~1.1K keys, or 256-key parts) stay on the 2-stage ring, whose 5 waves per CU win
+    there (B512 ctx1100: 207.8 vs 222.8 us, B64 ctx1152: 35.6 vs 40.7 us)."""
+    if _DEC_AUTO and nsplit > 1 and nsplit * split_len > 2048:
+        return DECODE_RING_NW[3]
+    return DECODE_NW
 # prefill kernel: 8-wave LDS-DMA variant (nw code 5, head_dim 64/128) or the
 # 4-wave register-staged kernel (nw code 4); GRAG_PREFILL_ATTN=v1 selects the latter
 PREFILL_NW = 4 if os.environ.get("GRAG_PREFILL_ATTN", "v2") == "v1" else 5
@@ -116,7 +128,9 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         out = torch.empty(T, Hq * D, dtype=q.dtype, device=q.device)
     nsplit = meta.num_splits if meta.is_decode else 1
     if meta.is_decode:
-        nw = meta.extra.get("decode_nw", DECODE_NW)
+        nw = meta.extra.get("decode_nw")
+        if nw is None:
+            nw = decode_variant(nsplit, meta.split_len)
     else:
         nw = meta.extra.get("prefill_nw", PREFILL_NW)
         if nw in (5, 6) and D not in (64, 128):

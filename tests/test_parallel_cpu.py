@@ -252,6 +252,11 @@ class _FakeAR:
     def fits(self, t):
         return False
 
+    def fits_bytes(self, t):  # the fp32 sum / all-gather ops: never taken either
+        return False
+
+    slot_bytes = 0
+
     def stage_error_check(self):
         pass
 

@@ -56,9 +56,14 @@ class FakeEngine:
             self.release.wait(10)
             self.mode = "ok"
         reqs, self.reqs = self.reqs, {}
-        for rid, cb in reqs.items():
-            seq = type("S", (), {"req_id": rid})()
-            cb(seq, "done", True)
+        finished = []
+        for rid, cb in reqs.items():  # streamed requests finish through their callback, the rest are returned
+            seq = type("S", (), {"req_id": rid, "on_token": cb})()
+            if cb is not None:
+                cb(seq, "done", True)
+            else:
+                finished.append(seq)
+        return finished
 
 
 def test_step_exception_fails_requests_then_recovers():
