@@ -685,24 +685,23 @@ def main():
 
 def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, dp_size, group, world, log):
     """The headline workload through the product's serving loop: the engine steps on its own
-    EngineRunner thread (engine/runner.py, as ``serve`` runs it); this thread only submits and waits.
-    Closed loop at the harness's concurrency: U groups of u queries in flight (staggered by S tokens, as
-    the harness fills its pipeline); whenever the oldest group completes, a new group arrives: its
+    EngineRunner thread (engine/runner.py, as ``serve`` runs it) and runs free (up to 8-step decode
+    replays); this thread only submits and waits.  Closed loop at the harness's concurrency: U groups of u
+    queries in flight, and the moment a group completes a new group arrives in its place.  An arrival's
     retrieval (embed + search + prompt) runs on the helper thread inside ``runner.arrival()`` (the
     admission hint: decode replays go one step at a time until its prompts are submitted) and its prompts
-    are submitted from that thread, as a server's request threads do.  The engine itself runs free (up to
-    8-step replays when no arrival is pending): nothing caps its windows to the pipeline as the harness
-    does.  Timed: ``steps`` x A completions; qps = completed queries / wall time, p50 TTFT = submission ->
-    first token.  ``steady_state_decode_ratio`` ~ 1.0 shows the window was steady state."""
-    import collections
-
+    are submitted from that thread, as a server's request threads do.  The fill submits a group every S
+    engine decode steps, so completions are spread out as in the harness's pipeline.  Timed: ``steps`` x A
+    completions after a warm-up of U completions; qps = completed queries / wall time; p50 TTFT =
+    submission -> first token; ``steady_state_decode_ratio`` ~ 1.0 shows the window was steady state."""
     import torch
 
     from githubrepostorag_amd.engine.runner import EngineRunner
     from githubrepostorag_amd.parallel import comm
 
     runner = EngineRunner(eng, watchdog_s=0)
-    inflight = collections.deque()  # oldest first: (handles, t_sub) or a Future of one
+    active = []    # (handles, t_sub) in flight
+    pending = []   # futures of arrivals being retrieved
 
     def arrive():
         with runner.arrival():
@@ -710,47 +709,59 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
             hs = [runner.submit(p, sp) for p in prompts]
         return hs, t_sub
 
-    def ntok(h):  # tokens a request has so far (0 until the runner thread admitted it)
-        if h.done.is_set():
-            return args.gen_len
-        s_ = eng.get(h.req_id)
-        return 0 if s_ is None else len(s_.output_ids)
+    def poll() -> list:
+        """Completed groups' TTFT lists; each is replaced by a new arrival at once."""
+        for f in [f for f in pending if f.done()]:
+            pending.remove(f)
+            active.append(f.result())
+        out = []
+        for g in [g for g in active if g[0][0].done.is_set() and all(h.done.is_set() for h in g[0])]:
+            active.remove(g)
+            hs, t_sub = g
+            for h in hs:
+                h.wait(0)  # raises a failed request's error
+            out.append([h.result.first_token_at - t_sub for h in hs])
+            pending.append(pool.submit(arrive))
+        return out
 
-    def complete_one():
-        """Wait for the oldest group, replace it with a new arrival; its queries' TTFTs (s)."""
-        g = inflight.popleft()
-        hs, t_sub = g.result() if hasattr(g, "result") else g
-        for h in hs:
-            h.wait(600)
-        inflight.append(pool.submit(arrive))
-        return [h.result.first_token_at - t_sub for h in hs]
+    def complete(n: int) -> list:
+        ttfts, got = [], 0
+        t_end = time.perf_counter() + 600
+        while got < n:
+            done = poll()
+            for t in done:
+                ttfts += t
+            got += len(done)
+            if not done:
+                if time.perf_counter() > t_end:
+                    raise TimeoutError("serving phase: no completions for 600 s")
+                time.sleep(0.0005)
+        return ttfts
 
     try:
-        with runner.arrival():  # fill with 1-step decode replays: the stagger lands exactly
-            for k in range(U - 1):
-                inflight.append(arrive())
-                d = max(1, round((k + 1) * S) - round(k * S))
+        with runner.arrival():  # fill: one group every S decode steps (1-step replays while filling)
+            d0 = eng.stats["decode_steps"]
+            for k in range(U):
+                active.append(arrive())
+                want = d0 + round((k + 1) * S)
                 t0 = time.perf_counter()
-                while min(ntok(h) for h in inflight[-1][0]) < 1 + d and time.perf_counter() - t0 < 120:
+                while eng.stats["decode_steps"] < want and time.perf_counter() - t0 < 120:
                     time.sleep(0.0002)
-            inflight.append(arrive())
-        for _ in range(max(1, args.warmup) * A):
-            complete_one()
+        complete(U)  # one full turnover of the pipeline (untimed)
         comm.barrier()
         if dev.type == "cuda":
             torch.cuda.synchronize()
         t_start = time.perf_counter()
         dec0 = eng.stats["decode_tokens"]
-        ttfts = []
-        for _ in range(steps * A):
-            ttfts += complete_one()
+        ttfts = complete(steps * A)
         dec1 = eng.stats["decode_tokens"]
         if dev.type == "cuda":
             torch.cuda.synchronize()
         comm.barrier()
         elapsed = time.perf_counter() - t_start
-        for g in inflight:  # drain (untimed)
-            hs, _ = g.result() if hasattr(g, "result") else g
+        for f in pending:  # drain (untimed)
+            active.append(f.result())
+        for hs, _ in active:
             for h in hs:
                 h.wait(600)
     finally:
@@ -771,9 +782,9 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
             # decode tokens the engine produced in the timed window / what the completed queries needed:
             # ~1.0 when the window was the pipeline's steady state (no backlog built or drained in it)
             "steady_state_decode_ratio": round((dec1 - dec0) / max(1, args.batch * steps * (args.gen_len - 1)), 3),
-            "loop": "engine/runner.py EngineRunner thread, closed loop at the harness's concurrency; arrivals "
-                    "submitted from the retrieval thread under runner.arrival() (1-step decode replays while a "
-                    "retrieval is in flight, up to 8-step replays otherwise)"}
+            "loop": "engine/runner.py EngineRunner thread (free-running, up to 8-step replays); closed loop at the "
+                    "harness's concurrency, a new group arriving as each completes; arrivals submitted from the "
+                    "retrieval thread under runner.arrival() (1-step replays while a retrieval is in flight)"}
 
 
 def _scope_tables(store, emb, corpus, rank, world, dev):
