@@ -709,13 +709,14 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
             hs = [runner.submit(p, sp) for p in prompts]
         return hs, t_sub
 
-    def poll() -> list:
-        """Completed groups' TTFT lists; each is replaced by a new arrival at once."""
+    def poll(quota: int) -> list:
+        """Up to ``quota`` completed groups' TTFT lists; each is replaced by a new arrival at once.  The
+        quota keeps every rank's arrival count identical (DP: each arrival's search is a collective)."""
         for f in [f for f in pending if f.done()]:
             pending.remove(f)
             active.append(f.result())
         out = []
-        for g in [g for g in active if g[0][0].done.is_set() and all(h.done.is_set() for h in g[0])]:
+        for g in [g for g in active if g[0][0].done.is_set() and all(h.done.is_set() for h in g[0])][:quota]:
             active.remove(g)
             hs, t_sub = g
             for h in hs:
@@ -728,7 +729,7 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
         ttfts, got = [], 0
         t_end = time.perf_counter() + 600
         while got < n:
-            done = poll()
+            done = poll(n - got)
             for t in done:
                 ttfts += t
             got += len(done)
