@@ -126,8 +126,8 @@ def parse():
                     help="ms between stack samples of the engine thread over the timed steps (0: off; diagnostics)")
     ap.add_argument("--arrival-cap", type=int, default=1,
                     help="1: the harness caps the decode window to one step while an arrival's retrieval is in "
-                         "flight (an admission policy of this bench loop; the serving runner's equivalent, "
-                         "GRAG_ARRIVAL_WINDOW, is off by default).  Reported as ttft_admission_policy")
+                         "flight (an admission policy of this bench loop; the serving runner paces its windows by the "
+                         "arrival rate instead, GRAG_ARRIVAL_WINDOW=auto).  Reported as ttft_admission_policy")
     ap.add_argument("--greedy", type=int, default=0,
                     help="1: greedy answers (temperature 0; BASELINE config 1) instead of the reference worker's "
                          "temperature 0.4 / top_p 0.8 / repetition_penalty 1.2")
@@ -212,6 +212,10 @@ def main():
         sys.exit(spawn_ranks(args.gpus))
     if args.switch_interval > 0:
         sys.setswitchinterval(args.switch_interval)
+    if os.environ.get("GRAG_DUMP_STACKS_AFTER"):  # debugging a stuck rank: every thread's stack, once
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["GRAG_DUMP_STACKS_AFTER"]), exit=False)
     if args.cpu:  # before torch initialises HIP: this process never touches a GPU
         os.environ["HIP_VISIBLE_DEVICES"] = ""
         os.environ["CUDA_VISIBLE_DEVICES"] = ""
@@ -623,8 +627,8 @@ def main():
             "p50_ttft_ms": round(p50, 2),
             # p50_ttft_ms is measured under this bench loop's admission policy, not the serving runner's default
             "ttft_admission_policy": ("harness: decode window capped to 1 step while an arrival's retrieval is in "
-                                      "flight (serving runner default: uncapped 8-step windows)")
-            if args.arrival_cap else "uncapped decode windows (serving runner default)",
+                                      "flight (serving runner: arrival-paced windows, serving_runner)")
+            if args.arrival_cap else "uncapped decode windows",
             "ingest_docs_per_s": None if ingest_dps is None else round(ingest_dps, 3),
             "ingest_docs_per_s_ref_cap": None if ingest_ref is None else ingest_ref["docs_per_s"],
             "config": {
@@ -783,7 +787,9 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
             # decode tokens the engine produced in the timed window / what the completed queries needed:
             # ~1.0 when the window was the pipeline's steady state (no backlog built or drained in it)
             "steady_state_decode_ratio": round((dec1 - dec0) / max(1, args.batch * steps * (args.gen_len - 1)), 3),
-            "loop": "engine/runner.py EngineRunner thread (free-running, up to 8-step replays); closed loop at the "
+            "arrival_window": os.environ.get("GRAG_ARRIVAL_WINDOW", "auto"),
+            "loop": "engine/runner.py EngineRunner thread (free-running, up to 8-step replays paced by the arrival "
+                    "rate: engine/runner.py _window); closed loop at the "
                     "harness's concurrency, a new group arriving as each completes; arrivals submitted from the "
                     "retrieval thread under runner.arrival() (1-step replays while a retrieval is in flight)"}
 

@@ -75,19 +75,32 @@ typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4_t;
 // vmcnt(0) in front of every ds_read); completion is tracked only by the
 // caller's explicit counted `s_waitcnt vmcnt(N)` (cdna guide §5.7 recipe:
 // M0 saved, set, used and restored inside one statement).
+template <bool NT = false>
 __device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
   const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds_dst;
   const uint32_t lu = __builtin_amdgcn_readfirstlane(lds);
   uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lu)
-      : "memory");
+  if constexpr (NT) {  // non-temporal: once-read streams (decode K/V, MI355X_MICROARCH 'nt-weights')
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off nt\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(lu)
+        : "memory");
+  } else {
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(lu)
+        : "memory");
+  }
 }
 
 template <int D, int NW, bool PAGED>
@@ -564,7 +577,7 @@ __global__ __launch_bounds__(64 * NW) void attn_prefill_kernel(AttnParams p) {
 // 96 KiB, and 512 resident waves divide the (sequence x kv-head) grid of
 // power-of-two batches into whole rounds (2 048 / 4 096 waves at 512 / 1024
 // live sequences) where 1 280 resident waves leave a 0.2-0.6 partial round.
-template <int D, int TK, int NS = 2>
+template <int D, int TK, int NS = 2, bool NT = false>
 __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
   static_assert(TK == 32 || TK == 64, "keys per tile");
   static_assert(NS >= 2 && NS <= 4, "ring stages");
@@ -632,8 +645,8 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
       const size_t off = (((size_t)blk * p.Hkv + kvh) * p.BS + (key % p.BS)) * D;
       const bf16* ks = p.k + off + ((lch ^ kswz<D>(row)) << 3);
       const bf16* vs = p.v + off + ((lch ^ vswz<D>(row)) << 3);
-      glds16(ks, kdst + i * 1024);
-      glds16(vs, vdst + i * 1024);
+      glds16<NT>(ks, kdst + i * 1024);
+      glds16<NT>(vs, vdst + i * 1024);
     }
   };
 
@@ -792,9 +805,13 @@ int launch(const AttnParams& prm, int nseq, hipStream_t stream) {
 }
 
 template <int D>
-int launch_decode(const AttnParams& prm, int nseq, int tk, int ns, hipStream_t stream) {
+int launch_decode(const AttnParams& prm, int nseq, int tk, int ns, bool nt, hipStream_t stream) {
   dim3 grid(nseq, prm.Hkv, prm.num_splits);
-  if (tk == 32 && ns == 4)
+  if (nt && tk == 32 && ns == 3)
+    paged_decode_kernel<D, 32, 3, true><<<grid, 64, 0, stream>>>(prm);
+  else if (nt && tk == 32)
+    paged_decode_kernel<D, 32, 2, true><<<grid, 64, 0, stream>>>(prm);
+  else if (tk == 32 && ns == 4)
     paged_decode_kernel<D, 32, 4><<<grid, 64, 0, stream>>>(prm);
   else if (tk == 32 && ns == 3)
     paged_decode_kernel<D, 32, 3><<<grid, 64, 0, stream>>>(prm);
@@ -827,10 +844,11 @@ int dispatch_nw(const AttnParams& prm, int nseq, int nw, bool paged, hipStream_t
   // nw == 1 / 3 with q_len == 1: LDS-DMA pipelined decode kernel with 64- / 32-key
   // tiles (32-key tiles halve the LDS ring so more single-wave workgroups share a
   // CU); nw == 2: the generic kernel with one wave per workgroup (A/B reference)
-  // nw == 7 / 8: 32-key tiles in a 4- / 3-stage ring
-  if (paged && (nw == 1 || nw == 3 || nw == 7 || nw == 8) && prm.tiles_per_seq == 1 && prm.G <= 16 &&
-      prm.BS % 16 == 0)
-    return launch_decode<D>(prm, nseq, nw == 1 ? 64 : 32, nw == 7 ? 4 : nw == 8 ? 3 : 2, stream);
+  // nw == 7 / 8: 32-key tiles in a 4- / 3-stage ring; nw == 11 / 12: 3 / 8 with non-temporal K/V loads
+  if (paged && (nw == 1 || nw == 3 || nw == 7 || nw == 8 || nw == 11 || nw == 12) && prm.tiles_per_seq == 1 &&
+      prm.G <= 16 && prm.BS % 16 == 0)
+    return launch_decode<D>(prm, nseq, nw == 1 ? 64 : 32, nw == 7 ? 4 : (nw == 8 || nw == 12) ? 3 : 2,
+                            nw >= 11, stream);
   if (nw == 5 || nw == 6) {  // LDS-DMA prefill: 8 waves, 2-stage (5) / staggered 3-stage (6) ring
     if constexpr (D == 128 || D == 64) {
       if (paged && prm.num_splits == 1 && prm.BS == 16 && prm.bt_stride <= kPrefillMaxBlocks)
@@ -838,7 +856,7 @@ int dispatch_nw(const AttnParams& prm, int nseq, int nw, bool paged, hipStream_t
     }
     return (int)hipErrorInvalidValue;
   }
-  if (nw == 3 || nw == 7 || nw == 8) nw = 1;
+  if (nw == 3 || nw == 7 || nw == 8 || nw == 11 || nw == 12) nw = 1;
   if (nw == 2) nw = 1;
   if (paged) {
     return nw == 1 ? launch<D, 1, true>(prm, nseq, stream) : launch<D, 4, true>(prm, nseq, stream);
@@ -861,7 +879,7 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
                                   float scale, int causal, int num_splits, int split_len,
                                   float* part_o, float* part_ml, int nw, hipStream_t stream) {
   if (nseq <= 0) return 0;
-  if (Hq % Hkv != 0 || BS <= 0 || nw < 1 || nw > 8) return (int)hipErrorInvalidValue;
+  if (Hq % Hkv != 0 || BS <= 0 || nw < 1 || (nw > 8 && nw != 11 && nw != 12)) return (int)hipErrorInvalidValue;
   if ((nw == 5 || nw == 6) && num_splits > 1) return (int)hipErrorInvalidValue;
   if (num_splits > 1 && (max_q_len != 1 || !part_o || !part_ml || split_len % KT != 0))
     return (int)hipErrorInvalidValue;

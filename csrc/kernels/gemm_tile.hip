@@ -96,25 +96,87 @@ struct Args {
   unsigned* cnt;   // stream-K arrival tickets, one per SK tile (zero at rest)
 };
 
-typedef f32x4_t Acc[4][2];
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-typedef bf16x8_t FragA[4][2];  // [mt][k-half]
-typedef bf16x8_t FragB[2][2];  // [nt][k-half]
 
-__device__ __forceinline__ void mma_cluster(Acc& acc, const FragA& a, const FragB& b) {
+// MFMA shape of a 64x32 quadrant (cdna guide §5.4 rule 28: the chip holds different clocks on the two
+// bf16 shapes, so both are built at the same output tile per wave and the faster one by wall is the
+// default; grag_gemm_tile_mfma() selects).  LDS bytes per quadrant are the same for both: every A / B
+// element a wave needs is read from LDS once per K-tile either way.
+//   MF 16: 4 x 2 tiles of v_mfma_f32_16x16x32_bf16, 2 k-steps of 32   (16 MFMAs per quadrant)
+//   MF 32: 2 x 1 tiles of v_mfma_f32_32x32x16_bf16, 4 k-steps of 16   ( 8 MFMAs per quadrant)
+// A quadrant's accumulators are 8 "chunks" of 4 consecutive output columns of one lane row:
+//   MF 16: chunk c = (mt, nt) = (c >> 1, c & 1): row 16 mt + (L & 15), col 16 nt + 4 (L >> 4)
+//   MF 32: chunk c = (mt, i)  = (c >> 2, c & 3): row 32 mt + (L & 31), col 8 i + 4 (L >> 5)
+template <int MF>
+struct Shape;
+template <>
+struct Shape<16> {
+  typedef f32x4_t Acc[4][2];  // [mt][nt]
+  typedef bf16x8_t FA[4][2];  // [mt][k-step]
+  typedef bf16x8_t FB[2][2];  // [nt][k-step]
+  static constexpr int kRows = 4, kCpr = 2;  // row slots per quadrant, chunks per row slot
+};
+template <>
+struct Shape<32> {
+  typedef f32x16_t Acc[2];    // [mt]
+  typedef bf16x8_t FA[2][4];  // [mt][k-step]
+  typedef bf16x8_t FB[4];     // [k-step]
+  static constexpr int kRows = 2, kCpr = 4;
+};
+
+template <int MF>
+__device__ __forceinline__ void mma_cluster(typename Shape<MF>::Acc& acc, const typename Shape<MF>::FA& a,
+                                            const typename Shape<MF>::FB& b) {
   __builtin_amdgcn_s_setprio(1);
+  if constexpr (MF == 16) {
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt][s], a[mt][s], acc[mt][nt], 0, 0, 0);
+        for (int nt = 0; nt < 2; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt][s], a[mt][s], acc[mt][nt], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[s], a[mt][s], acc[mt], 0, 0, 0);
+  }
   __builtin_amdgcn_s_setprio(0);
 }
 
-template <int EPI, int ACT>
+template <int MF>
+__device__ __forceinline__ f32x4_t chunk_get(const typename Shape<MF>::Acc& acc, int c) {
+  if constexpr (MF == 16) {
+    return acc[c >> 1][c & 1];
+  } else {
+    const int mt = c >> 2, i = 4 * (c & 3);
+    return f32x4_t{acc[mt][i], acc[mt][i + 1], acc[mt][i + 2], acc[mt][i + 3]};
+  }
+}
+template <int MF>
+__device__ __forceinline__ void chunk_set(typename Shape<MF>::Acc& acc, int c, const f32x4_t& v) {
+  if constexpr (MF == 16) {
+    acc[c >> 1][c & 1] = v;
+  } else {
+    const int mt = c >> 2, i = 4 * (c & 3);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[mt][i + r] = v[r];
+  }
+}
+template <int MF>
+__device__ __forceinline__ void acc_zero(typename Shape<MF>::Acc& acc) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) chunk_set<MF>(acc, c, f32x4_t{0.f, 0.f, 0.f, 0.f});
+}
+
+template <int EPI, int ACT, int MF>
 __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
+  using Acc = typename Shape<MF>::Acc;
+  using FragA = typename Shape<MF>::FA;
+  using FragB = typename Shape<MF>::FB;
+  constexpr int kRows = Shape<MF>::kRows, kCpr = Shape<MF>::kCpr;
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
 
   const int tid = threadIdx.x;
@@ -134,24 +196,39 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
     n0 = ((t % band) / gsz) * 256;
   };
 
-  // ---- fragment reads: row (L & 15) of a 16-row group, logical chunk 4s + L/16, swizzle (L>>1)&7
+  // ---- fragment reads, swizzle (row >> 1) & 7 (the slot row's low 4 bits are the lane's):
+  //   MF 16: row (L & 15) of a 16-row group, logical chunk 4s + L/16 (k-step s of 32)
+  //   MF 32: row (L & 31) of a 32-row group, logical chunk 2s + L/32 (k-step s of 16)
   const int cb = (L >> 4) ^ ((L >> 1) & 7);
   const int off0 = (L & 15) * 128 + cb * 16;
   const int off1 = (L & 15) * 128 + (cb ^ 4) * 16;
+  auto off32 = [&](int s) { return (L & 31) * 128 + (((2 * s + (L >> 5)) ^ ((L >> 1) & 7)) * 16); };
   auto readA = [&](FragA& a, int q, int buf) {
     const char* base = smem + buf * kBuf + q * kSlot + wr * 64 * 128;
+    if constexpr (MF == 16) {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      a[mt][0] = *reinterpret_cast<const bf16x8_t*>(base + mt * 2048 + off0);
-      a[mt][1] = *reinterpret_cast<const bf16x8_t*>(base + mt * 2048 + off1);
+      for (int mt = 0; mt < 4; ++mt) {
+        a[mt][0] = *reinterpret_cast<const bf16x8_t*>(base + mt * 2048 + off0);
+        a[mt][1] = *reinterpret_cast<const bf16x8_t*>(base + mt * 2048 + off1);
+      }
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) a[mt][s] = *reinterpret_cast<const bf16x8_t*>(base + mt * 4096 + off32(s));
     }
   };
   auto readB = [&](FragB& b, int q, int buf) {
     const char* base = smem + buf * kBuf + (2 + q) * kSlot + wc * 32 * 128;
+    if constexpr (MF == 16) {
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      b[nt][0] = *reinterpret_cast<const bf16x8_t*>(base + nt * 2048 + off0);
-      b[nt][1] = *reinterpret_cast<const bf16x8_t*>(base + nt * 2048 + off1);
+      for (int nt = 0; nt < 2; ++nt) {
+        b[nt][0] = *reinterpret_cast<const bf16x8_t*>(base + nt * 2048 + off0);
+        b[nt][1] = *reinterpret_cast<const bf16x8_t*>(base + nt * 2048 + off1);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) b[s] = *reinterpret_cast<const bf16x8_t*>(base + off32(s));
     }
   };
 
@@ -190,15 +267,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
       for (int i = 0; i < 2; ++i)
         glds16(srcB[q][i] + kt * 64, smem + buf * kBuf + (2 + q) * kSlot + (2 * w + i) * 1024);
     };
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        acc00[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        acc01[mt][nt] = acc00[mt][nt];
-        acc11[mt][nt] = acc00[mt][nt];
-        acc10[mt][nt] = acc00[mt][nt];
-      }
+    acc_zero<MF>(acc00);
+    acc_zero<MF>(acc01);
+    acc_zero<MF>(acc11);
+    acc_zero<MF>(acc10);
     // prologue: tile 0 (all 4 slots) + tile 1 (A q0, B q0, B q1); tile 1's A q1 goes out in P1(0)
     issueA(0, 0, 0);
     issueB(0, 0, 0);
@@ -225,7 +297,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
       if (STEADY || kt + 1 < nk) issueA(1, kt + 1, buf ^ 1);
       wait_lgkm0();
       bar();
-      mma_cluster(acc00, a, b0);
+      mma_cluster<MF>(acc00, a, b0);
       if (STEADY) wait_vm<8>(); else wait_vm<0>();
       bar();
       // P2: quadrant (0,1)
@@ -233,7 +305,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
       if (STEADY) issueA(0, kt + 2, buf);
       wait_lgkm0();
       bar();
-      mma_cluster(acc01, a, b1);
+      mma_cluster<MF>(acc01, a, b1);
       if (STEADY) wait_vm<8>(); else wait_vm<0>();
       bar();
       // P3: quadrant (1,1)
@@ -241,13 +313,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
       if (STEADY) issueB(0, kt + 2, buf);
       wait_lgkm0();
       bar();
-      mma_cluster(acc11, a, b1);
+      mma_cluster<MF>(acc11, a, b1);
       if (STEADY) wait_vm<8>(); else wait_vm<0>();
       bar();
       // P4: quadrant (1,0)
       if (STEADY) issueB(1, kt + 2, buf);
       bar();
-      mma_cluster(acc10, a, b0);
+      mma_cluster<MF>(acc10, a, b0);
       if (STEADY) wait_vm<8>(); else wait_vm<0>();
       bar();
     };
@@ -257,76 +329,86 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
     if (!lag) bar();
   };
 
-  // accumulator chunks (quadrant, mt, nt) in a fixed order: the stream-K slab layout
-#define GT_CHUNKS(X)                                                                                            \
-  X(acc00, 0, 0, 0) X(acc00, 1, 0, 1) X(acc00, 2, 1, 0) X(acc00, 3, 1, 1) X(acc00, 4, 2, 0) X(acc00, 5, 2, 1)  \
-  X(acc00, 6, 3, 0) X(acc00, 7, 3, 1) X(acc01, 8, 0, 0) X(acc01, 9, 0, 1) X(acc01, 10, 1, 0) X(acc01, 11, 1, 1) \
-  X(acc01, 12, 2, 0) X(acc01, 13, 2, 1) X(acc01, 14, 3, 0) X(acc01, 15, 3, 1) X(acc11, 16, 0, 0)             \
-  X(acc11, 17, 0, 1) X(acc11, 18, 1, 0) X(acc11, 19, 1, 1) X(acc11, 20, 2, 0) X(acc11, 21, 2, 1)             \
-  X(acc11, 22, 3, 0) X(acc11, 23, 3, 1) X(acc10, 24, 0, 0) X(acc10, 25, 0, 1) X(acc10, 26, 1, 0)             \
-  X(acc10, 27, 1, 1) X(acc10, 28, 2, 0) X(acc10, 29, 2, 1) X(acc10, 30, 3, 0) X(acc10, 31, 3, 1)
-
-  // ---- epilogue.  acc_qm_qn[mt][nt][r]: row m0 + 128 wr + 64 qm + 16 mt + (L & 15),
-  // col n0 + 64 wc + 32 qn + 16 nt + 4 (L >> 4) + r
-  // T21-style widened stores (cdna guide §5.5): a lane holds columns 4g..4g+3 (nt 0) and 16+4g..16+4g+3
-  // (nt 1) of its row, g = L >> 4.  One v_permlane16_swap per dword pair trades nt-1 data of 16-lane row
-  // 0 / 2 for nt-0 data of row 1 / 3, after which each lane holds 8 contiguous columns of one row:
-  // g = 0 -> 0..7, 1 -> 16..23, 2 -> 8..15, 3 -> 24..31 of the wave's 32-column block -- one 16-byte
-  // store instead of two 8-byte ones.  Partners share the row (L & 15), so a row guard keeps both
-  // lanes of every swap active together.
+  // ---- epilogue.  Quadrant (qm, qn) chunk c = (row slot rs, i): row m0 + 128 wr + 64 qm + rrow(rs),
+  // cols n0 + 64 wc + 32 qn + ccol(i) + 0..3 (chunk map at Shape<>).
+  // T21-style widened stores (cdna guide §5.5): one permlane swap per dword pair leaves each lane with 8
+  // contiguous columns of its row -> 16-byte stores.
+  //   MF 16: a lane holds cols 4g..4g+3 (i 0) and 16+4g.. (i 1), g = L >> 4; v_permlane16_swap trades i-1
+  //          data of 16-lane row 0 / 2 for i-0 data of row 1 / 3: g = 0 -> 0..7, 1 -> 16..23, 2 -> 8..15,
+  //          3 -> 24..31 of the wave's 32-column block (one store).
+  //   MF 32: a lane holds cols 8i + 4h.. (h = L >> 5); v_permlane32_swap of (i 0, i 1) and (i 2, i 3):
+  //          h = 0 -> 0..7 and 16..23, h = 1 -> 8..15 and 24..31 (two stores).
+  // Partners share the row, so a row guard keeps both lanes of every swap active together.
+  auto rrow = [&](int rs) { return MF == 16 ? 16 * rs + (L & 15) : 32 * rs + (L & 31); };
+  auto ccol = [&](int i) { return MF == 16 ? 16 * i + 4 * (L >> 4) : 8 * i + 4 * (L >> 5); };
   const bool wide_ok = ((uintptr_t)p.C & 15) == 0 && (p.ldc & 7) == 0;
-  const int wcol = ((L >> 4) & 1) * 16 + ((L >> 5) & 1) * 8;
-  auto store_row16 = [&](bf16* row_base, uint32_t (&d)[2][2]) {
+  auto store_row = [&](bf16* row_base, uint32_t (&d)[kCpr][2]) {
+    if constexpr (MF == 16) {
+      const int wcol = ((L >> 4) & 1) * 16 + ((L >> 5) & 1) * 8;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const auto r = __builtin_amdgcn_permlane16_swap(d[0][h], d[1][h], false, false);
-      d[0][h] = r[0];
-      d[1][h] = r[1];
+      for (int h = 0; h < 2; ++h) {
+        const auto r = __builtin_amdgcn_permlane16_swap(d[0][h], d[1][h], false, false);
+        d[0][h] = r[0];
+        d[1][h] = r[1];
+      }
+      *reinterpret_cast<u32x4_t*>(row_base + wcol) = u32x4_t{d[0][0], d[0][1], d[1][0], d[1][1]};
+    } else {
+      const int wcol = 8 * (L >> 5);
+#pragma unroll
+      for (int j = 0; j < 4; j += 2)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const auto r = __builtin_amdgcn_permlane32_swap(d[j][h], d[j + 1][h], false, false);
+          d[j][h] = r[0];
+          d[j + 1][h] = r[1];
+        }
+      *reinterpret_cast<u32x4_t*>(row_base + wcol) = u32x4_t{d[0][0], d[0][1], d[1][0], d[1][1]};
+      *reinterpret_cast<u32x4_t*>(row_base + wcol + 16) = u32x4_t{d[2][0], d[2][1], d[3][0], d[3][1]};
     }
-    *reinterpret_cast<u32x4_t*>(row_base + wcol) = u32x4_t{d[0][0], d[0][1], d[1][0], d[1][1]};
   };
   auto epilogue = [&](int m0, int n0, int split) {
-    const int mrow = m0 + wr * 128 + (L & 15);
-    const int ncol = n0 + wc * 64 + 4 * (L >> 4);
+    const int mrow = m0 + wr * 128;
     if constexpr (EPI == EPI_SILU) {
       bf16* C = (bf16*)p.C;
-      const int ocol = (n0 + wc * 64) / 2 + 4 * (L >> 4);
-      float bg[2][4], bu[2][4];
+      const int nb = n0 + wc * 64;  // this wave's 64-column gate/up block: output cols [nb / 2, +32)
+      const int obase = nb / 2;
+      float bg[kCpr][4], bu[kCpr][4];
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
+      for (int i = 0; i < kCpr; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int n = ncol + nt * 16 + r;
-          bg[nt][r] = (p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
-          bu[nt][r] = (p.bias && n + 32 < p.N) ? (float)p.bias[n + 32] : 0.f;
+          const int n = nb + ccol(i) + r;
+          bg[i][r] = (p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
+          bu[i][r] = (p.bias && n + 32 < p.N) ? (float)p.bias[n + 32] : 0.f;
         }
       // the wave's 32 output columns of this 64-column gate/up block are whole: 16-byte stores
-      const bool wide = wide_ok && 2 * ((n0 + wc * 64) / 2 + 32) <= p.N;
-      const int obase = (n0 + wc * 64) / 2;
+      const bool wide = wide_ok && 2 * (obase + 32) <= p.N;
       auto emit = [&](const Acc& g, const Acc& u, int qm) {
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const int m = mrow + qm * 64 + mt * 16;
+        for (int rs = 0; rs < kRows; ++rs) {
+          const int m = mrow + qm * 64 + rrow(rs);
           if (m >= p.M) continue;
           if (wide) {
-            uint32_t d[2][2];
+            uint32_t d[kCpr][2];
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
+            for (int i = 0; i < kCpr; ++i) {
+              const f32x4_t gv = chunk_get<MF>(g, rs * kCpr + i), uv = chunk_get<MF>(u, rs * kCpr + i);
 #pragma unroll
               for (int h = 0; h < 2; ++h)
-                d[nt][h] = pack_bf16x2(silu_f(g[mt][nt][2 * h] + bg[nt][2 * h]) * (u[mt][nt][2 * h] + bu[nt][2 * h]),
-                                       silu_f(g[mt][nt][2 * h + 1] + bg[nt][2 * h + 1]) *
-                                           (u[mt][nt][2 * h + 1] + bu[nt][2 * h + 1]));
-            store_row16(C + (size_t)m * p.ldc + obase, d);
+                d[i][h] = pack_bf16x2(silu_f(gv[2 * h] + bg[i][2 * h]) * (uv[2 * h] + bu[i][2 * h]),
+                                      silu_f(gv[2 * h + 1] + bg[i][2 * h + 1]) * (uv[2 * h + 1] + bu[i][2 * h + 1]));
+            }
+            store_row(C + (size_t)m * p.ldc + obase, d);
             continue;
           }
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            const int oc = ocol + nt * 16;
+          for (int i = 0; i < kCpr; ++i) {
+            const int oc = obase + ccol(i);
             if (2 * oc >= p.N) continue;
+            const f32x4_t gv = chunk_get<MF>(g, rs * kCpr + i), uv = chunk_get<MF>(u, rs * kCpr + i);
             bf16x4_t o;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = f2bits(silu_f(g[mt][nt][r] + bg[nt][r]) * (u[mt][nt][r] + bu[nt][r]));
+            for (int r = 0; r < 4; ++r) o[r] = f2bits(silu_f(gv[r] + bg[i][r]) * (uv[r] + bu[i][r]));
             *reinterpret_cast<bf16x4_t*>(C + (size_t)m * p.ldc + oc) = o;
           }
         }
@@ -334,47 +416,50 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
       emit(acc00, acc01, 0);
       emit(acc10, acc11, 1);
     } else {
-      float bv[2][2][4];
+      float bv[2][kCpr][4];
 #pragma unroll
       for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+        for (int i = 0; i < kCpr; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int n = ncol + qn * 32 + nt * 16 + r;
-            bv[qn][nt][r] = (EPI == EPI_STORE && p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
+            const int n = n0 + wc * 64 + qn * 32 + ccol(i) + r;
+            bv[qn][i][r] = (EPI == EPI_STORE && p.bias && n < p.N) ? (float)p.bias[n] : 0.f;
           }
       auto emit = [&](const Acc& acc, int qm, int qn) {
         const int nbase = n0 + wc * 64 + qn * 32;
         const bool wide = EPI == EPI_STORE && wide_ok && nbase + 32 <= p.N;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const int m = mrow + qm * 64 + mt * 16;
+        for (int rs = 0; rs < kRows; ++rs) {
+          const int m = mrow + qm * 64 + rrow(rs);
           if (m >= p.M) continue;
           if constexpr (EPI == EPI_STORE) {
             if (wide) {
-              uint32_t d[2][2];
+              uint32_t d[kCpr][2];
 #pragma unroll
-              for (int nt = 0; nt < 2; ++nt)
+              for (int i = 0; i < kCpr; ++i) {
+                const f32x4_t v = chunk_get<MF>(acc, rs * kCpr + i);
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                  d[nt][h] = pack_bf16x2(act_f<ACT>(acc[mt][nt][2 * h] + bv[qn][nt][2 * h]),
-                                         act_f<ACT>(acc[mt][nt][2 * h + 1] + bv[qn][nt][2 * h + 1]));
-              store_row16((bf16*)p.C + (size_t)m * p.ldc + nbase, d);
+                  d[i][h] = pack_bf16x2(act_f<ACT>(v[2 * h] + bv[qn][i][2 * h]),
+                                        act_f<ACT>(v[2 * h + 1] + bv[qn][i][2 * h + 1]));
+              }
+              store_row((bf16*)p.C + (size_t)m * p.ldc + nbase, d);
               continue;
             }
           }
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            const int n = ncol + qn * 32 + nt * 16;
+          for (int i = 0; i < kCpr; ++i) {
+            const int n = nbase + ccol(i);
             if (n >= p.N) continue;
+            const f32x4_t v = chunk_get<MF>(acc, rs * kCpr + i);
             if constexpr (EPI == EPI_PARTIAL) {
               float* ws = p.slab + ((size_t)split * p.M + m) * p.N + n;
-              *reinterpret_cast<f32x4_t*>(ws) = acc[mt][nt];
+              *reinterpret_cast<f32x4_t*>(ws) = v;
             } else {
               bf16x4_t o;
 #pragma unroll
-              for (int r = 0; r < 4; ++r) o[r] = f2bits(act_f<ACT>(acc[mt][nt][r] + bv[qn][nt][r]));
+              for (int r = 0; r < 4; ++r) o[r] = f2bits(act_f<ACT>(v[r] + bv[qn][i][r]));
               *reinterpret_cast<bf16x4_t*>((bf16*)p.C + (size_t)m * p.ldc + n) = o;
             }
           }
@@ -430,10 +515,16 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
       {
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             p.slab + (size_t)slot_of(j, ts) * 65536, 0, 65536 * 4, 0x00020000);
-#define GT_STORE(ACC, Q, MT, NT) \
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, ACC[MT][NT]), rs, tid * 16, Q * kThreads * 16, 16);
-        GT_CHUNKS(GT_STORE)
-#undef GT_STORE
+auto slab_store = [&](const Acc& acc, int q) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, chunk_get<MF>(acc, c)), rs, tid * 16,
+                                                   (q * 8 + c) * kThreads * 16, 16);
+        };
+        slab_store(acc00, 0);
+        slab_store(acc01, 1);
+        slab_store(acc11, 2);
+        slab_store(acc10, 3);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -460,10 +551,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
           if (c == j) {
             if (c == first) {
 #pragma unroll
-              for (int i = 0; i < 8; ++i) s[i] = acc[i >> 1][i & 1];
+              for (int i = 0; i < 8; ++i) s[i] = chunk_get<MF>(acc, i);
             } else {
 #pragma unroll
-              for (int i = 0; i < 8; ++i) s[i] += acc[i >> 1][i & 1];
+              for (int i = 0; i < 8; ++i) s[i] += chunk_get<MF>(acc, i);
             }
             continue;
           }
@@ -480,7 +571,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
           }
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i >> 1][i & 1] = s[i];
+        for (int i = 0; i < 8; ++i) chunk_set<MF>(acc, i, s[i]);
       };
       fold(acc00, 0);
       fold(acc01, 8);
@@ -489,7 +580,6 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
     }
     epilogue(m0, n0, split);
   }
-#undef GT_CHUNKS
 }
 
 // Split-K combine: out = epilogue(sum_s ws[s]) — 8 output columns per thread.
@@ -539,14 +629,25 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   *reinterpret_cast<bf16x8_t*>(C + (size_t)m * ldc + o) = pack8(v);
 }
 
+int g_mfma = 16;  // grag_gemm_tile_mfma()
+
 template <int EPI, int ACT>
 int launch(const Args& a, hipStream_t stream) {
   const int nwg = a.dp_tiles + a.sk_grid;
-  gemm_tile_kernel<EPI, ACT><<<nwg, kThreads, 0, stream>>>(a);
+  if (g_mfma == 32) gemm_tile_kernel<EPI, ACT, 32><<<nwg, kThreads, 0, stream>>>(a);
+  else gemm_tile_kernel<EPI, ACT, 16><<<nwg, kThreads, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
 }  // namespace
+
+// MFMA shape of the tile kernel for later launches (16: v_mfma_f32_16x16x32_bf16, the default; 32:
+// v_mfma_f32_32x32x16_bf16); any other value only queries.  Returns the previous shape.
+GRAG_API int grag_gemm_tile_mfma(int mf) {
+  const int prev = g_mfma;
+  if (mf == 16 || mf == 32) g_mfma = mf;
+  return prev;
+}
 
 // out = epilogue(sum_s ws[s]) for fp32 split-K planes ws[S][M][N] (also used by gemm_decode.hip).
 GRAG_API int grag_splitk_reduce(const void* ws, const void* bias, void* C, int ldc, int M, int N, int S, int epi,

@@ -164,7 +164,7 @@ class EngineLLM:
         out: list[CompletionResponse | None] = [None] * len(prompt_list)
         todo = list(range(len(prompt_list)))
         for attempt in range(self.retries + 1):
-            hs = [(i, self.runner.submit(ids[i], sp)) for i in todo]
+            hs = [(i, self.runner.submit(ids[i], sp, interactive=self.mode != "ingest")) for i in todo]
             failed = []
             for i, h in hs:
                 try:
@@ -192,7 +192,7 @@ class EngineLLM:
                 if cancel_check is None:
                     c = self.runner.generate(text, sp, on_token=on_token, timeout=self.timeout_s)
                 else:  # poll the job's cancel flag so a cancel aborts mid-decode
-                    h = self.runner.submit(text, sp, on_token=on_token)
+                    h = self.runner.submit(text, sp, on_token=on_token, interactive=self.mode != "ingest")
                     t_end = time.monotonic() + self.timeout_s
                     while not h.done.wait(0.05):
                         if cancel_check() or time.monotonic() > t_end:

@@ -131,7 +131,9 @@ class LLMEngine:
                       # host-side time by section (the GPU idles whenever one of these outlasts the queued work)
                       "host_sched_s": 0.0, "host_prefill_prep_s": 0.0, "host_prefill_launch_s": 0.0,
                       "host_prefill_sample_s": 0.0, "host_prefill_post_s": 0.0, "host_decode_prep_s": 0.0,
-                      "host_decode_post_s": 0.0, "capture_s": 0.0}
+                      "host_decode_post_s": 0.0, "capture_s": 0.0,
+                      # prompt tokens submitted / taken from the prefix cache at admission (the rest is prefill)
+                      "prompt_tokens": 0, "prefix_hit_tokens": 0}
         # optional per-step timeline (a list; None = off): (t_start, kind, rows, tokens, seconds) per step,
         # kind "prefill" / "decode" / "mixed" / "capture" — the ingest critical-path trace reads it
         self.trace: list | None = None
@@ -188,6 +190,7 @@ class LLMEngine:
         seq = Sequence(req_id, ids, params, on_token=on_token)
         with self._lock:
             self._seqs[req_id] = seq
+            self.stats["prompt_tokens"] += len(ids)
         self.sched.add(seq)
         return req_id
 
@@ -252,6 +255,7 @@ class LLMEngine:
             finished.append(s)
         adm = getattr(self.sched, "last_admitted", [])
         if adm:
+            self.stats["prefix_hit_tokens"] += sum(s.cached_prefix for s in adm)
             reset_slots(self.sampler, [(s.slot, s.params.temperature, s.params.top_p, s.params.top_k,
                                         s.params.repetition_penalty, s.all_ids, s.params.seed) for s in adm])
         self.stats["host_sched_s"] += time.perf_counter() - th

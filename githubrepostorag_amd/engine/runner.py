@@ -63,14 +63,20 @@ class GenerationHandle:
 
 
 class EngineRunner:
-    # arrival-aware decode window (GRAG_ARRIVAL_WINDOW=N): while requests keep arriving (one submitted
-    # within the last ARRIVAL_RECENT_S) a decode replay runs at most N steps, so a new prompt waits ~N
-    # decode steps before its prefill instead of a whole 8-step window.  Off by default: on the bench's
-    # agent e2e phase (64 concurrent 3-round jobs of short calls) N = 2 measured 11.1-11.9 vs 11.8-12.4
-    # jobs/s and p50 first-answer-token 4.26-4.59 vs 4.01-4.28 s (same box, profiles/ab_arrival_window_r2.txt):
-    # a chain of short calls pays for the extra replays more than it gains on admission
+    # arrival-aware decode window.  A hipGraph replay of K decode steps cannot be cut short, so a prompt
+    # submitted during one waits for the rest of it (up to 8 steps: ~220 ms at 1024 live rows) before its
+    # prefill.  GRAG_ARRIVAL_WINDOW:
+    #   "auto" (default): paced by the arrival rate -- while arrivals keep coming (one within the last two
+    #          mean gaps), a replay lasts at most half the mean gap between arrival events (EWMA; submits
+    #          within 2 ms are one event), at least one step: an arrival waits ~1/4 gap on average instead
+    #          of half a window.  No arrivals -> full windows.
+    #   N > 0: fixed cap of N steps while requests keep arriving (one within ARRIVAL_RECENT_S);
+    #   0:     off (full windows).  profiles/ab_arrival_window_r2.txt: fixed N = 2 on the agent phase
+    #          cost 4-6 % jobs/s; the paced form is measured in docs/STATUS.md (round 4).
     ARRIVAL_RECENT_S = 0.05
-    ARRIVAL_WINDOW = int(os.environ.get("GRAG_ARRIVAL_WINDOW", "0"))
+    _AW = os.environ.get("GRAG_ARRIVAL_WINDOW", "auto")
+    ARRIVAL_WINDOW = -1 if _AW == "auto" else int(_AW)
+    MAX_WINDOW = 8
 
     def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005, watchdog_s: float = 120.0,
                  on_health=None, tp=None, start: bool = True):
@@ -94,6 +100,9 @@ class EngineRunner:
         self._step_failed: BaseException | None = None  # TP: reported in the next control all-reduce
         self._ar_failed = False
         self._expecting = 0  # admission hints in flight (arrival())
+        self._gap = None      # EWMA of the gap between arrival events (s)
+        self._last_event = -1e9
+        self._step_s = None   # EWMA of one decode step's time (s), from the replays
         self.ctrl_stats = {"iterations": 0, "bytes": 0, "payloads": 0}
         self._thread = threading.Thread(target=self._loop if self.leader else self.follow, name="grag-engine",
                                         daemon=True)
@@ -105,7 +114,10 @@ class EngineRunner:
             self._wd.start()
 
     # ------------------------------------------------------------------ API
-    def submit(self, prompt, params: SamplingParams | None = None, on_token=None) -> GenerationHandle:
+    def submit(self, prompt, params: SamplingParams | None = None, on_token=None,
+               interactive: bool = True) -> GenerationHandle:
+        """``interactive``: someone waits for this request's first token (an agent call, an API request);
+        batch work (ingest) passes False and does not pace the arrival-aware decode window."""
         import uuid
 
         rid = uuid.uuid4().hex
@@ -113,7 +125,14 @@ class EngineRunner:
         with self._cv:
             self._handles[rid] = h
             self._pending.append((rid, prompt, params, on_token))
-            self._last_submit = time.monotonic()
+            if interactive:
+                now = time.monotonic()
+                self._last_submit = now
+                if now - self._last_event > 0.002:  # a new arrival event (a burst of submits is one)
+                    if self._last_event > 0:
+                        g = min(now - self._last_event, 5.0)
+                        self._gap = g if self._gap is None else 0.8 * self._gap + 0.2 * g
+                    self._last_event = now
             self._cv.notify()
         return h
 
@@ -136,9 +155,15 @@ class EngineRunner:
     def _window(self) -> int | None:
         if self._expecting > 0:
             return 1
-        if self.ARRIVAL_WINDOW <= 0:
+        if self.ARRIVAL_WINDOW == 0:
             return None
-        return self.ARRIVAL_WINDOW if time.monotonic() - self._last_submit < self.ARRIVAL_RECENT_S else None
+        now = time.monotonic()
+        if self.ARRIVAL_WINDOW > 0:
+            return self.ARRIVAL_WINDOW if now - self._last_submit < self.ARRIVAL_RECENT_S else None
+        g, d = self._gap, self._step_s
+        if g is None or d is None or now - self._last_event > 2 * g:
+            return None
+        return max(1, min(self.MAX_WINDOW, int(0.5 * g / d)))
 
     def generate(self, prompt, params: SamplingParams | None = None, on_token=None,
                  timeout: float | None = None) -> Completion:
@@ -364,7 +389,13 @@ class EngineRunner:
             self._step_t0 = time.monotonic()
             err = None
             try:
+                st = self.engine.stats
+                ds0, dt0 = st.get("decode_steps", 0), st.get("decode_s", 0.0)
                 self._complete(self.engine.step(max_window=win))
+                n = st.get("decode_steps", 0) - ds0
+                if n > 0:  # decode step time for the paced arrival window
+                    per = (st.get("decode_s", 0.0) - dt0) / n
+                    self._step_s = per if self._step_s is None else 0.7 * self._step_s + 0.3 * per
             except Exception as e:  # engine fault: fail every in-flight request, keep serving
                 log.exception("engine step failed")
                 err = e

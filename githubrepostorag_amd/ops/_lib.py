@@ -59,6 +59,7 @@ _SIGS = {
     "grag_bitmap_update": [P, P, I, I, P],
     "grag_gemm_tile": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "grag_splitk_reduce": [P, P, P, I, I, I, I, I, I, P],
+    "grag_gemm_tile_mfma": [I],
     "grag_gemm_decode": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_decode_has": [I, I, I],
     "grag_gemm_w4": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P],
@@ -93,6 +94,9 @@ def lib():
                 continue
             fn.argtypes = args
             fn.restype = ctypes.c_long if name.endswith("_ws_floats") else ctypes.c_int
+        mf = os.environ.get("GRAG_GEMM_MFMA")
+        if mf and getattr(handle, "grag_gemm_tile_mfma", None) is not None:
+            handle.grag_gemm_tile_mfma(int(mf))  # tile GEMM MFMA shape (16 default, 32)
         _lib = handle
         return _lib
 

@@ -19,17 +19,27 @@ _DEC_STAGES = int(os.environ.get("GRAG_DECODE_STAGES", "2"))
 DECODE_NW = {64: 1, 32: {2: 3, 3: 8, 4: 7}[_DEC_STAGES]}[int(os.environ.get("GRAG_DECODE_TK", "32"))]
 DECODE_RING_NW = {2: 3, 3: 8, 4: 7}  # stages -> nw code (microbench / A/B)
 _DEC_AUTO = "GRAG_DECODE_STAGES" not in os.environ and os.environ.get("GRAG_DECODE_TK", "32") == "32"
+# non-temporal K/V LDS-DMA loads (nt: the cache is read once per decode step; MI355X_MICROARCH 'nt-weights'):
+# codes 11 / 12 are 3 / 8 with nt.  profiles/mb_decode_nt_r4.json: B512 ctx1100 206.4 -> 186.8 us (5.59 -> 6.18
+# TB/s), B1024 413.7 -> 382.5, B256 113.3 -> 97.7, B176 ctx3000 (3 stages) 208.0 -> 197.0, B16 ctx6000 50.2 ->
+# 48.0; grids under ~1.5K waves gain nothing (B64 ctx1152 x 5 parts: 35.8 vs 36.7, B1: equal) -> default there
+DECODE_NT = {3: 11, 8: 12}
+DECODE_NT_MIN_WAVES = 1536
+_DEC_NT = os.environ.get("GRAG_DECODE_NT", "auto")
 
 
-def decode_variant(nsplit: int, split_len: int) -> int:
+def decode_variant(nsplit: int, split_len: int, waves: int | None = None) -> int:
     """Decode kernel per split plan (profiles/mb_decode_ring_r4.json, 32-key tiles): long-context decode
     (split-KV parts covering > 2048 keys: ingest's 3-6K-token prompts) keeps two tiles in flight per wave
     in a 3-stage ring (B176 ctx3000: 238.8 -> 207.8 us, B16 ctx6000: 53.5 -> 50.1 us); the serving
     batches (one part of ~1.1K keys, or 256-key parts) stay on the 2-stage ring, whose 5 waves per CU win
-    there (B512 ctx1100: 207.8 vs 222.8 us, B64 ctx1152: 35.6 vs 40.7 us)."""
-    if _DEC_AUTO and nsplit > 1 and nsplit * split_len > 2048:
-        return DECODE_RING_NW[3]
-    return DECODE_NW
+    there (B512 ctx1100: 207.8 vs 222.8 us, B64 ctx1152: 35.6 vs 40.7 us).  ``waves``: the launch's
+    (sequence x kv-head x split) count; grids of >= DECODE_NT_MIN_WAVES load K/V non-temporally."""
+    nw = DECODE_RING_NW[3] if _DEC_AUTO and nsplit > 1 and nsplit * split_len > 2048 else DECODE_NW
+    nt = _DEC_NT == "1" or (_DEC_NT == "auto" and waves is not None and waves >= DECODE_NT_MIN_WAVES)
+    return DECODE_NT.get(nw, nw) if nt else nw
+
+
 # prefill kernel: 8-wave LDS-DMA variant (nw code 5, head_dim 64/128) or the
 # 4-wave register-staged kernel (nw code 4); GRAG_PREFILL_ATTN=v1 selects the latter
 PREFILL_NW = 4 if os.environ.get("GRAG_PREFILL_ATTN", "v2") == "v1" else 5
@@ -130,7 +140,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     if meta.is_decode:
         nw = meta.extra.get("decode_nw")
         if nw is None:
-            nw = decode_variant(nsplit, meta.split_len)
+            nw = decode_variant(nsplit, meta.split_len, meta.num_seqs * Hkv * nsplit)
     else:
         nw = meta.extra.get("prefill_nw", PREFILL_NW)
         if nw in (5, 6) and D not in (64, 128):

@@ -205,6 +205,14 @@ def schedule(M: int, N: int, K: int, silu: bool = False) -> tuple[int, int]:
     return plan(M, N, K)
 
 
+def set_mfma(mf: int) -> int:
+    """Select the tile kernel's MFMA shape for later launches (16: v_mfma_f32_16x16x32_bf16, the default;
+    32: v_mfma_f32_32x32x16_bf16; csrc/kernels/gemm_tile.hip ``Shape``).  Returns the previous shape."""
+    from ._lib import lib
+
+    return int(lib().grag_gemm_tile_mfma(int(mf)))
+
+
 def _ws_floats(M: int, N: int, ksplit: int, sk: int) -> int:
     return ksplit * M * N if ksplit > 1 else (2 * abs(sk) * 65536 if sk else 0)
 

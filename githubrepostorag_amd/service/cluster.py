@@ -55,7 +55,7 @@ import subprocess
 import sys
 import threading
 import time
-from multiprocessing.connection import Client, Listener
+from multiprocessing.connection import AuthenticationError, Client, Listener, answer_challenge, deliver_challenge
 
 from . import metrics as M
 from .events import CancelFlags, EventLog
@@ -109,7 +109,9 @@ class ReplicaHub:
 
         self.events = events
         self.authkey = authkey or secrets.token_bytes(16)
-        self.listener = Listener((host, port), authkey=self.authkey)
+        # authentication runs on each connection's reader thread (never the accept thread: one slow or stuck
+        # client cannot hold up the other replicas' connects); a deep backlog absorbs connect bursts
+        self.listener = Listener((host, port), backlog=128)
         self.address = self.listener.address
         self.replicas: dict[int, _Replica] = {}
         self.owner: dict[str, _Replica] = {}
@@ -148,6 +150,13 @@ class ReplicaHub:
 
     def _reader(self, conn) -> None:
         rep = None
+        try:
+            deliver_challenge(conn, self.authkey)
+            answer_challenge(conn, self.authkey)
+        except (AuthenticationError, EOFError, OSError, AssertionError):
+            log.warning("replica hub: rejected a connection (authentication)")
+            conn.close()
+            return
         try:
             hello = conn.recv()
             if not (isinstance(hello, tuple) and hello and hello[0] == "hello"):

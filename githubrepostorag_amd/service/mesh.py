@@ -42,7 +42,7 @@ import queue
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
-from multiprocessing.connection import Client, Listener
+from multiprocessing.connection import AuthenticationError, Client, Listener, answer_challenge, deliver_challenge
 
 log = logging.getLogger(__name__)
 
@@ -161,12 +161,15 @@ class PeerMesh:
                  read_workers: int = 4):
         self.rank, self.nshards, self.authkey = rank, nshards, authkey
         self.store = store  # this replica's LOCAL shard (VectorStore); set before serving
-        self.listener = Listener((host, 0), authkey=authkey)
+        # the authentication handshake runs on the accepted connection's own thread (_serve), never on the
+        # accept thread: a slow peer cannot hold up the others, and a deep backlog absorbs connect bursts
+        self.listener = Listener((host, 0), backlog=128)
         self.address = self.listener.address
         self._peers: dict[int, tuple] = {}
         self._links: dict[int, _PeerLink] = {}
         self._lock = threading.Lock()
         self._ids = itertools.count(1)
+        self._connecting: dict[int, threading.Lock] = collections.defaultdict(threading.Lock)
         self._reads = ThreadPoolExecutor(read_workers, thread_name_prefix="mesh-read")
         self._writes = ThreadPoolExecutor(1, thread_name_prefix="mesh-write")  # routed writes applied in order
         self._closed = False
@@ -195,17 +198,20 @@ class PeerMesh:
             addr = self._peers.get(rank)
         if addr is None:
             return None
-        try:
-            ln = _PeerLink(rank, addr, self.authkey)
-        except (OSError, EOFError) as e:
-            log.warning("mesh: cannot reach shard %d at %s (%s)", rank, addr, e)
-            return None
         with self._lock:
-            cur = self._links.get(rank)
-            if cur is not None and cur.alive:  # another thread connected first
-                ln.close()
-                return cur
-            self._links[rank] = ln
+            gate = self._connecting[rank]
+        with gate:  # one connect per peer at a time; concurrent rounds wait for it and share the link
+            with self._lock:
+                cur = self._links.get(rank)
+                if cur is not None and cur.alive:
+                    return cur
+            try:
+                ln = _PeerLink(rank, addr, self.authkey)
+            except (OSError, EOFError, AuthenticationError) as e:
+                log.warning("mesh: cannot reach shard %d at %s (%s)", rank, addr, e)
+                return None
+            with self._lock:
+                self._links[rank] = ln
         return ln
 
     # ------------------------------------------------------------------ client: rounds
@@ -278,6 +284,13 @@ class PeerMesh:
             threading.Thread(target=self._serve, args=(conn,), name="mesh-serve", daemon=True).start()
 
     def _serve(self, conn) -> None:
+        try:
+            deliver_challenge(conn, self.authkey)
+            answer_challenge(conn, self.authkey)
+        except (AuthenticationError, EOFError, OSError, AssertionError):
+            log.warning("mesh: rejected a connection (authentication)")
+            conn.close()
+            return
         send_lock = threading.Lock()
         with self._lock:
             self._served.add(conn)
@@ -302,7 +315,8 @@ class PeerMesh:
                         self._writes.submit(lambda b=b: reply([self._run_one(*b)]))
                 if reads:
                     self._reads.submit(lambda reads=reads: reply(self._run_reads(reads)))
-        except (EOFError, OSError, ValueError, RuntimeError):  # RuntimeError: executors shut down (closing)
+        except (EOFError, OSError, ValueError, RuntimeError, TypeError):
+            # RuntimeError: executors shut down; TypeError: the connection was closed under recv() (close())
             pass
         finally:
             with self._lock:

@@ -18,6 +18,7 @@
 #   sweep=ARGS       bench with --agent-sweep (agent saturation curve)
 #   prof             rocprofv3 --kernel-trace --stats over a 2-step bench (scripts/profile_bench.sh)
 #   mb=WHAT          scripts/microbench.py --what WHAT (json in gpurun_out/<TAG>_mb_WHAT.json)
+#   py=SCRIPT,ARGS   python -u SCRIPT ARGS (',' separates args; log gpurun_out/<TAG>_py<i>.log)  (600 s)
 #
 # A step that exits 0 or 1 (a clean Python failure) lets the next one run; a fault, abort, segfault or
 # time limit (124 / 134 / 137 / 139) ends the session there (no more GPU work after a GPU fault).
@@ -43,6 +44,7 @@ run() {  # run LIMIT NAME CMD...
   case $rc in 0|1|2) return 0 ;; *) echo "== stopping: $name ended with $rc"; exit $rc ;; esac
 }
 
+npy=0
 REH="--steps 2 --warmup 1 --kv-cache-gb 48 --ingest-kv-gb 24 --ingest-files 48 --ingest-ref-cap-files 0 --agent-jobs 64"
 for step in "$@"; do
   key=${step%%=*}
@@ -61,6 +63,7 @@ for step in "$@"; do
              --agent-concurrency 4 --serving-steps 0 ${val//,/ } ;;
     sweep) run 1100 sweep python -u bench.py --no-ingest --agent-sweep "${val:-64,256,512,1024}" --steps 2 --warmup 1 ;;
     prof) run 700 prof bash scripts/profile_bench.sh ;;
+    py) npy=$((npy+1)); run 600 "py$npy" python -u ${val//,/ } ;;
     mb) run 400 "mb_$val" python -u scripts/microbench.py --what "$val" --out "gpurun_out/${TAG}_mb_$val.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -77,7 +77,10 @@ def attn_decode_bench(B, ctx, split_len):
     import copy
 
     arms = {}
-    for name, code in (("tk64", 1), ("tk32", 3), ("tk32_ns3", 8), ("tk32_ns4", 7)):
+    arms_codes = (("tk64", 1), ("tk32", 3), ("tk32_ns3", 8), ("tk32_ns4", 7))
+    if os.environ.get("MB_DECODE_ARMS") == "nt":  # default vs non-temporal K/V loads
+        arms_codes = (("tk32", 3), ("tk32_nt", 11), ("tk32_ns3", 8), ("tk32_ns3_nt", 12))
+    for name, code in arms_codes:
         mm = copy.copy(meta)
         mm.extra = {"decode_nw": code}
         arms[f"paged_decode_{name}_split{split_len}"] = (lambda mm=mm: A.paged_attention(q, kc, vc, mm, 0.088))

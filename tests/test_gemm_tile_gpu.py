@@ -293,3 +293,42 @@ def test_decode_batch_257_512_rows(dev, M, N, K, silu):
         r = ref(x[rows], w)
     assert y.shape == (M, N // 2 if silu else N)
     check(y[rows], r, K)
+
+
+@pytest.fixture()
+def mfma32():
+    prev = G.set_mfma(32)
+    yield
+    G.set_mfma(prev)
+
+
+def test_gemm_mfma32_variant(dev, mfma32):
+    """The v_mfma_f32_32x32x16_bf16 build of the tile kernel (same 64x32 quadrants per wave, its own
+    fragment reads, chunk map, permlane32 wide stores): plain / bias / GELU / SiLU*mul epilogues, ragged
+    tails, split-K planes and stream-K fixups against fp32, and the identity check for a transposed write."""
+    K = 256
+    x = torch.eye(K, dtype=torch.bfloat16, device=dev)
+    w = (torch.arange(K * 264, dtype=torch.float32).reshape(264, K) % 251 - 125).to(torch.bfloat16).to(dev)
+    b = rnd(264, dev=dev, seed=3)
+    assert torch.equal(G.gemm(x, w, b, ksplit=1).cpu(), (w.float().T + b.float()).to(torch.bfloat16).cpu())
+    for M, N, K in [(300, 520, 192), (1, 264, 128), (777, 3584, 640)]:
+        x, w = rnd(M, K, dev=dev, scale=0.5), rnd(N, K, dev=dev, seed=1, scale=0.5)
+        check(G.gemm(x, w, ksplit=1), ref(x, w), K)
+    M, N, K = 333, 1024, 384
+    x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+    check(G.gemm(x, w, b, act=G.ACT_GELU, ksplit=1), torch.nn.functional.gelu(ref(x, w, b)), K)
+    for M, I, K, ks, sk in [(700, 512, 384, 1, None), (160, 1024, 2048, 6, None), (768, 2048, 1024, 1, -20)]:
+        x = rnd(M, K, dev=dev, scale=0.3)
+        wg, wu = rnd(I, K, dev=dev, seed=1, scale=0.2), rnd(I, K, dev=dev, seed=2, scale=0.2)
+        bg, bu = rnd(I, dev=dev, seed=3), rnd(I, dev=dev, seed=4)
+        bgu = G.interleave_gate_up(bg.view(I, 1), bu.view(I, 1)).view(2 * I)
+        h = G.gemm_silu(x, G.interleave_gate_up(wg, wu), bgu, ksplit=ks, sk=sk)
+        check(h, torch.nn.functional.silu(ref(x, wg, bg)) * ref(x, wu, bu), K)
+    for M, N, K, S in [(192, 3584, 18944, 8), (200, 1024, 1024, 4)]:
+        x, w, b = rnd(M, K, dev=dev, scale=0.2), rnd(N, K, dev=dev, seed=1, scale=0.2), rnd(N, dev=dev, seed=2)
+        check(G.gemm(x, w, b, ksplit=S), ref(x, w, b), K)
+    for M, N, K, sk in [(512, 1536, 512, 20), (7040, 3584, 2048, -408), (1280, 4608, 1024, -270)]:
+        x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+        y = G.gemm(x, w, b, ksplit=1, sk=sk)
+        check(y, ref(x, w, b), K)
+        assert torch.equal(y, G.gemm(x, w, b, ksplit=1, sk=sk))

@@ -212,7 +212,7 @@ def test_paged_decode(dev, nsplit_len):
         m.part_o = torch.empty(ns * 5 * Hq * D, dtype=torch.float32, device=dev)
         m.part_ml = torch.empty(ns * 5 * Hq * 2, dtype=torch.float32, device=dev)
     ref = A.paged_attention_ref(q, kc, vc, meta, scale).reshape(q.shape[0], -1)
-    for code in (1, 3, 8, 7, 2):  # 64-key LDS-DMA tiles, 32-key tiles in a 2 / 3 / 4-stage ring, generic kernel
+    for code in (1, 3, 8, 7, 11, 12, 2):  # 64-key LDS-DMA tiles, 32-key tiles in a 2 / 3 / 4-stage ring (11 / 12: 2 / 3 stages, nt loads), generic kernel
         m.extra = {"decode_nw": code}
         out = A.paged_attention(q.to(dev), kc.to(dev), vc.to(dev), m, scale)
         close(out, ref, 2e-2)

@@ -145,3 +145,26 @@ def test_front_door_mesh_load_small():
     assert res["shard_rounds"] > 96 and res["round_p99_ms_max"] > 0
     assert all(r.get("rounds", 0) > 0 and r.get("degraded_rounds", 1) == 0 for r in res["per_replica"])
     assert res["served_reqs"] >= res["shard_rounds"] * 3  # each round asked all 3 other shards
+
+
+def test_mesh_stalled_or_bad_client_does_not_block_peers(mesh3):
+    """A connection that never finishes the authentication handshake (or fails it) must not hold up the
+    other peers' connects: the handshake runs on the connection's own thread, not the accept thread (the
+    8-replica CPU bench once stalled behind a burst of concurrent connects on a backlog-1 listener)."""
+    import socket
+    from multiprocessing.connection import AuthenticationError, Client
+
+    locs, meshes, facades = mesh3
+    ids, texts, vecs, metas = _rows(60, seed=4)
+    facades[0].table("chunk").upsert(ids, texts, vecs, metas)
+    stalled = [socket.create_connection(tuple(meshes[1].address)) for _ in range(4)]  # never speak
+    with pytest.raises(AuthenticationError):
+        Client(tuple(meshes[1].address), authkey=b"wrong-key-0123456")
+    for ln in list(meshes[2]._links.values()):  # force fresh connects from replica 2
+        ln.close()
+    meshes[2]._links.clear()
+    with round_health() as h:
+        facades[2].table("chunk").search(vecs[:3], 4)
+    assert h["degraded_rounds"] == 0
+    for s in stalled:
+        s.close()

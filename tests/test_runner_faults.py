@@ -97,3 +97,31 @@ def test_watchdog_releases_waiters_on_hung_step():
     finally:
         eng.release.set()
         r.shutdown()
+
+
+def test_arrival_paced_window():
+    """GRAG_ARRIVAL_WINDOW=auto (engine/runner.py _window): while interactive arrivals keep coming, a decode
+    replay lasts at most half the mean gap between arrival events; batch submits (ingest) do not pace it;
+    no recent arrival -> full windows; an open arrival() hint -> one step."""
+    eng = FakeEngine()
+    r = EngineRunner(eng, watchdog_s=0, start=False)
+    assert r.ARRIVAL_WINDOW == -1  # auto is the default
+    assert r._window() is None  # nothing measured yet
+    r._step_s = 0.010  # 10 ms decode steps
+    for _ in range(6):  # arrival events every 60 ms (each a burst of 4 submits)
+        for _ in range(4):
+            r.submit("q")
+        time.sleep(0.06)
+    assert r._gap is not None and 0.05 < r._gap < 0.2, r._gap
+    w = r._window()
+    assert w == max(1, min(8, int(0.5 * r._gap / 0.010))), (w, r._gap)
+    assert 2 <= w <= 8
+    with r.arrival():
+        assert r._window() == 1
+    r._last_event -= 10.0  # long quiet: full windows again
+    assert r._window() is None
+    g = r._gap
+    for _ in range(3):
+        r.submit("ingest prompt", interactive=False)
+        time.sleep(0.01)
+    assert r._gap == g and r._window() is None  # batch work does not pace the window
