@@ -139,6 +139,25 @@ void grag_alloc_register_many(void* a, const int32_t* blocks, const uint64_t* ha
   }
 }
 
+// Drop the hashes of n blocks (a step that registered its prefill blocks at scheduling time failed
+// before computing them: the cache must not serve their contents).  Unreferenced ones become plain free.
+void grag_alloc_unregister(void* a, int n, const int32_t* blocks) {
+  auto* al = static_cast<Allocator*>(a);
+  std::lock_guard<std::mutex> g(al->mu);
+  for (int i = 0; i < n; ++i) {
+    const int b = blocks[i];
+    if (b < 0 || b >= al->num_blocks || !al->hash_of[b]) continue;
+    auto it = al->by_hash.find(al->hash_of[b]);
+    if (it != al->by_hash.end() && it->second == b) al->by_hash.erase(it);
+    al->hash_of[b] = 0;
+    if (al->in_lru[b]) {
+      al->lru.erase(al->lru_pos[b]);
+      al->in_lru[b] = 0;
+      al->free_plain.push_back(b);
+    }
+  }
+}
+
 // Look up the longest cached prefix of `ntok` tokens. Fills out[] with the
 // reused block ids (refcount taken) and returns how many full blocks matched.
 int grag_alloc_match_prefix(void* a, const int32_t* toks, int ntok, int32_t* out, uint64_t* hashes_out) {

@@ -265,7 +265,13 @@ class LLMEngine:
         t0 = time.perf_counter() if self.trace is not None else 0.0
         tok0 = self.stats["prefill_tokens"] + self.stats["decode_tokens"]
         if kind in ("prefill", "mixed"):
-            finished += self._run_prefill(items)
+            try:
+                finished += self._run_prefill(items)
+            except BaseException:
+                # the step's prompt blocks were registered when scheduled (in-step prefix sharing): never let
+                # the cache serve blocks this failed step may not have written
+                self.kv.unregister(getattr(self.sched, "last_registered", []))
+                raise
         else:
             finished += self._run_decode([s for s, _, _ in items], max_window)
         if self.trace is not None:

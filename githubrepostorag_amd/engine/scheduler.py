@@ -13,11 +13,15 @@ Policy (what vLLM gave the reference at ``--max-num-seqs 4``, generalised):
 * waiting requests carry a priority (SamplingParams.priority): critical-path
   requests (ingest roll-up summaries, interactive agent calls) are admitted
   ahead of bulk extractor waves, FCFS within a priority;
-* prefix-aware admission: a waiting prompt whose first SIG_BLOCKS blocks are
-  identical to a prompt being prefilled in this very step is deferred by one
-  step, so it reuses those blocks from the prefix cache instead of computing
-  them again (waves submit the summary / title / keyword prompts of one chunk
-  together; without this every copy of the shared chunk would be prefilled).
+* in-step prefix sharing: a prefill item's full prompt blocks are registered in
+  the prefix cache when it is SCHEDULED, so a prompt admitted later in the same
+  step shares them (waves submit the summary / title / keyword prompts of one
+  chunk together; without this every copy of the shared chunk would be
+  prefilled).  Correct because each layer stores the whole step's K/V before
+  its attention reads the cache; a step that fails unregisters them
+  (``last_registered``).  (Round 3 deferred a prompt whose first 16 blocks
+  matched one in flight by a step instead: prompts under 256 tokens, most
+  extractor prompts, never qualified.)
 """
 from __future__ import annotations
 
@@ -92,13 +96,19 @@ class KVCacheManager:
             seq.cached_prefix = seq.num_computed
         return m * self.block_size
 
-    def register_full_blocks(self, seq: Sequence) -> None:
+    def register_full_blocks(self, seq: Sequence, upto: int | None = None) -> list[int]:
+        """Register the prompt's full blocks below ``upto`` (default: the computed tokens) under their
+        chained hashes; returns the newly registered block ids.  The scheduler registers a prefill item's
+        blocks when it schedules it (``upto`` = the item's end): a later prompt admitted in the SAME step
+        then shares them -- every layer stores the step's K/V for all its tokens before its attention
+        reads the cache, so the sharer reads them after they are written."""
         if not self.prefix_caching:
-            return
-        full = min(seq.num_computed, len(seq.prompt_ids)) // self.block_size
+            return []
+        end = seq.num_computed if upto is None else upto
+        full = min(end, len(seq.prompt_ids)) // self.block_size
         have = len(seq.block_hashes)
         if have >= full:
-            return
+            return []
         bs = self.block_size
         parent = seq.block_hashes[-1] if seq.block_hashes else 0
         n = full - have  # one hashing call and one registration call for all the newly full blocks
@@ -108,6 +118,13 @@ class KVCacheManager:
         blocks = np.asarray(seq.blocks[have:full], dtype=np.int32)
         rt().grag_alloc_register_many(self._h, blocks.ctypes.data, hashes.ctypes.data, n)
         seq.block_hashes.extend(int(h) for h in hashes)
+        return blocks.tolist()
+
+    def unregister(self, blocks: list[int]) -> None:
+        """Forget the hashes of blocks registered for a step that failed before computing them."""
+        if blocks:
+            arr = np.asarray(blocks, dtype=np.int32)
+            rt().grag_alloc_unregister(self._h, len(arr), arr.ctypes.data)
 
     def free(self, seq: Sequence) -> None:
         if seq.blocks:
@@ -134,10 +151,7 @@ class Scheduler:
         self.free_slots = list(range(max_num_seqs - 1, -1, -1))
         self.lock = threading.Lock()
         self.num_preemptions = 0
-
-    # 16 blocks = 256 tokens: a shared system prompt of a few dozen tokens is not worth a
-    # step of extra latency; a shared chunk of hundreds of tokens is
-    SIG_BLOCKS = 16
+        self.last_registered: list[int] = []  # prompt blocks registered by the last schedule() (rollback)
 
     def add(self, seq: Sequence) -> None:
         with self.lock:
@@ -150,20 +164,6 @@ class Scheduler:
             while i > 0 and self.waiting[i - 1].params.priority < pr:
                 i -= 1
             self.waiting.insert(i, seq)
-
-    def _sig(self, seq: Sequence) -> int:
-        """Chained hash of the first SIG_BLOCKS full prompt blocks (0 = shorter)."""
-        if seq.prefix_sig is None:
-            bs = self.kv.block_size
-            n = self.SIG_BLOCKS * bs
-            if not self.kv.prefix_caching or len(seq.prompt_ids) <= n:
-                seq.prefix_sig = 0
-            else:
-                toks = np.asarray(seq.prompt_ids[:n], dtype=np.int32)
-                hs = np.empty(self.SIG_BLOCKS, dtype=np.uint64)
-                rt().grag_hash_blocks(0, toks.ctypes.data, self.SIG_BLOCKS, bs, hs.ctypes.data)
-                seq.prefix_sig = int(hs[-1])
-        return seq.prefix_sig
 
     def has_work(self) -> bool:
         return bool(self.waiting or self.running)
@@ -241,11 +241,10 @@ class Scheduler:
                         items.append((seq, seq.num_computed, seq.num_computed + n))
                         budget -= n
             admitted = []
-            pending: set[int] = set()  # prefix signatures being computed in this step
-            for seq, a, _ in items:
-                if a < self.SIG_BLOCKS * self.kv.block_size and self._sig(seq):
-                    pending.add(seq.prefix_sig)
-            deferred = []
+            # the prompt blocks this step computes are registered now: later admissions share them
+            registered = []
+            for seq, _, b in items:
+                registered += self.kv.register_full_blocks(seq, upto=b)
             while self.waiting and budget > 0 and self.free_slots and len(self.running) < self.max_num_seqs:
                 seq = self.waiting[0]
                 if seq.total_len >= self.max_model_len:
@@ -254,12 +253,7 @@ class Scheduler:
                     self._finish(seq)
                     admitted.append(("rejected", seq))
                     continue
-                fresh = not seq.blocks
-                if fresh and self._sig(seq) and seq.prefix_sig in pending:
-                    # the same first blocks are being prefilled right now: take them from the cache next step
-                    deferred.append(self.waiting.popleft())
-                    continue
-                if fresh:
+                if not seq.blocks:
                     self.kv.match_prefix(seq)
                 tgt = self.prefill_target(seq)
                 n = min(tgt - seq.num_computed, budget)
@@ -272,10 +266,9 @@ class Scheduler:
                 self.prefilling.append(seq)
                 admitted.append(("admitted", seq))
                 items.append((seq, seq.num_computed, seq.num_computed + n))
+                registered += self.kv.register_full_blocks(seq, upto=seq.num_computed + n)
                 budget -= n
-                if seq.num_computed < self.SIG_BLOCKS * self.kv.block_size and seq.prefix_sig:
-                    pending.add(seq.prefix_sig)
-            self.waiting.extendleft(reversed(deferred))
+            self.last_registered = registered
             self.last_admitted = [s for tag, s in admitted if tag == "admitted"]
             self.last_rejected = [s for tag, s in admitted if tag == "rejected"]
             if items:

@@ -54,7 +54,6 @@ class Sequence:      # compare every field (that cost ~150 ms per step at 192 li
     cancelled: bool = False
     num_preemptions: int = 0
     detok: object = None  # tokenizer.IncrementalDetokenizer, created on the first output token
-    prefix_sig: int | None = None  # chained hash of the first SIG_BLOCKS prompt blocks (0 = too short)
 
     @property
     def all_ids(self) -> list[int]:

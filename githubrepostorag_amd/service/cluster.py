@@ -39,11 +39,13 @@ only):
   replica -> hub: ("hello", rank, capacity, info{..., mesh: address}) | ("event", job, name, data)
                   | ("health", info) | ("upsert", table, payload)          [mirror]
                   | ("shard_req", req, scope, op, payload)                 [shard round]
-                  | ("shard_res", origin, req, result) | ("shard_write", owner, scope, op, payload)
+                  | ("shard_res", origin, req, result) | ("shard_wreq", req, owner, scope, op, payload)
   hub -> replica: ("run", job, request) | ("cancel", job) | ("upsert", table, payload) | ("stop",)
                   | ("peers", {rank: mesh address})                        [mesh membership]
                   | ("shard_plan", req, n_parts) | ("shard_part", req, rank, result)
-                  | ("shard_exec", origin, req, scope, op, payload) | ("shard_apply", scope, op, payload)
+                  | ("shard_exec", origin, req, scope, op, payload) | ("shard_wexec", origin, req, scope, op, payload)
+A routed write (shard_wreq) is a one-part round: the owner applies it in arrival order (one writer thread)
+and answers with its applied count; an owner that is not connected answers None and the writer raises.
 """
 from __future__ import annotations
 
@@ -202,12 +204,18 @@ class ReplicaHub:
                         o = self.replicas.get(origin)
                     if o is not None:
                         o.send(("shard_part", req, rep.rank, result))
-                elif kind == "shard_write":
-                    _, owner, scope, op, payload = msg
+                elif kind == "shard_wreq":  # an acknowledged routed write: a one-part round to the owner
+                    _, req, owner, scope, op, payload = msg
                     with self._lock:
                         o = self.replicas.get(owner)
-                    if o is None or not o.send(("shard_apply", scope, op, payload)):
-                        log.warning("shard write for replica %d dropped: replica not connected", owner)
+                        if o is not None and o.alive:
+                            self._shard_pending.setdefault(owner, set()).add((rep.rank, req))
+                    rep.send(("shard_plan", req, 1))
+                    if o is None or not o.alive or not o.send(("shard_wexec", rep.rank, req, scope, op, payload)):
+                        with self._lock:
+                            self._shard_pending.get(owner, set()).discard((rep.rank, req))
+                        log.warning("shard write for replica %d not applied: replica not connected", owner)
+                        rep.send(("shard_part", req, owner, None))
         except (EOFError, OSError, ConnectionResetError):
             pass
         finally:
@@ -465,8 +473,26 @@ class HubShardTransport:
             with self._lock:
                 self._rounds.pop(req, None)
 
-    def write(self, origin: int, owner: int, scope: str, op: str, payload) -> None:
-        self._send(("shard_write", owner, scope, op, payload))
+    def write(self, origin: int, owner: int, scope: str, op: str, payload, timeout: float = 120.0):
+        """An acknowledged routed write (a one-part round to the owner): its applied count, or
+        ShardWriteError when the owner is gone or did not answer."""
+        from .mesh import ShardWriteError
+
+        req = next(self._ids)
+        st = {"n": None, "parts": {}, "ev": threading.Event()}
+        with self._lock:
+            self._rounds[req] = st
+        try:
+            self._send(("shard_wreq", req, owner, scope, op, payload))
+            if not st["ev"].wait(timeout):
+                raise ShardWriteError(f"shard {owner} did not acknowledge {op} on {scope} within {timeout:.0f}s")
+            res = st["parts"].get(owner)
+            if res is None:
+                raise ShardWriteError(f"shard {owner} did not apply {op} on {scope} (not connected or failed)")
+            return res
+        finally:
+            with self._lock:
+                self._rounds.pop(req, None)
 
     def deliver(self, msg) -> None:
         """Reader thread: a plan or a part of one of this replica's rounds."""
@@ -552,11 +578,18 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
         except (OSError, EOFError):
             pass
 
-    def shard_apply(scope, op, payload):
+    write_pool = ThreadPoolExecutor(1, thread_name_prefix="shard-write")  # routed writes: in arrival order
+
+    def shard_wexec(origin, req, scope, op, payload):
         try:
-            execute(local_store, scope, op, payload)
+            res = execute(local_store, scope, op, payload)
         except Exception:
-            log.exception("routed shard write (%s on %s) failed", op, scope)
+            log.exception("routed shard write (%s on %s) from replica %d failed", op, scope, origin)
+            res = None
+        try:
+            send(("shard_res", origin, req, res))
+        except (OSError, EOFError):
+            pass
 
     async def main():
         loop = asyncio.get_running_loop()
@@ -573,8 +606,8 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
                         transport.deliver(msg)
                     elif kind == "shard_exec":
                         shard_pool.submit(shard_exec, *msg[1:])
-                    elif kind == "shard_apply":
-                        shard_pool.submit(shard_apply, *msg[1:])
+                    elif kind == "shard_wexec":
+                        write_pool.submit(shard_wexec, *msg[1:])
                     else:
                         loop.call_soon_threadsafe(inbox.put_nowait, msg)
             except (EOFError, OSError):
@@ -634,6 +667,7 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
         asyncio.run(main())
     finally:
         shard_pool.shutdown(wait=False)
+        write_pool.shutdown(wait=False)
         if mesh is not None:
             mesh.close()
         try:

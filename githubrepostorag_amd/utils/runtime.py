@@ -25,6 +25,7 @@ _SIGS = {
     "grag_hash_block": ([U64, P, I], U64),
     "grag_hash_blocks": ([U64, P, I, I, P], None),
     "grag_alloc_register_many": ([P, P, P, I], None),
+    "grag_alloc_unregister": ([P, I, P], None),
     "grag_alloc_match_prefix": ([P, P, I, P, P], I),
     "grag_alloc_register": ([P, I, U64], None),
     "grag_alloc_stats": ([P, P], None),

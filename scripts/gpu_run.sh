@@ -18,6 +18,7 @@
 #   sweep=ARGS       bench with --agent-sweep (agent saturation curve)
 #   prof             rocprofv3 --kernel-trace --stats over a 2-step bench (scripts/profile_bench.sh)
 #   mb=WHAT          scripts/microbench.py --what WHAT (json in gpurun_out/<TAG>_mb_WHAT.json)
+#   profdec=ARGS     rocprofv3 kernel stats of one decode step (scripts/profile_decode_step.sh ARGS)  (400 s)
 #   py=SCRIPT,ARGS   python -u SCRIPT ARGS (',' separates args; log gpurun_out/<TAG>_py<i>.log)  (600 s)
 #
 # A step that exits 0 or 1 (a clean Python failure) lets the next one run; a fault, abort, segfault or
@@ -63,6 +64,7 @@ for step in "$@"; do
              --agent-concurrency 4 --serving-steps 0 ${val//,/ } ;;
     sweep) run 1100 sweep python -u bench.py --no-ingest --agent-sweep "${val:-64,256,512,1024}" --steps 2 --warmup 1 ;;
     prof) run 700 prof bash scripts/profile_bench.sh ;;
+    profdec) run 400 profdec env TAG="${TAG}" bash scripts/profile_decode_step.sh ${val//,/ } ;;
     py) npy=$((npy+1)); run 600 "py$npy" python -u ${val//,/ } ;;
     mb) run 400 "mb_$val" python -u scripts/microbench.py --what "$val" --out "gpurun_out/${TAG}_mb_$val.json" ;;
     *) echo "unknown step $step"; exit 2 ;;

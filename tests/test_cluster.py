@@ -231,3 +231,63 @@ def test_remote_llm_mode_uses_http_client():
         assert seen[0][0] == "/v1/chat/completions" and seen[0][1]["messages"][-1]["content"] == "hello there"
     finally:
         srv.shutdown()
+
+
+def test_hub_relay_writes_are_acknowledged_in_order():
+    """GRAG_SHARD_TRANSPORT=hub: a routed write is a one-part round -- the owner applies writes in arrival
+    order and answers its count; a write to an owner that is not connected raises (writes were
+    fire-and-forget and applied on a 4-thread pool)."""
+    import threading
+    from multiprocessing.connection import Client
+
+    from githubrepostorag_amd.service.cluster import HubShardTransport
+    from githubrepostorag_amd.service.mesh import ShardWriteError
+
+    hub = ReplicaHub(EventLog(), job_timeout=30.0)
+    try:
+        origin = Client(tuple(hub.address), authkey=hub.authkey)
+        owner = Client(tuple(hub.address), authkey=hub.authkey)
+        origin.send(("hello", 0, 1, {}))
+        owner.send(("hello", 1, 1, {}))
+        deadline = time.time() + 10
+        while hub.live_count() < 2 and time.time() < deadline:
+            time.sleep(0.01)
+        applied = []
+
+        def owner_loop():
+            try:
+                while True:
+                    msg = owner.recv()
+                    if msg[0] == "shard_wexec":
+                        _, o, req, scope, op, payload = msg
+                        applied.append(payload)
+                        owner.send(("shard_res", o, req, len(payload)))
+            except (EOFError, OSError):
+                pass
+
+        tr = HubShardTransport(origin.send, 0)
+
+        def origin_loop():
+            try:
+                while True:
+                    msg = origin.recv()
+                    if msg[0] in ("shard_plan", "shard_part"):
+                        tr.deliver(msg)
+            except (EOFError, OSError):
+                pass
+
+        threading.Thread(target=owner_loop, daemon=True).start()
+        threading.Thread(target=origin_loop, daemon=True).start()
+        assert [tr.write(0, 1, "chunk", "delete", [f"r{i}"] * (i + 1)) for i in range(5)] == [1, 2, 3, 4, 5]
+        assert [len(p) for p in applied] == [1, 2, 3, 4, 5]
+        with pytest.raises(ShardWriteError):
+            tr.write(0, 7, "chunk", "delete", ["x"])  # no replica 7
+        owner.close()
+        deadline = time.time() + 10
+        while hub.live_count() > 1 and time.time() < deadline:
+            time.sleep(0.01)
+        with pytest.raises(ShardWriteError):
+            tr.write(0, 1, "chunk", "delete", ["y"], timeout=10.0)
+        origin.close()
+    finally:
+        hub.close()

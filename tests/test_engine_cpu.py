@@ -159,18 +159,44 @@ def test_wordpiece_basic():
     assert np.asarray(wp.encode("x " * 500, 32)).shape == (32,)
 
 
-def test_prefix_aware_admission_defers_duplicates(model, tok):
-    """Prompts submitted together that share their first blocks: the first is
-    prefilled, the others are deferred one step and hit the prefix cache —
-    outputs identical to an engine without prefix caching."""
-    base = [(7 * i) % 480 + 10 for i in range(300)]  # 300 shared tokens > SIG_BLOCKS * 16
-    prompts = [base + [1], base + [2], base + [3]]
+def test_in_step_prefix_sharing(model, tok):
+    """Prompts admitted in the SAME prefill step share their common full blocks: the first registers its
+    prompt blocks when scheduled, the later ones match them (scheduler.py docstring) -- long (300-token)
+    and short (40-token) shared prefixes alike, and a prefix split over chunked-prefill steps; outputs
+    identical to an engine without prefix caching, and the prefill computes each shared block once."""
+    for n_shared, chunk in ((300, 16384), (40, 16384), (300, 128)):
+        base = [(7 * i) % 480 + 10 for i in range(n_shared)]
+        prompts = [base + [1], base + [2], base + [3, 4]]
+        eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_model_len=512, num_blocks=256,
+                                                 use_cuda_graph=False, max_num_batched_tokens=chunk))
+        outs = eng.generate(prompts, GREEDY)
+        shared = n_shared // 16 * 16
+        assert [o.cached_tokens for o in outs][1:] == [shared, shared], (n_shared, chunk)
+        assert eng.stats["prefill_tokens"] == sum(len(p) for p in prompts) - 2 * shared
+        _, ref = _gen(model, tok, prompts=prompts, enable_prefix_caching=False)
+        assert [o.token_ids for o in outs] == [o.token_ids for o in ref]
+
+
+def test_failed_prefill_step_unregisters_its_blocks(model, tok):
+    """A prefill step that raises must not leave its (never written) prompt blocks in the prefix cache."""
     eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_model_len=512, num_blocks=256,
                                              use_cuda_graph=False))
-    outs = eng.generate(prompts, GREEDY)
-    assert sum(o.cached_tokens >= 256 for o in outs) == 2
-    _, ref = _gen(model, tok, prompts=prompts, enable_prefix_caching=False)
-    assert [o.token_ids for o in outs] == [o.token_ids for o in ref]
+    prompt = [(5 * i) % 400 + 3 for i in range(100)]
+    eng.add_request(prompt, GREEDY)
+    real = eng._run_prefill
+
+    def boom(items):
+        raise RuntimeError("injected fault")
+
+    eng._run_prefill = boom
+    with pytest.raises(RuntimeError):
+        eng.step()
+    eng._run_prefill = real
+    assert eng.kv.stats()["cached_blocks"] == 0
+    from githubrepostorag_amd.engine.sequence import Sequence
+
+    probe = Sequence("p", prompt + [9], GREEDY)
+    assert eng.kv.match_prefix(probe) == 0
 
 
 def test_priority_admission_order(model, tok):
