@@ -707,10 +707,13 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
     active = []    # (handles, t_sub) in flight
     pending = []   # futures of arrivals being retrieved
 
+    sub_gap = []  # per arrival: retrieval (t_sub -> prompts submitted), seconds
+
     def arrive():
         with runner.arrival():
             prompts, t_sub, _ = prepare()
             hs = [runner.submit(p, sp) for p in prompts]
+        sub_gap.append(time.perf_counter() - t_sub)
         return hs, t_sub
 
     def poll(quota: int) -> list:
@@ -758,8 +761,10 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
             torch.cuda.synchronize()
         t_start = time.perf_counter()
         dec0 = eng.stats["decode_tokens"]
+        n_gap0 = len(sub_gap)
         ttfts = complete(steps * A)
         dec1 = eng.stats["decode_tokens"]
+        gaps = sub_gap[n_gap0:]
         if dev.type == "cuda":
             torch.cuda.synchronize()
         comm.barrier()
@@ -783,6 +788,9 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
     p50 = statistics.median([x for r in allt for x in r]) * 1000.0
     log(f"serving loop (EngineRunner + admission hint): {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms")
     return {"value": round(qps, 3), "p50_ttft_ms": round(p50, 2), "steps": steps,
+            # TTFT = retrieval (embed + search + prompt, until the prompts are submitted) + engine admission
+            # and prefill; the retrieval part's p50 over the timed arrivals (this rank)
+            "retrieval_p50_ms": round(statistics.median(gaps) * 1000.0, 2) if gaps else None,
             "ms_per_step": round(elapsed / steps * 1000.0, 2),
             # decode tokens the engine produced in the timed window / what the completed queries needed:
             # ~1.0 when the window was the pipeline's steady state (no backlog built or drained in it)

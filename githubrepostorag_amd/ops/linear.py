@@ -50,8 +50,15 @@ def enable_tuned_gemms() -> bool:
     if _TUNED["done"]:
         return _TUNED["table"] is not None
     _TUNED["done"] = True
-    if os.environ.get("GRAG_TUNED_GEMMS", "1") == "0" or not torch.cuda.is_available():
+    if os.environ.get("GRAG_TUNED_GEMMS", "1") == "0":
         return False
+    js = TUNING_DIR / "gemm_dispatch_gfx950.json"  # plain data: loaded on the host too (dispatch tests)
+    if js.exists():
+        raw = json.loads(js.read_text())["table"]
+        _TUNED["table"] = {tuple(map(int, k.split(","))): ([m for m, _ in v], [b for _, b in v])
+                           for k, v in raw.items()}
+    if not torch.cuda.is_available():
+        return _TUNED["table"] is not None
     csv = TUNING_DIR / "tunableop_gfx950.csv"
     try:
         if csv.exists():
@@ -61,11 +68,6 @@ def enable_tuned_gemms() -> bool:
             torch.cuda.tunable.read_file(str(csv))
     except Exception:  # validator mismatch (other ROCm/hipBLASLt build): library defaults
         torch.cuda.tunable.enable(False)
-    js = TUNING_DIR / "gemm_dispatch_gfx950.json"
-    if js.exists():
-        raw = json.loads(js.read_text())["table"]
-        _TUNED["table"] = {tuple(map(int, k.split(","))): ([m for m, _ in v], [b for _, b in v])
-                           for k, v in raw.items()}
     return _TUNED["table"] is not None
 
 

@@ -114,3 +114,50 @@ def test_deferred_splitk_plan():
     assert G.deferred_plan(384, 3584, 18944)[0] == "tile"  # 257-512-row decode: measured K-split plans
     assert G.deferred_plan(4096, 3584, 3584) is None
     assert G.deferred_plan(190, 37888, 3584) is None
+
+
+def test_config4_per_rank_projections_are_measured_and_owned_unless_the_library_won():
+    """BASELINE config 4 (Qwen2-72B TP=8): every per-rank projection has measured dispatch rows -- the
+    prefill table (scripts/sweep_prefill_gemm.py --models qwen2-72b-tp8, 512-row buckets) and the decode
+    table (scripts/gemm_dispatch_table.py --models qwen2-72b:8) -- so none falls to the library by default
+    (round 3: K = 3696 failed every owned kernel's K % 64; the FFN shard is now zero-padded to 3712,
+    models/qwen2.py FFN_PAD).  kernel_for() picks an owned kernel wherever the sweep did not measure the
+    library clearly faster; gate/up (fused SwiGLU) is owned at every M.  The measured library wins are
+    narrow-N / odd-K buckets (profiles/sweep_prefill_tp_r4.jsonl); owned overall >= 75 % of the buckets."""
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import FFN_PAD
+    from githubrepostorag_amd.ops import linear as L
+
+    c = decoder_config("qwen2-72b")
+    tp = 8
+    hq, hkv, D, H = c.num_heads // tp, c.num_kv_heads // tp, c.head_dim, c.hidden_size
+    inter = -(-(c.intermediate_size // tp) // FFN_PAD) * FFN_PAD
+    assert inter == 3712 and inter % 64 == 0
+    plain = {"qkv": ((hq + 2 * hkv) * D, H), "o": (H, hq * D), "down": (H, inter)}
+    ncu = G._num_cus
+    try:
+        G._num_cus = lambda: 256
+        L.enable_tuned_gemms()
+        table = G._prefill_table()
+        owned = total = 0
+        for name, (N, K) in plain.items():
+            assert (N, K, 0) in table, name  # measured prefill rows
+            assert L._TUNED["table"].get((N, K)) is not None, name  # measured decode rows
+            ms, rows = table[(N, K, 0)]
+            for M in [1, 4, 16, 32, 64, 96, 128, 192, 256] + list(range(512, 16385, 512)):
+                kind = L.kernel_for(M, N, K)
+                total += 1
+                if kind in L.OWNED_KINDS:
+                    owned += 1
+                    continue
+                # the library only where a measurement put it ahead
+                if M <= 128:
+                    assert L.measured_choice(M, N, K) == "library", (name, M, kind)
+                else:
+                    assert G.prefill_plan(M, N, K) is None and M >= G.PREFILL_MIN_M or \
+                        L.measured_choice(M, N, K) == "library", (name, M, kind)
+        assert owned >= 0.75 * total, (owned, total)
+        # gate/up: the fused SwiGLU kernel at every prefill M
+        assert all(G.prefill_plan(M, 2 * inter, H, silu=True) is not None for M in range(384, 16385, 512))
+    finally:
+        G._num_cus = ncu
