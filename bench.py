@@ -708,13 +708,15 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
     pending = []   # futures of arrivals being retrieved
 
     sub_gap = []  # per arrival: retrieval (t_sub -> prompts submitted), seconds
+    engine_part = []  # per completed group: prompts submitted -> first token (median over the group), seconds
 
     def arrive():
         with runner.arrival():
             prompts, t_sub, _ = prepare()
             hs = [runner.submit(p, sp) for p in prompts]
-        sub_gap.append(time.perf_counter() - t_sub)
-        return hs, t_sub
+        t_in = time.perf_counter()
+        sub_gap.append(t_in - t_sub)
+        return hs, t_sub, t_in
 
     def poll(quota: int) -> list:
         """Up to ``quota`` completed groups' TTFT lists; each is replaced by a new arrival at once.  The
@@ -725,10 +727,11 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
         out = []
         for g in [g for g in active if g[0][0].done.is_set() and all(h.done.is_set() for h in g[0])][:quota]:
             active.remove(g)
-            hs, t_sub = g
+            hs, t_sub, t_in = g
             for h in hs:
                 h.wait(0)  # raises a failed request's error
             out.append([h.result.first_token_at - t_sub for h in hs])
+            engine_part.append(statistics.median(h.result.first_token_at - t_in for h in hs))
             pending.append(pool.submit(arrive))
         return out
 
@@ -761,17 +764,17 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
             torch.cuda.synchronize()
         t_start = time.perf_counter()
         dec0 = eng.stats["decode_tokens"]
-        n_gap0 = len(sub_gap)
+        n_gap0, n_eng0 = len(sub_gap), len(engine_part)
         ttfts = complete(steps * A)
         dec1 = eng.stats["decode_tokens"]
-        gaps = sub_gap[n_gap0:]
+        gaps, engs = sub_gap[n_gap0:], engine_part[n_eng0:]
         if dev.type == "cuda":
             torch.cuda.synchronize()
         comm.barrier()
         elapsed = time.perf_counter() - t_start
         for f in pending:  # drain (untimed)
             active.append(f.result())
-        for hs, _ in active:
+        for hs, *_ in active:
             for h in hs:
                 h.wait(600)
     finally:
@@ -791,6 +794,7 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
             # TTFT = retrieval (embed + search + prompt, until the prompts are submitted) + engine admission
             # and prefill; the retrieval part's p50 over the timed arrivals (this rank)
             "retrieval_p50_ms": round(statistics.median(gaps) * 1000.0, 2) if gaps else None,
+            "submit_to_first_token_p50_ms": round(statistics.median(engs) * 1000.0, 2) if engs else None,
             "ms_per_step": round(elapsed / steps * 1000.0, 2),
             # decode tokens the engine produced in the timed window / what the completed queries needed:
             # ~1.0 when the window was the pipeline's steady state (no backlog built or drained in it)

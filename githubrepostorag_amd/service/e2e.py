@@ -22,6 +22,7 @@ import asyncio
 import json
 import socket
 import statistics
+import sys
 import threading
 import time
 
@@ -96,7 +97,26 @@ async def _drive(url: str, questions: list[str], concurrency: int, timeout_s: fl
                 return {"t0": t0, "first_token": first, "final": final, "error": err, "tokens": ntok,
                         "degraded": degraded}
 
-        return await asyncio.gather(*[one(q) for q in questions])
+        done = [0]
+
+        async def counted(q):
+            try:
+                return await one(q)
+            finally:
+                done[0] += 1
+
+        async def progress():  # a line every 20 s: long sweeps stay visibly alive
+            t_start = time.perf_counter()
+            while True:
+                await asyncio.sleep(20)
+                print(f"[e2e] {done[0]}/{len(questions)} jobs at concurrency {concurrency}, "
+                      f"{time.perf_counter() - t_start:.0f} s", file=sys.stderr, flush=True)
+
+        tick = asyncio.ensure_future(progress())
+        try:
+            return await asyncio.gather(*[counted(q) for q in questions])
+        finally:
+            tick.cancel()
 
 
 def _pct(xs: list[float], p: float) -> float | None:
