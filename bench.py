@@ -114,6 +114,11 @@ def parse():
                     help="end-to-end phase: agent-loop jobs through POST /rag/jobs + SSE over real HTTP "
                          "(0 disables); secondary fields e2e_ttft_p50_ms / p90 / agent_jobs_per_s")
     ap.add_argument("--agent-concurrency", type=int, default=64)
+    ap.add_argument("--agent-slots", type=int, default=256,
+                    help="jobs a replica runs at once (WORKER_MAX_JOBS); offered concurrency above it waits in "
+                         "the front door's FIFO queue (profiles/agent_saturation_r4.json: one thread per running "
+                         "job, throughput collapses past ~256 on one GPU: 11.6 -> 8.4 -> 3.1 jobs/s at 256 / 512 "
+                         "/ 1024 running jobs)")
     ap.add_argument("--agent-gen-len", type=int, default=32,
                     help="token cap of the agent's plan / expand / judge / rewrite calls (JSON or one line)")
     ap.add_argument("--agent-synth-len", type=int, default=256, help="token cap of the agent's synthesize call")
@@ -765,9 +770,11 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
         t_start = time.perf_counter()
         dec0 = eng.stats["decode_tokens"]
         n_gap0, n_eng0 = len(sub_gap), len(engine_part)
+        eng.trace = []  # engine steps of the timed window (kind, rows, tokens, seconds)
         ttfts = complete(steps * A)
         dec1 = eng.stats["decode_tokens"]
         gaps, engs = sub_gap[n_gap0:], engine_part[n_eng0:]
+        trace, eng.trace = eng.trace, None
         if dev.type == "cuda":
             torch.cuda.synchronize()
         comm.barrier()
@@ -795,6 +802,7 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
             # and prefill; the retrieval part's p50 over the timed arrivals (this rank)
             "retrieval_p50_ms": round(statistics.median(gaps) * 1000.0, 2) if gaps else None,
             "submit_to_first_token_p50_ms": round(statistics.median(engs) * 1000.0, 2) if engs else None,
+            "engine_steps": _trace_summary(trace),
             "ms_per_step": round(elapsed / steps * 1000.0, 2),
             # decode tokens the engine produced in the timed window / what the completed queries needed:
             # ~1.0 when the window was the pipeline's steady state (no backlog built or drained in it)
@@ -804,6 +812,18 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
                     "rate: engine/runner.py _window); closed loop at the "
                     "harness's concurrency, a new group arriving as each completes; arrivals submitted from the "
                     "retrieval thread under runner.arrival() (1-step replays while a retrieval is in flight)"}
+
+
+def _trace_summary(trace) -> dict:
+    """Engine steps of a window (LLMEngine.trace records): count, mean rows / tokens / ms per kind."""
+    out = {}
+    for kind in ("prefill", "mixed", "decode"):
+        st = [t for t in trace or [] if t[1] == kind]
+        if st:
+            out[kind] = {"steps": len(st), "mean_rows": round(sum(t[2] for t in st) / len(st), 1),
+                         "mean_tokens": round(sum(t[3] for t in st) / len(st), 1),
+                         "mean_ms": round(1000 * sum(t[4] for t in st) / len(st), 2)}
+    return out
 
 
 def _scope_tables(store, emb, corpus, rank, world, dev):
@@ -846,7 +866,8 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_gr
 
     conc = args.agent_concurrency
     levels = [int(x) for x in args.agent_sweep.split(",") if x.strip()]
-    slots = max([conc, *levels])  # a replica's job slots: the largest concurrency it will be driven at
+    # a replica's job slots: the largest concurrency it will be driven at, capped at --agent-slots (the rest queue)
+    slots = min(max([conc, *levels]), max(1, args.agent_slots))
     s = Settings(qwen_model=args.model, embed_model=args.encoder, qwen_max_output=args.agent_gen_len,
                  synth_max_tokens=args.agent_synth_len, worker_max_jobs=slots, max_rag_attempts=3,
                  default_namespace=corpus.namespace, job_timeout_s=1800, llm_retries=0, stream_tokens=True,
@@ -881,7 +902,8 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_gr
     res = None
     try:
         if world == 1:
-            res = run_e2e(create_app(APIState(runtime=rt)), qs, n_conc, warmup=warm, sweep=sweep)
+            res = run_e2e(create_app(APIState(runtime=rt)), qs, n_conc, warmup=warm, sweep=sweep,
+                          stats_fn=lambda: {**eng.stats, "preemptions": eng.sched.num_preemptions})
         else:
             import torch.distributed as dist
 
@@ -928,6 +950,7 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_gr
     if res is None:
         return None
     res["concurrency"] = n_conc
+    res["worker_slots_per_replica"] = slots
     res["llm_token_cap"] = args.agent_gen_len
     res["synthesize_token_cap"] = args.agent_synth_len
     res["tables"] = {"chunk": {"rows": corpus.n, "index": index.table.index_kind},

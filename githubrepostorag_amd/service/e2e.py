@@ -151,7 +151,7 @@ def _drive_child(url: str, questions: list[str], concurrency: int, timeout_s: fl
 
 def run_e2e(app, questions: list[str], concurrency: int, warmup: list[str] | None = None,
             timeout_s: float = 1800.0, sweep: list[tuple[list[str], int]] | None = None,
-            client_process: bool = True) -> dict:
+            client_process: bool = True, stats_fn=None) -> dict:
     """Serve ``app`` on localhost and push ``questions`` through the HTTP API at ``concurrency``.
     ``sweep``: further (questions, concurrency) runs on the same server, one after the other (a
     saturation curve); their summaries go to ``agent_saturation``."""
@@ -165,18 +165,28 @@ def run_e2e(app, questions: list[str], concurrency: int, warmup: list[str] | Non
             r = loop.run_until_complete(_drive(srv.url, qs, conc, timeout_s))
             return r, time.perf_counter() - t0
 
+        def delta(a, b):  # numeric engine counters accumulated over one run (stats_fn: a dict snapshot)
+            return {k: round(b[k] - a[k], 4) for k in b if isinstance(b.get(k), (int, float)) and k in a}
+
         try:
             if warmup:
                 drive(warmup, concurrency)
+            s0 = stats_fn() if stats_fn else None
             res, wall = drive(questions, concurrency)
+            eng_main = delta(s0, stats_fn()) if stats_fn else None
             curve = []
             for qs, conc in sweep or []:
+                s0 = stats_fn() if stats_fn else None
                 r, w = drive(qs, conc)
                 curve.append(dict(concurrency=conc, **_summary(r, w)))
+                if stats_fn:
+                    curve[-1]["engine"] = delta(s0, stats_fn())
         finally:
             if loop is not None:
                 loop.close()
     out = _summary(res, wall)
+    if eng_main is not None:
+        out["engine"] = eng_main
     if sweep:
         out["agent_saturation"] = curve
     return out

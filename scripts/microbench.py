@@ -60,6 +60,51 @@ def gemm_bench(M):
     return out
 
 
+def midm_bench(Ms=(128, 176, 192, 224, 256)):
+    """Qwen2-7B projections at 129-256 rows (ingest / agent decode batches): the dispatched kernel
+    (ops/linear.kernel_for, ops/gemm.mlp_gate_up) vs tile-kernel schedules (whole tiles, split-K,
+    stream-K rounds), on >= 1 GiB of rotating weight copies (cold weights, as in a decode step)."""
+    from githubrepostorag_amd.ops import gemm as G
+    from githubrepostorag_amd.ops.linear import kernel_for, linear
+
+    dev = torch.device("cuda")
+    out = {}
+    for name, N, K, silu in [("qkv", 4608, 3584, False), ("o", 3584, 3584, False),
+                             ("gate_up", 37888, 3584, True), ("down", 3584, 18944, False)]:
+        ncopy = max(2, min(16, (1 << 30) // (N * K * 2) + 1))
+        ws = [((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(ncopy)]
+        it = {"i": 0}
+
+        def nxt():
+            it["i"] = (it["i"] + 1) % ncopy
+            return ws[it["i"]]
+
+        for M in Ms:
+            x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+            arms = {"dispatched": (lambda: G.mlp_gate_up(x, nxt())) if silu else (lambda: linear(x, nxt()))}
+            tiles = -(-M // 256) * -(-N // 256)
+            scheds = [(1, 0), (1, 256), (1, -256), (2, 0), (3, 0), (4, 0)]
+            for ks, sk in scheds:
+                if not G.sk_ok(M, N, K, ks, sk) or (ks > 1 and tiles * ks > 4 * 256):
+                    continue
+                G.WS.reserve(dev, G._ws_floats(M, N, ks, sk))
+                if sk:
+                    G.WS.counters(dev)
+                arms[f"tile_{ks}_{sk}"] = ((lambda ks=ks, sk=sk: G.gemm_silu(x, nxt(), ksplit=ks, sk=sk)) if silu
+                                          else (lambda ks=ks, sk=sk: G.gemm(x, nxt(), ksplit=ks, sk=sk)))
+            r = rounds(arms, n=5, iters=30)
+            r["dispatched_kind"] = "mlp_gate_up" if silu else kernel_for(M, N, K)
+            gb = N * K * 2 / 1e9
+            for k, v in r.items():
+                if isinstance(v, dict):
+                    v["TB_s"] = round(gb / (v["min_us"] * 1e-6) / 1e3, 2)
+            out[f"{name}_M{M}"] = r
+            print(name, M, json.dumps(r), flush=True)
+        del ws
+        torch.cuda.empty_cache()
+    return out
+
+
 def attn_decode_bench(B, ctx, split_len):
     dev = torch.device("cuda")
     Hq, Hkv, D, BS = 28, 4, 128, 16
@@ -183,6 +228,8 @@ if __name__ == "__main__":
         res["prefill_16x1024"] = attn_prefill_bench(16, 1024)
         res["prefill_4x4096"] = attn_prefill_bench(4, 4096)
         res["prefill_2x11712"] = attn_prefill_bench(2, 11712)  # the reference's --max-model-len
+    if args.what == "midm":  # 129-256-row projections: dispatched kernel vs tile schedules
+        res.update(midm_bench())
     if args.what in ("all", "elementwise"):
         res["elementwise_T14336"] = elementwise_bench()
     if args.what in ("all", "sampler"):
