@@ -15,7 +15,7 @@
 #                    processes sharing the card (18 GB of weights each), small batch / index / KV; prefill
 #                    chunks of 480 tokens keep every all-reduce on the one-shot IPC path (gloo would stage
 #                    the large ones through the host)
-#   sweep=ARGS       bench with --agent-sweep (agent saturation curve)
+#   sweep=LEVELS     bench with --agent-sweep LEVELS (agent saturation curve); SWEEP_ARGS=a,b,.. extra bench args
 #   prof             rocprofv3 --kernel-trace --stats over a 2-step bench (scripts/profile_bench.sh)
 #   mb=WHAT          scripts/microbench.py --what WHAT (json in gpurun_out/<TAG>_mb_WHAT.json)
 #   profdec=ARGS     rocprofv3 kernel stats of one decode step (scripts/profile_decode_step.sh ARGS)  (400 s)
@@ -62,7 +62,8 @@ for step in "$@"; do
              --index-size 2000000 --nlist 1024 --nprobe 32 --batch 8 --inflight 2 --arrival-groups 2 --steps 2 \
              --warmup 1 --kv-cache-gb 6 --max-batched-tokens 480 --no-ingest --agent-jobs 4 \
              --agent-concurrency 4 --serving-steps 0 ${val//,/ } ;;
-    sweep) run 1100 sweep python -u bench.py --no-ingest --agent-sweep "${val:-64,256,512,1024}" --steps 2 --warmup 1 ;;
+    sweep) run 1100 sweep python -u bench.py --no-ingest --agent-sweep "${val:-64,256,512,1024}" --steps 2 --warmup 1 \
+             ${SWEEP_ARGS//,/ } ;;
     prof) run 700 prof bash scripts/profile_bench.sh ;;
     profdec) run 400 profdec env TAG="${TAG}" bash scripts/profile_decode_step.sh ${val//,/ } ;;
     py) npy=$((npy+1)); run 600 "py$npy" python -u ${val//,/ } ;;
