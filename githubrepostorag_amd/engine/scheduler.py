@@ -257,6 +257,13 @@ class Scheduler:
                     self.kv.match_prefix(seq)
                 tgt = self.prefill_target(seq)
                 n = min(tgt - seq.num_computed, budget)
+                # decode watermark: an admission must leave one free block per running sequence, so the next
+                # decode window's block-boundary crossings never preempt (admitting into the last free
+                # blocks and preempting at the next decode step recomputes whole prompts: at 1024 agent jobs
+                # on one GPU that thrash dominated, profiles/agent_saturation_r4.json)
+                if self.running and self.kv.num_free - self.kv.blocks_needed(seq, seq.num_computed + max(n, 0)) \
+                        < len(self.running) + 1:
+                    break
                 if n <= 0 or not self.kv.ensure(seq, seq.num_computed + n):
                     break
                 self.waiting.popleft()

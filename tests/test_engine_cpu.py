@@ -56,12 +56,25 @@ def test_chunked_prefill_and_small_batches_identical(model, tok):
 
 def test_preemption_recomputes_identically(model, tok):
     prompts = [[(7 * i + j) % 500 + 1 for j in range(31)] for i in range(4)]
-    _, a = _gen(model, tok, prompts=prompts)
-    # 16 usable blocks of 8 tokens hold the four 31-token prompts (4 blocks each) but not
-    # their growth past 32 tokens: decode must preempt the youngest and recompute it later
-    eng, b = _gen(model, tok, prompts=prompts, num_blocks=17, block_size=8, enable_prefix_caching=False)
+    # 16 usable blocks of 8 tokens: the admission watermark (a free block per running sequence) admits
+    # three 31-token prompts (4 blocks each); their growth to 51 tokens (7 blocks each) does not fit:
+    # decode must preempt the youngest and recompute it later
+    sp = SamplingParams(max_tokens=20, temperature=0.0, ignore_eos=True)
+    _, a = _gen(model, tok, prompts=prompts, sp=sp)
+    eng, b = _gen(model, tok, prompts=prompts, sp=sp, num_blocks=17, block_size=8, enable_prefix_caching=False)
     assert [x.token_ids for x in a] == [x.token_ids for x in b]
     assert eng.sched.num_preemptions > 0
+
+
+def test_admission_watermark_avoids_preemption(model, tok):
+    """Round 3 admitted the fourth 31-token prompt into the last free blocks and preempted at the next
+    block crossing; the watermark keeps one free block per running sequence, so growth to 38 tokens
+    (5 blocks each) finishes without a preemption."""
+    prompts = [[(7 * i + j) % 500 + 1 for j in range(31)] for i in range(4)]
+    eng, b = _gen(model, tok, prompts=prompts, num_blocks=17, block_size=8, enable_prefix_caching=False)
+    _, a = _gen(model, tok, prompts=prompts)
+    assert [x.token_ids for x in a] == [x.token_ids for x in b]
+    assert eng.sched.num_preemptions == 0
 
 
 def test_prefix_cache_hit(model, tok):
