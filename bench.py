@@ -148,6 +148,10 @@ def parse():
                     help="timed steps of the same workload through the SERVING loop (engine/runner.py "
                          "EngineRunner thread, arrivals submitted from the retrieval thread under the runner's "
                          "admission hint): serving_runner in the JSON.  -1: --steps; 0: skip")
+    ap.add_argument("--serving-open-load", type=float, default=0.9,
+                    help="after the closed loop: open-loop Poisson arrivals of query groups at this fraction of the "
+                         "closed loop's throughput through the same serving loop (serving_runner.open_loop: TTFT "
+                         "p50 / p90 at that load; 0: skip)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     if args.preset:
@@ -740,6 +744,38 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
             pending.append(pool.submit(arrive))
         return out
 
+    def open_loop(rate: float, n: int) -> dict:
+        """n query groups arriving at Poisson times (``rate`` groups/s per rank), each submitted through the
+        retrieval thread as in the closed loop; TTFT p50 / p90 and the achieved completion rate."""
+        import random
+
+        import torch.distributed as dist
+
+        rng = random.Random(4321 + (dist.get_rank() if dist.is_available() and dist.is_initialized() else 0))
+        comm.barrier()
+        t0 = time.perf_counter()
+        due, futs = t0, []
+        for _ in range(n):
+            due += rng.expovariate(rate)
+            dt = due - time.perf_counter()
+            if dt > 0:
+                time.sleep(dt)
+            futs.append(pool.submit(arrive))
+        groups = [f.result() for f in futs]
+        t_last_arrival = time.perf_counter()
+        tt = []
+        for hs, t_sub, _ in groups:
+            for h in hs:
+                c = h.wait(600)
+                tt.append(c.first_token_at - t_sub)
+        t_done = time.perf_counter()
+        tt.sort()
+        return {"offered_queries_per_s": round(rate * u, 3), "groups": n,
+                "achieved_queries_per_s": round(n * u / (t_done - t0), 3),
+                "arrival_window_s": round(t_last_arrival - t0, 2),
+                "p50_ttft_ms": round(1000 * tt[len(tt) // 2], 2),
+                "p90_ttft_ms": round(1000 * tt[min(len(tt) - 1, int(0.9 * len(tt)))], 2)}
+
     def complete(n: int) -> list:
         ttfts, got = [], 0
         t_end = time.perf_counter() + 600
@@ -784,6 +820,9 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
         for hs, *_ in active:
             for h in hs:
                 h.wait(600)
+        open_res = None
+        if args.serving_open_load > 0 and elapsed > 0:
+            open_res = open_loop(args.serving_open_load * u * steps * A / elapsed / u, steps * A)
     finally:
         runner.shutdown()
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -797,12 +836,18 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
     qps = args.batch * steps * dp_size / elapsed
     p50 = statistics.median([x for r in allt for x in r]) * 1000.0
     log(f"serving loop (EngineRunner + admission hint): {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms")
+    if open_res:
+        log(f"serving loop, open-loop Poisson arrivals at {open_res['offered_queries_per_s']} queries/s: "
+            f"p50 TTFT {open_res['p50_ttft_ms']} ms, p90 {open_res['p90_ttft_ms']} ms")
     return {"value": round(qps, 3), "p50_ttft_ms": round(p50, 2), "steps": steps,
             # TTFT = retrieval (embed + search + prompt, until the prompts are submitted) + engine admission
             # and prefill; the retrieval part's p50 over the timed arrivals (this rank)
             "retrieval_p50_ms": round(statistics.median(gaps) * 1000.0, 2) if gaps else None,
             "submit_to_first_token_p50_ms": round(statistics.median(engs) * 1000.0, 2) if engs else None,
             "engine_steps": _trace_summary(trace),
+            # closed loops bunch arrivals (a K-step replay completes several groups at once, and they are
+            # prefilled back to back); the open loop shows the TTFT of Poisson arrivals at a set load
+            "open_loop": open_res,
             "ms_per_step": round(elapsed / steps * 1000.0, 2),
             # decode tokens the engine produced in the timed window / what the completed queries needed:
             # ~1.0 when the window was the pipeline's steady state (no backlog built or drained in it)
