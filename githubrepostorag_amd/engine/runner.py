@@ -29,6 +29,7 @@ from __future__ import annotations
 import contextlib
 import logging
 import os
+import queue
 import threading
 import time
 
@@ -104,6 +105,11 @@ class EngineRunner:
         self._last_event = -1e9
         self._step_s = None   # EWMA of one decode step's time (s), from the replays
         self.ctrl_stats = {"iterations": 0, "bytes": 0, "payloads": 0}
+        self._notes: list = []  # streamed tokens / completions of the current step (engine thread)
+        self._stream_q: queue.SimpleQueue = queue.SimpleQueue()
+        self._streamer = threading.Thread(target=self._stream_loop, name="grag-stream", daemon=True)
+        if start:
+            self._streamer.start()
         self._thread = threading.Thread(target=self._loop if self.leader else self.follow, name="grag-engine",
                                         daemon=True)
         if start:
@@ -182,6 +188,9 @@ class EngineRunner:
             self._stop = True
             self._cv.notify()
         self._thread.join(timeout=10)
+        self._stream_q.put(None)
+        if self._streamer.is_alive():
+            self._streamer.join(timeout=10)
         if self._wd is not None:
             self._wd.join(timeout=2)
 
@@ -205,16 +214,44 @@ class EngineRunner:
             h.done.set()
 
     def _on_token_wrapper(self, user_cb):
+        """Engine-thread side of a streamed request: the step's token deltas and the completion are noted
+        and handed to the streamer thread in one batch after the step (``_flush_notes``), so the engine
+        thread never runs consumer code (event-log appends, SSE wake-ups) per token."""
         def cb(seq, delta, finished):
-            if user_cb is not None and delta:
-                user_cb(delta)
+            h = comp = None
             if finished:
                 h = self._handles.pop(seq.req_id, None)
                 self.engine.pop(seq.req_id)
                 if h is not None:
-                    h.result = self.engine.completion(seq)
-                    h.done.set()
+                    comp = self.engine.completion(seq)
+            if (user_cb is not None and delta) or h is not None:
+                self._notes.append((user_cb if delta else None, delta, h, comp))
         return cb
+
+    def _flush_notes(self) -> None:
+        if self._notes:
+            batch, self._notes = self._notes, []
+            self._stream_q.put(batch)
+
+    def _stream_loop(self) -> None:
+        """Runs the streamed requests' token callbacks and completions, one engine step's batch at a time,
+        in order; their asyncio wake-ups go out once per event loop per batch (utils/wakeups.py)."""
+        from ..utils.wakeups import deferred
+
+        while True:
+            batch = self._stream_q.get()
+            if batch is None:
+                return
+            with deferred():
+                for cb, delta, h, comp in batch:
+                    if cb is not None:
+                        try:
+                            cb(delta)
+                        except Exception:  # a broken consumer never stops the stream of the others
+                            log.exception("token callback failed")
+                    if h is not None:
+                        h.result = comp
+                        h.done.set()
 
     # ------------------------------------------------------------------ TP control plane
     # One iteration of a TP group = ONE int64 SUM all-reduce of a small header over the TP group (the
@@ -391,7 +428,10 @@ class EngineRunner:
             try:
                 st = self.engine.stats
                 ds0, dt0 = st.get("decode_steps", 0), st.get("decode_s", 0.0)
-                self._complete(self.engine.step(max_window=win))
+                try:
+                    self._complete(self.engine.step(max_window=win))
+                finally:
+                    self._flush_notes()
                 n = st.get("decode_steps", 0) - ds0
                 if n > 0:  # decode step time for the paced arrival window
                     per = (st.get("decode_s", 0.0) - dt0) / n

@@ -23,6 +23,8 @@ import time
 from collections import defaultdict
 from typing import AsyncIterator
 
+from ..utils.wakeups import wake
+
 
 class _JobLog:
     __slots__ = ("events", "cond", "created", "closed")
@@ -57,11 +59,8 @@ class EventLog:
             lg.cond.notify_all()
         with self._lock:
             waiters = list(self._waiters.get(job_id, []))
-        for loop, ev in waiters:
-            try:
-                loop.call_soon_threadsafe(ev.set)
-            except RuntimeError:
-                pass
+        for loop, ev in waiters:  # coalesced when the caller batches (utils/wakeups.deferred)
+            wake(loop, ev)
 
     async def emit(self, job_id: str, event: str, data) -> None:
         self.emit_sync(job_id, event, data)
