@@ -148,10 +148,10 @@ def parse():
                     help="timed steps of the same workload through the SERVING loop (engine/runner.py "
                          "EngineRunner thread, arrivals submitted from the retrieval thread under the runner's "
                          "admission hint): serving_runner in the JSON.  -1: --steps; 0: skip")
-    ap.add_argument("--serving-open-load", type=float, default=0.9,
-                    help="after the closed loop: open-loop Poisson arrivals of query groups at this fraction of the "
-                         "closed loop's throughput through the same serving loop (serving_runner.open_loop: TTFT "
-                         "p50 / p90 at that load; 0: skip)")
+    ap.add_argument("--serving-open-load", default="0.5,0.9",
+                    help="after the closed loop: open-loop Poisson arrivals of query groups at these fractions of "
+                         "the closed loop's throughput through the same serving loop (serving_runner.open_loop: "
+                         "TTFT p50 / p90 at each load; empty: skip)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     if args.preset:
@@ -820,9 +820,10 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
         for hs, *_ in active:
             for h in hs:
                 h.wait(600)
-        open_res = None
-        if args.serving_open_load > 0 and elapsed > 0:
-            open_res = open_loop(args.serving_open_load * u * steps * A / elapsed / u, steps * A)
+        open_res = []
+        loads = [float(x) for x in str(args.serving_open_load).split(",") if x.strip()]
+        for load in loads if elapsed > 0 else []:
+            open_res.append({"load": load, **open_loop(load * steps * A / elapsed, steps * A)})
     finally:
         runner.shutdown()
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -836,9 +837,9 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
     qps = args.batch * steps * dp_size / elapsed
     p50 = statistics.median([x for r in allt for x in r]) * 1000.0
     log(f"serving loop (EngineRunner + admission hint): {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms")
-    if open_res:
-        log(f"serving loop, open-loop Poisson arrivals at {open_res['offered_queries_per_s']} queries/s: "
-            f"p50 TTFT {open_res['p50_ttft_ms']} ms, p90 {open_res['p90_ttft_ms']} ms")
+    for o in open_res or []:
+        log(f"serving loop, open-loop Poisson arrivals at {o['offered_queries_per_s']} queries/s ({o['load']:.0%} "
+            f"of the closed loop): p50 TTFT {o['p50_ttft_ms']} ms, p90 {o['p90_ttft_ms']} ms")
     return {"value": round(qps, 3), "p50_ttft_ms": round(p50, 2), "steps": steps,
             # TTFT = retrieval (embed + search + prompt, until the prompts are submitted) + engine admission
             # and prefill; the retrieval part's p50 over the timed arrivals (this rank)

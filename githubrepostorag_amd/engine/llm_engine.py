@@ -262,7 +262,8 @@ class LLMEngine:
         if not items:
             return finished
         self.stats["steps"] += 1
-        t0 = time.perf_counter() if self.trace is not None else 0.0
+        trace = self.trace  # another thread may switch tracing on or off mid-step: the step's own view
+        t0 = time.perf_counter() if trace is not None else 0.0
         tok0 = self.stats["prefill_tokens"] + self.stats["decode_tokens"]
         if kind in ("prefill", "mixed"):
             try:
@@ -274,9 +275,9 @@ class LLMEngine:
                 raise
         else:
             finished += self._run_decode([s for s, _, _ in items], max_window)
-        if self.trace is not None:
-            self.trace.append((t0, kind, len(items), self.stats["prefill_tokens"] + self.stats["decode_tokens"] - tok0,
-                               time.perf_counter() - t0))
+        if trace is not None:
+            trace.append((t0, kind, len(items), self.stats["prefill_tokens"] + self.stats["decode_tokens"] - tok0,
+                          time.perf_counter() - t0))
         return finished
 
     # ------------------------------------------------------------------ helpers
