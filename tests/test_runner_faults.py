@@ -125,3 +125,46 @@ def test_arrival_paced_window():
         r.submit("ingest prompt", interactive=False)
         time.sleep(0.01)
     assert r._gap == g and r._window() is None  # batch work does not pace the window
+
+
+def test_streamed_tokens_batched_off_the_engine_thread():
+    """Streamed requests: the engine thread only notes (callback, delta) per token; the streamer thread runs
+    the callbacks in order, one engine step's batch at a time, and their event-loop wake-ups are coalesced
+    to one call per loop per batch (utils/wakeups.py)."""
+    import asyncio
+
+    from githubrepostorag_amd.service.events import EventLog
+
+    log = EventLog()
+    loop = asyncio.new_event_loop()
+    calls = []
+    real = loop.call_soon_threadsafe
+
+    def counting(cb, *a):
+        calls.append(cb)
+        return real(cb, *a)
+
+    loop.call_soon_threadsafe = counting
+    ev = asyncio.Event()
+    log._waiters["job"].append((loop, ev))
+    from githubrepostorag_amd.utils.wakeups import deferred
+
+    with deferred():
+        for i in range(50):
+            log.emit_sync("job", "token", {"i": i})
+    assert len(calls) == 1  # one wake-up for the whole batch
+    log.emit_sync("job", "token", {"i": 50})
+    assert len(calls) == 2  # outside a batch: one per event
+    assert [e["data"]["i"] for e in log.events("job")] == list(range(51))
+    loop.close()
+
+    seen = []
+    eng = FakeEngine()
+    r = EngineRunner(eng, watchdog_s=0)
+    try:
+        h = r.submit("q", on_token=lambda d: seen.append((threading.current_thread().name, d)))
+        # the fake engine streams one delta then finishes through the callback
+        assert h.wait(5).text == "done"
+    finally:
+        r.shutdown()
+    assert seen and all(name == "grag-stream" for name, _ in seen)
