@@ -5,6 +5,8 @@ vLLM, Cassandra, Redis) with one process per GPU."""
 from __future__ import annotations
 
 import logging
+import os
+import sys
 import time
 from pathlib import Path
 
@@ -99,6 +101,10 @@ class RAGRuntime:
             from . import metrics as M
 
             M.ENGINE_HEALTHY.set(1)
+            # the engine thread shares the interpreter with the API / job / retrieval threads: a 0.5 ms GIL
+            # switch interval (Python's default is 5 ms) bounds how long it waits at a step boundary
+            # (same-box A/B in profiles/ab_switch_r3.txt; the bench runs the same setting)
+            sys.setswitchinterval(float(os.environ.get("GRAG_SWITCH_INTERVAL_MS", "0.5")) / 1000.0)
             self.runner = EngineRunner(self.engine, watchdog_s=s.engine_watchdog_s,
                                        on_health=lambda ok: M.ENGINE_HEALTHY.set(1 if ok else 0),
                                        tp=self.tp_group)
