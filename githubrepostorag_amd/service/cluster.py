@@ -152,13 +152,19 @@ class ReplicaHub:
 
     def _reader(self, conn) -> None:
         rep = None
+        from .mesh import cut_connection
+
+        guard = threading.Timer(10.0, cut_connection, (conn,))  # a peer that never finishes the handshake
+        guard.start()
         try:
             deliver_challenge(conn, self.authkey)
             answer_challenge(conn, self.authkey)
-        except (AuthenticationError, EOFError, OSError, AssertionError):
+        except (AuthenticationError, EOFError, OSError, AssertionError, TypeError):
             log.warning("replica hub: rejected a connection (authentication)")
             conn.close()
             return
+        finally:
+            guard.cancel()
         try:
             hello = conn.recv()
             if not (isinstance(hello, tuple) and hello and hello[0] == "hello"):

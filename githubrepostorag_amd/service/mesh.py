@@ -61,6 +61,24 @@ class Parts(list):
         self.missing = list(missing)
 
 
+def cut_connection(conn) -> None:
+    """Shut a multiprocessing Connection's socket down (wakes a thread blocked reading it), then close it."""
+    import socket
+
+    try:
+        s = socket.fromfd(conn.fileno(), socket.AF_INET, socket.SOCK_STREAM)
+        try:
+            s.shutdown(socket.SHUT_RDWR)
+        finally:
+            s.close()
+    except (OSError, ValueError):
+        pass
+    try:
+        conn.close()
+    except OSError:
+        pass
+
+
 class _Pending:
     __slots__ = ("ev", "ok", "res")
 
@@ -284,13 +302,17 @@ class PeerMesh:
             threading.Thread(target=self._serve, args=(conn,), name="mesh-serve", daemon=True).start()
 
     def _serve(self, conn) -> None:
+        guard = threading.Timer(10.0, cut_connection, (conn,))  # a peer that never finishes the handshake
+        guard.start()
         try:
             deliver_challenge(conn, self.authkey)
             answer_challenge(conn, self.authkey)
-        except (AuthenticationError, EOFError, OSError, AssertionError):
+        except (AuthenticationError, EOFError, OSError, AssertionError, TypeError):
             log.warning("mesh: rejected a connection (authentication)")
             conn.close()
             return
+        finally:
+            guard.cancel()
         send_lock = threading.Lock()
         with self._lock:
             self._served.add(conn)

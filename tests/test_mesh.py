@@ -166,5 +166,18 @@ def test_mesh_stalled_or_bad_client_does_not_block_peers(mesh3):
     with round_health() as h:
         facades[2].table("chunk").search(vecs[:3], 4)
     assert h["degraded_rounds"] == 0
+    time.sleep(10.5)  # past the handshake guard: the stalled sockets are cut off, the good link stays up
+    for s in stalled:  # the challenge bytes, then EOF: the guard shut the stalled handshakes down
+        s.settimeout(5.0)
+        data = b""
+        while True:
+            chunk = s.recv(4096)
+            if not chunk:
+                break
+            data += chunk
+        assert b"#CHALLENGE#" in data
+    with round_health() as h:
+        facades[2].table("chunk").search(vecs[:3], 4)
+    assert h["degraded_rounds"] == 0
     for s in stalled:
         s.close()
