@@ -150,7 +150,7 @@ class _PeerLink:
                     if p is not None:
                         p.ok, p.res = ok, res
                         p.ev.set()
-        except (EOFError, OSError, ValueError):
+        except (EOFError, OSError, ValueError, TypeError):  # TypeError: the link was closed under recv()
             self._fail()
 
     def _fail(self) -> None:

@@ -262,7 +262,7 @@ def test_hub_relay_writes_are_acknowledged_in_order():
                         _, o, req, scope, op, payload = msg
                         applied.append(payload)
                         owner.send(("shard_res", o, req, len(payload)))
-            except (EOFError, OSError):
+            except (EOFError, OSError, TypeError):  # TypeError: closed under recv()
                 pass
 
         tr = HubShardTransport(origin.send, 0)
@@ -273,7 +273,7 @@ def test_hub_relay_writes_are_acknowledged_in_order():
                     msg = origin.recv()
                     if msg[0] in ("shard_plan", "shard_part"):
                         tr.deliver(msg)
-            except (EOFError, OSError):
+            except (EOFError, OSError, TypeError):
                 pass
 
         threading.Thread(target=owner_loop, daemon=True).start()
