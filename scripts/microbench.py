@@ -217,6 +217,11 @@ if __name__ == "__main__":
         for B, ctx, sl in ((512, 1100, 2048), (1024, 1100, 2048), (256, 1100, 1024), (64, 1152, 256),
                            (176, 3000, 1024), (16, 6000, 256), (1, 4096, 64)):
             res[f"decode_B{B}_ctx{ctx}_split{sl}"] = attn_decode_bench(B, ctx, sl)
+    if args.what == "decode_nt_splits":  # non-temporal K/V loads x split-KV part length at the serving batches
+        os.environ["MB_DECODE_ARMS"] = "nt"
+        for B, ctx, sl in ((512, 1100, 2048), (512, 1100, 1024), (512, 1100, 512), (1024, 1100, 2048),
+                           (1024, 1100, 1024), (256, 1100, 1024), (256, 1100, 512)):
+            res[f"decode_B{B}_ctx{ctx}_split{sl}"] = attn_decode_bench(B, ctx, sl)
     if args.what in ("all", "attn", "decode"):
         res["decode_B512_ctx1100_split256"] = attn_decode_bench(512, 1100, 256)  # the bench's decode step
     if args.what in ("all", "attn"):
