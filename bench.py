@@ -706,14 +706,16 @@ def serving_runner_phase(args, eng, prepare, pool, sp, U, u, A, S, steps, dev, d
     are submitted from that thread, as a server's request threads do.  The fill submits a group every S
     engine decode steps, so completions are spread out as in the harness's pipeline.  Timed: ``steps`` x A
     completions after a warm-up of U completions; qps = completed queries / wall time; p50 TTFT =
-    submission -> first token; ``steady_state_decode_ratio`` ~ 1.0 shows the window was steady state."""
+    submission -> first token; ``steady_state_decode_ratio`` ~ 1.0 shows the window was steady state.
+    Then ``--serving-open-load``: Poisson arrivals at fractions of the closed loop's rate (``open_loop``),
+    the TTFT a server sees at a set load without the closed loop's bunching."""
     import torch
 
     from githubrepostorag_amd.engine.runner import EngineRunner
     from githubrepostorag_amd.parallel import comm
 
     runner = EngineRunner(eng, watchdog_s=0)
-    active = []    # (handles, t_sub) in flight
+    active = []    # (handles, t_sub, t_submitted) of the groups in flight
     pending = []   # futures of arrivals being retrieved
 
     sub_gap = []  # per arrival: retrieval (t_sub -> prompts submitted), seconds
