@@ -235,3 +235,28 @@ def test_chunk_nodes_get_module_metadata():
                            component_kind="service", is_standalone=False, run_id="0", dev_forced=False,
                            doc_type="chunk")
     assert n.metadata["module"] == "billing" and n.metadata["scope"] == "chunk"
+
+
+def test_ingest_token_audit_small_repo():
+    """scripts/ingest_token_audit.py (the prefill floor quoted in profiles/ingest_critical_path_r4.txt) on
+    an 8-file repo: every call kind is seen, and an ideal block cache computes fewer tokens than submitted."""
+    import importlib.util
+    import os
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("ingest_token_audit", os.path.join(root, "scripts",
+                                                                                    "ingest_token_audit.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    runner = mod.FakeRunner(mod.load_tokenizer(None, 152064), 152064)
+    calls = [([1] * 40 + [2] * 10, 32), ([1] * 40 + [3] * 10, 32), ([5] * 20, 64)]
+    runner.calls.extend(calls)
+    u = mod.ideal_unique(runner.calls)
+    assert u == [50, 50 - 32, 20]  # the second prompt shares two full 16-token blocks with the first
+    old = sys.argv
+    try:
+        sys.argv = ["ingest_token_audit", "--files", "8"]
+        mod.main()
+    finally:
+        sys.argv = old
