@@ -152,6 +152,10 @@ def parse():
                     help="after the closed loop: open-loop Poisson arrivals of query groups at these fractions of "
                          "the closed loop's throughput through the same serving loop (serving_runner.open_loop: "
                          "TTFT p50 / p90 at each load; empty: skip)")
+    ap.add_argument("--low-load", type=int, default=1,
+                    help="1: the reference's own regime (vLLM --max-num-seqs 4 --max-model-len 11712): single-prompt "
+                         "TTFT at 1K / 4K / 11.6K tokens, decode TPOT at 1 / 4 / 16 live sequences x those contexts "
+                         "(engine/probe.py), and agent jobs at concurrency 1 and 4: low_load in the JSON")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     if args.preset:
@@ -575,6 +579,15 @@ def main():
                 f"e2e TTFT p50 {agent_res['e2e_ttft_p50_ms']} ms p90 {agent_res['e2e_ttft_p90_ms']} ms, "
                 f"errors {agent_res['errors']}")
 
+    # ---- the reference's own operating regime (one user, <= 4 sequences, up to 11.7K context)
+    low_load = None
+    if args.low_load and dev.type == "cuda" and tp == 1:
+        from githubrepostorag_amd.engine.probe import run_low_load
+
+        low_load = run_low_load(model, tok, kv_cache_gb=12.0, use_graph=not args.no_graph, log=log)
+        if agent_res is not None:
+            low_load["agent"] = agent_res.pop("low_concurrency", None)
+
     # ---- ingest phase (reported separately)
     ingest_dps = None
     ingest_stages = None
@@ -684,6 +697,7 @@ def main():
             "agent_steady_jobs_per_s": None if agent_res is None else agent_res.get("steady_jobs_per_s"),
             "agent_saturation": None if agent_res is None else agent_res.get("agent_saturation"),
             "agent_e2e": agent_res,
+            "low_load": low_load,
         }
         line = json.dumps(res)
         print(line, flush=True)
@@ -947,6 +961,10 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_gr
     for j, c in enumerate(levels):
         n = max(64, 2 * c) * dp_size
         sweep.append(([mix(10_000_000 * (j + 1) + i) for i in range(n)], c * dp_size))
+    # the reference's regime: one user (concurrency 1) and vLLM's 4 sequences (concurrency 4), few jobs each
+    low = [(4, 1), (8, 4)] if (args.low_load and world == 1) else []
+    for j, (n, c) in enumerate(low):
+        sweep.append(([mix(90_000_000 + 1000 * j + i) for i in range(n)], c))
     res = None
     try:
         if world == 1:
@@ -997,6 +1015,10 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_gr
             st()
     if res is None:
         return None
+    if low and res.get("agent_saturation"):
+        curve = res["agent_saturation"]
+        res["low_concurrency"] = [{k: v for k, v in r.items() if k != "engine"} for r in curve[len(levels):]]
+        res["agent_saturation"] = curve[:len(levels)] or None
     res["concurrency"] = n_conc
     res["worker_slots_per_replica"] = slots
     res["llm_token_cap"] = args.agent_gen_len

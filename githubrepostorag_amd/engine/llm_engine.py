@@ -271,7 +271,9 @@ class LLMEngine:
             except BaseException:
                 # the step's prompt blocks were registered when scheduled (in-step prefix sharing): never let
                 # the cache serve blocks this failed step may not have written
-                self.kv.unregister(getattr(self.sched, "last_registered", []))
+                bad = list(getattr(self.sched, "last_registered", []))
+                self.kv.unregister(bad)
+                self._rollback_prefill(items, set(bad))
                 raise
         else:
             finished += self._run_decode([s for s, _, _ in items], max_window)
@@ -279,6 +281,23 @@ class LLMEngine:
             trace.append((t0, kind, len(items), self.stats["prefill_tokens"] + self.stats["decode_tokens"] - tok0,
                           time.perf_counter() - t0))
         return finished
+
+    def _rollback_prefill(self, items, bad: set) -> None:
+        """Undo a failed prefill step's effect on its sequences, so a caller that keeps stepping never
+        attends over K/V the step did not write: a sequence whose already-computed prefix includes a
+        block registered (and so possibly matched) in this step restarts its prefill from scratch; every
+        other prefill item is reset to where the step started, its hash chain cut back to the blocks
+        computed before it (the step's blocks are registered again once they are really computed)."""
+        bs = self.cfg.block_size
+        for seq, a, b in items:
+            if not seq.is_prefill and b - a == 1 and seq.output_ids:
+                continue  # a decode row riding in a mixed step
+            if bad and any(blk in bad for blk in seq.blocks[: -(-a // bs)]):
+                self.kv.free(seq)
+                seq.cached_prefix = 0
+                continue
+            seq.num_computed = min(seq.num_computed, a)
+            del seq.block_hashes[a // bs:]
 
     # ------------------------------------------------------------------ helpers
     def _slots_of(self, seq: Sequence, start: int, end: int) -> np.ndarray:

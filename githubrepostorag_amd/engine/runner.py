@@ -206,10 +206,13 @@ class EngineRunner:
         for seq in finished or ():
             if seq.on_token is not None:
                 continue
+            # popped whether or not a handle still waits: the watchdog / _fail_all clear the handles of
+            # requests they abort, and those are reaped in a later step (their Sequence must not stay in
+            # engine._seqs)
+            self.engine.pop(seq.req_id)
             h = self._handles.pop(seq.req_id, None)
             if h is None:
                 continue
-            self.engine.pop(seq.req_id)
             h.result = self.engine.completion(seq)
             h.done.set()
 

@@ -153,12 +153,14 @@ def create_app(state: APIState | None = None, runtime_factory=None) -> FastAPI:
         from ..engine.sequence import SamplingParams
 
         stop = body.stop if isinstance(body.stop, list) else ([body.stop] if body.stop else [])
-        mt = getattr(body, "max_completion_tokens", None) or body.max_tokens or rt.settings.qwen_max_output
-        return SamplingParams(max_tokens=int(mt), temperature=body.temperature if body.temperature is not None else 0.7,
+        mt = getattr(body, "max_completion_tokens", None) or body.max_tokens
+        sp = SamplingParams(max_tokens=int(mt or rt.settings.qwen_max_output), temperature=body.temperature if body.temperature is not None else 0.7,
                               top_p=body.top_p if body.top_p is not None else 1.0,
                               top_k=getattr(body, "top_k", 0) or 0,
                               repetition_penalty=getattr(body, "repetition_penalty", None) or 1.0, stop=stop,
                               seed=getattr(body, "seed", None))
+        sp.max_tokens_explicit = bool(mt)  # vLLM: an unset max_tokens means "up to max_model_len"
+        return sp
 
     async def _generate(rt, text, sp, stream: bool, model: str, chat: bool):
         loop = asyncio.get_running_loop()
@@ -171,6 +173,14 @@ def create_app(state: APIState | None = None, runtime_factory=None) -> FastAPI:
             from ..engine.llm_engine import PromptTooLongError
 
             raise HTTPException(400, str(PromptTooLongError(len(ids), mml)))
+        if mml:
+            if not getattr(sp, "max_tokens_explicit", True):
+                sp.max_tokens = mml - len(ids)
+            elif len(ids) + sp.max_tokens > mml:  # vLLM's check: prompt + requested completion must fit
+                raise HTTPException(400, f"This model's maximum context length is {mml} tokens. However, you "
+                                         f"requested {len(ids) + sp.max_tokens} tokens ({len(ids)} in the messages, "
+                                         f"{sp.max_tokens} in the completion). Please reduce the length of the "
+                                         "messages or completion.")
         text = ids
         rid = f"{'chatcmpl' if chat else 'cmpl'}-{uuid.uuid4().hex}"
         created = int(time.time())

@@ -42,7 +42,7 @@ only):
                   | ("shard_res", origin, req, result) | ("shard_wreq", req, owner, scope, op, payload)
   hub -> replica: ("run", job, request) | ("cancel", job) | ("upsert", table, payload) | ("stop",)
                   | ("peers", {rank: mesh address})                        [mesh membership]
-                  | ("shard_plan", req, n_parts) | ("shard_part", req, rank, result)
+                  | ("shard_plan", req, n_parts, ranks) | ("shard_part", req, rank, result)
                   | ("shard_exec", origin, req, scope, op, payload) | ("shard_wexec", origin, req, scope, op, payload)
 A routed write (shard_wreq) is a one-part round: the owner applies it in arrival order (one writer thread)
 and answers with its applied count; an owner that is not connected answers None and the writer raises.
@@ -216,7 +216,7 @@ class ReplicaHub:
                         o = self.replicas.get(owner)
                         if o is not None and o.alive:
                             self._shard_pending.setdefault(owner, set()).add((rep.rank, req))
-                    rep.send(("shard_plan", req, 1))
+                    rep.send(("shard_plan", req, 1, [owner]))
                     if o is None or not o.alive or not o.send(("shard_wexec", rep.rank, req, scope, op, payload)):
                         with self._lock:
                             self._shard_pending.get(owner, set()).discard((rep.rank, req))
@@ -234,7 +234,7 @@ class ReplicaHub:
         with self._lock:
             for t in targets:
                 self._shard_pending.setdefault(t.rank, set()).add((origin.rank, req))
-        origin.send(("shard_plan", req, len(targets)))
+        origin.send(("shard_plan", req, len(targets), [t.rank for t in targets]))
         for t in targets:
             if not t.send(("shard_exec", origin.rank, req, scope, op, payload)):
                 with self._lock:
@@ -471,10 +471,17 @@ class HubShardTransport:
                             len(st["parts"]), st["n"], timeout)
             with self._lock:
                 parts = dict(st["parts"])
+                expected = st.get("ranks")
+                planned = st["n"] is not None
             from .mesh import Parts
 
-            return Parts([p for p in parts.values() if p is not None],
-                         missing=[r for r, p in parts.items() if p is None])
+            missing = [r for r, p in parts.items() if p is None]
+            # a shard that never answered before the timeout is missing too (the round is degraded); with no
+            # plan at all (the hub itself did not answer) the expected ranks are unknown: flagged as rank -1
+            missing += [r for r in (expected or []) if r not in parts]
+            if not planned:
+                missing.append(-1)
+            return Parts([p for p in parts.values() if p is not None], missing=missing)
         finally:
             with self._lock:
                 self._rounds.pop(req, None)
@@ -509,6 +516,7 @@ class HubShardTransport:
                 return
             if kind == "shard_plan":
                 st["n"] = msg[2]
+                st["ranks"] = list(msg[3]) if len(msg) > 3 else None
             else:  # keyed by the answering rank: a duplicate (e.g. an empty answer from the hub's
                 # failed-send path AND its replica-lost path) cannot complete the round early
                 st["parts"].setdefault(int(msg[2]), msg[3])

@@ -1,0 +1,94 @@
+"""Graph-timed, cold-weight sweep of the Qwen2-7B decode projections at 33-256 rows.
+
+Every arm is captured into one hipGraph of R launches that rotate over >= 1 GiB of weight copies (a decode
+step streams 15 GB of weights, so each matrix arrives cold from HBM), replayed back to back; the time per
+launch excludes Python / ctypes dispatch, unlike scripts/microbench.py's eager loop.  Arms per shape:
+  linear      ops/linear.linear (or mlp_gate_up): the dispatched kernel plus its split-K reduce
+  deferred    ops/linear.linear_deferred: the planes left for the consumer (RoPE / RMSNorm) to reduce,
+              the form the decoder runs for qkv / o / down (decode batches)
+Output: one JSON object {shape_M: {arm: {us, TB_s}}} (weights' bytes / time).
+
+python scripts/gemm_graph_sweep.py --Ms 64,128,176,256 --out gpurun_out/gemm_sweep.json
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from githubrepostorag_amd.ops import gemm as G  # noqa: E402
+from githubrepostorag_amd.ops.linear import enable_tuned_gemms, kernel_for, linear, linear_deferred  # noqa: E402
+
+SHAPES = {"qkv": (4608, 3584, False), "o": (3584, 3584, False), "gate_up": (37888, 3584, True),
+          "down": (3584, 18944, False)}
+
+
+def graph_time(fn, ws, reps: int) -> float:
+    """us per launch of fn(w) over the rotating copies, captured as one graph of `reps` launches."""
+    for w in ws[:2]:
+        fn(w)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn(ws[0])
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        for i in range(reps):
+            fn(ws[i % len(ws)])
+    g.replay()
+    torch.cuda.synchronize()
+    best = []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        e1.synchronize()
+        best.append(e0.elapsed_time(e1) * 1000.0 / reps)
+    best.sort()
+    return best[len(best) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--Ms", default="64,128,176,256")
+    ap.add_argument("--shapes", default="qkv,o,gate_up,down")
+    ap.add_argument("--reps", type=int, default=40)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    enable_tuned_gemms()
+    dev = torch.device("cuda")
+    out = {}
+    with torch.inference_mode():
+        for name in a.shapes.split(","):
+            N, K, silu = SHAPES[name]
+            ncopy = max(2, min(16, (1 << 30) // (N * K * 2) + 1))
+            ws = [((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(ncopy)]
+            for M in [int(m) for m in a.Ms.split(",")]:
+                x = ((torch.rand(M, K, device=dev) * 2 - 1)).to(torch.bfloat16)
+                arms = {}
+                if silu:
+                    arms["linear"] = lambda w: G.mlp_gate_up(x, w)
+                else:
+                    arms["linear"] = lambda w: linear(x, w)
+                    arms["deferred"] = lambda w: linear_deferred(x, w)
+                r = {"kernel": "mlp_gate_up" if silu else kernel_for(M, N, K)}
+                gb = N * K * 2 / 1e9
+                for k, fn in arms.items():
+                    us = graph_time(fn, ws, a.reps)
+                    r[k] = {"us": round(us, 2), "TB_s": round(gb / (us * 1e-6) / 1e3, 3)}
+                out[f"{name}_M{M}"] = r
+                print(name, M, json.dumps(r), flush=True)
+            del ws
+            torch.cuda.empty_cache()
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

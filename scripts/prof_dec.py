@@ -28,7 +28,8 @@ if a.plan == "tile":
     G.WS.reserve(dev, G._ws_floats(a.M, N, S, SK))
     fn = (lambda w: G.gemm_silu(x, w, ksplit=S, sk=SK)) if silu else (lambda w: G.gemm(x, w, ksplit=S, sk=SK))
 else:
-    plan = tuple(int(v) for v in a.plan.split(","))
+    plan = G.dec_plan(a.M, N, K, silu) if a.plan == "auto" else tuple(int(v) for v in a.plan.split(","))
+    print("plan", plan)
     G.WS.reserve(dev, G.dec_ws_floats(a.M, N, G.dec_ksplit(K, plan[3])))
     fn = lambda w: G.gemm_decode(x, w, epi=G.EPI_SILU if silu else G.EPI_STORE, plan=plan)  # noqa: E731
 for i in range(a.reps):

@@ -20,7 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--ctx", type=int, default=1100)
 ap.add_argument("--reps", type=int, default=30)
-ap.add_argument("--split-len", type=int, default=256)
+ap.add_argument("--split-len", type=int, default=0, help="keys per split-KV part (0: the engine's plan, llm_engine._split_len_for)")
 ap.add_argument("--model", default="qwen2-7b")
 a = ap.parse_args()
 
@@ -37,8 +37,11 @@ i32 = dict(dtype=torch.int32, device=dev)
 bt = (1 + torch.arange(B * nb, **i32)).view(B, nb)
 pos = torch.full((B,), ctx, **i32)
 slot = bt[:, ctx // BS] * BS + ctx % BS
-split_len = a.split_len
-nsplit = -(-(ctx + 1) // split_len)
+from githubrepostorag_amd.engine.llm_engine import _pow2_at_least, _split_len_for  # noqa: E402
+
+split_len = a.split_len or _split_len_for(B)
+nsplit = -(-(ctx + 1) // split_len) if a.split_len else _pow2_at_least(-(-(ctx + 1) // split_len))
+print(f"split-KV plan: {nsplit} parts of {split_len} keys")
 hq, d = model.hq, model.head_dim
 meta = AttnMetadata(q_start=torch.arange(B + 1, **i32), ctx_len=torch.full((B,), ctx + 1, **i32), block_tables=bt,
                     slot_mapping=slot, max_q_len=1, num_seqs=B, num_tokens=B, is_decode=True, num_splits=nsplit,

@@ -291,3 +291,24 @@ def test_hub_relay_writes_are_acknowledged_in_order():
         origin.close()
     finally:
         hub.close()
+
+
+def test_hub_fanout_timeout_reports_silent_shards_missing():
+    """A shard that never answers a hub-routed round before the timeout is reported missing (the round is
+    degraded), as is a round the hub never planned."""
+    from githubrepostorag_amd.service.cluster import HubShardTransport
+
+    tr = HubShardTransport(None, 0)
+
+    def send(msg):  # the hub plans ranks 1 and 2; only rank 1 answers
+        if msg[0] == "shard_req":
+            req = msg[1]
+            tr.deliver(("shard_plan", req, 2, [1, 2]))
+            tr.deliver(("shard_part", req, 1, ["hit"]))
+
+    tr._send = send
+    parts = tr.fanout(0, "chunk", "search", None, timeout=0.2)
+    assert list(parts) == [["hit"]] and parts.missing == [2]
+    tr._send = lambda msg: None  # no plan at all
+    parts = tr.fanout(0, "chunk", "search", None, timeout=0.1)
+    assert list(parts) == [] and parts.missing == [-1]

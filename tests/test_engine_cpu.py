@@ -212,6 +212,43 @@ def test_failed_prefill_step_unregisters_its_blocks(model, tok):
     assert eng.kv.match_prefix(probe) == 0
 
 
+def test_failed_prefill_step_rolls_back_sharers(model, tok):
+    """Two prompts sharing a prefix are admitted in one step (the second matches blocks the first registered
+    when scheduled); the step fails.  A caller that keeps stepping must get the outputs of a clean run: the
+    sharer restarts its prefill, the owner re-registers its blocks once they are really computed."""
+    cfg = EngineConfig(max_num_seqs=4, max_model_len=512, num_blocks=256, use_cuda_graph=False)
+    shared = [(7 * i) % 300 + 5 for i in range(64)]
+    p1, p2 = shared + [11, 12, 13], shared + [21, 22]
+
+    def clean():
+        e = LLMEngine(model, tok, cfg)
+        return [c.token_ids for c in e.generate([p1, p2], GREEDY)]
+
+    want = clean()
+    eng = LLMEngine(model, tok, cfg)
+    r1, r2 = eng.add_request(p1, GREEDY), eng.add_request(p2, GREEDY)
+    real = eng._run_prefill
+    seen = {}
+
+    def boom(items):
+        seen["items"] = [(s.req_id, a, b) for s, a, b in items]
+        raise RuntimeError("injected fault")
+
+    eng._run_prefill = boom
+    with pytest.raises(RuntimeError):
+        eng.step()
+    eng._run_prefill = real
+    assert [r for r, _, _ in seen["items"]] == [r1, r2]
+    assert seen["items"][1][1] > 0  # the sharer had matched the owner's (unwritten) blocks
+    s1, s2 = eng.get(r1), eng.get(r2)
+    assert s1.num_computed == 0 and s2.num_computed == 0 and s1.block_hashes == [] and s2.blocks == []
+    while eng.has_unfinished():
+        eng.step()
+    assert [eng.get(r).output_ids for r in (r1, r2)] == want
+    probe = Sequence("p", shared + [9], GREEDY)
+    assert eng.kv.match_prefix(probe) == 64  # the owner's blocks are registered again, now computed
+
+
 def test_priority_admission_order(model, tok):
     """A high-priority request jumps the waiting queue (FCFS within a priority)."""
     eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=1, max_model_len=512, num_blocks=256,
@@ -330,5 +367,15 @@ def test_over_long_prompt_rejected_by_engine_and_fitted_by_agent_llm(model, tok)
             assert bad.status_code == 400 and "maximum context length is 128" in bad.json()["detail"]
             ok = client.post("/v1/completions", json={"prompt": "hello", "max_tokens": 4, "temperature": 0})
             assert ok.status_code == 200 and ok.json()["choices"][0]["finish_reason"] in ("length", "stop")
+            # vLLM: prompt + max_tokens beyond max_model_len is a 400, not a completion cut short at the limit
+            n = len(tok.encode("hello"))
+            over = client.post("/v1/completions", json={"prompt": "hello", "max_tokens": 129 - n})
+            assert over.status_code == 400 and "in the completion" in over.json()["detail"]
+            fits = client.post("/v1/completions", json={"prompt": "hello", "max_tokens": 128 - n, "temperature": 0})
+            assert fits.status_code == 200
+            # chat with max_tokens unset: up to max_model_len (vLLM's default), not a 400
+            unset = client.post("/v1/chat/completions", json={"messages": [{"role": "user", "content": "hello"}],
+                                                               "temperature": 0})
+            assert unset.status_code == 200, unset.text
     finally:
         runner.shutdown()

@@ -31,6 +31,7 @@ class FakeEngine:
         self.mode = "ok"
         self.release = threading.Event()
         self.stats = {}
+        self.popped = []
 
     def add_request(self, prompt, params, req_id, on_token):
         self.reqs[req_id] = on_token
@@ -42,6 +43,7 @@ class FakeEngine:
         pass
 
     def pop(self, rid):
+        self.popped.append(rid)
         return None
 
     def completion(self, seq):
@@ -94,6 +96,26 @@ def test_watchdog_releases_waiters_on_hung_step():
         eng.release.set()  # the stuck step finally returns
         assert r.generate("p", timeout=5).text == "done"
         assert r.healthy and not r.hung and health == [False, True]
+    finally:
+        eng.release.set()
+        r.shutdown()
+
+
+def test_watchdog_reaped_request_is_popped_when_the_step_returns():
+    """A callback-free request the watchdog failed (its handle dropped) finishes in the stuck step once it
+    returns: the runner still pops it from the engine (else its Sequence would stay in engine._seqs)."""
+    eng = FakeEngine()
+    eng.mode = "hang"
+    r = EngineRunner(eng, watchdog_s=0.4)
+    try:
+        h = r.submit("p")
+        with pytest.raises(TimeoutError, match="watchdog"):
+            h.wait(8)
+        eng.release.set()
+        t0 = time.monotonic()
+        while h.req_id not in eng.popped and time.monotonic() - t0 < 5:
+            time.sleep(0.01)
+        assert h.req_id in eng.popped
     finally:
         eng.release.set()
         r.shutdown()
