@@ -49,6 +49,27 @@ class GenerationHandle:
         self.done = threading.Event()
         self.result: Completion | None = None
         self.error: BaseException | None = None
+        self._callbacks: list = []
+        self._cb_lock = threading.Lock()
+
+    def add_done_callback(self, fn) -> None:
+        """fn(handle) once the request completes or fails (at once if it already has), on the thread
+        that completes it: keep it short (an enqueue), it runs on the engine / streamer thread."""
+        with self._cb_lock:
+            if not self.done.is_set():
+                self._callbacks.append(fn)
+                return
+        fn(self)
+
+    def _finish(self) -> None:
+        with self._cb_lock:
+            self.done.set()
+            cbs, self._callbacks = self._callbacks, []
+        for fn in cbs:
+            try:
+                fn(self)
+            except Exception:
+                log.exception("generation done-callback failed")
 
     def wait(self, timeout: float | None = None) -> Completion:
         if not self.done.wait(timeout):
@@ -78,10 +99,16 @@ class EngineRunner:
     _AW = os.environ.get("GRAG_ARRIVAL_WINDOW", "auto")
     ARRIVAL_WINDOW = -1 if _AW == "auto" else int(_AW)
     MAX_WINDOW = 8
+    # prefill token budget per step while interactive arrivals keep coming (0: the engine's own
+    # max_num_batched_tokens): a burst of prompts is prefilled over a few steps, first come first, so the
+    # first of them do not wait for the whole burst's prefill (a decode replay of K steps is the other
+    # wait an arrival sees: paced by _window)
+    INTERACTIVE_PREFILL = int(os.environ.get("GRAG_INTERACTIVE_PREFILL", "0"))
 
     def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005, watchdog_s: float = 120.0,
-                 on_health=None, tp=None, start: bool = True):
+                 on_health=None, tp=None, start: bool = True, interactive_prefill: int | None = None):
         self.engine = engine
+        self.interactive_prefill = self.INTERACTIVE_PREFILL if interactive_prefill is None else interactive_prefill
         self._last_submit = -1e9
         self.tp = tp if tp is not None and not tp.trivial else None
         self.leader = self.tp is None or self.tp.rank == 0
@@ -171,6 +198,17 @@ class EngineRunner:
             return None
         return max(1, min(self.MAX_WINDOW, int(0.5 * g / d)))
 
+    def _prefill_budget(self) -> int | None:
+        """This step's prefill token cap: the interactive budget while arrivals are pending or paced."""
+        if not self.interactive_prefill or self.tp is not None:
+            return None
+        if self._expecting > 0:
+            return self.interactive_prefill
+        g = self._gap
+        if g is not None and time.monotonic() - self._last_event <= 2 * g:
+            return self.interactive_prefill
+        return None
+
     def generate(self, prompt, params: SamplingParams | None = None, on_token=None,
                  timeout: float | None = None) -> Completion:
         return self.submit(prompt, params, on_token).wait(timeout)
@@ -214,7 +252,7 @@ class EngineRunner:
             if h is None:
                 continue
             h.result = self.engine.completion(seq)
-            h.done.set()
+            h._finish()
 
     def _on_token_wrapper(self, user_cb):
         """Engine-thread side of a streamed request: the step's token deltas and the completion are noted
@@ -254,7 +292,7 @@ class EngineRunner:
                             log.exception("token callback failed")
                     if h is not None:
                         h.result = comp
-                        h.done.set()
+                        h._finish()
 
     # ------------------------------------------------------------------ TP control plane
     # One iteration of a TP group = ONE int64 SUM all-reduce of a small header over the TP group (the
@@ -422,7 +460,7 @@ class EngineRunner:
                     h = self._handles.pop(rid, None)
                     if h is not None:
                         h.error = e
-                        h.done.set()
+                        h._finish()
             if self.tp is not None:  # after the adds, as the followers do
                 for rid in aborts:
                     self.engine.abort(rid)
@@ -432,7 +470,7 @@ class EngineRunner:
                 st = self.engine.stats
                 ds0, dt0 = st.get("decode_steps", 0), st.get("decode_s", 0.0)
                 try:
-                    self._complete(self.engine.step(max_window=win))
+                    self._complete(self.engine.step(max_window=win, prefill_budget=self._prefill_budget()))
                 finally:
                     self._flush_notes()
                 n = st.get("decode_steps", 0) - ds0
@@ -494,7 +532,7 @@ class EngineRunner:
             for rid, h in handles.items():
                 self._abort_mirrored(rid)
                 h.error = err
-                h.done.set()
+                h._finish()
 
     def _abort_mirrored(self, rid: str) -> None:
         """Abort that every TP rank applies at the same iteration (queued for the
@@ -514,7 +552,7 @@ class EngineRunner:
             self.engine.abort(rid)
         for rid, h in handles:
             h.error = err
-            h.done.set()
+            h._finish()
         try:
             for s in self.engine.sched.reap_cancelled():
                 self.engine.pop(s.req_id)
@@ -527,7 +565,7 @@ class EngineRunner:
         for rid, h in handles.items():
             self._abort_mirrored(rid)
             h.error = err
-            h.done.set()
+            h._finish()
         try:  # drop the aborted sequences from the scheduler
             self.engine.sched.reap_cancelled()
         except Exception:

@@ -221,11 +221,14 @@ class Scheduler:
         self.waiting.appendleft(v)
         return True
 
-    def schedule(self):
+    def schedule(self, budget: int | None = None):
         """Returns ("prefill", [(seq, start, end)]), ("mixed", prefill items then
-        one-token decode items), ("decode", [(seq, pos, pos+1)]) or (None, [])."""
+        one-token decode items), ("decode", [(seq, pos, pos+1)]) or (None, []).
+        ``budget``: this step's prefill token budget (default max_num_batched_tokens; the serving loop
+        passes a smaller one while interactive arrivals queue, so one step never carries a burst's worth
+        of prompts and the first of them reach their first token sooner)."""
         with self.lock:
-            budget = self.max_num_batched_tokens
+            budget = min(budget or self.max_num_batched_tokens, self.max_num_batched_tokens)
             items = []
             # continue partially prefilled running sequences (the ones whose prompt is done drop out here)
             if self.prefilling:

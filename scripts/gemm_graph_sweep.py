@@ -58,6 +58,10 @@ def main():
     ap.add_argument("--Ms", default="64,128,176,256")
     ap.add_argument("--shapes", default="qkv,o,gate_up,down")
     ap.add_argument("--reps", type=int, default=40)
+    ap.add_argument("--packed", type=int, default=0,
+                    help="1: also the decode kernel on the unit-packed weight layout (ops/gemm.py DecPacked) vs the "
+                         "natural [N, K] layout, same plan (dec_plan, or --plan)")
+    ap.add_argument("--plan", default="", help="mt,nwv,ntw,ksplit[,gs] for the packed A/B (default dec_plan)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     enable_tuned_gemms()
@@ -76,13 +80,24 @@ def main():
                 else:
                     arms["linear"] = lambda w: linear(x, w)
                     arms["deferred"] = lambda w: linear_deferred(x, w)
-                r = {"kernel": "mlp_gate_up" if silu else kernel_for(M, N, K)}
+                plan = tuple(int(v) for v in a.plan.replace(":", ",").split(",")) if a.plan else G.dec_plan(M, N, K, silu)
+                if a.packed and plan is not None:
+                    pks = [G.DecPacked(w, silu) for w in ws]
+                    G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, plan[3])))
+                    epi = G.EPI_SILU if silu else G.EPI_STORE
+                    arms["dec_natural"] = lambda w, plan=plan, epi=epi: G.gemm_decode(x, w, epi=epi, plan=plan)
+                    pk_of = {id(w): p for w, p in zip(ws, pks)}
+                    arms["dec_packed"] = lambda w, plan=plan, epi=epi: G.gemm_decode(x, w, epi=epi, plan=plan,
+                                                                                     packed=pk_of[id(w)])
+                r = {"kernel": "mlp_gate_up" if silu else kernel_for(M, N, K), "plan": plan}
                 gb = N * K * 2 / 1e9
                 for k, fn in arms.items():
                     us = graph_time(fn, ws, a.reps)
                     r[k] = {"us": round(us, 2), "TB_s": round(gb / (us * 1e-6) / 1e3, 3)}
                 out[f"{name}_M{M}"] = r
                 print(name, M, json.dumps(r), flush=True)
+                if a.packed and plan is not None:
+                    del pks, pk_of
             del ws
             torch.cuda.empty_cache()
     if a.out:

@@ -30,7 +30,8 @@ def test_bench_single_process_cpu():
     assert res["n_gpus"] == 1 and res["steps"] == 2 and res["warmup"] == 1
     assert res["metric"].startswith("RAG queries/sec") and res["value"] > 0 and res["higher_is_better"]
     assert res["scaling"] == "weak" and res["config"]["global_batch"] == 3
-    assert res["ingest_docs_per_s"] > 0 and res["p50_ttft_ms"] > 0
+    assert res["ingest_docs_per_s"] > 0 and res["p50_ttft_ms"] > 0 and res["p90_ttft_ms"] >= res["p50_ttft_ms"]
+    assert res["headline_loop"].startswith("serving loop") and res["harness_loop"]["value"] > 0
     ref = res["ingest_ref_cap"]  # the one-cap-for-every-call ingest pass (2048 by default)
     assert res["ingest_docs_per_s_ref_cap"] > 0 and ref["token_cap"] == 48 and ref["files"] == 3
 
@@ -74,7 +75,9 @@ def test_bench_self_launch_two_ranks():
         env.pop(k, None)
     res = _run([sys.executable, "bench.py", "--gpus", "2", *TINY], env)
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 6 and res["config"]["parallelism"] == "dp2"
-    assert res["value"] > 0 and "ttft_admission_policy" in res
+    assert res["value"] > 0 and "ttft_admission_policy" in res["harness_loop"]
+    # the headline comes from the serving loop (per-query arrivals, lockstep retrieval rounds over 2 ranks)
+    assert res["headline_loop"].startswith("serving loop") and res["serving_runner"]["value"] == res["value"]
 
 
 def test_bench_self_launch_eight_ranks():
@@ -89,9 +92,13 @@ def test_bench_self_launch_eight_ranks():
     args = list(TINY)
     args[args.index("--agent-jobs") + 1] = "4"  # per GPU: 32 jobs over the 8 replicas
     args[args.index("--ingest-files") + 1] = "2"
-    res = _run([sys.executable, "bench.py", "--gpus", "8", *args, "--serving-steps", "0"], env)
+    res = _run([sys.executable, "bench.py", "--gpus", "8", *args], env)  # exactly the driver's form
     assert res["n_gpus"] == 8 and res["config"]["parallelism"] == "dp8" and res["config"]["global_batch"] == 24
     assert res["value"] > 0 and res["ingest_docs_per_s"] > 0
+    # serving loop over 8 ranks: per-query arrivals, lockstep retrieval rounds, open loops at 50 / 90 %
+    srv = res["serving_runner"]
+    assert res["headline_loop"].startswith("serving loop") and srv["value"] == res["value"]
+    assert [o["load"] for o in srv["open_loop"]] == [0.5, 0.9] and res["p50_ttft_ms"] > 0
     ae = res["agent_e2e"]
     assert ae["front_door"] == "front door + 8 sharded replicas" and ae["errors"] == 0 and ae["jobs"] == 32
     assert ae["degraded_jobs"] == 0
