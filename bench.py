@@ -159,6 +159,9 @@ def parse():
                     help="1: the reference's own regime (vLLM --max-num-seqs 4 --max-model-len 11712): single-prompt "
                          "TTFT at 1K / 4K / 11.6K tokens, decode TPOT at 1 / 4 / 16 live sequences x those contexts "
                          "(engine/probe.py), and agent jobs at concurrency 1 and 4: low_load in the JSON")
+    ap.add_argument("--recall-queries", type=int, default=64,
+                    help="queries per rank for recall@top-k of the IVF search vs an exact scan of every shard "
+                         "(index_recall; 0: skip)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     if args.preset:
@@ -555,6 +558,21 @@ def main():
         for r in rids:
             eng.pop(r)
     log(f"harness loop: {qps:.3f} queries/s, p50 TTFT {p50:.1f} ms, {ms_step:.1f} ms/step")
+
+    # ---- index quality next to index speed: recall@k of the filtered IVF search (the timed loop's nprobe and
+    # its neighbours) against an exact scan of every shard, on fresh queries (all ranks: the search is collective)
+    recall = None
+    if args.recall_queries > 0 and args.index_kind == "ivf":
+        qs = [synthetic.question(77_000_000 + dp_rank * 10_000 + i) for i in range(args.recall_queries)]
+        with side_stream(dev):
+            qv = emb.embed_queries(qs)
+            npbs = sorted({max(1, args.nprobe // 2), args.nprobe, 2 * args.nprobe, 4 * args.nprobe})
+            recall = index.recall(qv, args.top_k, {"namespace": corpus.namespace}, nprobes=npbs)
+        at = {r["nprobe"]: r["recall_at_k"] for r in recall["by_nprobe"]}
+        recall["recall_at_10" if args.top_k == 10 else f"recall_at_{args.top_k}"] = at.get(args.nprobe)
+        log(f"recall@{args.top_k} vs exact scan ({args.recall_queries} queries/rank): "
+            + ", ".join(f"nprobe {r['nprobe']}: {r['recall_at_k']} ({r['search_ms']} ms)" for r in recall["by_nprobe"])
+            + f"; exact scan {recall['exact_scan_ms']} ms")
     eng_stats = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()}
 
     # ---- the same workload through the serving loop (reported next to the harness numbers)
@@ -723,6 +741,8 @@ def main():
             "agent_saturation": None if agent_res is None else agent_res.get("agent_saturation"),
             "agent_e2e": agent_res,
             "low_load": low_load,
+            "index_recall": recall,
+            "recall_at_10": None if recall is None else recall.get("recall_at_10"),
         }
         line = json.dumps(res)
         print(line, flush=True)

@@ -125,6 +125,7 @@ struct DArgs {
   int units, gs, ksplit, kt_split;  // wave units per K-range, workgroups per K-range
   int msplit;                       // row blocks of 16*MT (adjacent on one XCD: the W lines are shared in L2)
   int packed;                       // W in the unit-packed layout (grag_gemm_decode doc)
+  unsigned long long* stamps;       // diagnostics (grag_gemm_decode_stamps): per workgroup {start, end, xcc} or null
 };
 
 // NTW 16-row n-tiles per wave (32 or 64 W rows): the A fragment read from LDS feeds NTW MFMAs, so NTW = 4
@@ -145,6 +146,7 @@ void gemm_dec_kernel(DArgs p) {
   const int L = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = L & 15, h4 = L >> 4;
+  const unsigned long long t_start = p.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int split = b % p.ksplit;
   const int mb = (b / p.ksplit) % p.msplit, g = b / (p.ksplit * p.msplit);
@@ -269,6 +271,15 @@ void gemm_dec_kernel(DArgs p) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-reads land before the workgroup retires
+  if (p.stamps && tid == 0) {  // diagnostics: 100 MHz constant clock (comparable across CUs / XCDs), main loop end
+    unsigned long long* st = p.stamps + 4 * (size_t)blockIdx.x;
+    st[0] = t_start;
+    st[1] = __builtin_amdgcn_s_memrealtime();
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    st[2] = xcc;
+    st[3] = (unsigned long long)b;
+  }
 
   // ---- epilogue: acc[mt][nt][r] = D[W row (wr[nt] + 4 h4 + r)][A row (16 mt + li)]
   if (!active) return;
@@ -340,6 +351,13 @@ int launch_v(const DArgs& a, int epi, int act, int nwg, hipStream_t s) {
 // depth kDepth): (nwv 4, ntw 2): mt 4, 8, 16;  (nwv 5, ntw 2): mt 4, 8, 12 (balanced grids; mt 16 needs
 // more than the 256 registers a wave gets at two waves per SIMD);  (nwv 8, ntw 2): mt 12.  ntw = 4 measured no faster than 2 at M = 192 (profiles/gemm_decode_ab_v3.jsonl) and is
 // not instantiated.
+static unsigned long long* g_dec_stamps = nullptr;
+
+// Diagnostics: while set, every grag_gemm_decode launch writes per workgroup (blockIdx.x) 4 u64 words
+// {s_memrealtime at start, at the end of the main loop, XCC id, logical block} to `buf` (grid size x 32 B);
+// null turns it off.  Not for graph capture.
+GRAG_API void grag_gemm_decode_stamps(void* buf) { g_dec_stamps = (unsigned long long*)buf; }
+
 GRAG_API int grag_gemm_decode_has(int mt, int nwv, int ntw) {
   if (ntw != 2) return 0;
   if (nwv == 4) return mt == 4 || mt == 8 || mt == 16;
@@ -398,6 +416,7 @@ GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, vo
   a.gs = gs;
   a.msplit = msplit;
   a.packed = packed;
+  a.stamps = g_dec_stamps;
   a.ksplit = ksplit;
   a.kt_split = kts;
   const int nwg = gs * ksplit * msplit;

@@ -98,11 +98,44 @@ class ShardedIndex:
         self.table.add_virtual(view, X_local)
         self._finish(train_sample, iters, seed)
 
+    def recall(self, Q: torch.Tensor, k: int, flt: dict | None = None, nprobes=(None,)) -> dict:
+        """recall@k of the IVF search against the exact scan over every shard, for each nprobe in
+        ``nprobes`` (None: the index's own), with the wall time of each search (collective: every rank calls
+        it with its own queries)."""
+        import time
+
+        def timed(fn):
+            if Q.is_cuda:
+                torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = fn()
+            if Q.is_cuda:
+                torch.cuda.synchronize()
+            return out, time.perf_counter() - t0
+
+        (_, truth), t_exact = timed(lambda: self.search(Q, k, flt, exact=True))
+        truth = truth.cpu().tolist()
+        out = {"queries": Q.shape[0], "k": k, "exact_scan_ms": round(t_exact * 1000, 2), "by_nprobe": []}
+        keep = self.table.nprobe
+        try:
+            for npb in nprobes:
+                self.table.nprobe = int(npb or keep)
+                self.search(Q, k, flt)  # warm the plan for this nprobe
+                (_, got), t = timed(lambda: self.search(Q, k, flt))
+                got = got.cpu().tolist()
+                hit = sum(len({x for x in a if x >= 0} & {x for x in b if x >= 0}) for a, b in zip(got, truth))
+                tot = sum(len([x for x in b if x >= 0]) for b in truth)
+                out["by_nprobe"].append({"nprobe": self.table.nprobe, "recall_at_k": round(hit / max(1, tot), 4),
+                                         "search_ms": round(t * 1000, 2)})
+        finally:
+            self.table.nprobe = keep
+        return out
+
     @property
     def local_size(self) -> int:
         return self.table.count()
 
-    def _local(self, Q: torch.Tensor, k: int, flt: dict | None = None):
+    def _local(self, Q: torch.Tensor, k: int, flt: dict | None = None, exact: bool = False):
         """This shard's top-k for every query, with the whole filter applied the way
         ``VectorTable.search`` applies it: up to four predicates fused in the scan,
         further ones ANDed into the row bitmap, and host-side checks (unindexed
@@ -128,7 +161,13 @@ class ShardedIndex:
                 bitmap = _and_bitmap(t.live, m)
                 preds = preds[:4]
             kk = max(k, min(32, k + 8)) if checks else k
-            s, i = t._scan(Q.to(self.device, t.dtype), kk, preds, bitmap, None)
+            if exact and t.n:  # every live row of the shard (IVF: the same fused scan over all slots)
+                from ..ops.topk import score_topk
+
+                s, i = score_topk(t.vectors[: t.n], Q.to(self.device, t.dtype), kk, preds=preds, bitmap=bitmap,
+                                  row_ids=t.slot_row if t.ivf else None)
+            else:
+                s, i = t._scan(Q.to(self.device, t.dtype), kk, preds, bitmap, None)
             t._track_read()
         if checks:  # exact host checks on the over-fetched rows, then back to [nq, k]
             sl, il = s.float().cpu().tolist(), i.cpu().tolist()
@@ -148,19 +187,20 @@ class ShardedIndex:
 
     @guarded
     @torch.inference_mode()
-    def search(self, Q: torch.Tensor, k: int, flt: dict | None = None):
-        """This rank's queries Q [nq, d] -> global top-k (scores fp32, ids int64)."""
+    def search(self, Q: torch.Tensor, k: int, flt: dict | None = None, exact: bool = False):
+        """This rank's queries Q [nq, d] -> global top-k (scores fp32, ids int64).  ``exact``: every shard
+        scans all its rows (the ground truth recall is measured against) instead of the probed IVF lists."""
         g = self.group
         Q = Q.to(self.device, torch.bfloat16)
         if g.trivial:
-            return self._local(Q, k, flt)
+            return self._local(Q, k, flt, exact)
         nq = Q.shape[0]
         sizes = g.all_gather(torch.tensor([nq], dtype=torch.int64, device=self.device)).view(-1)
         qmax = int(sizes.max())
         Qp = torch.zeros(qmax, Q.shape[1], dtype=Q.dtype, device=self.device)
         Qp[:nq] = Q
         Qall = g.all_gather(Qp).view(g.size * qmax, -1)  # C4
-        s, i = self._local(Qall, k, flt)
+        s, i = self._local(Qall, k, flt, exact)
         kk = s.shape[1]
         packed = torch.empty(g.size * qmax, kk, 2, dtype=torch.int64, device=self.device)
         packed[..., 0] = i

@@ -62,6 +62,7 @@ _SIGS = {
     "grag_gemm_tile_mfma": [I],
     "grag_gemm_decode": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_decode_has": [I, I, I],
+    "grag_gemm_decode_stamps": [P],
     "grag_gemm_w4": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_w4_has": [I, I],
 }

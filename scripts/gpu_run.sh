@@ -20,6 +20,7 @@
 #   mb=WHAT          scripts/microbench.py --what WHAT (json in gpurun_out/<TAG>_mb_WHAT.json)
 #   profdec=ARGS     rocprofv3 kernel stats of one decode step (scripts/profile_decode_step.sh ARGS)  (400 s)
 #   pmcdec=ARGS      PMC passes over scripts/prof_dec.py ARGS (scripts/pmc_dec.sh; csv under gpurun_out/pmc_<TAG>_pmcN)
+#   pmcpy=SCRIPT,ARGS PMC passes over any python script (scripts/pmc_py.sh; summary: scripts/pmc_dump.py)
 #   py=SCRIPT,ARGS   python -u SCRIPT ARGS (',' separates args; log gpurun_out/<TAG>_py<i>.log)  (600 s)
 #
 # A step that exits 0 or 1 (a clean Python failure) lets the next one run; a fault, abort, segfault or
@@ -68,6 +69,7 @@ for step in "$@"; do
     prof) run 700 prof bash scripts/profile_bench.sh ;;
     profdec) run 400 profdec env TAG="${TAG}" bash scripts/profile_decode_step.sh ${val//,/ } ;;
     pmcdec) run 400 "pmcdec_$npy" env TAG="${TAG}_pmc$npy" ARGS="${val//,/ }" bash scripts/pmc_dec.sh; npy=$((npy+1)) ;;
+    pmcpy) run 600 "pmcpy_$npy" env TAG="${TAG}_pmcpy$npy" bash scripts/pmc_py.sh ${val//,/ }; npy=$((npy+1)) ;;
     py) npy=$((npy+1)); run 600 "py$npy" python -u ${val//,/ } ;;
     mb) run 400 "mb_$val" python -u scripts/microbench.py --what "$val" --out "gpurun_out/${TAG}_mb_$val.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
