@@ -159,6 +159,10 @@ def parse():
                     help="1: the reference's own regime (vLLM --max-num-seqs 4 --max-model-len 11712): single-prompt "
                          "TTFT at 1K / 4K / 11.6K tokens, decode TPOT at 1 / 4 / 16 live sequences x those contexts "
                          "(engine/probe.py), and agent jobs at concurrency 1 and 4: low_load in the JSON")
+    ap.add_argument("--concurrent-ingest", type=int, default=1,
+                    help="1: after the ingest phase, ingest the synthetic repo again on ONE engine that also serves "
+                         "open-loop query arrivals at 50 %% of the serving loop's rate (BASELINE config 4's concurrent "
+                         "ingest + query streams on one server): concurrent_ingest in the JSON")
     ap.add_argument("--recall-queries", type=int, default=64,
                     help="queries per rank for recall@top-k of the IVF search vs an exact scan of every shard "
                          "(index_recall; 0: skip)")
@@ -653,6 +657,12 @@ def main():
                           "llm_calls": st2.get("llm_calls")}
             log(f"ingest at a {args.ingest_ref_cap}-token cap on every call: {n2} docs/rank in {float(tt2.item()):.2f}s")
 
+    concurrent = None
+    if (args.concurrent_ingest and not args.no_ingest and args.ingest_files > 0 and tp == 1 and serving_res
+            and serving_res.get("open_loop")):
+        base = next((o for o in serving_res["open_loop"] if abs(o["load"] - 0.5) < 1e-6), serving_res["open_loop"][0])
+        concurrent = concurrent_phase(args, model, tok, emb, prepare, sp, u, dev, group, world, dp_rank, base, log)
+
     if rank == 0:
         # headline loop: the product's serving loop (EngineRunner, per-query arrivals) when it ran (TP = 1): its
         # closed-loop queries/s is `value`, its TTFT is the open-loop TTFT at the highest load <= 90 % of that
@@ -742,6 +752,7 @@ def main():
             "agent_e2e": agent_res,
             "low_load": low_load,
             "index_recall": recall,
+            "concurrent_ingest": concurrent,
             "recall_at_10": None if recall is None else recall.get("recall_at_10"),
         }
         line = json.dumps(res)
@@ -1022,6 +1033,96 @@ def _open_loop(runner, prepare, sp, u, pg, dev, rate: float, n: int) -> dict:
             "retrieval_batch_mean": round(statistics.mean(pump.batches), 2) if pump.batches else None,
             "p50_ttft_ms": round(1000 * tt[len(tt) // 2], 2),
             "p90_ttft_ms": round(1000 * tt[min(len(tt) - 1, int(0.9 * len(tt)))], 2)}
+
+
+def concurrent_phase(args, model, tok, emb, prepare, sp, u, dev, group, world, dp_rank, base, log) -> dict:
+    """BASELINE config 4's second half on one GPU: the ingest pipeline (bulk waves + roll-ups, the same
+    synthetic repo as the ingest phase) and open-loop query arrivals at the serving loop's ``base`` load
+    share ONE engine (one EngineRunner), as the reference's single vLLM server takes both
+    (helm/templates/qwen-deployment.yaml:32-33).  Queries are admitted ahead of ingest work (priority 2 vs the
+    roll-ups' 1 and the waves' 0) and cap the prefill per step while they arrive (interactive_prefill).
+    Reports ingest docs/s and query TTFT p50 / p90 next to the ingest-free numbers (``base``)."""
+    import dataclasses
+    import random
+    import threading
+
+    import torch
+    import torch.distributed as dist
+
+    from githubrepostorag_amd.agent.llm import EngineLLM
+    from githubrepostorag_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from githubrepostorag_amd.engine.runner import EngineRunner
+    from githubrepostorag_amd.engine.sequence import SamplingParams
+    from githubrepostorag_amd.ingest.bench_ingest import run_ingest_bench
+    from githubrepostorag_amd.parallel import comm
+
+    seqs = args.ingest_seqs + 256
+    sizes = tuple(sorted({*EngineConfig.graph_batch_sizes, *range(256, seqs + 1, 128), seqs}))
+    mml = min(8192, model.cfg.max_position)
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=seqs, max_num_batched_tokens=16384, max_model_len=mml,
+                                             use_cuda_graph=not args.no_graph and dev.type == "cuda",
+                                             seed=dp_rank, kv_cache_gb=args.ingest_kv_gb,
+                                             graph_batch_sizes=tuple(b for b in sizes if b <= seqs)))
+    q_sp = dataclasses.replace(sp, priority=2)
+    if dev.type == "cuda" and not args.no_graph:
+        t0 = time.perf_counter()
+        n = eng.warmup_graphs(max_ctx=[c for c in (2048, 4096, mml) if c <= mml], windows=(1, 2, 4, 8),
+                              params=SamplingParams(temperature=EngineLLM.INGEST["temperature"],
+                                                    top_p=EngineLLM.INGEST["top_p"]))
+        n += eng.warmup_graphs(max_ctx=[2048, 4096], windows=(1, 2, 4, 8), params=q_sp)
+        log(f"concurrent phase: {n} decode graphs captured in {time.perf_counter() - t0:.1f}s")
+    runner = EngineRunner(eng, watchdog_s=0, interactive_prefill=args.interactive_prefill)
+    pg = group if world > 1 else None
+    rate = base["offered_queries_per_s"]
+    out = {}
+    try:
+        done = threading.Event()
+
+        def ingest():
+            try:
+                out["ingest"] = run_ingest_bench(model, tok, emb, args.ingest_files, seed=dp_rank, runner=runner)
+            finally:
+                done.set()
+
+        pump = _ArrivalPump(runner, prepare, q_sp, u, pg, dev)
+        comm.barrier()
+        th = threading.Thread(target=ingest, name="bench-concurrent-ingest", daemon=True)
+        rng = random.Random(8642 + (dist.get_rank() if dist.is_available() and dist.is_initialized() else 0))
+        t0 = time.perf_counter()
+        th.start()
+        due, n = t0, 0
+        while not done.is_set():
+            due += rng.expovariate(rate)
+            dt = due - time.perf_counter()
+            if dt > 0 and done.wait(dt):
+                break
+            pump.arrive(1)
+            n += 1
+        t_ing = time.perf_counter() - t0
+        th.join()
+        tt = [pump.get()[0] for _ in range(n)]
+        pump.drain_and_stop(completed=n)
+    finally:
+        runner.shutdown()
+        del eng
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+    docs, secs, st = out["ingest"]
+    tt.sort()
+    p50 = 1000 * tt[len(tt) // 2] if tt else None
+    p90 = 1000 * tt[min(len(tt) - 1, int(0.9 * len(tt)))] if tt else None
+    res = {"ingest_docs_per_s": round(docs / secs, 3), "ingest_seconds": round(secs, 2), "files": docs,
+           "queries": n, "offered_queries_per_s": round(rate, 3), "achieved_queries_per_s": round(n / t_ing, 3),
+           "p50_ttft_ms": None if p50 is None else round(p50, 2), "p90_ttft_ms": None if p90 is None else round(p90, 2),
+           "ingest_free": {"load": base["load"], "p50_ttft_ms": base["p50_ttft_ms"], "p90_ttft_ms": base["p90_ttft_ms"]},
+           "ttft_p50_vs_ingest_free": None if p50 is None else round(p50 / base["p50_ttft_ms"], 3),
+           "engine": (st or {}).get("engine"),
+           "setup": "one LLMEngine + EngineRunner (max_model_len 8192) shared by the ingest pipeline and the "
+                    "serving loop's per-query arrivals (Poisson at the ingest-free open loop's load, until the "
+                    "ingest ends); queries at priority 2, ingest roll-ups 1, extractor waves 0"}
+    log(f"concurrent ingest + queries: ingest {res['ingest_docs_per_s']} docs/s, {n} queries at {rate:.1f}/s, TTFT "
+        f"p50 {res['p50_ttft_ms']} ms (ingest-free {base['p50_ttft_ms']} ms), p90 {res['p90_ttft_ms']} ms")
+    return res
 
 
 def _trace_summary(trace) -> dict:

@@ -33,7 +33,8 @@ log = logging.getLogger(__name__)
 def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs: int = 256,
                      max_model_len: int = 8192, use_graph: bool = True, summary_tokens: int = 128,
                      mixed_batches: bool = False, tp=None, token_cap: int | None = None,
-                     kv_cache_gb: float | None = None) -> tuple[int, float, dict]:
+                     kv_cache_gb: float | None = None, runner: EngineRunner | None = None
+                     ) -> tuple[int, float, dict]:
     """Returns (documents ingested, seconds, per-stage seconds).
 
     ``token_cap``: one generation cap for every LLM call instead of the per-call lengths above (the
@@ -42,8 +43,14 @@ def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs:
     ``tp`` (a tensor-parallel group the model is sharded over): the group's TP
     rank 0 runs the pipeline and owns the request queue; the other ranks mirror
     its engine in lockstep (engine/runner.py ``follow``) until it shuts down, and
-    report 0 documents (one ingest per TP group)."""
+    report 0 documents (one ingest per TP group).
+
+    ``runner``: run on this (already warmed) engine runner instead of an engine of its own -- ingest sharing
+    one engine with interactive serving traffic (BASELINE config 4's concurrent ingest + query streams); the
+    runner is left running."""
     dev = torch.device(getattr(model, "device", "cpu"))
+    if runner is not None:
+        return _ingest_on(runner, runner.engine, tok, emb, n_files, seed, summary_tokens, token_cap, dev)
     sizes = tuple(sorted({*EngineConfig.graph_batch_sizes, *range(256, max_num_seqs + 1, 128), max_num_seqs}))
     eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max_num_seqs, max_num_batched_tokens=16384,
                                              max_model_len=max_model_len, use_cuda_graph=use_graph, seed=seed,
@@ -68,34 +75,39 @@ def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs:
             torch.cuda.empty_cache()
         return 0, time.perf_counter() - t0, {"tp_follower": True}
     try:
-        llm = EngineLLM(runner, tok, max_tokens=token_cap or summary_tokens, mode="ingest", timeout_s=3600.0,
-                        retries=0)
-        store = VectorStore(emb.dim, dev)
-        ctl = IngestController(llm=llm, store=store, embedder=emb, settings=Settings(data_dir=None),
-                               summary_tokens=summary_tokens, token_cap=token_cap)
-        _, files = synthetic_repo(seed, n_files, f"bench-repo-{seed}")
-        docs = [Document(f["text"], {"file_path": f["file_path"], "file_name": f["file_path"].split("/")[-1]})
-                for f in files]
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
-        eng.trace = []  # per-step timeline for the critical-path summary below
-        t0 = time.perf_counter()
-        res = ctl.ingest_component(repo=f"bench-repo-{seed}", namespace="bench", documents=docs, force=True)
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        st = dict(res["stage_seconds"])
-        st["engine"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()
-                        if isinstance(v, (int, float))}
-        st["llm_calls"] = ctl.extractors.wave.calls + ctl.hier.wave.calls + ctl.hier.extract.wave.calls
-        st["timeline"] = critical_path(eng.trace, t0, dt)
-        eng.trace = None
-        return res["documents"], dt, st
+        return _ingest_on(runner, eng, tok, emb, n_files, seed, summary_tokens, token_cap, dev)
     finally:
         runner.shutdown()
         del eng
         if dev.type == "cuda":
             torch.cuda.empty_cache()
+
+
+def _ingest_on(runner, eng, tok, emb, n_files, seed, summary_tokens, token_cap, dev):
+    """The timed ingest_component pass over a synthetic repo, on ``runner``'s engine."""
+    llm = EngineLLM(runner, tok, max_tokens=token_cap or summary_tokens, mode="ingest", timeout_s=3600.0,
+                    retries=0)
+    store = VectorStore(emb.dim, dev)
+    ctl = IngestController(llm=llm, store=store, embedder=emb, settings=Settings(data_dir=None),
+                           summary_tokens=summary_tokens, token_cap=token_cap)
+    _, files = synthetic_repo(seed, n_files, f"bench-repo-{seed}")
+    docs = [Document(f["text"], {"file_path": f["file_path"], "file_name": f["file_path"].split("/")[-1]})
+            for f in files]
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    eng.trace = []  # per-step timeline for the critical-path summary below
+    t0 = time.perf_counter()
+    res = ctl.ingest_component(repo=f"bench-repo-{seed}", namespace="bench", documents=docs, force=True)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = dict(res["stage_seconds"])
+    st["engine"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()
+                    if isinstance(v, (int, float))}
+    st["llm_calls"] = ctl.extractors.wave.calls + ctl.hier.wave.calls + ctl.hier.extract.wave.calls
+    st["timeline"] = critical_path(eng.trace, t0, dt)
+    eng.trace = None
+    return res["documents"], dt, st
 
 
 def critical_path(trace: list, t0: float, total: float, bucket: float = 1.0) -> dict:
