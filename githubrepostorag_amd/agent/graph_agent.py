@@ -128,12 +128,16 @@ class GraphAgent:
         self.embed_fn = embed_fn
 
     # ------------------------------------------------------------------ helpers
-    def _complete(self, prompt: str, ctx: RunContext, purpose: str = "llm", **kw) -> str:
+    # The nodes are generators: every LLM call yields ("llm", prompt, kwargs) and every index search yields
+    # ("search", scope, query, filters); a driver answers them -- ``run`` on the calling thread (blocking
+    # calls, the worker's thread-per-job mode), ``arun`` on an asyncio loop (awaited engine futures, searches
+    # on a small executor: thousands of concurrent jobs without a thread each).  One copy of the node logic.
+    def _complete(self, prompt: str, ctx: RunContext, purpose: str = "llm", **kw):
         ctx.check()
         if ctx.cancel_check is not None:
             kw["cancel_check"] = ctx.cancel_check
         with ctx.trace.span("llm", purpose=purpose) as sp:
-            r = self.llm.complete(prompt, **kw)
+            r = yield ("llm", prompt, kw)
             for k in ("ttft_s", "tokens", "error"):
                 v = getattr(r, k, None)
                 if v is not None:
@@ -141,9 +145,13 @@ class GraphAgent:
         return r.text
 
     def _expand(self, question: str, info: dict, ctx: RunContext) -> list[str]:
+        """Query expansion on the calling thread (the generator form is _expand_g)."""
+        return self._drive_sync(self._expand_g(question, info, ctx))
+
+    def _expand_g(self, question: str, info: dict, ctx: RunContext):
         try:
-            resp = self._complete(prompts.expand_query(question, info.get("repo"), info.get("scope")), ctx,
-                                  "expand").strip()
+            resp = (yield from self._complete(prompts.expand_query(question, info.get("repo"), info.get("scope")),
+                                              ctx, "expand")).strip()
             s, e = resp.find("["), resp.rfind("]") + 1
             if s >= 0 and e > s:
                 qs = json.loads(resp[s:e])
@@ -164,10 +172,10 @@ class GraphAgent:
             fb += ["application settings", "environment configuration", "setup parameters"]
         return fb[:3] if fb else [question]
 
-    def _search(self, scope: str, q: str, filters: dict, ctx: RunContext | None = None) -> list:
+    def _search(self, scope: str, q: str, filters: dict, ctx: RunContext | None = None):
         tr = ctx.trace if ctx is not None else NULL_TRACE
         with tr.span("search", scope=scope) as sp:
-            docs = self.retrievers[scope].invoke(q, filter=filters) or []
+            docs = (yield ("search", scope, q, filters)) or []
             sp["hits"] = len(docs)
         return docs
 
@@ -181,7 +189,7 @@ class GraphAgent:
         if rh:
             filters["repo"] = rh
         try:
-            data = _json_object(self._complete(prompts.plan_scope(q), ctx, "plan").strip())
+            data = _json_object((yield from self._complete(prompts.plan_scope(q), ctx, "plan")).strip())
             scope = data.get("scope") or ("code" if looks_codey(q) else "project")
             _merge_filters(filters, data.get("filters"))
             if st.get("repo"):  # an explicit repo_name pins the filter
@@ -210,17 +218,17 @@ class GraphAgent:
         if st.get("repo") and filters.get("repo") != st["repo"]:  # judge suggestions cannot unpin it
             filters = {**filters, "repo": st["repo"]}
         attempt = st.get("attempt", 0)
-        docs = self._search(scope, q, filters, ctx)
+        docs = yield from self._search(scope, q, filters, ctx)
         n0 = len(docs)
         if len(docs) < 3 or attempt > 0:
-            expanded = self._expand(q, {"repo": filters.get("repo"), "scope": scope}, ctx)
+            expanded = yield from self._expand_g(q, {"repo": filters.get("repo"), "scope": scope}, ctx)
             all_docs = list(docs)
             seen = {hash(_content(d)) for d in docs}
             for eq in expanded:
                 if len(all_docs) >= self.router_top_k:
                     break
                 try:
-                    for d in self._search(scope, eq, filters, ctx):
+                    for d in (yield from self._search(scope, eq, filters, ctx)):
                         if len(all_docs) >= self.router_top_k:
                             break
                         h = hash(_content(d))
@@ -258,7 +266,7 @@ class GraphAgent:
                          for it in inv):
             quality = "semantically_relevant"
         try:
-            data = _json_object(self._complete(prompts.judge(q, quality, inv), ctx, "judge").strip())
+            data = _json_object((yield from self._complete(prompts.judge(q, quality, inv), ctx, "judge")).strip())
         except Cancelled:
             raise
         except Exception as e:
@@ -302,7 +310,7 @@ class GraphAgent:
         if attempt == 1:
             ctx_s = " ".join(filters[k] for k in ("repo", "module") if k in filters)
             try:
-                sharp = self._complete(prompts.rewrite(base, ctx_s), ctx, "rewrite").strip().strip("\"'").strip()
+                sharp = (yield from self._complete(prompts.rewrite(base, ctx_s), ctx, "rewrite")).strip().strip("\"'").strip()
                 if not sharp or len(sharp) < 10:
                     raise ValueError("rewrite too short")
             except Cancelled:
@@ -311,7 +319,7 @@ class GraphAgent:
                 log.warning("rewrite failed: %s", e)
                 sharp = " ".join([base] + ([f"in {ctx_s}"] if ctx_s else []))
         else:
-            exp = self._expand(base, {"repo": filters.get("repo"), "scope": st.get("scope")}, ctx)
+            exp = yield from self._expand_g(base, {"repo": filters.get("repo"), "scope": st.get("scope")}, ctx)
             sharp = exp[0] if exp else base
         ctx.turns.append({"stage": "rewrite", "attempt": attempt + 1, "query": sharp, "filters": dict(filters)})
         ctx.notify({"stage": "rewrite", "action": "retry", "attempt": attempt + 1, "query": sharp,
@@ -336,12 +344,12 @@ class GraphAgent:
             kw = {"on_token": ctx.on_answer_token} if ctx.on_answer_token else {}
             if self.synth_max_tokens:
                 kw["max_tokens"] = self.synth_max_tokens
-            text = self._complete(prompts.synthesize(system, q, blocks), ctx, "synthesize", **kw)
+            text = yield from self._complete(prompts.synthesize(system, q, blocks), ctx, "synthesize", **kw)
             if has_content and len(docs) >= 3 and any(p in text.lower() for p in _CONSERVATIVE):
                 try:
-                    retry = self._complete(prompts.synthesize(prompts.SYNTH_RETRY, q, blocks), ctx,
-                                           "synthesize_retry",
-                                           **({"max_tokens": self.synth_max_tokens} if self.synth_max_tokens else {}))
+                    retry = yield from self._complete(
+                        prompts.synthesize(prompts.SYNTH_RETRY, q, blocks), ctx, "synthesize_retry",
+                        **({"max_tokens": self.synth_max_tokens} if self.synth_max_tokens else {}))
                     if not any(p in retry.lower() for p in _CONSERVATIVE[:3]):
                         text = retry
                 except Cancelled:
@@ -363,6 +371,52 @@ class GraphAgent:
         return {**st, "answer": text, "sources": sources, "debug": debug}
 
     # ------------------------------------------------------------------ run
+    def _run_g(self, question: str, ctx: RunContext, namespace: str | None, force_level: str | None,
+               repo: str | None, top_k: int | None):
+        tr = ctx.trace
+        st: dict = {"query": question, "force_level": force_level, "repo": repo, "top_k": top_k}
+        ns = namespace or self.namespace
+        if ns:
+            st["filters"] = {"namespace": ns}
+        with tr.span("plan"):
+            st = yield from self.plan_scope(st, ctx)
+        while True:
+            attempt = st.get("attempt", 0)
+            with tr.span("retrieve", attempt=attempt, scope=st.get("scope")):
+                st = yield from self.retrieve(st, ctx)
+            with tr.span("judge", attempt=attempt):
+                st = yield from self.judge(st, ctx)
+            with tr.span("rewrite", attempt=attempt):
+                st = yield from self.rewrite_or_end(st, ctx)
+            if not st.get("needs_more"):
+                break
+        with tr.span("synthesize"):
+            st = yield from self.synthesize(st, ctx)
+        debug = dict(st.get("debug") or {})
+        debug["turns"] = ctx.turns
+        return {"answer": st.get("answer", ""), "sources": st.get("sources", []), "debug": debug,
+                "scope": st.get("scope", "")}
+
+    def _invoke(self, scope: str, q: str, filters: dict) -> list:
+        return self.retrievers[scope].invoke(q, filter=filters)
+
+    def _drive_sync(self, gen):
+        """Answer a node generator's requests on this thread (blocking LLM calls and searches)."""
+        val, exc = None, None
+        while True:
+            try:
+                req = gen.throw(exc) if exc is not None else gen.send(val)
+            except StopIteration as stop:
+                return stop.value
+            val, exc = None, None
+            try:
+                if req[0] == "llm":
+                    val = self.llm.complete(req[1], **req[2])
+                else:
+                    val = self._invoke(*req[1:])
+            except BaseException as e:  # raised at the node's yield, where its own handlers see it
+                exc = e
+
     def run(self, question: str, *, namespace: str | None = None, progress_cb=None, cancel_check=None,
             force_level: str | None = None, on_answer_token=None, trace=None, repo: str | None = None,
             top_k: int | None = None) -> dict:
@@ -371,29 +425,53 @@ class GraphAgent:
         (rag_shared/models.py:6-14): here ``repo`` pins the repo
         filter of every retrieval and ``top_k`` caps the retrieved documents."""
         ctx = RunContext(progress_cb, cancel_check, on_answer_token, trace=trace or NULL_TRACE)
-        tr = ctx.trace
-        st: dict = {"query": question, "force_level": force_level, "repo": repo, "top_k": top_k}
-        ns = namespace or self.namespace
-        if ns:
-            st["filters"] = {"namespace": ns}
-        with tr.span("plan"):
-            st = self.plan_scope(st, ctx)
+        return self._drive_sync(self._run_g(question, ctx, namespace, force_level, repo, top_k))
+
+    async def arun(self, question: str, *, namespace: str | None = None, progress_cb=None, cancel_check=None,
+                   force_level: str | None = None, on_answer_token=None, trace=None, repo: str | None = None,
+                   top_k: int | None = None, search_executor=None, health: dict | None = None) -> dict:
+        """``run`` on an asyncio loop: LLM calls are awaited (``llm.acomplete``: an engine future, no thread
+        held while the request waits for its tokens; an LLM without it runs ``complete`` on the executor),
+        searches run on ``search_executor`` (they block on the GPU) and their shard-round health is
+        accumulated into ``health`` (index/sharded_store.round_health per search)."""
+        import asyncio
+
+        from ..index.sharded_store import round_health
+
+        loop = asyncio.get_running_loop()
+        ctx = RunContext(progress_cb, cancel_check, on_answer_token, trace=trace or NULL_TRACE)
+        acomplete = getattr(self.llm, "acomplete", None)
+
+        def search(scope, q, filters):
+            with round_health() as rec:
+                docs = self._invoke(scope, q, filters)
+            return docs, rec
+
+        gen = self._run_g(question, ctx, namespace, force_level, repo, top_k)
+        val, exc = None, None
         while True:
-            attempt = st.get("attempt", 0)
-            with tr.span("retrieve", attempt=attempt, scope=st.get("scope")):
-                st = self.retrieve(st, ctx)
-            with tr.span("judge", attempt=attempt):
-                st = self.judge(st, ctx)
-            with tr.span("rewrite", attempt=attempt):
-                st = self.rewrite_or_end(st, ctx)
-            if not st.get("needs_more"):
-                break
-        with tr.span("synthesize"):
-            st = self.synthesize(st, ctx)
-        debug = dict(st.get("debug") or {})
-        debug["turns"] = ctx.turns
-        return {"answer": st.get("answer", ""), "sources": st.get("sources", []), "debug": debug,
-                "scope": st.get("scope", "")}
+            try:
+                req = gen.throw(exc) if exc is not None else gen.send(val)
+            except StopIteration as stop:
+                return stop.value
+            val, exc = None, None
+            try:
+                if req[0] == "llm":
+                    if acomplete is not None:
+                        val = await acomplete(req[1], **req[2])
+                    else:
+                        val = await loop.run_in_executor(search_executor, lambda r=req: self.llm.complete(r[1], **r[2]))
+                else:
+                    val, rec = await loop.run_in_executor(search_executor, search, *req[1:])
+                    if health is not None:
+                        health["rounds"] += rec["rounds"]
+                        health["degraded_rounds"] += rec["degraded_rounds"]
+                        health["missing_shards"].update(rec["missing_shards"])
+            except asyncio.CancelledError:
+                gen.close()
+                raise
+            except BaseException as e:
+                exc = e
 
 
 _lock = threading.Lock()

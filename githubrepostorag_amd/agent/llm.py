@@ -213,6 +213,61 @@ class EngineLLM:
                 time.sleep(0.05 * (attempt + 1))
         return CompletionResponse(f"Error: {err}", True)
 
+    CANCEL_POLL_S = 0.25  # acomplete: how often a waiting call checks its job's cancel flag
+
+    async def acomplete(self, prompt: str, on_token: Callable[[str], None] | None = None,
+                        **kw) -> CompletionResponse:
+        """``complete`` for a coroutine: the request is submitted to the engine runner and its completion
+        awaited as a future (set from the engine / streamer thread), so a waiting call holds no thread."""
+        import asyncio
+
+        loop = asyncio.get_running_loop()
+        text = self.tok.apply_chat_template(self._messages(prompt), True,
+                                            None if self.allow_thinking else False)
+        sp = self.params(**kw)
+        ids = self.fit(self.tok.encode(text), sp.max_tokens)
+        cancel_check = kw.get("cancel_check")
+        err = None
+
+        def _resolve(fut, h):
+            if not fut.done():
+                fut.set_result(h)
+
+        for attempt in range(self.retries + 1):
+            h = None
+            try:
+                fut = loop.create_future()
+                h = self.runner.submit(ids, sp, on_token=on_token, interactive=self.mode != "ingest")
+                h.add_done_callback(lambda hh, fut=fut: loop.call_soon_threadsafe(_resolve, fut, hh))
+                t_end = loop.time() + self.timeout_s
+                while not fut.done():
+                    wait = max(0.0, t_end - loop.time())
+                    if cancel_check is not None:
+                        wait = min(wait, self.CANCEL_POLL_S)
+                    await asyncio.wait({fut}, timeout=wait)
+                    if fut.done():
+                        break
+                    if (cancel_check is not None and cancel_check()) or loop.time() >= t_end:
+                        h.cancel()
+                        if cancel_check is not None and cancel_check():
+                            from .graph_agent import Cancelled
+
+                            raise Cancelled()
+                        raise TimeoutError("generation timed out")
+                c = h.wait(0)
+                return CompletionResponse(self._post(prompt, c.text), False, c.ttft_s, len(c.token_ids))
+            except asyncio.CancelledError:
+                if h is not None:
+                    h.cancel()
+                raise
+            except Exception as e:  # bounded retry, then the reference's "errors become content"
+                if type(e).__name__ == "Cancelled":
+                    raise
+                err = e
+                log.warning("LLM call failed (attempt %d): %s", attempt + 1, e)
+                await asyncio.sleep(0.05 * (attempt + 1))
+        return CompletionResponse(f"Error: {err}", True)
+
     def stream_complete(self, prompt: str, **kw):
         yield self.complete(prompt, **kw)
 
@@ -260,6 +315,22 @@ class HTTPLLM:
 class MeteredLLM:
     def __init__(self, base):
         self._base = base
+        if hasattr(base, "acomplete"):
+            self.acomplete = self._acomplete
+
+    async def _acomplete(self, prompt: str, **kw) -> CompletionResponse:
+        from ..service import metrics as M
+
+        t0 = time.perf_counter()
+        try:
+            out = await self._base.acomplete(prompt, **kw)
+        except Exception:
+            M.WORKER_LLM_DURATION.observe(time.perf_counter() - t0)
+            M.WORKER_LLM_CALLS_TOTAL.labels(result="error").inc()
+            raise
+        M.WORKER_LLM_DURATION.observe(time.perf_counter() - t0)
+        M.WORKER_LLM_CALLS_TOTAL.labels(result="error" if getattr(out, "error", False) else "ok").inc()
+        return out
 
     def complete(self, prompt: str, **kw) -> CompletionResponse:
         from ..service import metrics as M

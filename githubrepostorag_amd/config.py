@@ -99,6 +99,10 @@ class Settings:
     llm_timeout_s: float = field(default_factory=lambda: _float("LLM_TIMEOUT", 60.0))  # remote (HTTP) LLM calls
     llm_retries: int = field(default_factory=lambda: _int("LLM_RETRIES", 1))
     stream_tokens: bool = field(default_factory=lambda: _bool("STREAM_TOKENS", True))
+    # the agent runs as a coroutine on the worker's event loop (LLM calls await engine futures; searches on a
+    # small executor) instead of one thread per running job (AGENT_ASYNC=0: the thread-per-job mode)
+    agent_async: bool = field(default_factory=lambda: _bool("AGENT_ASYNC", True))
+    search_threads: int = field(default_factory=lambda: _int("SEARCH_THREADS", 16))
     # coalesce concurrent jobs' query embeddings into one encoder pass (0 disables)
     embed_batch_window_ms: float = field(default_factory=lambda: _float("EMBED_BATCH_WINDOW_MS", 1.0))
     # POST /ingest is off by default; `local` sources must resolve under INGEST_ROOT

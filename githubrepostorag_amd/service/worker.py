@@ -6,9 +6,12 @@ event sequence per job:
   started -> [final{cancelled}] -> iteration -> turn* -> [token*] -> retrieval
   -> final{answer, sources}        (or error{message} -> final{error:true})
 
-The agent runs in a thread-pool executor (it blocks on GPU generations);
-its progress callback is bound per job (no shared singleton state) and
-publishes thread-safely into the job's replayable event log.  Cancellation
+The agent runs as a coroutine on the worker's event loop (``GraphAgent.arun``:
+its LLM calls await engine futures, its index searches run on a small shared
+executor), so a running job holds no thread and thousands can wait on the
+engine at once; ``AGENT_ASYNC=0`` keeps the thread-per-job mode.  Its progress
+callback is bound per job (no shared singleton state) and publishes into the
+job's replayable event log.  Cancellation
 is checked before every agent node and aborts the job's in-flight LLM
 requests (the reference checked once, before any work).
 """
@@ -111,12 +114,19 @@ class JobQueue:
 
 class RAGWorker:
     def __init__(self, runtime, events: EventLog, flags: CancelFlags, max_jobs: int = 10,
-                 job_timeout: float = 300.0, keep_result: float = 3600.0, stream_tokens: bool = True):
+                 job_timeout: float = 300.0, keep_result: float = 3600.0, stream_tokens: bool = True,
+                 agent_async: bool | None = None):
         self.runtime = runtime
         self.events = events
         self.flags = flags
         self.stream_tokens = stream_tokens
-        self.executor = concurrent.futures.ThreadPoolExecutor(max_workers=max_jobs, thread_name_prefix="rag-job")
+        s = getattr(runtime, "settings", None)
+        # coroutine agent (GraphAgent.arun): a running job holds no thread; its searches share a small pool
+        self.agent_async = bool(getattr(s, "agent_async", True)) if agent_async is None else agent_async
+        n_exec = max(1, int(getattr(s, "search_threads", 16))) if self.agent_async else max_jobs
+        self.executor = concurrent.futures.ThreadPoolExecutor(max_workers=n_exec,
+                                                              thread_name_prefix="rag-search" if self.agent_async
+                                                              else "rag-job")
         self.queue = JobQueue({"run_rag_job": self.run_rag_job}, max_jobs, job_timeout, keep_result)
         self.queue.ctx["on_timeout"] = self._on_timeout
 
@@ -166,7 +176,16 @@ class RAGWorker:
                                     top_k=req.get("top_k") or None)
                 return res, health
 
-            result, health = await loop.run_in_executor(self.executor, run_agent)
+            if self.agent_async:
+                health = {"rounds": 0, "degraded_rounds": 0, "missing_shards": set()}
+                result = await agent.arun(query, namespace=namespace, progress_cb=progress,
+                                          cancel_check=lambda: self.flags.is_cancelled_sync(job_id),
+                                          force_level=forced,
+                                          on_answer_token=on_token if self.stream_tokens else None, trace=trace,
+                                          repo=req.get("repo_name") or None, top_k=req.get("top_k") or None,
+                                          search_executor=self.executor, health=health)
+            else:
+                result, health = await loop.run_in_executor(self.executor, run_agent)
             M.WORKER_RETRIEVAL_DURATION.observe(time.perf_counter() - t_rag)
             sources = result.get("sources") or []
             debug = result.get("debug") or {}

@@ -198,3 +198,45 @@ def test_helpers():
     assert clean_selector_response('{"choice": 3, "reason": "x"}') == "3"
     assert clean_selector_response("I pick 2 because") == "2"
     assert clean_selector_response("") == "1"
+
+
+def _arun(agent, q, **kw):
+    import asyncio
+    import concurrent.futures
+
+    with concurrent.futures.ThreadPoolExecutor(2) as ex:
+        return asyncio.run(agent.arun(q, search_executor=ex, **kw))
+
+
+@pytest.mark.parametrize("judge", [None, json.dumps({"coverage": 0.1, "needs_more": True, "stage_down": "file"})])
+def test_async_driver_matches_sync(judge):
+    """GraphAgent.arun (coroutine driver: LLM calls awaited or on the executor, searches on the executor)
+    walks the same nodes and returns the same result as the thread-per-job ``run``."""
+    def make():
+        return GraphAgent(ScriptedLLM(_router(judge=judge)), _retrievers(), namespace="default")
+
+    want = make().run("How does the payments service publish events?")
+    got = _arun(make(), "How does the payments service publish events?")
+    assert got["answer"] == want["answer"] and got["scope"] == want["scope"]
+    assert [t["stage"] for t in got["debug"]["turns"]] == [t["stage"] for t in want["debug"]["turns"]]
+    assert got["sources"] == want["sources"]
+
+
+def test_async_driver_llm_errors_and_cancel():
+    """Node-level fallbacks see errors raised by awaited calls (thrown back into the node generator), and a
+    cancel check stops the coroutine with Cancelled."""
+    class ALLM:  # an LLM with acomplete: the plan call fails, the rest answer
+        def __init__(self):
+            self.calls = 0
+
+        async def acomplete(self, prompt, **kw):
+            self.calls += 1
+            if prompt.startswith("Choose the best search scope"):
+                raise RuntimeError("boom")
+            return ScriptedLLM(_router()).complete(prompt, **kw)
+
+    llm = ALLM()
+    out = _arun(GraphAgent(llm, _retrievers()), "Why does this method throw a NullPointerException?")
+    assert out["scope"] == "code" and out["answer"] == "The answer is [1]." and llm.calls >= 3
+    with pytest.raises(Cancelled):
+        _arun(GraphAgent(ALLM(), _retrievers()), "q", cancel_check=lambda: True)

@@ -379,3 +379,42 @@ def test_over_long_prompt_rejected_by_engine_and_fitted_by_agent_llm(model, tok)
             assert unset.status_code == 200, unset.text
     finally:
         runner.shutdown()
+
+
+def test_engine_llm_acomplete_many_coroutines_and_cancel(model, tok):
+    """EngineLLM.acomplete: 48 concurrent coroutines share the engine through awaited futures (no thread per
+    call) and get the same text as the blocking complete(); a cancel check aborts an in-flight call."""
+    import asyncio
+
+    from githubrepostorag_amd.agent.graph_agent import Cancelled
+    from githubrepostorag_amd.agent.llm import EngineLLM
+    from githubrepostorag_amd.engine.runner import EngineRunner
+
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=16, max_model_len=512, num_blocks=512,
+                                             use_cuda_graph=False))
+    runner = EngineRunner(eng)
+    try:
+        llm = EngineLLM(runner, tok, max_tokens=6, mode="worker", timeout_s=120.0)
+        prompts = [f"question number {i} about widgets" for i in range(48)]
+        want = [llm.complete(p, temperature=0.0).text for p in prompts[:4]]
+
+        async def many():
+            return await asyncio.gather(*[llm.acomplete(p, temperature=0.0) for p in prompts])
+
+        got = asyncio.run(many())
+        assert [r.text for r in got[:4]] == want and not any(r.error for r in got)
+        llm.CANCEL_POLL_S = 0.01
+        flag = {"c": False}
+
+        async def cancelled():
+            async def flip():
+                await asyncio.sleep(0.02)
+                flag["c"] = True
+            asyncio.ensure_future(flip())
+            return await llm.acomplete("a long answer please", max_tokens=400, ignore_eos=True,
+                                       cancel_check=lambda: flag["c"])
+
+        with pytest.raises(Cancelled):
+            asyncio.run(cancelled())
+    finally:
+        runner.shutdown()
