@@ -85,10 +85,14 @@ __global__ __launch_bounds__(kThreads) void ar_oneshot_kernel(Peers peers, int r
   if (threadIdx.x < W && threadIdx.x != rank)
     st_release_sys(&peers.flags[threadIdx.x][b * kMaxRanks + rank], ep);
   if (threadIdx.x < W && threadIdx.x != rank) {
+    // bounded by WALL time, not iterations: `spin_max` = s_memrealtime ticks (100 MHz) a block waits for a
+    // peer before giving up with the error word set (an iteration count was unbounded in practice: a system-
+    // scope acquire load per iteration on an oversubscribed device made 1 << 24 iterations minutes long)
     const unsigned* f = &peers.flags[rank][b * kMaxRanks + threadIdx.x];
-    long it = 0;
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime() + (unsigned long long)spin_max;
+    unsigned it = 0;
     while (ld_acquire_sys(f) < ep) {
-      if (++it > spin_max) {
+      if ((++it & 63u) == 0 && __builtin_amdgcn_s_memrealtime() > t_end) {
         atomicOr(err, 1u);
         s_fail = 1;
         break;

@@ -632,7 +632,8 @@ class LLMEngine:
         n = len(seqs)
         # under TP the graphs hold the decode's collectives (one-shot IPC all-reduce, RCCL logits gather);
         # replicated scheduling makes every TP rank pick, capture and replay the same graph in lockstep
-        use_graph = self.on_gpu and self.cfg.use_cuda_graph and n <= max(self.cfg.graph_batch_sizes)
+        use_graph = (self.on_gpu and self.cfg.use_cuda_graph and n <= max(self.cfg.graph_batch_sizes)
+                     and getattr(self.model.tp, "capturable", True))  # gloo-staged TP collectives: eager decode
         K = self._window(seqs, max_window) if use_graph else 1
         max_ctx = max(len(s.prompt_ids) + len(s.output_ids) for s in seqs) + K - 1
         if use_graph:
@@ -786,7 +787,7 @@ class LLMEngine:
         of graphs captured.  ``max_ctx`` may be a list (one split plan per context length).  ``params``:
         capture for the sampler launch chain these sampling parameters select (top-k / top-p rounds)
         instead of the live slots' (e.g. an ingest engine warmed before its first request)."""
-        if not (self.on_gpu and self.cfg.use_cuda_graph):
+        if not (self.on_gpu and self.cfg.use_cuda_graph and getattr(self.model.tp, "capturable", True)):
             return 0
         prev = self.sampler.rounds_override
         if params is not None:

@@ -103,6 +103,12 @@ class Group:
 
     custom_ar = None  # parallel.custom_ar.IpcAllReduce: one-shot xGMI all-reduce for small messages
 
+    @property
+    def capturable(self) -> bool:
+        """Whether this group's decode-time collectives can live inside a hipGraph: RCCL or the one-shot IPC
+        kernels can; gloo (host-staged, the shared-GPU rehearsal) cannot."""
+        return self.trivial or self.custom_ar is not None or _INFO.backend == "nccl"
+
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         """C1: small bf16 messages (decode [B, hidden]) and small fp32 ones (the
         TP sampler's histograms) take the one-shot IPC all-reduce when attached;

@@ -54,16 +54,22 @@ def _alloc(nbytes: int) -> int:
     return p.value
 
 
+TIMEOUT_S = float(os.environ.get("GRAG_AR_TIMEOUT_S", "5"))  # a peer slower than this fails the exchange
+TICKS_PER_S = 100_000_000  # s_memrealtime: 100 MHz
+
+
 class IpcAllReduce:
     def __init__(self, regions: list[int], rank: int, device, slot_bytes: int, owned: list[int],
-                 opened: list[int], grid: int = 64, spin_max: int = 1 << 24):
+                 opened: list[int], grid: int = 64, timeout_s: float | None = None):
         self.regions = regions
         self.W = len(regions)
         self.rank = rank
         self.device = torch.device(device)
         self.slot_bytes = slot_bytes
         self.grid = grid
-        self.spin_max = spin_max
+        # the kernel's wait bound in s_memrealtime ticks (csrc/kernels/allreduce.hip: wall time, then the
+        # error word is set and the step raises CommError -> the TP group detaches to RCCL together)
+        self.spin_max = int((TIMEOUT_S if timeout_s is None else timeout_s) * TICKS_PER_S)
         self._owned, self._opened = owned, opened
         self._arr = (ctypes.c_void_p * self.W)(*regions)
         self.epochs = torch.zeros(grid, dtype=torch.int32, device=self.device)
@@ -198,6 +204,18 @@ def enable_for_group(group, device) -> IpcAllReduce | None:
         return None
     import torch.distributed as dist
 
+    # ranks sharing ONE device (a single-GPU rehearsal of a TP group): W spinning exchange kernels from W
+    # processes on one card depend on the hardware scheduler mapping every process's queue at once; past
+    # GRAG_CUSTOM_AR_SHARED_MAX ranks per device (default 2: the tested TP=2 rehearsal) the group stays on
+    # its process-group collectives.  One process per GPU (the 8-GPU node) is unaffected.
+    p = torch.cuda.get_device_properties(dev)
+    ident = f"{p.pci_domain_id}:{p.pci_bus_id}:{p.pci_device_id}:{p.uuid}"
+    ids = [None] * group.size
+    dist.all_gather_object(ids, ident, group=group.pg)
+    shared = max(ids.count(i) for i in ids)
+    if shared > int(os.environ.get("GRAG_CUSTOM_AR_SHARED_MAX", "2")):
+        log.warning("%d TP ranks share one device: one-shot all-reduce off (process-group collectives)", shared)
+        return None
     try:
         ar = IpcAllReduce.create(group.pg, group.rank, group.size, dev)
         g = torch.Generator(device=dev).manual_seed(1234 + group.rank)

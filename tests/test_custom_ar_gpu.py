@@ -103,6 +103,30 @@ def test_oneshot_f32_sum_and_gather_simulated_ranks(dev):
             c.close()
 
 
+def test_oneshot_lost_peer_times_out_on_wall_clock(dev):
+    """Fault injection: rank 1 never arrives.  Rank 0's kernel gives up after its WALL-clock bound (not an
+    iteration count: a system-scope acquire per spin made 1 << 24 iterations minutes long on a busy device)
+    and sets the error word, which the engine turns into CommError -> the TP group detaches to RCCL."""
+    import time
+
+    from githubrepostorag_amd.parallel.custom_ar import IpcAllReduce
+
+    comms = IpcAllReduce.simulated(2, dev, slot_bytes=1 << 20, grid=32)
+    try:
+        comms[0].spin_max = int(0.2 * 100_000_000)  # 0.2 s in s_memrealtime ticks
+        x = torch.ones(4096, dtype=torch.bfloat16, device=dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        comms[0].all_reduce(x)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        assert comms[0].failed(), "a lost peer must set the error word"
+        assert 0.15 < dt < 3.0, dt
+    finally:
+        for c in comms:
+            c.close()
+
+
 def _hip():
     return ctypes.CDLL("libamdhip64.so")
 
