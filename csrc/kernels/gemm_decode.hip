@@ -38,6 +38,8 @@
 //     SiLU(gate)*up for the gate/up weight stored interleaved in 32-row blocks
 //     (ops/gemm.py interleave_gate_up): a wave's two n-tiles are then the 16
 //     gate rows and the 16 matching up rows, so the product forms in registers.
+#include <type_traits>
+
 #include "common.h"
 
 using namespace grag;
@@ -48,6 +50,16 @@ GRAG_API int grag_splitk_reduce(const void* ws, const void* bias, void* C, int l
 namespace {
 
 enum { EPI_STORE = 0, EPI_SILU = 1, EPI_PARTIAL = 2 };
+
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): a compile-time loop (register arrays
+// indexed by its constant stay in registers)
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(static_cast<F&&>(f));
+  }
+}
 enum { ACT_NONE = 0, ACT_GELU = 1, ACT_GELU_TANH = 3 };
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
@@ -130,9 +142,15 @@ struct DArgs {
 
 // NTW 16-row n-tiles per wave (32 or 64 W rows): the A fragment read from LDS feeds NTW MFMAs, so NTW = 4
 // halves the LDS read traffic per MFMA (at NTW = 2 it equals the LDS bandwidth at full MFMA rate).
-template <int EPI, int ACT, int MT, int D, int NWV, int NTW>
+// TQ > 0 (tail split, NWV = 8): a workgroup owns 4 or 5 wave units; waves 0-3 compute one unit each over all
+// MT row tiles, and a 5th unit is shared by waves 4-7, TQ = MT / 4 row tiles each.  The CU's 4 SIMDs (two
+// waves each) then carry 1.25 units of MFMA work apiece where a 5-wave workgroup put 2 units on one SIMD
+// (profiles/pmc_dec_r5.txt: Qwen2-7B gate/up at 176 rows, 4.625 units per CU on 256 CUs; the doubled SIMD
+// paced every K-step barrier).  Waves 4-7 load the shared unit's W rows alike (L1 / L2 hits after the first).
+template <int EPI, int ACT, int MT, int D, int NWV, int NTW, int TQ = 0>
 __global__ __launch_bounds__(64 * NWV, (NWV == 4 && NTW == 2 && (D + 1) * MT * 2 <= 80) ? 2 : 1)
 void gemm_dec_kernel(DArgs p) {
+  static_assert(TQ == 0 || (NWV == 8 && TQ * 4 == MT), "tail split: 8 waves, MT = 4 TQ");
   constexpr int NST = D + 1;            // LDS stages = W register slots
   constexpr int ABYTES = MT * 16 * 128;  // one K-step of A
   constexpr int NPC = MT * 2;                  // A pieces (1 KiB = 8 rows x 128 B) per K-step
@@ -153,8 +171,17 @@ void gemm_dec_kernel(DArgs p) {
   const int m0 = mb * 16 * MT;
   const int u0 = (int)((long)g * p.units / p.gs);
   const int cnt = (int)((long)(g + 1) * p.units / p.gs) - u0;
-  const bool active = w < cnt;                    // wave-uniform
-  const int q = u0 + min(w, cnt - 1);             // this wave's unit (an idle wave repeats the last one)
+  bool active = w < cnt;                          // wave-uniform
+  int q = u0 + min(w, cnt - 1);                   // this wave's unit (an idle wave repeats the last one)
+  if constexpr (TQ > 0) {
+    if (w >= 4) {
+      active = cnt > 4;
+      q = u0 + (cnt > 4 ? 4 : min(w - 4, cnt - 1));
+    } else {
+      active = w < min(cnt, 4);
+    }
+  }
+  const bool tail_wave = TQ > 0 && w >= 4;
   const int ks = p.K >> 6;
   const int kb = split * p.kt_split;
   const int ke = min(ks, kb + p.kt_split);
@@ -223,18 +250,21 @@ void gemm_dec_kernel(DArgs p) {
   // fence between each read group and the MFMA group before it: left alone, hipcc (short of registers at two
   // waves per SIMD) reads one fragment, waits lgkmcnt(0) and issues two MFMAs, exposing the LDS latency
   // before every MFMA pair (measured: the MFMA pipe idle about half the time at M = 192).
-  constexpr int APF = MT >= 8 ? 2 : 1;
-  auto compute = [&](int slot, bf16x8_t (&wreg)[GW]) {
-    const char* As = smem + slot * ABYTES;
+  // row tiles [MB, MB + NM) of the staged A against this wave's W fragments into acc[MB .. MB + NM)
+  auto compute_n = [&](auto nm_c, auto mb_c, int slot, bf16x8_t (&wreg)[GW]) {
+    constexpr int NM = decltype(nm_c)::value;
+    constexpr int MB = decltype(mb_c)::value;
+    constexpr int APF = NM >= 8 ? 2 : 1;
+    const char* As = smem + slot * ABYTES + MB * 2048;
     bf16x8_t af[APF + 1][2];
 #pragma unroll
-    for (int j = 0; j < APF; ++j) {
+    for (int j = 0; j < APF && j < NM; ++j) {
       af[j][0] = *reinterpret_cast<const bf16x8_t*>(As + j * 2048 + aoff0);
       af[j][1] = *reinterpret_cast<const bf16x8_t*>(As + j * 2048 + aoff1);
     }
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      if (mt + APF < MT) {
+    for (int mt = 0; mt < NM; ++mt) {
+      if (mt + APF < NM) {
         af[(mt + APF) % (APF + 1)][0] = *reinterpret_cast<const bf16x8_t*>(As + (mt + APF) * 2048 + aoff0);
         af[(mt + APF) % (APF + 1)][1] = *reinterpret_cast<const bf16x8_t*>(As + (mt + APF) * 2048 + aoff1);
       }
@@ -242,10 +272,25 @@ void gemm_dec_kernel(DArgs p) {
       const bf16x8_t a0 = af[mt % (APF + 1)][0], a1 = af[mt % (APF + 1)][1];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[2 * nt], a0, acc[mt][nt], 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[2 * nt + 1], a1, acc[mt][nt], 0, 0, 0);
+        acc[MB + mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[2 * nt], a0, acc[MB + mt][nt], 0, 0, 0);
+        acc[MB + mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[2 * nt + 1], a1, acc[MB + mt][nt], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // tail split: one body per group of TQ row tiles behind a wave-uniform guard -- the own waves run all four
+  // groups, a tail wave the group of its quarter -- so every MFMA appears once in the code and the
+  // accumulator of row tile t is acc[t] in both roles (no second, register-hungry copy of the loop)
+  const int g_lo = tail_wave ? w - 4 : 0, g_hi = tail_wave ? w - 3 : 4;
+  auto compute = [&](int slot, bf16x8_t (&wreg)[GW]) {
+    if constexpr (TQ > 0) {
+      static_for<4>([&](auto gc) {
+        constexpr int G = decltype(gc)::value;
+        if (G >= g_lo && G < g_hi) compute_n(std::integral_constant<int, TQ>{}, std::integral_constant<int, G * TQ>{},
+                                             slot, wreg);
+      });
+    } else {
+      compute_n(std::integral_constant<int, MT>{}, std::integral_constant<int, 0>{}, slot, wreg);
     }
   };
 
@@ -283,59 +328,65 @@ void gemm_dec_kernel(DArgs p) {
 
   // ---- epilogue: acc[mt][nt][r] = D[W row (wr[nt] + 4 h4 + r)][A row (16 mt + li)]
   if (!active) return;
-  if constexpr (EPI == EPI_SILU) {
-    bf16* C = (bf16*)p.C;
-    constexpr int NP = NTW / 2;  // gate/up tile pairs: (nt, nt + NP)
+  // row tile mt is stored when its group is this wave's (tail split) -- every tile for the own waves
+  auto mine = [&](int mt) { return TQ == 0 || (mt >= g_lo * TQ && mt < g_hi * TQ); };
+  {
+    constexpr int NM = MT;
+    const int mr0 = m0;
+    if constexpr (EPI == EPI_SILU) {
+      bf16* C = (bf16*)p.C;
+      constexpr int NP = NTW / 2;  // gate/up tile pairs: (nt, nt + NP)
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int gr = wr[j] + 4 * h4, ur = wr[j + NP] + 4 * h4;
-      if (ur >= p.N) continue;
-      const int oc = (gr >> 6) * 32 + (gr & 31);  // gate row 64 q + c  ->  output column 32 q + c
-      float bg[4], bu[4];
+      for (int j = 0; j < NP; ++j) {
+        const int gr = wr[j] + 4 * h4, ur = wr[j + NP] + 4 * h4;
+        if (ur >= p.N) continue;
+        const int oc = (gr >> 6) * 32 + (gr & 31);  // gate row 64 q + c  ->  output column 32 q + c
+        float bg[4], bu[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        bg[r] = p.bias ? (float)p.bias[gr + r] : 0.f;
-        bu[r] = p.bias ? (float)p.bias[ur + r] : 0.f;
-      }
+        for (int r = 0; r < 4; ++r) {
+          bg[r] = p.bias ? (float)p.bias[gr + r] : 0.f;
+          bu[r] = p.bias ? (float)p.bias[ur + r] : 0.f;
+        }
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int m = m0 + mt * 16 + li;
-        if (m >= p.M) continue;
-        bf16x4_t o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bits(silu_f(acc[mt][j][r] + bg[r]) * (acc[mt][j + NP][r] + bu[r]));
-        *reinterpret_cast<bf16x4_t*>(C + (size_t)m * p.ldc + oc) = o;
-      }
-    }
-  } else {
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-      const int n = wr[nt] + 4 * h4;
-      if (n >= p.N) continue;
-      float bv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bv[r] = (EPI == EPI_STORE && p.bias) ? (float)p.bias[n + r] : 0.f;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int m = m0 + mt * 16 + li;
-        if (m >= p.M) continue;
-        if constexpr (EPI == EPI_PARTIAL) {
-          float* ws = (float*)p.C + ((size_t)split * p.M + m) * p.N + n;
-          *reinterpret_cast<f32x4_t*>(ws) = acc[mt][nt];
-        } else {
+        for (int mt = 0; mt < NM; ++mt) {
+          const int m = mr0 + mt * 16 + li;
+          if (m >= p.M || !mine(mt)) continue;
           bf16x4_t o;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = f2bits(act_f<ACT>(acc[mt][nt][r] + bv[r]));
-          *reinterpret_cast<bf16x4_t*>((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+          for (int r = 0; r < 4; ++r) o[r] = f2bits(silu_f(acc[mt][j][r] + bg[r]) * (acc[mt][j + NP][r] + bu[r]));
+          *reinterpret_cast<bf16x4_t*>(C + (size_t)m * p.ldc + oc) = o;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int n = wr[nt] + 4 * h4;
+        if (n >= p.N) continue;
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = (EPI == EPI_STORE && p.bias) ? (float)p.bias[n + r] : 0.f;
+#pragma unroll
+        for (int mt = 0; mt < NM; ++mt) {
+          const int m = mr0 + mt * 16 + li;
+          if (m >= p.M || !mine(mt)) continue;
+          if constexpr (EPI == EPI_PARTIAL) {
+            float* ws = (float*)p.C + ((size_t)split * p.M + m) * p.N + n;
+            *reinterpret_cast<f32x4_t*>(ws) = acc[mt][nt];
+          } else {
+            bf16x4_t o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = f2bits(act_f<ACT>(acc[mt][nt][r] + bv[r]));
+            *reinterpret_cast<bf16x4_t*>((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+          }
         }
       }
     }
   }
 }
 
-template <int MT, int D, int NWV, int NTW>
+template <int MT, int D, int NWV, int NTW, int TQ = 0>
 int launch_v(const DArgs& a, int epi, int act, int nwg, hipStream_t s) {
-#define GO(E, AC) gemm_dec_kernel<E, AC, MT, D, NWV, NTW><<<nwg, 64 * NWV, 0, s>>>(a)
+#define GO(E, AC) gemm_dec_kernel<E, AC, MT, D, NWV, NTW, TQ><<<nwg, 64 * NWV, 0, s>>>(a)
   if (epi == EPI_PARTIAL) GO(EPI_PARTIAL, ACT_NONE);
   else if (epi == EPI_SILU) GO(EPI_SILU, ACT_NONE);
   else if (act == ACT_GELU) GO(EPI_STORE, ACT_GELU);
@@ -358,13 +409,17 @@ static unsigned long long* g_dec_stamps = nullptr;
 // null turns it off.  Not for graph capture.
 GRAG_API void grag_gemm_decode_stamps(void* buf) { g_dec_stamps = (unsigned long long*)buf; }
 
-GRAG_API int grag_gemm_decode_has(int mt, int nwv, int ntw) {
+// tail = 1: the 8-wave tail split (gemm_dec_kernel TQ = mt / 4): at most 5 wave units per workgroup
+GRAG_API int grag_gemm_decode_has_t(int mt, int nwv, int ntw, int tail) {
+  if (tail) return ntw == 2 && nwv == 8 && (mt == 4 || mt == 8 || mt == 12 || mt == 16);
   if (ntw != 2) return 0;
   if (nwv == 4) return mt == 4 || mt == 8 || mt == 16;
   if (nwv == 5) return mt == 4 || mt == 8 || mt == 12;
   if (nwv == 8) return mt == 12;
   return 0;
 }
+
+GRAG_API int grag_gemm_decode_has(int mt, int nwv, int ntw) { return grag_gemm_decode_has_t(mt, nwv, ntw, 0); }
 
 // y = epilogue(x @ w^T) for M <= 16 * mt rows.  epi 0 store (act 0/1/3), 1 silu*mul (w gate/up interleaved in
 // 32-row blocks, out [M, N/2]).  ksplit > 1: fp32 planes into ws (ksplit * M * N floats), then
@@ -376,12 +431,12 @@ GRAG_API int grag_gemm_decode_has(int mt, int nwv, int ntw) {
 // Requirements (checked):
 // K % 64 == 0, N % (16 * ntw) == 0 (silu: N % 64 == 0), lda/ldw % 8 == 0,
 // ldc % 4 == 0, 16-B aligned A/W.
-GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, void* C, int lda, int ldw, int ldc,
-                              int M, int N, int K, int epi, int act, int mt, int nwv, int ntw, int ksplit, int gs,
-                              int packed, void* ws, hipStream_t stream) {
+GRAG_API int grag_gemm_decode_t(const void* A, const void* W, const void* bias, void* C, int lda, int ldw, int ldc,
+                                int M, int N, int K, int epi, int act, int mt, int nwv, int ntw, int ksplit, int gs,
+                                int packed, int tail, void* ws, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   const int msplit = (M + 16 * mt - 1) / (16 * mt);
-  if (!grag_gemm_decode_has(mt, nwv, ntw) || msplit > 4) return (int)hipErrorInvalidValue;
+  if (!grag_gemm_decode_has_t(mt, nwv, ntw, tail) || msplit > 4) return (int)hipErrorInvalidValue;
   if (K % 64 != 0 || K < 64 || N % (16 * ntw) != 0 || lda % 8 != 0 || ldw % 8 != 0 || ldc % 4 != 0)
     return (int)hipErrorInvalidValue;
   if (epi == EPI_SILU && N % 64 != 0) return (int)hipErrorInvalidValue;
@@ -391,7 +446,7 @@ GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, vo
     if (units % nwv != 0) return (int)hipErrorInvalidValue;
     gs = units / nwv;
   }
-  if (gs > units || (units + gs - 1) / gs > nwv) return (int)hipErrorInvalidValue;
+  if (gs > units || (units + gs - 1) / gs > (tail ? 5 : nwv)) return (int)hipErrorInvalidValue;
   // epi 2 (EPI_PARTIAL): leave the fp32 planes in ws for a consumer that reduces them itself
   // (grag_splitk_add_rmsnorm: split-K reduce + residual add + RMSNorm in one pass)
   const bool keep = epi == EPI_PARTIAL;
@@ -422,7 +477,11 @@ GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, vo
   const int nwg = gs * ksplit * msplit;
   const int e = ksplit > 1 ? EPI_PARTIAL : epi;
   int err;
-  if (nwv == 4) err = mt == 4 ? launch_v<4, kDepth, 4, 2>(a, e, act, nwg, stream)
+  if (tail) err = mt == 4 ? launch_v<4, kDepth, 8, 2, 1>(a, e, act, nwg, stream)
+                 : mt == 8 ? launch_v<8, kDepth, 8, 2, 2>(a, e, act, nwg, stream)
+                 : mt == 12 ? launch_v<12, kDepth, 8, 2, 3>(a, e, act, nwg, stream)
+                            : launch_v<16, kDepth, 8, 2, 4>(a, e, act, nwg, stream);
+  else if (nwv == 4) err = mt == 4 ? launch_v<4, kDepth, 4, 2>(a, e, act, nwg, stream)
                      : mt == 8 ? launch_v<8, kDepth, 4, 2>(a, e, act, nwg, stream)
                                : launch_v<16, kDepth, 4, 2>(a, e, act, nwg, stream);
   else if (nwv == 5) err = mt == 4 ? launch_v<4, kDepth, 5, 2>(a, e, act, nwg, stream)
@@ -431,4 +490,11 @@ GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, vo
   else err = launch_v<12, kDepth, 8, 2>(a, e, act, nwg, stream);
   if (err || ksplit == 1 || keep) return err;
   return grag_splitk_reduce(ws, bias, C, ldc, M, N, ksplit, epi, act, stream);
+}
+
+GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, void* C, int lda, int ldw, int ldc,
+                              int M, int N, int K, int epi, int act, int mt, int nwv, int ntw, int ksplit, int gs,
+                              int packed, void* ws, hipStream_t stream) {
+  return grag_gemm_decode_t(A, W, bias, C, lda, ldw, ldc, M, N, K, epi, act, mt, nwv, ntw, ksplit, gs, packed, 0, ws,
+                            stream);
 }

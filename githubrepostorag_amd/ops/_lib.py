@@ -62,6 +62,8 @@ _SIGS = {
     "grag_gemm_tile_mfma": [I],
     "grag_gemm_decode": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_decode_has": [I, I, I],
+    "grag_gemm_decode_t": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P],
+    "grag_gemm_decode_has_t": [I, I, I, I],
     "grag_gemm_decode_stamps": [P],
     "grag_gemm_w4": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_w4_has": [I, I],

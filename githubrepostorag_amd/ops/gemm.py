@@ -357,6 +357,8 @@ def dec_plan(M: int, N: int, K: int, silu: bool = False) -> tuple | None:
     if not _DEC_ON or M < 1 or M > DEC_MAX_M or K % 256 or N % 32 or (silu and N % 64):
         return None
     ncu = _num_cus()
+    if silu and DEC_TAIL:
+        return dec_tail_plan(M, N, ncu)
     units = N // 32
     deep = K >= 4 * N  # down_proj-like
     if M <= 128:
@@ -386,6 +388,24 @@ def dec_plan(M: int, N: int, K: int, silu: bool = False) -> tuple | None:
     if silu or deep or units % 4 or units // 4 >= ncu:
         return None
     return 16, 4, 2, dec_ksplit(K, max(1, ncu // (units // 4)))
+
+
+DEC_TAIL = os.environ.get("GRAG_DEC_TAIL", "0") == "1"
+
+
+def dec_tail_plan(M: int, N: int, ncu: int | None = None, ksplit: int = 1) -> tuple | None:
+    """The 8-wave tail-split schedule (gemm_decode.hip TQ): every workgroup gets 4 or 5 wave units dealt
+    evenly over about one workgroup per CU; waves 0-3 own 4 of them, waves 4-7 split the 5th by row tiles.
+    (mt, 8, 2, ksplit, gs, 1) or None when the units do not fill 4-5-unit workgroups."""
+    ncu = ncu or _num_cus()
+    mt = next((m for m in (4, 8, 12, 16) if 16 * m >= M), None)
+    if mt is None:
+        return None
+    units = N // 32
+    gs = min(units, max(-(-units // 5), ncu // max(1, ksplit)))
+    if -(-units // gs) > 5:
+        return None
+    return mt, 8, 2, ksplit, gs, 1
 
 
 def dec_ws_floats(M: int, N: int, ksplit: int) -> int:
@@ -434,14 +454,15 @@ def gemm_decode(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
         return gemm_silu(x, w, b) if epi == EPI_SILU else gemm(x, w, b, act)
     mt, nwv, ntw, ks, *rest = plan or dec_plan(M, N, K, epi == EPI_SILU)
     gs = rest[0] if rest else 0
+    tail = rest[1] if len(rest) > 1 else 0
     ks = dec_ksplit(K, ks)
     if out is None:
         out = torch.empty(M, N // 2 if epi == EPI_SILU else N, dtype=x.dtype, device=x.device)
     fl = dec_ws_floats(M, N, ks)
     ws = WS.get(x.device, fl) if fl else None
     wsrc = w if packed is None else packed.data
-    call("grag_gemm_decode", ptr(x), ptr(wsrc), ptr(b), ptr(out), x.stride(0), w.stride(0), out.stride(0),
-         M, N, K, epi, act, mt, nwv, ntw, ks, gs, 0 if packed is None else 2 if packed.silu else 1, ptr(ws))
+    call("grag_gemm_decode_t", ptr(x), ptr(wsrc), ptr(b), ptr(out), x.stride(0), w.stride(0), out.stride(0),
+         M, N, K, epi, act, mt, nwv, ntw, ks, gs, 0 if packed is None else 2 if packed.silu else 1, tail, ptr(ws))
     return out
 
 
@@ -493,8 +514,9 @@ def gemm_deferred(x: torch.Tensor, w: torch.Tensor, how: tuple[str, int, tuple])
     ws = WS.get(x.device, fl)
     if kind == "decode":
         mt, nwv, ntw, ksp, *rest = p
-        call("grag_gemm_decode", ptr(x), ptr(w), ptr(None), ptr(None), x.stride(0), w.stride(0), N,
-             M, N, K, EPI_PARTIAL, ACT_NONE, mt, nwv, ntw, ksp, rest[0] if rest else 0, 0, ptr(ws))
+        call("grag_gemm_decode_t", ptr(x), ptr(w), ptr(None), ptr(None), x.stride(0), w.stride(0), N,
+             M, N, K, EPI_PARTIAL, ACT_NONE, mt, nwv, ntw, ksp, rest[0] if rest else 0, 0,
+             rest[1] if len(rest) > 1 else 0, ptr(ws))
     else:
         call("grag_gemm_tile", ptr(x), ptr(w), ptr(None), ptr(None), x.stride(0), w.stride(0), N,
              M, N, K, EPI_PARTIAL, ACT_NONE, ks, 0, ptr(ws), ptr(None))

@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--packed", type=int, default=0,
                     help="1: also the decode kernel on the unit-packed weight layout (ops/gemm.py DecPacked) vs the "
                          "natural [N, K] layout, same plan (dec_plan, or --plan)")
+    ap.add_argument("--tail", type=int, default=0, help="1: also the 8-wave tail-split decode schedules")
     ap.add_argument("--plan", default="", help="mt,nwv,ntw,ksplit[,gs] for the packed A/B (default dec_plan)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -89,6 +90,14 @@ def main():
                     pk_of = {id(w): p for w, p in zip(ws, pks)}
                     arms["dec_packed"] = lambda w, plan=plan, epi=epi: G.gemm_decode(x, w, epi=epi, plan=plan,
                                                                                      packed=pk_of[id(w)])
+                if a.tail:  # the 8-wave tail-split schedule at the K-splits that give 4-5 units per workgroup
+                    epi = G.EPI_SILU if silu else G.EPI_STORE
+                    for ks in ([1] if silu else [k for k in (4, 7, 8, 10, 14) if G.dec_ksplit(K, k) == k]):
+                        tp = G.dec_tail_plan(M, N, ksplit=ks)
+                        if tp is None:
+                            continue
+                        G.WS.reserve(dev, G.dec_ws_floats(M, N, ks))
+                        arms[f"tail_ks{ks}"] = lambda w, tp=tp, epi=epi: G.gemm_decode(x, w, epi=epi, plan=tp)
                 r = {"kernel": "mlp_gate_up" if silu else kernel_for(M, N, K), "plan": plan}
                 gb = N * K * 2 / 1e9
                 for k, fn in arms.items():

@@ -201,12 +201,42 @@ def test_gemm_decode_packed(dev, M, N, K, plan, silu):
     assert torch.equal(y0.cpu(), y1.cpu())
 
 
+# tail split (8 waves: 4 own units + a 5th unit split by row tiles over waves 4-7): 4- and 5-unit workgroups
+# in one grid, every mt, plain / split-K / SiLU / packed, ragged M
+@pytest.mark.parametrize("M,N,K,plan", [(176, 4608, 3584, (12, 8, 2, 7, 32, 1)), (64, 3584, 3584, (4, 8, 2, 7, 25, 1)),
+                                        (250, 3584, 18944, (16, 8, 2, 8, 25, 1)), (120, 2080, 512, (8, 8, 2, 1, 14, 1)),
+                                        (33, 1024, 256, (4, 8, 2, 1, 7, 1))])
+def test_gemm_decode_tail_split(dev, M, N, K, plan):
+    x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+    G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, plan[3])))
+    y = G.gemm_decode(x, w, b, plan=plan)
+    check(y, ref(x, w, b), K)
+    y1 = G.gemm_decode(x, w, b, plan=plan, packed=G.DecPacked(w))
+    assert torch.equal(y.cpu(), y1.cpu())
+
+
+@pytest.mark.parametrize("M", [40, 128, 176, 256])
+def test_gemm_decode_silu_tail_split(dev, M):
+    I, K = 2336, 512  # 146 wave units over 32 workgroups: 4 and 5 per workgroup
+    x = rnd(M, K, dev=dev, scale=0.5)
+    wg, wu = rnd(I, K, dev=dev, seed=1, scale=0.2), rnd(I, K, dev=dev, seed=2, scale=0.2)
+    bg, bu = rnd(I, dev=dev, seed=3), rnd(I, dev=dev, seed=4)
+    wgu = G.interleave_gate_up(wg, wu)
+    bgu = G.interleave_gate_up(bg.view(I, 1), bu.view(I, 1)).view(2 * I)
+    plan = G.dec_tail_plan(M, 2 * I, ncu=32)
+    assert plan is not None and plan[4] == 32 and plan[5] == 1
+    h = G.gemm_decode(x, wgu, bgu, epi=G.EPI_SILU, plan=plan)
+    check(h, torch.nn.functional.silu(ref(x, wg, bg)) * ref(x, wu, bu), K)
+    h1 = G.gemm_decode(x, wgu, bgu, epi=G.EPI_SILU, plan=plan, packed=G.DecPacked(wgu, True))
+    assert torch.equal(h.cpu(), h1.cpu())
+
+
 def test_gemm_decode_identity_asymmetric(dev):
     # A = I with an asymmetric W catches a transposed C write
     K = 256
     w = (torch.arange(K * 256, dtype=torch.float32).reshape(256, K) % 251 - 125).to(torch.bfloat16).to(dev)
     for M, plan in ((200, (16, 4, 2, 1)), (190, (12, 8, 2, 1)), (190, (12, 5, 2, 1, 4)), (120, (8, 5, 2, 1, 3)),
-                    (250, (4, 5, 2, 1, 2))):
+                    (250, (4, 5, 2, 1, 2)), (190, (12, 8, 2, 1, 2, 1)), (250, (16, 8, 2, 1, 2, 1))):
         x = torch.eye(K, dtype=torch.bfloat16, device=dev)[:M].contiguous()
         y = G.gemm_decode(x, w, plan=plan)
         assert torch.equal(y.cpu(), w.float().T[:M].to(torch.bfloat16).cpu())
