@@ -403,6 +403,16 @@ int launch_v(const DArgs& a, int epi, int act, int nwg, hipStream_t s) {
 // more than the 256 registers a wave gets at two waves per SIMD);  (nwv 8, ntw 2): mt 12.  ntw = 4 measured no faster than 2 at M = 192 (profiles/gemm_decode_ab_v3.jsonl) and is
 // not instantiated.
 static unsigned long long* g_dec_stamps = nullptr;
+static int g_dec_depth = 0;  // 0: kDepth; 6 / 8: deeper rings where the LDS takes them (A/B, grag_gemm_decode_depth)
+
+// K-steps issued ahead for later launches (A/B of the ring depth): 0 = the default (kDepth = 4); 6 for mt 4 / 8
+// and 8 for mt 4 on the 4- and 5-wave grids (the A ring of (depth + 1) x 16 mt x 128 B must fit the LDS).
+// Returns the previous setting.
+GRAG_API int grag_gemm_decode_depth(int d) {
+  const int prev = g_dec_depth;
+  g_dec_depth = d;
+  return prev;
+}
 
 // Diagnostics: while set, every grag_gemm_decode launch writes per workgroup (blockIdx.x) 4 u64 words
 // {s_memrealtime at start, at the end of the main loop, XCC id, logical block} to `buf` (grid size x 32 B);
@@ -481,6 +491,11 @@ GRAG_API int grag_gemm_decode_t(const void* A, const void* W, const void* bias, 
                  : mt == 8 ? launch_v<8, kDepth, 8, 2, 2>(a, e, act, nwg, stream)
                  : mt == 12 ? launch_v<12, kDepth, 8, 2, 3>(a, e, act, nwg, stream)
                             : launch_v<16, kDepth, 8, 2, 4>(a, e, act, nwg, stream);
+  else if (g_dec_depth == 8 && mt == 4 && (nwv == 4 || nwv == 5))
+    err = nwv == 4 ? launch_v<4, 8, 4, 2>(a, e, act, nwg, stream) : launch_v<4, 8, 5, 2>(a, e, act, nwg, stream);
+  else if (g_dec_depth >= 6 && (mt == 4 || mt == 8) && (nwv == 4 || nwv == 5))
+    err = nwv == 4 ? (mt == 4 ? launch_v<4, 6, 4, 2>(a, e, act, nwg, stream) : launch_v<8, 6, 4, 2>(a, e, act, nwg, stream))
+                   : (mt == 4 ? launch_v<4, 6, 5, 2>(a, e, act, nwg, stream) : launch_v<8, 6, 5, 2>(a, e, act, nwg, stream));
   else if (nwv == 4) err = mt == 4 ? launch_v<4, kDepth, 4, 2>(a, e, act, nwg, stream)
                      : mt == 8 ? launch_v<8, kDepth, 4, 2>(a, e, act, nwg, stream)
                                : launch_v<16, kDepth, 4, 2>(a, e, act, nwg, stream);

@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from githubrepostorag_amd.ops import gemm as G  # noqa: E402
+from githubrepostorag_amd.ops._lib import lib  # noqa: E402
 from githubrepostorag_amd.ops.linear import enable_tuned_gemms, kernel_for, linear, linear_deferred  # noqa: E402
 
 SHAPES = {"qkv": (4608, 3584, False), "o": (3584, 3584, False), "gate_up": (37888, 3584, True),
@@ -62,6 +63,7 @@ def main():
                     help="1: also the decode kernel on the unit-packed weight layout (ops/gemm.py DecPacked) vs the "
                          "natural [N, K] layout, same plan (dec_plan, or --plan)")
     ap.add_argument("--tail", type=int, default=0, help="1: also the 8-wave tail-split decode schedules")
+    ap.add_argument("--depths", default="", help="ring depths to A/B on the dispatched decode plan (e.g. 6,8)")
     ap.add_argument("--plan", default="", help="mt,nwv,ntw,ksplit[,gs] for the packed A/B (default dec_plan)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -98,6 +100,27 @@ def main():
                             continue
                         G.WS.reserve(dev, G.dec_ws_floats(M, N, ks))
                         arms[f"tail_ks{ks}"] = lambda w, tp=tp, epi=epi: G.gemm_decode(x, w, epi=epi, plan=tp)
+                for d in [int(v) for v in a.depths.split(",") if v.strip()]:
+                    if plan is None or plan[0] > (4 if d == 8 else 8) or plan[1] not in (4, 5):
+                        continue
+                    epi = G.EPI_SILU if silu else G.EPI_STORE
+                    G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, plan[3])))
+
+                    def deep(w, d=d, plan=plan, epi=epi):
+                        prev = lib().grag_gemm_decode_depth(d)
+                        try:
+                            return G.gemm_decode(x, w, epi=epi, plan=plan)
+                        finally:
+                            lib().grag_gemm_decode_depth(prev)
+                    arms[f"depth{d}"] = deep
+                    if a.packed:
+                        def deep_pk(w, d=d, plan=plan, epi=epi):
+                            prev = lib().grag_gemm_decode_depth(d)
+                            try:
+                                return G.gemm_decode(x, w, epi=epi, plan=plan, packed=pk_of[id(w)])
+                            finally:
+                                lib().grag_gemm_decode_depth(prev)
+                        arms[f"depth{d}_packed"] = deep_pk
                 r = {"kernel": "mlp_gate_up" if silu else kernel_for(M, N, K), "plan": plan}
                 gb = N * K * 2 / 1e9
                 for k, fn in arms.items():

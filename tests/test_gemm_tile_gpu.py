@@ -362,3 +362,28 @@ def test_gemm_mfma32_variant(dev, mfma32):
         y = G.gemm(x, w, b, ksplit=1, sk=sk)
         check(y, ref(x, w, b), K)
         assert torch.equal(y, G.gemm(x, w, b, ksplit=1, sk=sk))
+
+
+@pytest.mark.parametrize("depth", [6, 8])
+@pytest.mark.parametrize("M,N,K,plan,silu", [(64, 3584, 3584, (4, 4, 2, 7), False), (128, 4608, 3584, (8, 4, 2, 7), False),
+                                             (60, 2112, 1024, (4, 5, 2, 1, 14), True),
+                                             (100, 2112, 1024, (8, 5, 2, 1, 14), True)])
+def test_gemm_decode_deep_ring(dev, depth, M, N, K, plan, silu):
+    """Deeper K-step rings (grag_gemm_decode_depth: 6 for mt 4 / 8, 8 for mt 4) give the default ring's
+    results bit for bit (same accumulation order)."""
+    from githubrepostorag_amd.ops._lib import lib
+
+    if depth == 8 and plan[0] != 4:
+        pytest.skip("depth 8: mt 4 only")
+    x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+    epi = G.EPI_SILU if silu else G.EPI_STORE
+    G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, plan[3])))
+    y0 = G.gemm_decode(x, w, b, epi=epi, plan=plan)
+    prev = lib().grag_gemm_decode_depth(depth)
+    try:
+        y1 = G.gemm_decode(x, w, b, epi=epi, plan=plan)
+    finally:
+        lib().grag_gemm_decode_depth(prev)
+    assert torch.equal(y0.cpu(), y1.cpu())
+    if not silu:
+        check(y1, ref(x, w, b), K)
