@@ -963,9 +963,10 @@ def serving_runner_phase(args, eng, prepare, sp, U, u, A, S, steps, dev, dp_size
         pump.drain_and_stop(completed=U * u + steps * B)
         comm.barrier()
         loads = [float(x) for x in str(args.serving_open_load).split(",") if x.strip()]
+        n_open = max(4 * B, min(steps * B, 768))  # arrivals per load level (bounds the bench's wall time)
         for load in loads:
             res_open.append({"load": load, **_open_loop(runner, prepare, sp, u, pg, dev, load * B * steps / elapsed,
-                                                         steps * B)})
+                                                         n_open)})
             comm.barrier()
     finally:
         runner.shutdown()

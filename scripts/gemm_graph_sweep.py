@@ -75,7 +75,7 @@ def main():
             N, K, silu = SHAPES[name]
             ncopy = max(2, min(16, (1 << 30) // (N * K * 2) + 1))
             ws = [((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(ncopy)]
-            for M in [int(m) for m in a.Ms.split(",")]:
+            for M in [int(m) for m in a.Ms.replace(":", ",").split(",")]:
                 x = ((torch.rand(M, K, device=dev) * 2 - 1)).to(torch.bfloat16)
                 arms = {}
                 if silu:
@@ -100,7 +100,7 @@ def main():
                             continue
                         G.WS.reserve(dev, G.dec_ws_floats(M, N, ks))
                         arms[f"tail_ks{ks}"] = lambda w, tp=tp, epi=epi: G.gemm_decode(x, w, epi=epi, plan=tp)
-                for d in [int(v) for v in a.depths.split(",") if v.strip()]:
+                for d in [int(v) for v in a.depths.replace(":", ",").split(",") if v.strip()]:
                     if plan is None or plan[0] > (4 if d == 8 else 8) or plan[1] not in (4, 5):
                         continue
                     epi = G.EPI_SILU if silu else G.EPI_STORE
