@@ -27,6 +27,15 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_kernel(
   bf16x8_t* rr = residual ? reinterpret_cast<bf16x8_t*>(residual + (size_t)row * H) : nullptr;
   float v[VPT][8];
   float ss = 0.f;
+  // gamma is loaded before the reduction, so its latency overlaps the row loads instead of following the
+  // block sum (at decode batches of 1-16 rows these kernels are latency chains, not bandwidth)
+  const bf16x8_t* wr = reinterpret_cast<const bf16x8_t*>(w);
+  bf16x8_t gv[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) gv[i] = wr[idx];
+  }
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * kThreads;
@@ -55,14 +64,13 @@ __global__ __launch_bounds__(kThreads) void rmsnorm_kernel(
   }
   ss = block_sum(ss, red);
   const float inv = rsqrtf(ss / (float)H + eps);
-  const bf16x8_t* wr = reinterpret_cast<const bf16x8_t*>(w);
   bf16x8_t* orow = reinterpret_cast<bf16x8_t*>(out + (size_t)row * H);
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * kThreads;
     if (idx < nvec) {
       float g[8], o[8];
-      unpack8(wr[idx], g);
+      unpack8(gv[i], g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * g[j];
       orow[idx] = pack8(o);
@@ -87,6 +95,13 @@ __global__ __launch_bounds__(kThreads) void splitk_rmsnorm_kernel(
   bf16x8_t* rr = reinterpret_cast<bf16x8_t*>(residual + (size_t)row * H);
   float v[VPT][8];
   float ss = 0.f;
+  const bf16x8_t* wr = reinterpret_cast<const bf16x8_t*>(w);
+  bf16x8_t gv[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (idx < nvec) gv[i] = wr[idx];
+  }
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * kThreads;
@@ -115,14 +130,13 @@ __global__ __launch_bounds__(kThreads) void splitk_rmsnorm_kernel(
   }
   ss = block_sum(ss, red);
   const float inv = rsqrtf(ss / (float)H + eps);
-  const bf16x8_t* wr = reinterpret_cast<const bf16x8_t*>(w);
   bf16x8_t* orow = reinterpret_cast<bf16x8_t*>(out + (size_t)row * H);
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * kThreads;
     if (idx < nvec) {
       float g[8], o[8];
-      unpack8(wr[idx], g);
+      unpack8(gv[i], g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * g[j];
       orow[idx] = pack8(o);

@@ -139,9 +139,21 @@ def cmd_replica(args) -> int:
         rt.warmup()
     host, port = args.hub.rsplit(":", 1)
     key = bytes.fromhex(os.environ["GRAG_HUB_AUTHKEY"])
+    group = None
+    if args.shards > 1 and os.environ.get("GRAG_SHARD_TRANSPORT") == "collective" and "WORLD_SIZE" in os.environ:
+        from .parallel import comm  # the replicas' process group (spawn_replicas): shard rounds as collectives
+
+        comm.init_distributed()
+        group = comm.world_group()
+        dev = str(getattr(rt, "device", "cpu"))
+        if dev.startswith("cuda") and os.environ.get("GRAG_SHARD_IPC", "1") != "0":
+            from .parallel.custom_ar import enable_for_group
+
+            # payloads through the one-shot IPC gather: replicas on one card, or xGMI peers on a node
+            enable_for_group(group, dev)
     try:
         return run_replica(rt, (host, int(port)), key, args.rank, shards=args.shards,
-                           health_every=float(os.environ.get("GRAG_HEALTH_EVERY", "5")))
+                           health_every=float(os.environ.get("GRAG_HEALTH_EVERY", "5")), group=group)
     finally:
         if hasattr(rt, "close"):
             rt.close()

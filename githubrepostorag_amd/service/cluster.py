@@ -538,7 +538,7 @@ def attach_sharded_store(runtime, transport, rank: int, nshards: int):
 
 
 def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | None = None,
-                health_every: float = 5.0, shards: int = 1) -> int:
+                health_every: float = 5.0, shards: int = 1, group=None) -> int:
     """Serve jobs from the hub until it says stop or the connection drops (blocking).
     ``shards`` > 1: this replica holds shard ``rank`` of a row-sharded index and answers
     the other replicas' shard rounds (service/cluster.py docstring)."""
@@ -558,17 +558,28 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
 
     transport = None
     mesh = None
+    coll = None
     local_store = getattr(runtime, "store", None)
+    kind = os.environ.get("GRAG_SHARD_TRANSPORT", "collective" if group is not None else "mesh")
     if shards > 1 and local_store is not None:
-        if os.environ.get("GRAG_SHARD_TRANSPORT", "mesh") == "hub":
+        if kind == "hub":
             transport = HubShardTransport(send, rank)
         else:  # replica-to-replica rounds (service/mesh.py); the hub only tells us who the peers are
             from .mesh import PeerMesh
 
             transport = mesh = PeerMesh(rank, shards, authkey, host=os.environ.get("GRAG_MESH_HOST", "127.0.0.1"))
+            if kind == "collective" and group is not None and group.size == shards:
+                # reads as lockstep collectives over the replicas' process group (service/collective.py: RCCL
+                # over xGMI with one replica per GPU); routed writes stay on the mesh
+                from .collective import CollectiveShardTransport
+
+                transport = coll = CollectiveShardTransport(rank, shards, group, getattr(runtime, "device", "cpu"),
+                                                            fallback=mesh)
         local_store = attach_sharded_store(runtime, transport, rank, shards)
         if mesh is not None:
             mesh.store = local_store
+        if coll is not None:
+            coll.store = local_store
     # other replicas' shard rounds and routed writes run here, off the job loop (GPU search + sync)
     shard_pool = ThreadPoolExecutor(4, thread_name_prefix="shard-exec")
     events = _ForwardingEvents(send)
@@ -644,6 +655,8 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
                     h = runtime.health() if hasattr(runtime, "health") else {}
                     if mesh is not None:
                         h = {**h, "mesh_stats": mesh.round_stats()}
+                    if coll is not None:
+                        h = {**h, "collective_stats": coll.round_stats()}
                     send(("health", {"device": str(getattr(runtime, "device", "cpu")), **h}))
                 except Exception:  # pragma: no cover
                     pass
@@ -682,6 +695,8 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
     finally:
         shard_pool.shutdown(wait=False)
         write_pool.shutdown(wait=False)
+        if coll is not None:
+            coll.close()  # collective: the rounds stop once every replica has asked to
         if mesh is not None:
             mesh.close()
         try:
@@ -694,7 +709,14 @@ def run_replica(runtime, address, authkey: bytes, rank: int, capacity: int | Non
 def spawn_replicas(n: int, address, authkey: bytes, extra_args=(), gpus: list[int] | None = None,
                    env: dict | None = None, shards: int = 1) -> list[subprocess.Popen]:
     """Start one replica child process per GPU (HIP_VISIBLE_DEVICES pins it; never an exec of this
-    process).  The authkey travels in the environment, not on the command line."""
+    process).  The authkey travels in the environment, not on the command line.  With
+    GRAG_SHARD_TRANSPORT=collective the replicas also form a torch.distributed group (rank = replica)
+    for their shard rounds (service/collective.py)."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        pg_port = sk.getsockname()[1]
     procs = []
     for r in range(n):
         e = dict(os.environ, **(env or {}))
@@ -702,6 +724,12 @@ def spawn_replicas(n: int, address, authkey: bytes, extra_args=(), gpus: list[in
         if gpus is not None:
             e["HIP_VISIBLE_DEVICES"] = str(gpus[r])
         e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if shards > 1 and e.get("GRAG_SHARD_TRANSPORT") == "collective":
+            # the replicas' process group (service/collective.py): RCCL when each has its own GPU
+            e.update(RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                     MASTER_PORT=str(pg_port))
+            if gpus is None or len(set(gpus[:n])) < n:
+                e.setdefault("GRAG_DIST_BACKEND", "gloo")
         cmd = [sys.executable, "-m", "githubrepostorag_amd", "replica", "--hub", f"{address[0]}:{address[1]}",
                "--rank", str(r), "--shards", str(shards), *extra_args]
         procs.append(subprocess.Popen(cmd, env=e))
@@ -730,7 +758,8 @@ def gpu_demo_runtime(settings):
 def demo_runtime(settings):
     """A CPU replica runtime with a scripted LLM and a tiny encoder over three chunks (tests, and a
     GPU-less rehearsal of ``serve --replicas``: ``replica --factory
-    githubrepostorag_amd.service.cluster:demo_runtime``).  GRAG_DEMO_LLM_DELAY (s) slows each LLM call."""
+    githubrepostorag_amd.service.cluster:demo_runtime``).  GRAG_DEMO_LLM_DELAY (s) slows each LLM call;
+    GRAG_DEMO_DEVICE=cuda keeps the tables (and the shard rounds' searches) on the GPU."""
     from ..agent.llm import ScriptedLLM
     from ..embed.service import Embedder
     from ..index.store import VectorStore
@@ -749,8 +778,9 @@ def demo_runtime(settings):
             return '["alt query"]'
         return f"Widgets are handled in [1] (replica pid {os.getpid()})."
 
+    dev = os.environ.get("GRAG_DEMO_DEVICE", "cpu")
     emb = Embedder.from_name("encoder-tiny", device="cpu", seed=3)
-    store = VectorStore(emb.dim, "cpu")
+    store = VectorStore(emb.dim, dev)
     texts = ["widgets code", "gadget service", "billing module"]
     # row ids split over two shards (crc32 mod 2: widgets -> 1, gadget / billing -> 0)
     store.table("chunk").upsert(["widgets", "gadget", "billing"], texts, emb.embed_documents(texts),
@@ -767,5 +797,5 @@ def demo_runtime(settings):
                                       v, [{"namespace": "default", "repo": f"r{i % 7}", "module": f"m{i % 23}",
                                            "file_path": f"m{i % 23}/f{i % 97}.py"} for i in range(extra)])
     settings.worker_max_jobs = int(os.environ.get("GRAG_DEMO_SLOTS", settings.worker_max_jobs))
-    return RAGRuntime(settings, device="cpu", llm=ScriptedLLM(router), embedder=emb, store=store,
+    return RAGRuntime(settings, device=dev, llm=ScriptedLLM(router), embedder=emb, store=store,
                       build_engine=False)

@@ -53,6 +53,50 @@ class ShardWriteError(RuntimeError):
     """A routed write did not reach (or was not applied by) its owning shard."""
 
 
+def run_one(store, req_id, scope, op, payload):
+    """One shard operation on ``store`` -> (req_id, ok, result or error text)."""
+    from ..index.sharded_store import execute
+
+    try:
+        return (req_id, True, execute(store, scope, op, payload))
+    except Exception as e:  # answer anyway: the origin must not wait for a failed shard
+        log.exception("shard %s on %s failed", op, scope)
+        return (req_id, False, f"{type(e).__name__}: {e}")
+
+
+def run_reads(store, reads, stats: dict | None = None):
+    """Coalesced reads of one message / round: plain searches sharing (table, k, filter) run as ONE
+    stacked search (one fused score+top-k launch for all their queries); the rest one by one."""
+    import numpy as np
+
+    out, groups = [], {}
+    for item in reads:
+        req_id, scope, op, payload = item
+        if op == "search":
+            Q, k, flt = payload
+            key = (scope, int(k), repr(sorted((flt or {}).items())))
+            groups.setdefault(key, []).append(item)
+        else:
+            out.append(run_one(store, *item))
+    for (scope, k, _), items in groups.items():
+        if len(items) == 1:
+            out.append(run_one(store, *items[0]))
+            continue
+        flt = items[0][3][2]
+        qs = [np.asarray(it[3][0], dtype=np.float32).reshape(-1, np.asarray(it[3][0]).shape[-1]) for it in items]
+        res = run_one(store, -1, scope, "search", (np.concatenate(qs), k, flt))
+        if not res[1]:
+            out.extend((it[0], False, res[2]) for it in items)
+            continue
+        if stats is not None:
+            stats["stacked_searches"] = stats.get("stacked_searches", 0) + 1
+        hits, a = res[2], 0
+        for it, q in zip(items, qs):
+            out.append((it[0], True, hits[a:a + q.shape[0]]))
+            a += q.shape[0]
+    return out
+
+
 class Parts(list):
     """Results of the shards that answered a round; ``missing`` = ranks that did not."""
 
@@ -349,44 +393,10 @@ class PeerMesh:
                 pass
 
     def _run_one(self, req_id, scope, op, payload):
-        from ..index.sharded_store import execute
-
-        try:
-            return (req_id, True, execute(self.store, scope, op, payload))
-        except Exception as e:  # answer anyway: the origin must not wait for a failed shard
-            log.exception("mesh: %s on %s failed", op, scope)
-            return (req_id, False, f"{type(e).__name__}: {e}")
+        return run_one(self.store, req_id, scope, op, payload)
 
     def _run_reads(self, reads):
-        """Coalesced reads of one message: plain searches sharing (table, k, filter) run as ONE stacked
-        search (one fused score+top-k launch for all their queries); the rest one by one."""
-        import numpy as np
-
-        out, groups = [], {}
-        for item in reads:
-            req_id, scope, op, payload = item
-            if op == "search":
-                Q, k, flt = payload
-                key = (scope, int(k), repr(sorted((flt or {}).items())))
-                groups.setdefault(key, []).append(item)
-            else:
-                out.append(self._run_one(*item))
-        for (scope, k, _), items in groups.items():
-            if len(items) == 1:
-                out.append(self._run_one(*items[0]))
-                continue
-            flt = items[0][3][2]
-            qs = [np.asarray(it[3][0], dtype=np.float32).reshape(-1, np.asarray(it[3][0]).shape[-1]) for it in items]
-            res = self._run_one(-1, scope, "search", (np.concatenate(qs), k, flt))
-            if not res[1]:
-                out.extend((it[0], False, res[2]) for it in items)
-                continue
-            self.stats["stacked_searches"] += 1
-            hits, a = res[2], 0
-            for it, q in zip(items, qs):
-                out.append((it[0], True, hits[a:a + q.shape[0]]))
-                a += q.shape[0]
-        return out
+        return run_reads(self.store, reads, self.stats)
 
     def close(self) -> None:
         self._closed = True

@@ -3,7 +3,9 @@
 N replica processes (service/cluster.py ``demo_runtime`` with GRAG_DEMO_ROWS rows per scope table, a
 scripted LLM that sleeps GRAG_DEMO_LLM_DELAY per call) hold 1/N of every table each; the front door
 serves ``POST /rag/jobs`` + SSE over real HTTP (service/e2e.py) and every retrieval round of every job
-fans out replica-to-replica over the shard mesh (service/mesh.py).  Reports jobs/s, and per replica the
+fans out replica-to-replica over the shard mesh (service/mesh.py), or with --transport collective as
+lockstep rounds over the replicas' process group (service/collective.py; --device cuda: tables on the
+GPU and the rounds' payloads through the one-shot IPC gather).  Reports jobs/s, and per replica the
 mesh's rounds, rounds/s, round latency p50 / p99 and degraded rounds.
 
   python scripts/mesh_load.py --replicas 8 --jobs 512 --concurrency 256 [--out profiles/mesh_load_r4.json]
@@ -20,7 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def run(replicas: int = 8, jobs: int = 512, concurrency: int = 256, rows: int = 2000, delay: float = 0.002,
-        slots: int = 64, transport: str = "mesh") -> dict:
+        slots: int = 64, transport: str = "mesh", device: str = "cpu") -> dict:
     from githubrepostorag_amd.config import Settings
     from githubrepostorag_amd.service.api import APIState, create_app
     from githubrepostorag_amd.service.cluster import ClusterRuntimeView, ReplicaHub, spawn_replicas
@@ -31,10 +33,15 @@ def run(replicas: int = 8, jobs: int = 512, concurrency: int = 256, rows: int = 
     hub = ReplicaHub(events, job_timeout=600.0)
     env = {"GRAG_DEMO_LLM_DELAY": str(delay), "GRAG_DEMO_SLOTS": str(slots), "GRAG_DEMO_ROWS": str(rows),
            "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": "", "OMP_NUM_THREADS": "1",
-           "GRAG_SHARD_TRANSPORT": transport, "GRAG_HEALTH_EVERY": "0.5"}
+           "GRAG_SHARD_TRANSPORT": transport, "GRAG_HEALTH_EVERY": "0.5", "GRAG_DEMO_DEVICE": device}
+    gpus = None
+    if device.startswith("cuda"):  # every replica on the one visible card (the 1-GPU box)
+        env.pop("CUDA_VISIBLE_DEVICES")
+        env.pop("HIP_VISIBLE_DEVICES")
+        gpus = [0] * replicas
     procs = spawn_replicas(replicas, hub.address, hub.authkey,
-                           ["--factory", "githubrepostorag_amd.service.cluster:demo_runtime", "--device", "cpu"],
-                           env=env, shards=replicas)
+                           ["--factory", "githubrepostorag_amd.service.cluster:demo_runtime", "--device", device],
+                           env=env, shards=replicas, gpus=gpus)
     try:
         t0 = time.time()
         while hub.live_count() < replicas:
@@ -47,9 +54,9 @@ def run(replicas: int = 8, jobs: int = 512, concurrency: int = 256, rows: int = 
         res = run_e2e(create_app(state), qs, concurrency, warmup=qs[:min(16, jobs)])
         time.sleep(1.5)  # replicas report mesh stats every 0.5 s
         reps = hub.health()["replicas"]
-        mesh = [dict(rank=r["rank"], **(r.get("mesh_stats") or {})) for r in reps]
+        mesh = [dict(rank=r["rank"], **(r.get("collective_stats") or r.get("mesh_stats") or {})) for r in reps]
         rounds = sum(m.get("rounds", 0) for m in mesh)
-        return {"replicas": replicas, "transport": transport, "rows_per_table": rows, "jobs": res["jobs"],
+        return {"replicas": replicas, "transport": transport, "device": device, "rows_per_table": rows, "jobs": res["jobs"],
                 "concurrency": concurrency, "jobs_per_s": res["jobs_per_s"], "errors": res["errors"],
                 "degraded_jobs": res["degraded_jobs"], "job_latency_p50_ms": res["job_latency_p50_ms"],
                 "shard_rounds": rounds,
@@ -75,10 +82,11 @@ def main():
     ap.add_argument("--concurrency", type=int, default=256)
     ap.add_argument("--rows", type=int, default=2000)
     ap.add_argument("--delay", type=float, default=0.002)
-    ap.add_argument("--transport", default="mesh", choices=["mesh", "hub"])
+    ap.add_argument("--transport", default="mesh", choices=["mesh", "hub", "collective"])
+    ap.add_argument("--device", default="cpu", help="cuda: every replica's tables on the visible GPU")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    res = run(a.replicas, a.jobs, a.concurrency, a.rows, a.delay, transport=a.transport)
+    res = run(a.replicas, a.jobs, a.concurrency, a.rows, a.delay, transport=a.transport, device=a.device)
     print(json.dumps({k: v for k, v in res.items() if k != "per_replica"}))
     if a.out:
         with open(a.out, "w") as f:
