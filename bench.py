@@ -238,7 +238,9 @@ def main():
     if os.environ.get("GRAG_DUMP_STACKS_AFTER"):  # debugging a stuck rank: every thread's stack, once
         import faulthandler
 
-        faulthandler.dump_traceback_later(float(os.environ["GRAG_DUMP_STACKS_AFTER"]), exit=False)
+        # every N seconds (GRAG_DUMP_STACKS_REPEAT=1) or once
+        faulthandler.dump_traceback_later(float(os.environ["GRAG_DUMP_STACKS_AFTER"]), exit=False,
+                                          repeat=os.environ.get("GRAG_DUMP_STACKS_REPEAT") == "1")
     if args.cpu:  # before torch initialises HIP: this process never touches a GPU
         os.environ["HIP_VISIBLE_DEVICES"] = ""
         os.environ["CUDA_VISIBLE_DEVICES"] = ""

@@ -399,14 +399,16 @@ int launch_v(const DArgs& a, int epi, int act, int nwg, hipStream_t s) {
 }  // namespace
 
 // Variants compiled (mt = 16-row tiles of M, nwv = waves per workgroup, ntw = 16-row W tiles per wave;
-// depth kDepth): (nwv 4, ntw 2): mt 4, 8, 16;  (nwv 5, ntw 2): mt 4, 8, 12 (balanced grids; mt 16 needs
+// depth kDepth): (nwv 4, ntw 2): mt 1, 2, 4, 8, 16;  (nwv 5, ntw 2): mt 1, 2, 4, 8, 12 (mt 1 / 2 also at
+// depth 8 and 12: 1-32 rows hold 2-4 KB of A per K-step, so the W ring takes the registers; balanced grids; mt 16 needs
 // more than the 256 registers a wave gets at two waves per SIMD);  (nwv 8, ntw 2): mt 12.  ntw = 4 measured no faster than 2 at M = 192 (profiles/gemm_decode_ab_v3.jsonl) and is
 // not instantiated.
 static unsigned long long* g_dec_stamps = nullptr;
 static int g_dec_depth = 0;  // 0: kDepth; 6 / 8: deeper rings where the LDS takes them (A/B, grag_gemm_decode_depth)
 
 // K-steps issued ahead for later launches (A/B of the ring depth): 0 = the default (kDepth = 4); 6 for mt 4 / 8
-// and 8 for mt 4 on the 4- and 5-wave grids (the A ring of (depth + 1) x 16 mt x 128 B must fit the LDS).
+// and 8 for mt 4 on the 4- and 5-wave grids (the A ring of (depth + 1) x 16 mt x 128 B must fit the LDS);
+// 8 or 12 for mt 1 / 2 (>= 12 -> 12).
 // Returns the previous setting.
 GRAG_API int grag_gemm_decode_depth(int d) {
   const int prev = g_dec_depth;
@@ -423,8 +425,8 @@ GRAG_API void grag_gemm_decode_stamps(void* buf) { g_dec_stamps = (unsigned long
 GRAG_API int grag_gemm_decode_has_t(int mt, int nwv, int ntw, int tail) {
   if (tail) return ntw == 2 && nwv == 8 && (mt == 4 || mt == 8 || mt == 12 || mt == 16);
   if (ntw != 2) return 0;
-  if (nwv == 4) return mt == 4 || mt == 8 || mt == 16;
-  if (nwv == 5) return mt == 4 || mt == 8 || mt == 12;
+  if (nwv == 4) return mt == 1 || mt == 2 || mt == 4 || mt == 8 || mt == 16;
+  if (nwv == 5) return mt == 1 || mt == 2 || mt == 4 || mt == 8 || mt == 12;
   if (nwv == 8) return mt == 12;
   return 0;
 }
@@ -491,7 +493,13 @@ GRAG_API int grag_gemm_decode_t(const void* A, const void* W, const void* bias, 
                  : mt == 8 ? launch_v<8, kDepth, 8, 2, 2>(a, e, act, nwg, stream)
                  : mt == 12 ? launch_v<12, kDepth, 8, 2, 3>(a, e, act, nwg, stream)
                             : launch_v<16, kDepth, 8, 2, 4>(a, e, act, nwg, stream);
-  else if (g_dec_depth == 8 && mt == 4 && (nwv == 4 || nwv == 5))
+  else if (mt <= 2) {  // 1-32 rows (the reference's 1-4 live sequences): a 2-4 KB A ring, so the W ring can be deep
+    const int d = g_dec_depth >= 12 ? 12 : g_dec_depth >= 8 ? 8 : kDepth;
+#define SK(MT_, D_) (nwv == 4 ? launch_v<MT_, D_, 4, 2>(a, e, act, nwg, stream) : launch_v<MT_, D_, 5, 2>(a, e, act, nwg, stream))
+    err = mt == 1 ? (d == 12 ? SK(1, 12) : d == 8 ? SK(1, 8) : SK(1, kDepth))
+                  : (d == 12 ? SK(2, 12) : d == 8 ? SK(2, 8) : SK(2, kDepth));
+#undef SK
+  } else if (g_dec_depth == 8 && mt == 4 && (nwv == 4 || nwv == 5))
     err = nwv == 4 ? launch_v<4, 8, 4, 2>(a, e, act, nwg, stream) : launch_v<4, 8, 5, 2>(a, e, act, nwg, stream);
   else if (g_dec_depth >= 6 && (mt == 4 || mt == 8) && (nwv == 4 || nwv == 5))
     err = nwv == 4 ? (mt == 4 ? launch_v<4, 6, 4, 2>(a, e, act, nwg, stream) : launch_v<8, 6, 4, 2>(a, e, act, nwg, stream))

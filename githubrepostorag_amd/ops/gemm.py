@@ -317,8 +317,12 @@ def gemm_silu(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None = N
 DEC_DEPTH = 4  # K-steps issued ahead by the decode kernel (ring of DEC_DEPTH + 1 LDS / register slots)
 _DEC_ON = os.environ.get("GRAG_DECODE_GEMM", "1") != "0"
 # (mt, nwv, ntw) compiled: mt 16-row tiles of M, nwv waves per workgroup, ntw 16-row W tiles per wave
-DEC_VARIANTS = [(4, 4, 2), (4, 5, 2), (8, 4, 2), (8, 5, 2), (12, 5, 2), (12, 8, 2), (16, 4, 2)]
+DEC_VARIANTS = [(1, 4, 2), (1, 5, 2), (2, 4, 2), (2, 5, 2), (4, 4, 2), (4, 5, 2), (8, 4, 2), (8, 5, 2), (12, 5, 2),
+                (12, 8, 2), (16, 4, 2)]
 DEC_MAX_M = int(os.environ.get("GRAG_DECODE_MAX_M", "256"))
+# smallest batch the decode kernel takes in the dispatch (ops/linear.kernel_for, mlp_gate_up): 33 keeps 1-32 rows on
+# the skinny / stream kernels and the tile kernel's gate/up; 1 sends them to the 1- / 2-row-tile decode variants
+DEC_MIN_M = int(os.environ.get("GRAG_DEC_MIN_M", "33"))
 
 
 def dec_variants(M: int) -> list[tuple[int, int, int]]:
@@ -363,7 +367,7 @@ def dec_plan(M: int, N: int, K: int, silu: bool = False) -> tuple | None:
     deep = K >= 4 * N  # down_proj-like
     if M <= 128:
         if silu or units >= 4 * ncu:  # FFN-wide: balanced 5-wave grid over every CU, no K-split
-            mt = 4 if M <= 64 else 8
+            mt = -(-M // 16) if M <= 32 else 4 if M <= 64 else 8
             gs = dec_balanced_gs(N, 2, 5, 1, ncu)
             return None if gs is None else (mt, 5, 2, 1, gs)
         vs = [v for v in dec_variants(M) if v[1] == 4 and N % (16 * v[1] * v[2]) == 0]
@@ -552,7 +556,7 @@ def mlp_gate_up(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None =
     """SwiGLU input half for an interleaved gate/up weight: the fused tile
     kernel when it takes the shape, else library GEMM + reshape (same math)."""
     M, K = x.shape
-    if x.is_cuda and M >= 33 and supported(x, w_gu) and dec_plan(M, w_gu.shape[0], K, True) is not None \
+    if x.is_cuda and M >= DEC_MIN_M and supported(x, w_gu) and dec_plan(M, w_gu.shape[0], K, True) is not None \
             and dec_capture_ok(x.device, M, w_gu.shape[0], K, True):
         return gemm_decode(x, w_gu, b_gu, epi=EPI_SILU)
     if not x.is_cuda or (supported(x, w_gu) and capture_ok(x.device, M, w_gu.shape[0], K, True)):

@@ -269,7 +269,7 @@ def kernel_for(M: int, N: int, K: int, tile_ok: bool = True, dev: torch.device |
     the split-K / stream-K workspaces (None: plan as in steady state, workspaces ready)."""
     capturing = dev is not None and torch.cuda.is_current_stream_capturing()
     if tile_ok:
-        if TILE_MIN_M <= M and _tile.dec_plan(M, N, K) is not None and (
+        if min(TILE_MIN_M, _tile.DEC_MIN_M) <= M and _tile.dec_plan(M, N, K) is not None and (
                 dev is None or _tile.dec_capture_ok(dev, M, N, K)):
             return "decode"
         if use_tile(M, N, K) and (dev is None or _tile.capture_ok(dev, M, N, K)):

@@ -1,4 +1,4 @@
-"""Graph-timed, cold-weight sweep of the Qwen2-7B decode projections at 33-256 rows.
+"""Graph-timed, cold-weight sweep of the Qwen2-7B decode projections at 1-256 rows.
 
 Every arm is captured into one hipGraph of R launches that rotate over >= 1 GiB of weight copies (a decode
 step streams 15 GB of weights, so each matrix arrives cold from HBM), replayed back to back; the time per
@@ -100,8 +100,13 @@ def main():
                             continue
                         G.WS.reserve(dev, G.dec_ws_floats(M, N, ks))
                         arms[f"tail_ks{ks}"] = lambda w, tp=tp, epi=epi: G.gemm_decode(x, w, epi=epi, plan=tp)
+                if plan is not None and M < 33:  # 1-32 rows: the 1- / 2-row-tile decode variants vs the dispatch
+                    epi = G.EPI_SILU if silu else G.EPI_STORE
+                    G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, plan[3])))
+                    arms["decode"] = lambda w, plan=plan, epi=epi: G.gemm_decode(x, w, epi=epi, plan=plan)
                 for d in [int(v) for v in a.depths.replace(":", ",").split(",") if v.strip()]:
-                    if plan is None or plan[0] > (4 if d == 8 else 8) or plan[1] not in (4, 5):
+                    if plan is None or plan[1] not in (4, 5) or plan[0] > (2 if d == 12 else 4 if d == 8 else 8) \
+                            or (plan[0] <= 2 and d == 6):
                         continue
                     epi = G.EPI_SILU if silu else G.EPI_STORE
                     G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, plan[3])))

@@ -387,3 +387,34 @@ def test_gemm_decode_deep_ring(dev, depth, M, N, K, plan, silu):
     assert torch.equal(y0.cpu(), y1.cpu())
     if not silu:
         check(y1, ref(x, w, b), K)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [0, 8, 12])
+@pytest.mark.parametrize("M,N,K,silu", [(1, 4608, 3584, False), (4, 3584, 18944, False), (16, 3584, 3584, False),
+                                        (23, 4608, 1024, False), (32, 2112, 1024, True), (3, 2112, 1024, True)])
+def test_gemm_decode_small_rows(dev, depth, M, N, K, silu):
+    """The 1- / 2-row-tile decode variants (1-32 rows, the reference's 1-4 live sequences) at the default ring
+    and the deep ones (8, 12): the dispatch plan's results against the fp32 reference, and every depth bit for
+    bit the default's."""
+    from githubrepostorag_amd.ops._lib import lib
+
+    plan = G.dec_plan(M, N, K, silu)
+    assert plan is not None and plan[0] == -(-M // 16), plan
+    x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+    epi = G.EPI_SILU if silu else G.EPI_STORE
+    G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, plan[3])))
+    y0 = G.gemm_decode(x, w, b, epi=epi, plan=plan)
+    prev = lib().grag_gemm_decode_depth(depth)
+    try:
+        y1 = G.gemm_decode(x, w, b, epi=epi, plan=plan)
+    finally:
+        lib().grag_gemm_decode_depth(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(y0.cpu(), y1.cpu())
+    if silu:
+        r = ref(x, w, b).view(M, -1, 2, 32)
+        want = torch.nn.functional.silu(r[:, :, 0]) * r[:, :, 1]
+        check(y1, want.reshape(M, -1), K)
+    else:
+        check(y1, ref(x, w, b), K)
