@@ -1236,8 +1236,15 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_gr
                 obj = [(tuple(hub.address), hub.authkey)]
             dist.broadcast_object_list(obj, src=0)
             addr, key = obj[0]
+            rgroup = None
+            if os.environ.get("GRAG_SHARD_TRANSPORT") == "collective":
+                # opt-in: the replicas' shard rounds as lockstep collectives (service/collective.py) on a
+                # communicator of their own; the default stays the socket mesh
+                from githubrepostorag_amd.parallel import comm
+
+                rgroup = comm.Group(list(range(world)), pg=dist.new_group(list(range(world))))
             th = threading.Thread(target=run_replica, args=(rt, addr, key, rank),
-                                  kwargs={"shards": world, "capacity": slots if leader else 0},
+                                  kwargs={"shards": world, "capacity": slots if leader else 0, "group": rgroup},
                                   name="bench-replica", daemon=True)
             th.start()
             if rank == 0:
