@@ -2,7 +2,7 @@
 paged_decode_kernel + attn_combine_kernel) over batch x context: one hipGraph of R launches per arm (the
 decode step replays attention from a graph too), K/V in random blocks, us per call incl. the combine.
 
-python scripts/attn_sweep.py --grid 1:1024,1:4096,1:11600,4:4096,16:4096,176:1500 --splits 64,128,256,512
+python scripts/attn_sweep.py --grid 1:1024/1:4096/1:11600/4:4096/16:4096/176:1500 --splits 64:128:256:512
 """
 import argparse
 import json
@@ -54,7 +54,7 @@ def main():
     Hq, Hkv, D, BS = 28, 4, 128, 16
     out = {}
     with torch.inference_mode():
-        for cell in a.grid.split(","):
+        for cell in a.grid.replace("/", ",").split(","):  # ',' or '/' between cells (gpu_run.sh eats commas)
             B, ctx = (int(v) for v in cell.split(":"))
             nb = B * (-(-ctx // BS)) + 1
             kc = torch.randn(nb, Hkv, BS, D, device=dev, dtype=torch.bfloat16)

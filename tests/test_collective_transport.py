@@ -85,25 +85,31 @@ def _check(rank, world, device="cpu", ipc=False, n_rows=300):
     if [[x.row_id for x in hs] for hs in via_coll.table("chunk").search_pairs(Q[0], pairs, 4)] != ref:
         out["mismatch"].append("pairs")
     out["count"] = via_coll.table("chunk").count()
-    # concurrent fan-outs from 32 threads share lockstep rounds (and stacked launches on the shards)
+    # concurrent fan-outs from 32 threads share lockstep rounds (and stacked launches on the shards); the
+    # mesh runs the same load for comparison
     Qc = torch.nn.functional.normalize(torch.randn(32, D, generator=torch.Generator().manual_seed(rank)), dim=1)
     ref = [[h.row_id for h in hs] for hs in flat.table("chunk").search(Qc, 5, {"namespace": "default"})]
-    res, errs = [None] * 32, []
+    for name, st in (("mesh", via_mesh), ("collective", via_coll)):
+        res, errs = [None] * 32, []
 
-    def job(i):
-        try:
-            res[i] = [h.row_id for h in via_coll.table("chunk").search(Qc[i:i + 1], 5, {"namespace": "default"})[0]]
-        except Exception as e:  # pragma: no cover
-            errs.append(repr(e))
+        def job(i, st=st, res=res, errs=errs):
+            try:
+                res[i] = [h.row_id for h in st.table("chunk").search(Qc[i:i + 1], 5, {"namespace": "default"})[0]]
+            except Exception as e:  # pragma: no cover
+                errs.append(repr(e))
 
-    b0 = coll.stats["busy_rounds"]
-    ths = [threading.Thread(target=job, args=(i,)) for i in range(32)]
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join()
-    out["concurrent_ok"] = not errs and res == ref
-    out["busy_rounds"] = coll.stats["busy_rounds"] - b0
+        b0 = coll.stats["busy_rounds"]
+        dist.barrier()
+        ths = [threading.Thread(target=job, args=(i,)) for i in range(32)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        bad = [(i, res[i], ref[i]) for i in range(32) if res[i] != ref[i]]
+        out[f"concurrent_{name}"] = {"errors": errs[:3], "mismatches": len(bad), "first": bad[:2]}
+        if name == "collective":
+            out["concurrent_ok"] = not errs and not bad
+            out["busy_rounds"] = coll.stats["busy_rounds"] - b0
     # round latency of each transport (sequential single-query fan-outs)
     lat = {}
     for name, st in (("mesh", via_mesh), ("collective", via_coll)):
@@ -129,7 +135,7 @@ def test_collective_transport_matches_flat_and_mesh_cpu():
     for r, o in enumerate(outs):
         assert o["mismatch"] == [], (r, o["mismatch"])
         assert o["count"] == 300
-        assert o["concurrent_ok"], r
+        assert o["concurrent_ok"], (r, o["concurrent_mesh"], o["concurrent_collective"])
         assert o["busy_rounds"] < 32, o["busy_rounds"]  # 32 fan-outs shared rounds
         assert o["closed"]
         assert o["stats"]["degraded_rounds"] == 0 and o["stats"]["served"] > 0
@@ -143,7 +149,8 @@ def test_collective_transport_device_exchange_two_replicas_on_one_gpu():
     outs = run_ranks(_check, 2, "cuda:0", True)
     for r, o in enumerate(outs):
         assert o["mismatch"] == [], (r, o["mismatch"])
-        assert o["count"] == 300 and o["concurrent_ok"] and o["closed"]
+        assert o["count"] == 300 and o["closed"]
+        assert o["concurrent_ok"], (r, o["concurrent_mesh"], o["concurrent_collective"], o["stats"])
         assert o["stats"]["device_exchanges"] > 0 and o["stats"].get("device_detached", 0) == 0
         print(f"replica {r}: round p50 mesh {o['p50_ms']['mesh']:.3f} ms, "
               f"collective {o['p50_ms']['collective']:.3f} ms; {o['stats']}")
