@@ -155,6 +155,9 @@ def parse():
                     help="after the closed loop: open-loop Poisson arrivals of query groups at these fractions of "
                          "the closed loop's throughput through the same serving loop (serving_runner.open_loop: "
                          "TTFT p50 / p90 at each load; empty: skip)")
+    ap.add_argument("--bulk-prefill", type=int, default=1024,
+                    help="of --interactive-prefill, the prefill tokens per step bulk work (ingest) may take while "
+                         "interactive arrivals keep coming (EngineRunner bulk_prefill; 0: no separate cap)")
     ap.add_argument("--low-load", type=int, default=1,
                     help="1: the reference's own regime (vLLM --max-num-seqs 4 --max-model-len 11712): single-prompt "
                          "TTFT at 1K / 4K / 11.6K tokens, decode TPOT at 1 / 4 / 16 live sequences x those contexts "
@@ -924,7 +927,8 @@ def serving_runner_phase(args, eng, prepare, sp, U, u, A, S, steps, dev, dp_size
 
     B = u * A
     pg = group if world > 1 else None
-    runner = EngineRunner(eng, watchdog_s=0, interactive_prefill=args.interactive_prefill)
+    runner = EngineRunner(eng, watchdog_s=0, interactive_prefill=args.interactive_prefill,
+                          bulk_prefill=args.bulk_prefill)
     res_open = []
     try:
         pump = _ArrivalPump(runner, prepare, sp, u, pg, dev)
@@ -1002,6 +1006,7 @@ def serving_runner_phase(args, eng, prepare, sp, U, u, A, S, steps, dev, dp_size
             "steady_state_decode_ratio": round((dec1 - dec0) / max(1, B * steps * (args.gen_len - 1)), 3),
             "arrival_window": os.environ.get("GRAG_ARRIVAL_WINDOW", "auto"),
             "interactive_prefill_tokens": args.interactive_prefill or None,
+            "bulk_prefill_tokens": args.bulk_prefill or None,
             "loop": "engine/runner.py EngineRunner thread (free-running; decode replays paced by the arrival rate: "
                     "engine/runner.py _window); per-query arrivals through a retrieval micro-batcher "
                     "(_ArrivalPump), each prompt submitted on its own; closed loop at the harness's concurrency"}
@@ -1074,7 +1079,8 @@ def concurrent_phase(args, model, tok, emb, prepare, sp, u, dev, group, world, d
                                                     top_p=EngineLLM.INGEST["top_p"]))
         n += eng.warmup_graphs(max_ctx=[2048, 4096], windows=(1, 2, 4, 8), params=q_sp)
         log(f"concurrent phase: {n} decode graphs captured in {time.perf_counter() - t0:.1f}s")
-    runner = EngineRunner(eng, watchdog_s=0, interactive_prefill=args.interactive_prefill)
+    runner = EngineRunner(eng, watchdog_s=0, interactive_prefill=args.interactive_prefill,
+                          bulk_prefill=args.bulk_prefill)
     pg = group if world > 1 else None
     rate = base["offered_queries_per_s"]
     out = {}

@@ -229,14 +229,15 @@ class LLMEngine:
                           seq.cached_prefix, seq.first_token_time)
 
     # ------------------------------------------------------------------ step
-    def step(self, max_window: int | None = None, prefill_budget: int | None = None) -> list[Sequence]:
+    def step(self, max_window: int | None = None, prefill_budget: int | None = None,
+             bulk_budget: int | None = None) -> list[Sequence]:
         """Run one scheduler step; returns sequences that finished in it.
         ``max_window`` caps the decode window (tokens per sequence this step); ``prefill_budget`` caps this
         step's prefill tokens (Scheduler.schedule)."""
         t0 = time.perf_counter()
         try:
             with self._on_stream():
-                return self._step(max_window, prefill_budget)
+                return self._step(max_window, prefill_budget, bulk_budget)
         finally:
             self.stats["step_s"] += time.perf_counter() - t0
 
@@ -244,12 +245,13 @@ class LLMEngine:
         return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
 
     @torch.inference_mode()
-    def _step(self, max_window: int | None = None, prefill_budget: int | None = None) -> list[Sequence]:
+    def _step(self, max_window: int | None = None, prefill_budget: int | None = None,
+              bulk_budget: int | None = None) -> list[Sequence]:
         th = time.perf_counter()
         finished = self.sched.reap_cancelled()
         for s in finished:
             self._notify(s, None, True)
-        kind, items = self.sched.schedule(prefill_budget)
+        kind, items = self.sched.schedule(prefill_budget, bulk_budget)
         for s in getattr(self.sched, "last_rejected", []):
             s.finish_time = time.perf_counter()
             self._notify(s, None, True)

@@ -27,6 +27,7 @@ returns, the engine is marked healthy again.
 from __future__ import annotations
 
 import contextlib
+import dataclasses
 import logging
 import os
 import queue
@@ -37,6 +38,7 @@ import torch
 
 from ..utils.gpu_guard import set_device_of
 from .llm_engine import LLMEngine
+from .scheduler import INTERACTIVE_PRIORITY
 from .sequence import Completion, SamplingParams
 
 log = logging.getLogger(__name__)
@@ -104,11 +106,17 @@ class EngineRunner:
     # first of them do not wait for the whole burst's prefill (a decode replay of K steps is the other
     # wait an arrival sees: paced by _window)
     INTERACTIVE_PREFILL = int(os.environ.get("GRAG_INTERACTIVE_PREFILL", "0"))
+    # of that budget, the tokens bulk work (ingest: submitted with interactive=False) may take per step while
+    # interactive arrivals keep coming: the step an arrival waits for and the step carrying its prompt stay
+    # short; 0 = no separate cap
+    BULK_PREFILL = int(os.environ.get("GRAG_BULK_PREFILL", "1024"))
 
     def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005, watchdog_s: float = 120.0,
-                 on_health=None, tp=None, start: bool = True, interactive_prefill: int | None = None):
+                 on_health=None, tp=None, start: bool = True, interactive_prefill: int | None = None,
+                 bulk_prefill: int | None = None):
         self.engine = engine
         self.interactive_prefill = self.INTERACTIVE_PREFILL if interactive_prefill is None else interactive_prefill
+        self.bulk_prefill = self.BULK_PREFILL if bulk_prefill is None else bulk_prefill
         self._last_submit = -1e9
         self.tp = tp if tp is not None and not tp.trivial else None
         self.leader = self.tp is None or self.tp.rank == 0
@@ -155,6 +163,10 @@ class EngineRunner:
 
         rid = uuid.uuid4().hex
         h = GenerationHandle(self, rid)
+        if interactive:  # someone waits for it: ahead of bulk work in admission and in each step's budget
+            p = params if params is not None else SamplingParams()
+            if p.priority < INTERACTIVE_PRIORITY:
+                params = dataclasses.replace(p, priority=INTERACTIVE_PRIORITY)
         with self._cv:
             self._handles[rid] = h
             self._pending.append((rid, prompt, params, on_token))
@@ -198,16 +210,15 @@ class EngineRunner:
             return None
         return max(1, min(self.MAX_WINDOW, int(0.5 * g / d)))
 
-    def _prefill_budget(self) -> int | None:
-        """This step's prefill token cap: the interactive budget while arrivals are pending or paced."""
+    def _prefill_budget(self) -> tuple[int | None, int | None]:
+        """This step's (prefill token cap, bulk share of it): the interactive budget while arrivals are
+        pending or paced, and then at most BULK_PREFILL tokens of it for bulk requests."""
         if not self.interactive_prefill or self.tp is not None:
-            return None
-        if self._expecting > 0:
-            return self.interactive_prefill
+            return None, None
         g = self._gap
-        if g is not None and time.monotonic() - self._last_event <= 2 * g:
-            return self.interactive_prefill
-        return None
+        if self._expecting > 0 or (g is not None and time.monotonic() - self._last_event <= 2 * g):
+            return self.interactive_prefill, (self.bulk_prefill or None)
+        return None, None
 
     def generate(self, prompt, params: SamplingParams | None = None, on_token=None,
                  timeout: float | None = None) -> Completion:
@@ -470,7 +481,8 @@ class EngineRunner:
                 st = self.engine.stats
                 ds0, dt0 = st.get("decode_steps", 0), st.get("decode_s", 0.0)
                 try:
-                    self._complete(self.engine.step(max_window=win, prefill_budget=self._prefill_budget()))
+                    pb, bb = self._prefill_budget()
+                    self._complete(self.engine.step(max_window=win, prefill_budget=pb, bulk_budget=bb))
                 finally:
                     self._flush_notes()
                 n = st.get("decode_steps", 0) - ds0

@@ -34,6 +34,10 @@ from ..utils.runtime import rt
 from .sequence import Sequence, SeqStatus
 
 
+# requests someone waits on (EngineRunner.submit(interactive=True) raises them to this); below it is bulk work
+INTERACTIVE_PRIORITY = 2
+
+
 class KVCacheManager:
     SCRATCH_BLOCK = 0  # never handed out: padding rows of graph-captured batches point here
 
@@ -221,34 +225,54 @@ class Scheduler:
         self.waiting.appendleft(v)
         return True
 
-    def schedule(self, budget: int | None = None):
+    def schedule(self, budget: int | None = None, bulk_budget: int | None = None):
         """Returns ("prefill", [(seq, start, end)]), ("mixed", prefill items then
         one-token decode items), ("decode", [(seq, pos, pos+1)]) or (None, []).
         ``budget``: this step's prefill token budget (default max_num_batched_tokens; the serving loop
         passes a smaller one while interactive arrivals queue, so one step never carries a burst's worth
-        of prompts and the first of them reach their first token sooner)."""
+        of prompts and the first of them reach their first token sooner).  ``bulk_budget``: of that, at most
+        this many tokens for requests below INTERACTIVE_PRIORITY (ingest beside the serving loop: the step an
+        arrival waits for, and the step that carries its prompt, stay short)."""
         with self.lock:
             budget = min(budget or self.max_num_batched_tokens, self.max_num_batched_tokens)
             items = []
+            admitted = []
+            # the prompt blocks this step computes are registered as they are scheduled: later admissions of
+            # the same step share them
+            registered = []
             # continue partially prefilled running sequences (the ones whose prompt is done drop out here)
             if self.prefilling:
                 self.prefilling = [q for q in self.prefilling if q.status == SeqStatus.RUNNING and q.is_prefill]
-            for seq in self.prefilling:
-                if budget <= 0:
+            # one merged order: chunks of prompts already in prefill and new admissions, higher priority first,
+            # in-flight prompts first within a priority -- an interactive arrival (priority 2) takes this step's
+            # budget ahead of the remaining chunks of a bulk ingest prompt admitted earlier
+            pf = sorted(self.prefilling, key=lambda q: -q.params.priority) if self.prefilling else []
+            i = 0
+            admit_ok = True
+            bulk_left = bulk_budget if bulk_budget is not None else 1 << 30
+
+            def cap(seq, n):  # the bulk share of this step's budget
+                return n if seq.params.priority >= INTERACTIVE_PRIORITY else min(n, bulk_left)
+
+            while budget > 0:
+                can_admit = (admit_ok and self.waiting and self.free_slots
+                             and len(self.running) < self.max_num_seqs)
+                if i < len(pf) and (not can_admit or pf[i].params.priority >= self.waiting[0].params.priority):
+                    seq = pf[i]
+                    i += 1
+                    out_ids = seq.output_ids
+                    if seq.num_computed < len(seq.prompt_ids) + len(out_ids) - (1 if out_ids else 0):  # is_prefill
+                        tgt = self.prefill_target(seq)
+                        n = cap(seq, min(tgt - seq.num_computed, budget))
+                        if n > 0 and self.kv.ensure(seq, seq.num_computed + n):
+                            items.append((seq, seq.num_computed, seq.num_computed + n))
+                            registered += self.kv.register_full_blocks(seq, upto=seq.num_computed + n)
+                            budget -= n
+                            if seq.params.priority < INTERACTIVE_PRIORITY:
+                                bulk_left -= n
+                    continue
+                if not can_admit:
                     break
-                out_ids = seq.output_ids
-                if seq.num_computed < len(seq.prompt_ids) + len(out_ids) - (1 if out_ids else 0):  # is_prefill
-                    tgt = self.prefill_target(seq)
-                    n = min(tgt - seq.num_computed, budget)
-                    if n > 0 and self.kv.ensure(seq, seq.num_computed + n):
-                        items.append((seq, seq.num_computed, seq.num_computed + n))
-                        budget -= n
-            admitted = []
-            # the prompt blocks this step computes are registered now: later admissions share them
-            registered = []
-            for seq, _, b in items:
-                registered += self.kv.register_full_blocks(seq, upto=b)
-            while self.waiting and budget > 0 and self.free_slots and len(self.running) < self.max_num_seqs:
                 seq = self.waiting[0]
                 if seq.total_len >= self.max_model_len:
                     self.waiting.popleft()
@@ -256,19 +280,24 @@ class Scheduler:
                     self._finish(seq)
                     admitted.append(("rejected", seq))
                     continue
+                if seq.params.priority < INTERACTIVE_PRIORITY and bulk_left <= 0:
+                    admit_ok = False  # (waiting is priority-ordered: only bulk requests follow)
+                    continue
                 if not seq.blocks:
                     self.kv.match_prefix(seq)
                 tgt = self.prefill_target(seq)
-                n = min(tgt - seq.num_computed, budget)
+                n = cap(seq, min(tgt - seq.num_computed, budget))
                 # decode watermark: an admission must leave one free block per running sequence, so the next
                 # decode window's block-boundary crossings never preempt (admitting into the last free
                 # blocks and preempting at the next decode step recomputes whole prompts: at 1024 agent jobs
                 # on one GPU that thrash dominated, profiles/agent_saturation_r4.json)
                 if self.running and self.kv.num_free - self.kv.blocks_needed(seq, seq.num_computed + max(n, 0)) \
                         < len(self.running) + 1:
-                    break
+                    admit_ok = False
+                    continue
                 if n <= 0 or not self.kv.ensure(seq, seq.num_computed + n):
-                    break
+                    admit_ok = False
+                    continue
                 self.waiting.popleft()
                 seq.slot = self.free_slots.pop()
                 seq.status = SeqStatus.RUNNING
@@ -278,6 +307,8 @@ class Scheduler:
                 items.append((seq, seq.num_computed, seq.num_computed + n))
                 registered += self.kv.register_full_blocks(seq, upto=seq.num_computed + n)
                 budget -= n
+                if seq.params.priority < INTERACTIVE_PRIORITY:
+                    bulk_left -= n
             self.last_registered = registered
             self.last_admitted = [s for tag, s in admitted if tag == "admitted"]
             self.last_rejected = [s for tag, s in admitted if tag == "rejected"]

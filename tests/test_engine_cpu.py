@@ -264,6 +264,51 @@ def test_priority_admission_order(model, tok):
     assert order == [ids[0], ids[2], ids[3], ids[1]]
 
 
+def test_interactive_prefill_ahead_of_bulk_chunks(model, tok):
+    """A higher-priority arrival takes the next step's prefill budget ahead of the remaining chunks of a bulk
+    prompt already in chunked prefill (ingest running beside the serving loop); greedy outputs unchanged."""
+    cfg = EngineConfig(max_num_seqs=4, max_model_len=512, num_blocks=256, max_num_batched_tokens=32,
+                       use_cuda_graph=False)
+    bulk = SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True)
+    hi = SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True, priority=2)
+    long_prompt = [(7 * i) % 200 + 3 for i in range(160)]  # 5 chunks of 32
+    eng = LLMEngine(model, tok, cfg)
+    rb = eng.add_request(long_prompt, bulk)
+    eng.step()  # first chunk of the bulk prompt
+    rh = eng.add_request([11, 12, 13, 14], hi)
+    eng.step()
+    h, b = eng.get(rh), eng.get(rb)
+    assert h.num_computed == 4, h.num_computed  # the arrival was prefilled in this step ...
+    assert b.num_computed == 32 + 28, b.num_computed  # ... and the bulk prompt took the rest of the budget
+    while eng.has_unfinished():
+        eng.step()
+    ref = LLMEngine(model, tok, cfg)
+    r1, r2 = ref.add_request(long_prompt, bulk), ref.add_request([11, 12, 13, 14], hi)
+    while ref.has_unfinished():
+        ref.step()
+    assert eng.get(rb).output_ids == ref.get(r1).output_ids and eng.get(rh).output_ids == ref.get(r2).output_ids
+
+
+def test_bulk_budget_caps_low_priority_prefill(model, tok):
+    """``bulk_budget``: requests below INTERACTIVE_PRIORITY take at most that many of a step's prefill tokens;
+    interactive ones are not capped (EngineRunner passes it while arrivals keep coming)."""
+    from githubrepostorag_amd.engine.scheduler import INTERACTIVE_PRIORITY
+
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_model_len=512, num_blocks=256,
+                                             max_num_batched_tokens=64, use_cuda_graph=False))
+    bulk = SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True)
+    hi = SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True, priority=INTERACTIVE_PRIORITY)
+    rb = eng.add_request([(5 * i) % 200 + 3 for i in range(100)], bulk)
+    rh = eng.add_request([(3 * i) % 200 + 3 for i in range(40)], hi)
+    eng.step(prefill_budget=64, bulk_budget=8)
+    assert eng.get(rh).num_computed == 40 and eng.get(rb).num_computed == 8
+    eng.step(prefill_budget=64, bulk_budget=8)  # the interactive prompt decodes; bulk gets 8 more
+    assert eng.get(rb).num_computed <= 16
+    while eng.has_unfinished():
+        eng.step()
+    assert eng.get(rb).finish_reason and eng.get(rh).finish_reason
+
+
 def test_mixed_prefill_decode_steps_identical(model, tok):
     """Decode tokens riding along in prefill steps (one weight pass for both)
     give the same greedy outputs as separate prefill / decode steps."""

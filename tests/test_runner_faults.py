@@ -49,7 +49,7 @@ class FakeEngine:
     def completion(self, seq):
         return Completion(seq.req_id, "done", [1], "length", 1, 0.0, 0.0)
 
-    def step(self, max_window=None, prefill_budget=None):
+    def step(self, max_window=None, prefill_budget=None, bulk_budget=None):
         if self.mode == "raise":
             self.mode = "ok"
             self.reqs.clear()
