@@ -131,6 +131,10 @@ __global__ __launch_bounds__(64 * NWAVES) void score_topk_kernel(TopkParams p) {
   const int d = p.d;
   const int RB = 2 * d;   // bytes per query row in LDS
   const int CPR = d / 8;  // 16-B chunks per row
+  // XOR swizzle within aligned blocks of SWZ + 1 chunks: SWZ + 1 = the largest power of two (<= 16) dividing
+  // CPR, so (ch ^ m) stays inside the row for every d % 32 == 0 (d = 32 / 64 / 96 rows have 4 / 8 / 12
+  // chunks: a plain 15-mask would write past the row and past the tile)
+  const int SWZ = min(16, CPR & -CPR) - 1;
 
   int64_t r0, r1;
   int64_t slot_base;
@@ -145,7 +149,7 @@ __global__ __launch_bounds__(64 * NWAVES) void score_topk_kernel(TopkParams p) {
     slot_base = ((int64_t)blockIdx.y * p.nchunks + blockIdx.x) * NQ;
   }
 
-  // stage the query tile: row qq, chunk ch -> qq*RB + ((ch ^ (qq & 15)) << 4)
+  // stage the query tile: row qq, chunk ch -> qq*RB + ((ch ^ (qq & SWZ)) << 4)
   for (int c = threadIdx.x; c < NQ * CPR; c += 64 * NWAVES) {
     const int qq = c / CPR, ch = c % CPR;
     int qidx;
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(64 * NWAVES) void score_topk_kernel(TopkParams p) {
     else qidx = blockIdx.y * NQ + qq;
     bf16x8_t val = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
     if (qidx >= 0 && qidx < p.nq) val = *reinterpret_cast<const bf16x8_t*>(p.Q + (int64_t)qidx * d + ch * 8);
-    *reinterpret_cast<bf16x8_t*>(qlds + qq * RB + ((ch ^ (qq & 15)) << 4)) = val;
+    *reinterpret_cast<bf16x8_t*>(qlds + qq * RB + ((ch ^ (qq & SWZ)) << 4)) = val;
   }
   __syncthreads();
 
@@ -203,7 +207,7 @@ __global__ __launch_bounds__(64 * NWAVES) void score_topk_kernel(TopkParams p) {
           for (int qt = 0; qt < NQT; ++qt) {
             const int qq = qt * 16 + li;
             const int ch = 4 * (c + u) + h4;
-            const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(qlds + qq * RB + ((ch ^ (qq & 15)) << 4));
+            const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(qlds + qq * RB + ((ch ^ (qq & SWZ)) << 4));
             acc[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b, acc[qt], 0, 0, 0);
           }
         }

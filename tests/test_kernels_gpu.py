@@ -233,7 +233,8 @@ def _unit(n, d, dev, seed):
     return (x / x.norm(dim=1, keepdim=True)).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("nq,k,d", [(1, 10, 384), (5, 16, 1024), (40, 10, 768), (64, 8, 256), (20, 32, 384)])
+@pytest.mark.parametrize("nq,k,d", [(1, 10, 384), (5, 16, 1024), (40, 10, 768), (64, 8, 256), (20, 32, 384),
+                                    (32, 5, 32), (40, 10, 64), (16, 8, 96)])
 def test_score_topk(dev, nq, k, d):
     X = _unit(20000, d, dev, 1)
     Q = _unit(nq, d, dev, 2)
