@@ -320,9 +320,18 @@ _DEC_ON = os.environ.get("GRAG_DECODE_GEMM", "1") != "0"
 DEC_VARIANTS = [(1, 4, 2), (1, 5, 2), (2, 4, 2), (2, 5, 2), (4, 4, 2), (4, 5, 2), (8, 4, 2), (8, 5, 2), (12, 5, 2),
                 (12, 8, 2), (16, 4, 2)]
 DEC_MAX_M = int(os.environ.get("GRAG_DECODE_MAX_M", "256"))
-# smallest batch the decode kernel takes in the dispatch (ops/linear.kernel_for, mlp_gate_up): 33 keeps 1-32 rows on
-# the skinny / stream kernels and the tile kernel's gate/up; 1 sends them to the 1- / 2-row-tile decode variants
+# batches from this size take the decode kernel on every projection shape (A/B knob); below it dec_small decides
 DEC_MIN_M = int(os.environ.get("GRAG_DEC_MIN_M", "33"))
+
+
+def dec_small(M: int, N: int, K: int, silu: bool = False) -> bool:
+    """1-32 rows (the reference's 1-4 live sequences): the 1- / 2-row-tile decode variants where the hipGraph-
+    timed cold-weight sweep measured them faster (profiles/gemm_graph_sweep_r5_depths_smallM.json): gate/up
+    49-52 us vs the tile kernel's 76-79 (5.2-5.5 TB/s), down_proj (K >= 4 N) 30-31 vs skinny / library
+    31-38 us; qkv / o stay on skinny / library (9-12 vs 12-13 us).  Deeper rings (8 / 12) measured slower."""
+    if M >= 33 or M < 1:
+        return False
+    return M >= DEC_MIN_M or silu or K >= 4 * N
 
 
 def dec_variants(M: int) -> list[tuple[int, int, int]]:
@@ -556,7 +565,7 @@ def mlp_gate_up(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None =
     """SwiGLU input half for an interleaved gate/up weight: the fused tile
     kernel when it takes the shape, else library GEMM + reshape (same math)."""
     M, K = x.shape
-    if x.is_cuda and M >= DEC_MIN_M and supported(x, w_gu) and dec_plan(M, w_gu.shape[0], K, True) is not None \
+    if x.is_cuda and (M >= 33 or dec_small(M, w_gu.shape[0], K, True)) and supported(x, w_gu) and dec_plan(M, w_gu.shape[0], K, True) is not None \
             and dec_capture_ok(x.device, M, w_gu.shape[0], K, True):
         return gemm_decode(x, w_gu, b_gu, epi=EPI_SILU)
     if not x.is_cuda or (supported(x, w_gu) and capture_ok(x.device, M, w_gu.shape[0], K, True)):

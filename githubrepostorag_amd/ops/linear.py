@@ -269,7 +269,7 @@ def kernel_for(M: int, N: int, K: int, tile_ok: bool = True, dev: torch.device |
     the split-K / stream-K workspaces (None: plan as in steady state, workspaces ready)."""
     capturing = dev is not None and torch.cuda.is_current_stream_capturing()
     if tile_ok:
-        if min(TILE_MIN_M, _tile.DEC_MIN_M) <= M and _tile.dec_plan(M, N, K) is not None and (
+        if (TILE_MIN_M <= M or _tile.dec_small(M, N, K)) and _tile.dec_plan(M, N, K) is not None and (
                 dev is None or _tile.dec_capture_ok(dev, M, N, K)):
             return "decode"
         if use_tile(M, N, K) and (dev is None or _tile.capture_ok(dev, M, N, K)):
@@ -336,7 +336,7 @@ def linear_deferred(x: torch.Tensor, w: torch.Tensor):
             and w.dtype == torch.bfloat16 and x.stride(1) == 1 and w.stride(1) == 1 and _tile.supported(x, w)):
         M, K = x.shape
         N = w.shape[0]
-        if M >= TILE_MIN_M:
+        if M >= TILE_MIN_M or _tile.dec_small(M, N, K):
             how = _tile.deferred_plan(M, N, K)
             if how is not None and (not torch.cuda.is_current_stream_capturing()
                                     or _tile.WS.ready(x.device, how[1] * M * N)):
