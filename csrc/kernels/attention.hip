@@ -790,6 +790,262 @@ __global__ __launch_bounds__(D) void attn_combine_kernel(AttnParams p) {
   p.out[(size_t)tok * p.out_stride + (size_t)head * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
 }
 
+// ---------------------------------------------------------------------------
+// Small-batch decode (the reference's own regime: 1-16 live sequences, contexts up to 11.7K; vLLM
+// --max-num-seqs 4).  paged_decode_kernel puts ONE wave on a (sequence, kv head, split) and merges the
+// splits in a second launch: at B = 1 the grid is 4 kv heads x splits, each wave walks its tiles one
+// round trip at a time, and the combine pass re-reads every split's partial -- 15 / 25 / 38-49 us per
+// layer at 1K / 4K / 11.6K keys for 2 / 8 / 24 MB of K/V (profiles/attn_sweep_r5.json).  Here:
+//   * NW waves share one (sequence, kv head, split) and take its 32-key tiles round robin, each wave with
+//     its own 2-stage LDS-DMA ring (the single-wave kernel's body), so a split keeps NW tiles in flight and
+//     the split count -- the number of partials to merge -- drops NW-fold for the same parallelism;
+//   * the waves' (m, l, O) merge in LDS (the rings' space, after a barrier);
+//   * the splits of one (sequence, kv head) merge IN this launch: each workgroup writes its partial, takes
+//     an agent-scope ticket (release fence first, as gemm_stream.hip's split tiles), and the last arriver
+//     (acquire) reads the others' partials and writes the output; it resets its counter, so the launch
+//     replays inside hipGraphs without a memset.  No second kernel, no partial round trip for the others.
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, unsigned* counters) {
+  constexpr int TK = 32, NS = 2;
+  constexpr int NT16 = TK / 16, NCC = TK / 32;
+  constexpr int RB = 2 * D;
+  constexpr int CPR = D / 8;
+  constexpr int NC = D / 32;
+  constexpr int ND = D / 16;
+  constexpr int TILE = TK * RB;      // bytes per K (or V) tile
+  constexpr int NI = TILE / 1024;    // LDS-DMA instructions per tile per tensor
+  constexpr int RPI = 1024 / RB;     // rows per instruction
+  static_assert((NS - 1) * 2 * NI <= 63, "vmcnt range");
+  static_assert((NW * 16 * D + NW * 32 + 1) * 4 <= NW * NS * 2 * TILE, "merge scratch fits in the rings");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h4 = lane >> 4, li = lane & 15;
+  const int seq = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
+  const int ctx = p.ctx_len[seq];
+  const int kv_lo = split * p.split_len;
+  const int kv_hi = min(ctx, kv_lo + p.split_len);
+  if (kv_lo >= kv_hi) return;  // (workgroup-uniform) past this sequence's last split: no ticket either
+  const int G = p.G;
+  const int tok = p.q_start[seq];
+  const int nvalid = min(p.num_splits, (ctx + p.split_len - 1) / p.split_len);
+  bf16x8_t qf[NC];
+  {
+    const bf16* qp = p.q + (size_t)tok * p.q_stride + (size_t)(kvh * G + (li < G ? li : 0)) * D + 8 * h4;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) qf[c] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * c);
+  }
+  const int32_t* bt = p.block_tables + (size_t)seq * p.bt_stride;
+  const int lrow = lane / CPR, lch = lane % CPR;
+  const int nblk_seq = (ctx + p.BS - 1) / p.BS;
+  int win = ((kv_lo + w * TK) / p.BS) >> 6;
+  int bvec = bt[min((win << 6) + lane, nblk_seq - 1)];
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): Q and block ids retired before the counted DMA pipeline
+#pragma unroll
+  for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(qf[c]));
+  asm volatile("" : "+v"(bvec));
+
+  char* ring = smem + w * NS * 2 * TILE;
+  auto issue = [&](int kt0, int stage) {
+    char* kdst = ring + stage * 2 * TILE;
+    char* vdst = kdst + TILE;
+    const int wn = (kt0 / p.BS) >> 6;
+    if (wn != win) {
+      win = wn;
+      bvec = bt[min((wn << 6) + lane, nblk_seq - 1)];
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int key0 = min(kt0 + i * RPI, ctx - 1);
+      const int blk = __builtin_amdgcn_readlane(bvec, (key0 / p.BS) & 63);
+      const int row = i * RPI + lrow;
+      const int key = min(kt0 + row, ctx - 1);
+      const size_t off = (((size_t)blk * p.Hkv + kvh) * p.BS + (key % p.BS)) * D;
+      glds16(p.k + off + ((lch ^ kswz<D>(row)) << 3), kdst + i * 1024);
+      glds16(p.v + off + ((lch ^ vswz<D>(row)) << 3), vdst + i * 1024);
+    }
+  };
+
+  float m = -INFINITY, lsum = 0.f;
+  f32x4_t o[ND];
+#pragma unroll
+  for (int n = 0; n < ND; ++n) o[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int ntot = (kv_hi - kv_lo + TK - 1) / TK;
+  const int nmine = w < ntot ? (ntot - w + NW - 1) / NW : 0;  // this wave's tiles: w, w + NW, ...
+  if (nmine > 0) issue(kv_lo + w * TK, 0);
+  for (int t = 0; t < nmine; ++t) {
+    const int stage = t & 1;
+    const int kt0 = kv_lo + (w + t * NW) * TK;
+    if (t + 1 < nmine) {
+      issue(kt0 + NW * TK, stage ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");  // tile t landed, t + 1 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const char* k_lds = ring + stage * 2 * TILE;
+    const char* v_lds = k_lds + TILE;
+    f32x4_t sc[NT16];
+#pragma unroll
+    for (int tt = 0; tt < NT16; ++tt) {
+      sc[tt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int row = 16 * tt + li;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const bf16x8_t a =
+            *reinterpret_cast<const bf16x8_t*>(k_lds + row * RB + (((4 * c + h4) ^ kswz<D>(row)) << 4));
+        sc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[c], sc[tt], 0, 0, 0);
+      }
+    }
+    float tmax = -INFINITY;
+    const bool tail = kt0 + TK > kv_hi;
+#pragma unroll
+    for (int tt = 0; tt < NT16; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (tail) {
+          const int key = kt0 + 16 * tt + 4 * h4 + r;
+          sc[tt][r] = key >= kv_hi ? -INFINITY : sc[tt][r];
+        }
+        tmax = fmaxf(tmax, sc[tt][r]);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_cand = fmaxf(m, tmax * p.scale_log2);
+    if (__any(m_cand > m + kRescaleLog2)) {
+      const float m_use = m_cand == -INFINITY ? 0.f : m_cand;
+      const float alpha = exp2f(m - m_use);
+      m = m_cand;
+      lsum *= alpha;
+#pragma unroll
+      for (int n = 0; n < ND; ++n) o[n] *= alpha;
+    }
+    const float nm = m == -INFINITY ? 0.f : -m;
+    float pr[NT16][4];
+#pragma unroll
+    for (int tt = 0; tt < NT16; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pr[tt][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[tt][r], p.scale_log2, nm));
+        lsum += pr[tt][r];
+      }
+    const int tq = li >> 2, tp = li & 3;
+#pragma unroll
+    for (int cc = 0; cc < NCC; ++cc) {
+      bf16x8_t bp;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bp[r] = f2bits(pr[2 * cc][r]);
+        bp[4 + r] = f2bits(pr[2 * cc + 1][r]);
+      }
+      const int r0 = 32 * cc + 4 * h4 + tq;
+      const int r1 = r0 + 16;
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+        const int unit = 4 * n + tp;
+        const int b0 = r0 * RB + ((unit ^ (vswz<D>(r0) << 1)) << 3);
+        const int b1 = r1 * RB + ((unit ^ (vswz<D>(r1) << 1)) << 3);
+        const bf16x4_t a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(v_lds + b0));
+        const bf16x4_t a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(v_lds + b1));
+        const bf16x8_t a = bf16x8_t{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bp, o[n], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this stage's LDS reads done before its refill
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+
+  // ---- the waves' states merge in LDS (the rings are free once every wave passed the barrier)
+  __syncthreads();
+  float* so = reinterpret_cast<float*>(smem);  // [NW][16 rows][D]: lane (li, h4) holds O[row li][16 n + 4 h4 + r]
+  float* sml = so + NW * 16 * D;               // [NW][16][2]: (m, l)
+  unsigned* flag = reinterpret_cast<unsigned*>(sml + NW * 32);
+#pragma unroll
+  for (int n = 0; n < ND; ++n)
+    *reinterpret_cast<f32x4_t*>(so + (w * 16 + li) * D + 16 * n + 4 * h4) = o[n];
+  if (h4 == 0) {
+    sml[(w * 16 + li) * 2] = m;
+    sml[(w * 16 + li) * 2 + 1] = lsum;
+  }
+  __syncthreads();
+  const bool single = nvalid <= 1;
+  for (int idx = threadIdx.x; idx < G * D; idx += 64 * NW) {
+    const int row = idx / D, d = idx % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int wv = 0; wv < NW; ++wv) M = fmaxf(M, sml[(wv * 16 + row) * 2]);
+    float L = 0.f, acc = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int wv = 0; wv < NW; ++wv) {
+        const float wt = exp2f(sml[(wv * 16 + row) * 2] - M);
+        L += sml[(wv * 16 + row) * 2 + 1] * wt;
+        acc += so[(wv * 16 + row) * D + d] * wt;
+      }
+    }
+    const int head = kvh * G + row;
+    if (single) {
+      p.out[(size_t)tok * p.out_stride + (size_t)head * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+    } else {
+      const size_t base = ((size_t)split * p.total_q + tok) * p.Hq + head;
+      p.part_o[base * D + d] = acc;
+      if (d == 0) {
+        p.part_ml[base * 2] = M;
+        p.part_ml[base * 2 + 1] = L;
+      }
+    }
+  }
+  if (single) return;
+
+  // ---- the splits of this (sequence, kv head) merge in the last arriving workgroup
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned* cnt = counters + (size_t)seq * p.Hkv + kvh;
+    const unsigned tk = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = tk == (unsigned)(nvalid - 1) ? 1u : 0u;
+    if (last) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (flag[0] == 0u) return;
+  for (int idx = threadIdx.x; idx < G * D; idx += 64 * NW) {
+    const int row = idx / D, d = idx % D;
+    const int head = kvh * G + row;
+    float M = -INFINITY;
+    for (int sp = 0; sp < nvalid; ++sp) M = fmaxf(M, p.part_ml[(((size_t)sp * p.total_q + tok) * p.Hq + head) * 2]);
+    const float Mu = M == -INFINITY ? 0.f : M;
+    float L = 0.f, acc = 0.f;
+#pragma unroll 4
+    for (int sp = 0; sp < nvalid; ++sp) {
+      const size_t base = ((size_t)sp * p.total_q + tok) * p.Hq + head;
+      const float wt = exp2f(p.part_ml[base * 2] - Mu);
+      L += p.part_ml[base * 2 + 1] * wt;
+      acc += p.part_o[base * D + d] * wt;
+    }
+    p.out[(size_t)tok * p.out_stride + (size_t)head * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+  }
+}
+
+template <int D, int NW>
+int launch_decode_mw(const AttnParams& prm, int nseq, unsigned* counters, hipStream_t stream) {
+  constexpr int lds = NW * 2 * 2 * 32 * 2 * D;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)paged_decode_mw_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  paged_decode_mw_kernel<D, NW><<<dim3(nseq, prm.Hkv, prm.num_splits), 64 * NW, lds, stream>>>(prm, counters);
+  return (int)hipGetLastError();
+}
+
 template <int D, int NW, bool PAGED>
 int launch(const AttnParams& prm, int nseq, hipStream_t stream) {
   dim3 grid(nseq * prm.tiles_per_seq, prm.Hkv, prm.num_splits);
@@ -918,6 +1174,50 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
     case 32: return dispatch_nw<32>(prm, nseq, nw, true, stream);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// Small-batch decode (paged_decode_mw_kernel): nw = 2 or 4 waves per (sequence, kv head, split), the splits
+// merged in the same launch by the last arriving workgroup.  counters: >= nseq * Hkv zero-initialised
+// uint32 words (each reset by its last arriver); num_splits > 1 needs part_o / part_ml as
+// grag_paged_attention.  head_dim 64 / 128, G <= 16, BS % 16 == 0, split_len % 32 == 0.
+GRAG_API int grag_paged_decode_mw(const void* q, int q_stride, const void* k_cache, const void* v_cache, void* out,
+                                  int out_stride, const int32_t* block_tables, int bt_stride, const int32_t* q_start,
+                                  const int32_t* ctx_len, int nseq, int total_q, int Hq, int Hkv, int D, int BS,
+                                  float scale, int num_splits, int split_len, float* part_o, float* part_ml,
+                                  unsigned* counters, int nw, hipStream_t stream) {
+  if (nseq <= 0) return 0;
+  if (Hq % Hkv != 0 || Hq / Hkv > 16 || BS <= 0 || BS % 16 != 0 || (nw != 2 && nw != 4) || (D != 64 && D != 128))
+    return (int)hipErrorInvalidValue;
+  if (num_splits < 1) num_splits = 1;
+  if (num_splits > 1 && (!part_o || !part_ml || !counters || split_len <= 0 || split_len % 32 != 0))
+    return (int)hipErrorInvalidValue;
+  AttnParams prm{};
+  prm.q = (const bf16*)q;
+  prm.k = (const bf16*)k_cache;
+  prm.v = (const bf16*)v_cache;
+  prm.out = (bf16*)out;
+  prm.part_o = part_o;
+  prm.part_ml = part_ml;
+  prm.block_tables = block_tables;
+  prm.q_start = q_start;
+  prm.ctx_len = ctx_len;
+  prm.q_stride = q_stride;
+  prm.out_stride = out_stride;
+  prm.Hq = Hq;
+  prm.Hkv = Hkv;
+  prm.G = Hq / Hkv;
+  prm.BS = BS;
+  prm.bt_stride = bt_stride;
+  prm.tiles_per_seq = 1;
+  prm.num_splits = num_splits;
+  prm.split_len = num_splits > 1 ? split_len : (1 << 30);
+  prm.total_q = total_q;
+  prm.scale_log2 = scale * 1.4426950408889634f;
+  prm.causal = 1;
+  if (D == 128) return nw == 4 ? launch_decode_mw<128, 4>(prm, nseq, counters, stream)
+                               : launch_decode_mw<128, 2>(prm, nseq, counters, stream);
+  return nw == 4 ? launch_decode_mw<64, 4>(prm, nseq, counters, stream)
+                 : launch_decode_mw<64, 2>(prm, nseq, counters, stream);
 }
 
 // Contiguous (varlen) self-attention over packed QKV rows, e.g. encoder

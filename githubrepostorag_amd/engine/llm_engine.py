@@ -149,6 +149,9 @@ class LLMEngine:
             self._part_ml = torch.empty(max_split * self._max_b * hq * 2, dtype=torch.float32, device=self.device)
             # sampler scratch for the largest decode batch up front: graphs captured later all see one buffer
             self.sampler.workspace(self._max_b)
+            from ..ops.attention import decode_counters  # small-batch decode tickets: before any capture
+
+            decode_counters(self.device)
             # the engine's own (non-default) stream: retrieval / API threads issue their copies and syncs
             # on other streams; with the engine on the legacy default stream their runtime calls stalled
             # the engine thread (profiles/timeline_r2_*.txt).  Weights and the KV cache were written on

@@ -28,6 +28,28 @@ DECODE_NT_MIN_WAVES = 1536
 _DEC_NT = os.environ.get("GRAG_DECODE_NT", "auto")
 
 
+# small-batch decode (csrc/kernels/attention.hip paged_decode_mw_kernel): codes 22 / 24 = 2 / 4 waves per
+# (sequence, kv head, split), the splits merged in-launch by the last arriving workgroup.  Taken by the
+# dispatch when sequences x kv heads <= DECODE_MW_ROWS (GRAG_DECODE_MW: 0 = off)
+DECODE_MW = {22: 2, 24: 4}
+DECODE_MW_CODE = int(os.environ.get("GRAG_DECODE_MW_CODE", "24"))
+DECODE_MW_ROWS = int(os.environ.get("GRAG_DECODE_MW", "0"))
+_COUNTERS: dict = {}
+
+
+def decode_counters(dev: torch.device) -> torch.Tensor:
+    """The small-batch decode kernel's per-(sequence, kv head) tickets (zeroed once; every last arriver resets
+    its word, so hipGraph replays need no memset).  Allocate before any capture (LLMEngine does)."""
+    dev = torch.device(dev)
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    c = _COUNTERS.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("decode ticket counters must be allocated before hipGraph capture")
+        c = _COUNTERS[key] = torch.zeros(1 << 16, dtype=torch.int32, device=torch.device("cuda", key))
+    return c
+
+
 def decode_variant(nsplit: int, split_len: int, waves: int | None = None) -> int:
     """Decode kernel per split plan (profiles/mb_decode_ring_r4.json, 32-key tiles): long-context decode
     (split-KV parts covering > 2048 keys: ingest's 3-6K-token prompts) keeps two tiles in flight per wave
@@ -140,6 +162,18 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     if meta.is_decode:
         nw = meta.extra.get("decode_nw")
         if nw is None:
+            nw = decode_variant(nsplit, meta.split_len, meta.num_seqs * Hkv * nsplit)
+            if DECODE_MW_ROWS and meta.num_seqs * Hkv <= DECODE_MW_ROWS:
+                nw = DECODE_MW_CODE
+        if nw in DECODE_MW and D in (64, 128) and Hq // Hkv <= 16 and BS % 16 == 0 \
+                and (nsplit == 1 or meta.split_len % 32 == 0) and meta.num_seqs * Hkv <= (1 << 16):
+            call("grag_paged_decode_mw", ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(out), out.stride(0),
+                 ptr(meta.block_tables), meta.block_tables.stride(0), ptr(meta.q_start), ptr(meta.ctx_len),
+                 meta.num_seqs, T, Hq, Hkv, D, BS, float(scale), nsplit, meta.split_len if nsplit > 1 else 0,
+                 ptr(meta.part_o) if nsplit > 1 else None, ptr(meta.part_ml) if nsplit > 1 else None,
+                 ptr(decode_counters(q.device)), DECODE_MW[nw])
+            return out
+        if nw in DECODE_MW:
             nw = decode_variant(nsplit, meta.split_len, meta.num_seqs * Hkv * nsplit)
     else:
         nw = meta.extra.get("prefill_nw", PREFILL_NW)

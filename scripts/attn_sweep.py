@@ -15,7 +15,7 @@ import torch  # noqa: E402
 from githubrepostorag_amd.engine.llm_engine import _pow2_at_least, _split_len_for  # noqa: E402
 from githubrepostorag_amd.ops import attention as A  # noqa: E402
 
-VARIANTS = {"ns2": 3, "ns3": 8, "ns4": 7, "ns2_nt": 11, "ns3_nt": 12}
+VARIANTS = {"ns2": 3, "ns3": 8, "ns4": 7, "ns2_nt": 11, "ns3_nt": 12, "mw2": 22, "mw4": 24}
 
 
 def graph_us(fn, reps=20):
@@ -47,10 +47,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--grid", default="1:1024,1:4096,1:11600,4:4096,4:11600,16:4096,16:11600,176:1500")
     ap.add_argument("--splits", default="64:128:256:512:1024")
-    ap.add_argument("--variants", default="ns2:ns3:ns4")
+    ap.add_argument("--variants", default="ns2:ns3:mw2:mw4")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda")
+    A.decode_counters(dev)
     Hq, Hkv, D, BS = 28, 4, 128, 16
     out = {}
     with torch.inference_mode():
@@ -64,7 +65,7 @@ def main():
             gb = B * ctx * Hkv * D * 2 * 2 / 1e9
             res = {"bytes_gb": round(gb, 4), "engine_split_len": _split_len_for(B)}
             for sl in [int(v) for v in a.splits.replace(":", ",").split(",")]:
-                if sl % A.KV_TILE:
+                if sl % 32:
                     continue
                 ns = -(-ctx // sl)
                 for vname in a.variants.replace(":", ",").split(","):

@@ -22,6 +22,7 @@
 #   pmcdec=ARGS      PMC passes over scripts/prof_dec.py ARGS (scripts/pmc_dec.sh; csv under gpurun_out/pmc_<TAG>_pmcN)
 #   pmcpy=SCRIPT,ARGS PMC passes over any python script (scripts/pmc_py.sh; summary: scripts/pmc_dump.py)
 #   py=SCRIPT,ARGS   python -u SCRIPT ARGS (',' separates args; log gpurun_out/<TAG>_py<i>.log)  (600 s)
+#   envpy=A=1+B=2,SCRIPT,ARGS  the same with environment variables ('+' separates them)
 #
 # A step that exits 0 or 1 (a clean Python failure) lets the next one run; a fault, abort, segfault or
 # time limit (124 / 134 / 137 / 139) ends the session there (no more GPU work after a GPU fault).
@@ -71,6 +72,7 @@ for step in "$@"; do
     pmcdec) run 400 "pmcdec_$npy" env TAG="${TAG}_pmc$npy" ARGS="${val//,/ }" bash scripts/pmc_dec.sh; npy=$((npy+1)) ;;
     pmcpy) run 600 "pmcpy_$npy" env TAG="${TAG}_pmcpy$npy" bash scripts/pmc_py.sh ${val//,/ }; npy=$((npy+1)) ;;
     py) npy=$((npy+1)); run 600 "py$npy" python -u ${val//,/ } ;;
+    envpy) npy=$((npy+1)); ev=${val%%,*}; rest=${val#*,}; run 600 "py$npy" env ${ev//+/ } python -u ${rest//,/ } ;;
     mb) run 400 "mb_$val" python -u scripts/microbench.py --what "$val" --out "gpurun_out/${TAG}_mb_$val.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

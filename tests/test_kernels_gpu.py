@@ -218,6 +218,45 @@ def test_paged_decode(dev, nsplit_len):
         close(out, ref, 2e-2)
 
 
+@pytest.mark.parametrize("Hq,Hkv,D", [(28, 4, 128), (14, 2, 64)])
+@pytest.mark.parametrize("sl", [0, 32, 128, 256])
+def test_paged_decode_small_batch_mw(dev, Hq, Hkv, D, sl):
+    """The small-batch decode kernel (2 / 4 waves per split, in-launch last-arriver merge of the splits):
+    sequences with different split counts (early-exit workgroups), a 1-key context, a context ending
+    mid-tile; replayed three times in one hipGraph (the tickets reset themselves) against the fp32 reference."""
+    lens_ctx = [1, 45, 300, 1200, 4100]
+    B = len(lens_ctx)
+    q, kc, vc, meta = _paged_setup(dev, [1] * B, lens_ctx, Hq, Hkv, D, seed=5)
+    scale = 1 / math.sqrt(D)
+    ref = A.paged_attention_ref(q, kc, vc, meta, scale).reshape(B, -1)
+    A.decode_counters(dev)
+    for code in (22, 24):
+        m = _to(meta, dev)
+        m.is_decode = True
+        if sl:
+            ns = -(-max(lens_ctx) // sl)
+            m.num_splits, m.split_len = ns, sl
+            m.part_o = torch.empty(ns * B * Hq * D, dtype=torch.float32, device=dev)
+            m.part_ml = torch.empty(ns * B * Hq * 2, dtype=torch.float32, device=dev)
+        m.extra = {"decode_nw": code}
+        qd, kd, vd = q.to(dev), kc.to(dev), vc.to(dev)
+        out = A.paged_attention(qd, kd, vd, m, scale)
+        close(out, ref, 2e-2)
+        o2 = torch.empty_like(out)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(3):
+                A.paged_attention(qd, kd, vd, m, scale, out=o2)
+        for _ in range(2):
+            o2.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            close(o2, ref, 2e-2)
+        assert int(A.decode_counters(dev)[: B * Hkv].abs().sum()) == 0
+
+
 @pytest.mark.parametrize("H,D", [(12, 32), (12, 64), (16, 64)])
 def test_varlen_attention(dev, H, D):
     lens = [5, 130, 64, 1]
