@@ -71,7 +71,7 @@ def main():
     dev = torch.device("cuda")
     out = {}
     with torch.inference_mode():
-        for name in a.shapes.split(","):
+        for name in a.shapes.replace(":", ",").split(","):
             N, K, silu = SHAPES[name]
             ncopy = max(2, min(16, (1 << 30) // (N * K * 2) + 1))
             ws = [((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(ncopy)]
@@ -104,6 +104,13 @@ def main():
                     epi = G.EPI_SILU if silu else G.EPI_STORE
                     G.WS.reserve(dev, G.dec_ws_floats(M, N, G.dec_ksplit(K, plan[3])))
                     arms["decode"] = lambda w, plan=plan, epi=epi: G.gemm_decode(x, w, epi=epi, plan=plan)
+                    ks = G.dec_ksplit(K, plan[3])
+                    if not silu and ks > 1:  # the planes left for RoPE / RMSNorm (no reduce launch)
+                        for kk in sorted({ks, G.dec_ksplit(K, 2 * plan[3])}):
+                            pl = (plan[0], plan[1], plan[2], kk)
+                            G.WS.reserve(dev, G.dec_ws_floats(M, N, kk))
+                            arms[f"dec_deferred_ks{kk}"] = lambda w, pl=pl, kk=kk: G.gemm_deferred(
+                                x, w, ("decode", kk, pl))
                 for d in [int(v) for v in a.depths.replace(":", ",").split(",") if v.strip()]:
                     if plan is None or plan[1] not in (4, 5) or plan[0] > (2 if d == 12 else 4 if d == 8 else 8) \
                             or (plan[0] <= 2 and d == 6):
