@@ -324,14 +324,16 @@ DEC_MAX_M = int(os.environ.get("GRAG_DECODE_MAX_M", "256"))
 DEC_MIN_M = int(os.environ.get("GRAG_DEC_MIN_M", "33"))
 
 
-def dec_small(M: int, N: int, K: int, silu: bool = False) -> bool:
+def dec_small(M: int, N: int, K: int, silu: bool = False, deferred: bool = False) -> bool:
     """1-32 rows (the reference's 1-4 live sequences): the 1- / 2-row-tile decode variants where the hipGraph-
     timed cold-weight sweep measured them faster (profiles/gemm_graph_sweep_r5_depths_smallM.json): gate/up
     49-52 us vs the tile kernel's 76-79 (5.2-5.5 TB/s), down_proj (K >= 4 N) 30-31 vs skinny / library
-    31-38 us; qkv / o stay on skinny / library (9-12 vs 12-13 us).  Deeper rings (8 / 12) measured slower."""
+    31-38 us; qkv / o stay on skinny / library (9-12 vs 12-13 us) unless their split-K reduce is ``deferred``
+    into RoPE / RMSNorm (ops/linear.linear_deferred): then qkv 9.2-9.5 vs 12 us, o 8.2-8.7 vs 8.4-9.4 us
+    (profiles/gemm_graph_sweep_r5_smallM_deferred.json).  Deeper rings (8 / 12) measured slower."""
     if M >= 33 or M < 1:
         return False
-    return M >= DEC_MIN_M or silu or K >= 4 * N
+    return M >= DEC_MIN_M or silu or K >= 4 * N or deferred
 
 
 def dec_variants(M: int) -> list[tuple[int, int, int]]:

@@ -336,7 +336,7 @@ def linear_deferred(x: torch.Tensor, w: torch.Tensor):
             and w.dtype == torch.bfloat16 and x.stride(1) == 1 and w.stride(1) == 1 and _tile.supported(x, w)):
         M, K = x.shape
         N = w.shape[0]
-        if M >= TILE_MIN_M or _tile.dec_small(M, N, K):
+        if M >= TILE_MIN_M or _tile.dec_small(M, N, K, deferred=True):
             how = _tile.deferred_plan(M, N, K)
             if how is not None and (not torch.cuda.is_current_stream_capturing()
                                     or _tile.WS.ready(x.device, how[1] * M * N)):

@@ -69,6 +69,8 @@ def main():
                     continue
                 ns = -(-ctx // sl)
                 for vname in a.variants.replace(":", ",").split(","):
+                    if VARIANTS[vname] not in A.DECODE_MW and sl % A.KV_TILE:
+                        continue  # the single-wave kernel takes parts of whole 64-key tiles
                     meta = A.AttnMetadata(
                         q_start=torch.arange(B + 1, device=dev, dtype=torch.int32),
                         ctx_len=torch.full((B,), ctx, device=dev, dtype=torch.int32), block_tables=bt,

@@ -82,7 +82,7 @@ def test_qkv_rope_kvstore(dev):
     close(vc, vr, 1e-2)
 
 
-@pytest.mark.parametrize("T", [48, 190, 240])
+@pytest.mark.parametrize("T", [1, 4, 16, 32, 48, 190, 240])
 def test_qkv_rope_kvstore_from_splitk_planes(dev, T):
     """Qwen2-7B qkv at decode batches as deferred K-split planes (reduce folded into the RoPE / KV-store pass)
     against the unfused path (split-K reduce to bf16, then RoPE): identical q / K / V bits."""
@@ -103,8 +103,13 @@ def test_qkv_rope_kvstore_from_splitk_planes(dev, T):
                torch.zeros(NB, Hkv, BS, D, dtype=torch.bfloat16, device=dev)) for _ in range(2)]
     q1 = E.qkv_rope_kvstore(part, bias, pos, cs, slots, *caches[0], Hq, Hkv, D)
     q2 = E.qkv_rope_kvstore(linear(x, w), bias, pos, cs, slots, *caches[1], Hq, Hkv, D)
-    assert torch.equal(q1, q2)
-    assert torch.equal(caches[0][0], caches[1][0]) and torch.equal(caches[0][1], caches[1][1])
+    if T >= 33:  # linear() runs the same K-split plan + reduce there: identical bits
+        assert torch.equal(q1, q2)
+        assert torch.equal(caches[0][0], caches[1][0]) and torch.equal(caches[0][1], caches[1][1])
+    else:  # 1-32 rows: linear() is the library / skinny GEMM (other accumulation order)
+        close(q1, q2, 3e-2)
+        close(caches[0][0], caches[1][0], 3e-2)
+        close(caches[0][1], caches[1][1], 3e-2)
 
 
 def test_silu_mul_bias_act(dev):
@@ -420,7 +425,8 @@ def test_linear_splitk_down_proj(dev, M):
     close(gemm_splitk(x, w, None, 2), ref, 3e-2, 2e-2)
 
 
-@pytest.mark.parametrize("M,Nn,K", [(48, 3584, 3584), (128, 3584, 18944), (190, 3584, 3584), (190, 3584, 18944),
+@pytest.mark.parametrize("M,Nn,K", [(1, 3584, 3584), (4, 3584, 18944), (16, 3584, 3584), (48, 3584, 3584),
+                                   (128, 3584, 18944), (190, 3584, 3584), (190, 3584, 18944),
                                    (240, 3584, 3584), (384, 3584, 18944), (512, 3584, 3584)])
 def test_splitk_deferred_rmsnorm(dev, M, Nn, K):
     """o_proj / down_proj at decode batches: the K-split planes left unreduced (EPI_PARTIAL) and reduced
