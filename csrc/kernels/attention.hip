@@ -1016,20 +1016,46 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, 
   }
   __syncthreads();
   if (flag[0] == 0u) return;
+  // last arriver: every split's (m, l) of the G rows staged in LDS in one parallel pass, the per-split
+  // weights formed once per row, then ONE pass over the partial O vectors (independent loads per thread)
+  float* wm = reinterpret_cast<float*>(smem);  // [nvalid][16]: m, then the split's weight
+  float* wl = wm + nvalid * 16;                // [nvalid][16]: l
+  float* rowL = wl + nvalid * 16;              // [16]
+  for (int e = threadIdx.x; e < nvalid * 16; e += 64 * NW) {
+    const int sp = e >> 4, row = e & 15;
+    float mv = -INFINITY, lv = 0.f;
+    if (row < G) {
+      const size_t base = (((size_t)sp * p.total_q + tok) * p.Hq + kvh * G + row) * 2;
+      mv = p.part_ml[base];
+      lv = p.part_ml[base + 1];
+    }
+    wm[e] = mv;
+    wl[e] = lv;
+  }
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int row = threadIdx.x;
+    float M = -INFINITY;
+    for (int sp = 0; sp < nvalid; ++sp) M = fmaxf(M, wm[sp * 16 + row]);
+    const float Mu = M == -INFINITY ? 0.f : M;
+    float L = 0.f;
+    for (int sp = 0; sp < nvalid; ++sp) {
+      const float wt = exp2f(wm[sp * 16 + row] - Mu);
+      wm[sp * 16 + row] = wt;
+      L += wl[sp * 16 + row] * wt;
+    }
+    rowL[row] = L;
+  }
+  __syncthreads();
   for (int idx = threadIdx.x; idx < G * D; idx += 64 * NW) {
     const int row = idx / D, d = idx % D;
     const int head = kvh * G + row;
-    float M = -INFINITY;
-    for (int sp = 0; sp < nvalid; ++sp) M = fmaxf(M, p.part_ml[(((size_t)sp * p.total_q + tok) * p.Hq + head) * 2]);
-    const float Mu = M == -INFINITY ? 0.f : M;
-    float L = 0.f, acc = 0.f;
-#pragma unroll 4
-    for (int sp = 0; sp < nvalid; ++sp) {
-      const size_t base = ((size_t)sp * p.total_q + tok) * p.Hq + head;
-      const float wt = exp2f(p.part_ml[base * 2] - Mu);
-      L += p.part_ml[base * 2 + 1] * wt;
-      acc += p.part_o[base * D + d] * wt;
-    }
+    const float* po = p.part_o + ((size_t)tok * p.Hq + head) * D + d;
+    const size_t sstride = (size_t)p.total_q * p.Hq * D;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int sp = 0; sp < nvalid; ++sp) acc += po[sp * sstride] * wm[sp * 16 + row];
+    const float L = rowL[row];
     p.out[(size_t)tok * p.out_stride + (size_t)head * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
   }
 }
@@ -1191,6 +1217,7 @@ GRAG_API int grag_paged_decode_mw(const void* q, int q_stride, const void* k_cac
   if (num_splits < 1) num_splits = 1;
   if (num_splits > 1 && (!part_o || !part_ml || !counters || split_len <= 0 || split_len % 32 != 0))
     return (int)hipErrorInvalidValue;
+  if ((num_splits * 32 + 16) * 4 > nw * 2 * 2 * 32 * 2 * D) return (int)hipErrorInvalidValue;  // merge scratch
   AttnParams prm{};
   prm.q = (const bf16*)q;
   prm.k = (const bf16*)k_cache;

@@ -86,6 +86,22 @@ def _split_len_for(batch: int) -> int:
     return 2 * KV_TILE
 
 
+def _decode_plan(model, B: int, max_ctx: int, max_model_len: int, graph: bool = True) -> tuple[int, int]:
+    """(nsplit, split_len) of the decode attention for a batch of B sequences: the small-batch kernel's plan
+    (ops/attention.decode_mw_plan) when it takes the batch, else split parts of _split_len_for(B) keys
+    (graphs: a power-of-two split count, so one capture serves a range of contexts)."""
+    from ..ops.attention import decode_mw_plan
+
+    mw = decode_mw_plan(B, getattr(model, "hkv", 1), max_ctx, max_model_len) if model.device.type == "cuda" else None
+    if mw is not None:
+        return mw
+    split_len = _split_len_for(B)
+    need = -(-max_ctx // split_len)
+    if graph:
+        return min(_pow2_at_least(need), -(-max_model_len // split_len)), split_len
+    return max(1, need), split_len
+
+
 def _pow2_at_least(n: int) -> int:
     p = 1
     while p < n:
@@ -465,8 +481,7 @@ class LLMEngine:
         ns = len(samp_rows)
         t_rows = dev[o:o + ns]; o += ns
         t_samp = dev[o:o + ns]
-        split_len = _split_len_for(n_dec)
-        nsplit = max(1, -(-max_ctx // split_len))
+        nsplit, split_len = _decode_plan(self.model, n_dec, max_ctx, self.cfg.max_model_len, graph=False)
         hq, dh = self.model.hq, self.model.head_dim
         meta = AttnMetadata(q_start=p_qs, ctx_len=p_ctx, block_tables=p_bt, slot_mapping=t_slot,
                             max_q_len=max(b - a for _, a, b in pitems), num_seqs=n_pref, num_tokens=Tp)
@@ -644,8 +659,7 @@ class LLMEngine:
         if use_graph:
             width = self.max_blocks_per_seq
             B = next(b for b in self.cfg.graph_batch_sizes if b >= n)
-            split_len = _split_len_for(B)
-            nsplit = min(_pow2_at_least(-(-max_ctx // split_len)), -(-self.cfg.max_model_len // split_len))
+            nsplit, split_len = _decode_plan(self.model, B, max_ctx, self.cfg.max_model_len)
             g = self._graphs.get((B, nsplit, split_len, K, self.sampler.rounds))
             if g is None:
                 g = self._capture(B, nsplit, split_len, K)
@@ -661,8 +675,7 @@ class LLMEngine:
             self.stats["decode_wait_s"] += time.perf_counter() - tw
             self.stats["graph_replays"] += 1
         else:
-            split_len = _split_len_for(n)
-            nsplit = max(1, -(-max_ctx // split_len))
+            nsplit, split_len = _decode_plan(self.model, n, max_ctx, self.cfg.max_model_len, graph=False)
             width = max(len(s.blocks) for s in seqs)
             dev = self._to_dev(self._decode_inputs(seqs, n, width, 1))
             out = torch.empty(1, n, dtype=torch.int32, device=self.device)
@@ -811,8 +824,7 @@ class LLMEngine:
     def _warmup_graphs(self, batch_sizes, max_ctx, windows) -> int:
         n = 0
         for B in batch_sizes or self.cfg.graph_batch_sizes:
-            split_len = _split_len_for(B)
-            nsplit = min(_pow2_at_least(-(-max_ctx // split_len)), -(-self.cfg.max_model_len // split_len))
+            nsplit, split_len = _decode_plan(self.model, B, max_ctx, self.cfg.max_model_len)
             for K in windows:
                 if K > max(1, self.cfg.decode_window):
                     continue

@@ -35,6 +35,23 @@ DECODE_MW = {22: 2, 24: 4}
 DECODE_MW_CODE = int(os.environ.get("GRAG_DECODE_MW_CODE", "24"))
 DECODE_MW_ROWS = int(os.environ.get("GRAG_DECODE_MW", "0"))
 _COUNTERS: dict = {}
+MW_SPLITS = int(os.environ.get("GRAG_DECODE_MW_SPLITS", "32"))  # split slots per (sequence, kv head)
+MW_TARGET_WG = 256  # about one workgroup per CU over the batch's (sequence, kv head, split) grid
+
+
+def decode_mw_plan(B: int, Hkv: int, max_ctx: int, max_model_len: int, force: bool = False) -> tuple[int, int] | None:
+    """(nsplit, split_len) of the small-batch decode kernel, or None when the dispatch does not take it:
+    about one workgroup per CU over (sequence, kv head, split), at most MW_SPLITS splits, parts of a power of
+    two times 128 keys (4 waves x one 32-key tile) -- so one captured graph serves every context up to
+    nsplit x split_len and the split length doubles, not the graph count, as the context grows."""
+    if not force and (not DECODE_MW_ROWS or B * Hkv > DECODE_MW_ROWS):
+        return None
+    target = max(1, min(MW_SPLITS, MW_TARGET_WG // max(1, B * Hkv)))
+    per = -(-max(1, max_ctx) // target)
+    split_len = 128
+    while split_len < per:
+        split_len *= 2
+    return max(1, min(target, -(-max_model_len // split_len))), split_len
 
 
 def decode_counters(dev: torch.device) -> torch.Tensor:

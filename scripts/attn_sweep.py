@@ -82,6 +82,20 @@ def main():
                     us = graph_us(lambda: A.paged_attention(q, kc, vc, meta, 0.088, out=o))
                     res[f"split{sl}_{vname}"] = {"us": round(us, 2), "TB_s": round(gb / (us * 1e-6) / 1e3, 3),
                                                  "waves": B * Hkv * ns}
+            # the small-batch kernel at its own plan (ops/attention.decode_mw_plan)
+            mns, msl = A.decode_mw_plan(B, Hkv, ctx, 11712, force=True)
+            for vname in ("mw2", "mw4"):
+                meta = A.AttnMetadata(
+                    q_start=torch.arange(B + 1, device=dev, dtype=torch.int32),
+                    ctx_len=torch.full((B,), ctx, device=dev, dtype=torch.int32), block_tables=bt,
+                    slot_mapping=torch.zeros(B, dtype=torch.int32, device=dev), max_q_len=1, num_seqs=B,
+                    num_tokens=B, is_decode=True, num_splits=mns, split_len=msl,
+                    part_o=torch.empty(mns * B * Hq * D, device=dev), part_ml=torch.empty(mns * B * Hq * 2, device=dev))
+                meta.extra = {"decode_nw": VARIANTS[vname]}
+                o = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=dev)
+                us = graph_us(lambda: A.paged_attention(q, kc, vc, meta, 0.088, out=o))
+                res[f"mwplan_{vname}"] = {"us": round(us, 2), "TB_s": round(gb / (us * 1e-6) / 1e3, 3),
+                                          "nsplit": mns, "split_len": msl}
             # the engine's own plan (llm_engine._run_decode: split_len by batch, nsplit a power of two)
             sl = _split_len_for(B)
             ns = _pow2_at_least(-(-ctx // sl))
