@@ -77,10 +77,8 @@ def _split_len_for(batch: int) -> int:
     combine pass and the partial round trip: B512 ctx1100 251 -> 233 / 225 / 210 us at parts of 512 /
     1024 / 2048 keys, B256 ctx1100 125 -> 105 us at 2048 (profiles/mb_decode_splits_r3.json).  The part
     length still caps one wave's keys, so a long sequence among short ones is split."""
-    if batch >= 384:
+    if batch >= 128:  # B176 ctx1500: one 2048-key part 96.5 us vs 256-key parts 121.2 (profiles/attn_sweep_r5_mw.json)
         return 32 * KV_TILE
-    if batch >= 192:
-        return 16 * KV_TILE
     if batch >= 8:
         return 4 * KV_TILE
     return 2 * KV_TILE

@@ -33,25 +33,29 @@ _DEC_NT = os.environ.get("GRAG_DECODE_NT", "auto")
 # dispatch when sequences x kv heads <= DECODE_MW_ROWS (GRAG_DECODE_MW: 0 = off)
 DECODE_MW = {22: 2, 24: 4}
 DECODE_MW_CODE = int(os.environ.get("GRAG_DECODE_MW_CODE", "24"))
-DECODE_MW_ROWS = int(os.environ.get("GRAG_DECODE_MW", "0"))
+DECODE_MW_ROWS = int(os.environ.get("GRAG_DECODE_MW", "16"))
 _COUNTERS: dict = {}
-MW_SPLITS = int(os.environ.get("GRAG_DECODE_MW_SPLITS", "32"))  # split slots per (sequence, kv head)
-MW_TARGET_WG = 256  # about one workgroup per CU over the batch's (sequence, kv head, split) grid
+MW_SPLITS = int(os.environ.get("GRAG_DECODE_MW_SPLITS", "20"))  # target parts per sequence at B = 1
 
 
 def decode_mw_plan(B: int, Hkv: int, max_ctx: int, max_model_len: int, force: bool = False) -> tuple[int, int] | None:
-    """(nsplit, split_len) of the small-batch decode kernel, or None when the dispatch does not take it:
-    about one workgroup per CU over (sequence, kv head, split), at most MW_SPLITS splits, parts of a power of
-    two times 128 keys (4 waves x one 32-key tile) -- so one captured graph serves every context up to
-    nsplit x split_len and the split length doubles, not the graph count, as the context grows."""
+    """(nsplit, split_len) of the small-batch decode kernel, or None when the dispatch does not take it.
+    Parts: the power of two (>= 128 keys: 4 waves x one 32-key tile) nearest in log2 to the context over
+    MW_SPLITS / sqrt(B) parts -- the hipGraph-timed sweep's best cells (profiles/attn_sweep_r5_mw.json, 4-wave
+    kernel): B1 1K / 4K / 11.6K -> 128 / 256 / 512 keys (11.1 / 15.5 / 25.6 us vs 14.9 / 25.5 / 38.0 for the
+    single-wave kernel's best plan), B4 4K / 11.6K -> 512 / 1024 (19.0 / 32.3 vs 25.7 / 40.7).  nsplit counts
+    parts up to max_model_len, so one captured graph serves a context range (empty parts exit at once)."""
     if not force and (not DECODE_MW_ROWS or B * Hkv > DECODE_MW_ROWS):
         return None
-    target = max(1, min(MW_SPLITS, MW_TARGET_WG // max(1, B * Hkv)))
-    per = -(-max(1, max_ctx) // target)
-    split_len = 128
-    while split_len < per:
-        split_len *= 2
-    return max(1, min(target, -(-max_model_len // split_len))), split_len
+    import math
+
+    per = max(1.0, max_ctx * math.sqrt(B) / MW_SPLITS)
+    split_len = max(128, 1 << int(round(math.log2(per))))
+    need = -(-max(1, max_ctx) // split_len)
+    ns = 1
+    while ns < need:
+        ns *= 2
+    return max(1, min(ns, -(-max_model_len // split_len))), split_len
 
 
 def decode_counters(dev: torch.device) -> torch.Tensor:
@@ -74,7 +78,11 @@ def decode_variant(nsplit: int, split_len: int, waves: int | None = None) -> int
     batches (one part of ~1.1K keys, or 256-key parts) stay on the 2-stage ring, whose 5 waves per CU win
     there (B512 ctx1100: 207.8 vs 222.8 us, B64 ctx1152: 35.6 vs 40.7 us).  ``waves``: the launch's
     (sequence x kv-head x split) count; grids of >= DECODE_NT_MIN_WAVES load K/V non-temporally."""
-    nw = DECODE_RING_NW[3] if _DEC_AUTO and nsplit > 1 and nsplit * split_len > 2048 else DECODE_NW
+    # round 5 (profiles/attn_sweep_r5_mw.json, same box): the 3-stage ring lost at B16 4K (45.2 vs 32.1 us at
+    # 256-key parts) and tied elsewhere (B16 11.6K 78.0 vs 76.4, B176 1.5K 98.8 vs 96.5): 2 stages unless
+    # GRAG_DECODE_STAGES asks (the round-4 auto rule is kept behind GRAG_DECODE_RING_AUTO=1)
+    auto3 = _DEC_AUTO and os.environ.get("GRAG_DECODE_RING_AUTO") == "1"
+    nw = DECODE_RING_NW[3] if auto3 and nsplit > 1 and nsplit * split_len > 2048 else DECODE_NW
     nt = _DEC_NT == "1" or (_DEC_NT == "auto" and waves is not None and waves >= DECODE_NT_MIN_WAVES)
     return DECODE_NT.get(nw, nw) if nt else nw
 
