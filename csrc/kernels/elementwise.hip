@@ -25,7 +25,8 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return 0.5f * x * (1.f + t);
 }
 
-// One block per token.  Work units (16 B each):
+// One block per token (few tokens: gridDim.y blocks of 64 threads per token share its units, so a decode step
+// of 1-32 sequences spreads the row over several CUs).  Work units (16 B each):
 //   [0, (Hq+Hkv)*D/16)           rotary units: 8 pairs (i..i+7, i+D/2..i+D/2+7)
 //   [.., + Hkv*D/8)              v copy units
 // PL: the projection arrives as S fp32 split-K planes [S][T][ld] (ops/gemm.py SplitKPartial): the reduce is
@@ -43,7 +44,8 @@ __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
   auto load8 = [&](int col, float* x) {
     if constexpr (PL) {
       f32x4_t a = *reinterpret_cast<const f32x4_t*>(prow + col), b = *reinterpret_cast<const f32x4_t*>(prow + col + 4);
-      for (int s = 1; s < S; ++s) {
+#pragma unroll 8
+      for (int s = 1; s < S; ++s) {  // (unrolled: the planes' loads issue back to back; sums stay in plane order)
         a += *reinterpret_cast<const f32x4_t*>(prow + s * plane + col);
         b += *reinterpret_cast<const f32x4_t*>(prow + s * plane + col + 4);
       }
@@ -67,7 +69,7 @@ __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
   const float* cs = cos_sin ? cos_sin + (size_t)pos * D : nullptr;
   const int blk = slot >= 0 ? slot / BS : 0;
   const int off = slot >= 0 ? slot % BS : 0;
-  for (int u = threadIdx.x; u < n_rot + n_v; u += kThreads) {
+  for (int u = blockIdx.y * blockDim.x + threadIdx.x; u < n_rot + n_v; u += gridDim.y * blockDim.x) {
     if (u < n_rot) {
       const int head = u / upp;  // 0..Hq-1 are q heads, then k heads
       const int i0 = (u % upp) * 8;
@@ -267,6 +269,12 @@ int grid_for(size_t total) {
 
 }  // namespace
 
+// Blocks of qkv_rope_kernel: one per token; under 32 tokens, one 64-thread block per 64 units of each token.
+static dim3 rope_grid(int T, int Hq, int Hkv, int D) {
+  const int units = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
+  return dim3(T, T < 32 ? (units + 63) / 64 : 1);
+}
+
 GRAG_API int grag_qkv_rope_kvstore(const void* qkv, int ld, const void* bias,
                                    const int32_t* positions, const float* cos_sin,
                                    const int32_t* slot_mapping, void* q_out, void* k_cache,
@@ -274,7 +282,8 @@ GRAG_API int grag_qkv_rope_kvstore(const void* qkv, int ld, const void* bias,
                                    hipStream_t stream) {
   if (T <= 0) return 0;
   if (D % 16 != 0 || ld % 8 != 0) return (int)hipErrorInvalidValue;
-  qkv_rope_kernel<false><<<T, kThreads, 0, stream>>>((const bf16*)qkv, ld, (const bf16*)bias, positions,
+  const dim3 g = rope_grid(T, Hq, Hkv, D);
+  qkv_rope_kernel<false><<<g, g.y > 1 ? 64 : kThreads, 0, stream>>>((const bf16*)qkv, ld, (const bf16*)bias, positions,
                                                      cos_sin, slot_mapping, (bf16*)q_out,
                                                      (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, D, BS, nullptr, 1, 0);
   return (int)hipGetLastError();
@@ -289,7 +298,8 @@ GRAG_API int grag_qkv_rope_kvstore_planes(const float* planes, int S, int N, con
                                           hipStream_t stream) {
   if (T <= 0) return 0;
   if (D % 16 != 0 || N % 8 != 0 || S < 1 || N != (Hq + 2 * Hkv) * D) return (int)hipErrorInvalidValue;
-  qkv_rope_kernel<true><<<T, kThreads, 0, stream>>>(nullptr, N, (const bf16*)bias, positions, cos_sin,
+  const dim3 g = rope_grid(T, Hq, Hkv, D);
+  qkv_rope_kernel<true><<<g, g.y > 1 ? 64 : kThreads, 0, stream>>>(nullptr, N, (const bf16*)bias, positions, cos_sin,
                                                     slot_mapping, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache,
                                                     Hq, Hkv, D, BS, planes, S, (size_t)T * N);
   return (int)hipGetLastError();

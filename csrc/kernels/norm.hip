@@ -326,6 +326,86 @@ GRAG_API int grag_rmsnorm(const void* x, void* residual, const void* w, void* ou
 }
 
 // residual += sum_s ws[s] ; out = RMSNorm(residual) * w   (ws: S fp32 planes [T][H], 16-B aligned)
+// Small batches (1-16 rows, the reference's 1-4 live sequences): splitk_rmsnorm_kernel gives a row ONE
+// workgroup, which then reads all S planes of the row alone (7-9 x 14 KB at Qwen2-7B: 5.6 us at B = 1).
+// Here a row is cut into 64-unit chunks (8 columns per unit), one 64-thread workgroup each: every chunk sums
+// its planes into the residual (bf16, as the one-block kernel) and its share of sum(h^2); the chunk sums go
+// to part_ss and an agent-scope ticket per row names the last arriving chunk (release / acquire fences as
+// gemm_stream.hip), which adds the chunk sums in chunk order and normalises the whole row.  The ticket resets
+// itself, so the launch replays inside hipGraphs.
+__global__ __launch_bounds__(64) void splitk_rmsnorm_small_kernel(
+    const float* __restrict__ ws, int S, size_t plane, bf16* __restrict__ residual, const bf16* __restrict__ w,
+    bf16* __restrict__ out, int H, float eps, float* __restrict__ part_ss, unsigned* __restrict__ counters) {
+  const int row = blockIdx.x, c = blockIdx.y, nch = gridDim.y;
+  const int nvec = H >> 3;
+  const int u = c * 64 + threadIdx.x;
+  const float* hr = ws + (size_t)row * H;
+  bf16x8_t* rr = reinterpret_cast<bf16x8_t*>(residual + (size_t)row * H);
+  float ss = 0.f;
+  if (u < nvec) {
+    float a[8];
+    unpack8(rr[u], a);
+#pragma unroll 8
+    for (int sp = 0; sp < S; ++sp) {
+      const float* q = hr + sp * plane + u * 8;
+      const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(q), x1 = *reinterpret_cast<const f32x4_t*>(q + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { a[j] += x0[j]; a[j + 4] += x1[j]; }
+    }
+    const bf16x8_t sum = pack8(a);
+    rr[u] = sum;
+    unpack8(sum, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  __shared__ unsigned last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's residual store landed before the release
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part_ss[(size_t)row * nch + c] = ss;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned tk = __hip_atomic_fetch_add(&counters[row], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = tk == (unsigned)(nch - 1) ? 1u : 0u;
+    if (last) {
+      __hip_atomic_store(&counters[row], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  float tot = 0.f;
+  for (int k = 0; k < nch; ++k) tot += part_ss[(size_t)row * nch + k];  // chunk order: deterministic
+  const float inv = rsqrtf(tot / (float)H + eps);
+  const bf16x8_t* wr = reinterpret_cast<const bf16x8_t*>(w);
+  bf16x8_t* orow = reinterpret_cast<bf16x8_t*>(out + (size_t)row * H);
+  for (int v = threadIdx.x; v < nvec; v += 64) {
+    float a[8], g[8];
+    unpack8(rr[v], a);
+    unpack8(wr[v], g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = a[j] * inv * g[j];
+    orow[v] = pack8(a);
+  }
+}
+
+// Small-batch form of grag_splitk_add_rmsnorm (T <= 64 rows): part_ss >= T * ceil(H / 512) floats of scratch,
+// counters >= T zero-initialised uint32 words (each reset by its last arriver).
+GRAG_API int grag_splitk_add_rmsnorm_small(const void* ws, int S, void* residual, const void* w, void* out, int T,
+                                           int H, float eps, float* part_ss, unsigned* counters,
+                                           hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8 != 0 || S < 1 || ws == nullptr || residual == nullptr || !part_ss || !counters || T > 64)
+    return (int)hipErrorInvalidValue;
+  const int nch = (H / 8 + 63) / 64;
+  splitk_rmsnorm_small_kernel<<<dim3(T, nch), 64, 0, stream>>>((const float*)ws, S, (size_t)T * H, (bf16*)residual,
+                                                              (const bf16*)w, (bf16*)out, H, eps, part_ss, counters);
+  return (int)hipGetLastError();
+}
+
 GRAG_API int grag_splitk_add_rmsnorm(const void* ws, int S, void* residual, const void* w, void* out, int T,
                                      int H, float eps, hipStream_t stream) {
   if (T <= 0) return 0;

@@ -166,6 +166,9 @@ class LLMEngine:
             from ..ops.attention import decode_counters  # small-batch decode tickets: before any capture
 
             decode_counters(self.device)
+            from ..ops.norm import norm_ws
+
+            norm_ws(self.device)
             # the engine's own (non-default) stream: retrieval / API threads issue their copies and syncs
             # on other streams; with the engine on the legacy default stream their runtime calls stalled
             # the engine thread (profiles/timeline_r2_*.txt).  Weights and the KV cache were written on

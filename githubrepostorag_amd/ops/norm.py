@@ -1,6 +1,8 @@
 """Normalisation / embedding ops (HIP on device tensors, fp32 reference on CPU)."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._lib import call, ptr
@@ -22,6 +24,24 @@ def rmsnorm_ref(x, w, eps, residual=None):
     return y.to(x.dtype)
 
 
+SMALL_ROWS = int(os.environ.get("GRAG_NORM_SMALL_ROWS", "16"))
+_NORM_WS: dict = {}
+
+
+def norm_ws(dev) -> tuple[torch.Tensor, torch.Tensor]:
+    """(tickets [64] int32, zeroed; chunk sums [64 * 64] fp32) of the small-batch split-K RMSNorm; allocated
+    before any hipGraph capture (LLMEngine does) -- every last arriver resets its ticket."""
+    dev = torch.device(dev)
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    ws = _NORM_WS.get(key)
+    if ws is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("norm ticket workspace must be allocated before hipGraph capture")
+        d = torch.device("cuda", key)
+        ws = _NORM_WS[key] = (torch.zeros(64, dtype=torch.int32, device=d), torch.zeros(64 * 64, device=d))
+    return ws
+
+
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None,
             out: torch.Tensor | None = None) -> torch.Tensor:
     """y = RMSNorm(x [+ residual]) * w.  With ``residual`` the sum is written
@@ -31,8 +51,13 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
             x = x.materialize()
         else:
             out = torch.empty(x.M, x.N, dtype=x.dtype, device=x.device) if out is None else out
-            call("grag_splitk_add_rmsnorm", ptr(x.planes), x.S, ptr(residual), ptr(w), ptr(out), x.M, x.N,
-                 float(eps))
+            if x.M <= SMALL_ROWS:  # 1-16 rows: the row's planes reduced by ceil(N / 512) workgroups
+                ws = norm_ws(x.device)
+                call("grag_splitk_add_rmsnorm_small", ptr(x.planes), x.S, ptr(residual), ptr(w), ptr(out), x.M, x.N,
+                     float(eps), ptr(ws[1]), ptr(ws[0]))
+            else:
+                call("grag_splitk_add_rmsnorm", ptr(x.planes), x.S, ptr(residual), ptr(w), ptr(out), x.M, x.N,
+                     float(eps))
             return out
     if not _on_gpu(x):
         return rmsnorm_ref(x, w, eps, residual)

@@ -456,6 +456,42 @@ def test_splitk_deferred_rmsnorm(dev, M, Nn, K):
     close(y, y2, 5e-2)
 
 
+@pytest.mark.parametrize("M,Nn,K", [(1, 3584, 3584), (4, 3584, 18944), (16, 3584, 3584), (3, 896, 4864)])
+def test_splitk_rmsnorm_small_rows_graph(dev, M, Nn, K):
+    """1-16 rows: the chunked split-K RMSNorm (ticket merge) against the one-block kernel's fp32 reference,
+    eagerly and replayed twice in a hipGraph (the tickets reset themselves)."""
+    from githubrepostorag_amd.ops import gemm as G
+    from githubrepostorag_amd.ops.linear import linear_deferred
+
+    x = rnd(M, K, dev=dev, scale=0.5)
+    w = rnd(Nn, K, dev=dev, scale=0.05, seed=1)
+    r = rnd(M, Nn, dev=dev, seed=2)
+    g = rnd(Nn, dev=dev, seed=3)
+    N.norm_ws(dev)
+    h32 = x.float().cpu() @ w.float().cpu().T
+    s32 = (h32 + r.float().cpu()).to(torch.bfloat16).float()
+    y32 = s32 * torch.rsqrt(s32.pow(2).mean(-1, keepdim=True) + 1e-6) * g.float().cpu()
+    part = linear_deferred(x, w)
+    assert isinstance(part, G.SplitKPartial), G.deferred_plan(M, Nn, K)
+    r1 = r.clone()
+    y = N.rmsnorm(part, g, 1e-6, residual=r1)
+    close(r1, s32, 3e-2)
+    close(y, y32, 5e-2)
+    r2 = r.clone()
+    out = torch.empty(M, Nn, dtype=torch.bfloat16, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        N.rmsnorm(linear_deferred(x, w), g, 1e-6, residual=r2, out=out)
+    for _ in range(2):
+        r2.copy_(r)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(r2, r1) and torch.equal(out, y)
+    assert int(N.norm_ws(dev)[0].abs().sum()) == 0
+
+
 def test_splitk_deferred_in_graph(dev):
     """The deferred projection + fused norm replay correctly inside a hipGraph (workspace sized eagerly)."""
     from githubrepostorag_amd.ops.linear import linear_deferred
