@@ -49,6 +49,7 @@ run() {  # run LIMIT NAME CMD...
 }
 
 npy=0
+npd=0
 REH="--steps 2 --warmup 1 --kv-cache-gb 48 --ingest-kv-gb 24 --ingest-files 48 --ingest-ref-cap-files 0 --agent-jobs 64"
 for step in "$@"; do
   key=${step%%=*}
@@ -68,7 +69,7 @@ for step in "$@"; do
     sweep) run 1100 sweep python -u bench.py --no-ingest --agent-sweep "${val:-64,256,512,1024}" --steps 2 --warmup 1 \
              ${SWEEP_ARGS//,/ } ;;
     prof) run 700 prof bash scripts/profile_bench.sh ;;
-    profdec) run 400 profdec env TAG="${TAG}" bash scripts/profile_decode_step.sh ${val//,/ } ;;
+    profdec) npd=$((npd+1)); run 400 "profdec$npd" env TAG="${TAG}_$npd" bash scripts/profile_decode_step.sh ${val//,/ } ;;
     pmcdec) run 400 "pmcdec_$npy" env TAG="${TAG}_pmc$npy" ARGS="${val//,/ }" bash scripts/pmc_dec.sh; npy=$((npy+1)) ;;
     pmcpy) run 600 "pmcpy_$npy" env TAG="${TAG}_pmcpy$npy" bash scripts/pmc_py.sh ${val//,/ }; npy=$((npy+1)) ;;
     py) npy=$((npy+1)); run 600 "py$npy" python -u ${val//,/ } ;;
