@@ -24,7 +24,9 @@ def rmsnorm_ref(x, w, eps, residual=None):
     return y.to(x.dtype)
 
 
-SMALL_ROWS = int(os.environ.get("GRAG_NORM_SMALL_ROWS", "16"))
+# the chunked ticket-merge kernel measured slower than one workgroup per row at B = 1 (8.6 vs 5.6 us: the
+# agent-scope release / acquire round trips outweigh the parallel plane reads; profiles/decode_step_b1_r5.txt)
+SMALL_ROWS = int(os.environ.get("GRAG_NORM_SMALL_ROWS", "0"))
 _NORM_WS: dict = {}
 
 

@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--tail", type=int, default=0, help="1: also the 8-wave tail-split decode schedules")
     ap.add_argument("--depths", default="", help="ring depths to A/B on the dispatched decode plan (e.g. 6,8)")
     ap.add_argument("--plan", default="", help="mt,nwv,ntw,ksplit[,gs] for the packed A/B (default dec_plan)")
+    ap.add_argument("--hot", type=int, default=0, help="1: also every arm on one weight copy (cache-hot)")
     ap.add_argument("--wnt", type=int, default=0, help="1: also the decode kernel with non-temporal weight loads")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -145,6 +146,9 @@ def main():
                             lib().grag_gemm_decode_wnt(prev)
                     arms["dec_default"] = lambda w, plan=plan, epi=epi: G.gemm_decode(x, w, epi=epi, plan=plan)
                     arms["dec_wnt"] = wnt
+                if a.hot:  # the same weight every launch: served from the 256 MB MALL / L2 when it fits
+                    for k in list(arms):
+                        arms[k + "_hot"] = (lambda f: (lambda w, f=f: f(ws[0])))(arms[k])
                 r = {"kernel": "mlp_gate_up" if silu else kernel_for(M, N, K), "plan": plan}
                 gb = N * K * 2 / 1e9
                 for k, fn in arms.items():
