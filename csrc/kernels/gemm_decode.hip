@@ -95,25 +95,18 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
 // Two 16-B W loads of one row: k [32s + 8 h4, +8) for s = 0, 1 (bytes 16 h4 and 64 + 16 h4 of the 128-B
 // line).  Default cache policy: the two half-line requests of a row share the L2 line (nontemporal loads
 // measured 5-20 % slower here: profiles/gemm_decode_ab_v2.jsonl).
+// The trailing s_nop: hipcc's hazard pass does not see into the asm, and a VALU write of the address VGPRs
+// right after the second load (register reuse across a branch showed it) must not land before the load has
+// read them (the same guard as glds16's).
 __device__ __forceinline__ void ldw2(bf16x8_t& lo, bf16x8_t& hi, const bf16* p) {
   asm volatile(
       "global_load_dwordx4 %0, %2, off\n\t"
-      "global_load_dwordx4 %1, %2, off offset:64"
+      "global_load_dwordx4 %1, %2, off offset:64\n\t"
+      "s_nop 1"
       : "=&v"(lo), "=&v"(hi)
       : "v"(p)
       : "memory");
 }
-// The same with the non-temporal hint: the weight stream (read once per step) should not evict the activation
-// tile every workgroup of an XCD re-reads from L2 (A / W A/B at 64-256 rows: grag_gemm_decode_wnt).
-__device__ __forceinline__ void ldw2_nt(bf16x8_t& lo, bf16x8_t& hi, const bf16* p) {
-  asm volatile(
-      "global_load_dwordx4 %0, %2, off nt\n\t"
-      "global_load_dwordx4 %1, %2, off offset:64 nt"
-      : "=&v"(lo), "=&v"(hi)
-      : "v"(p)
-      : "memory");
-}
-
 // Retire everything but the N youngest vector-memory ops; the named W registers are read-write here, so
 // nothing that consumes them can be scheduled above the wait.
 template <int N, int G>
@@ -148,7 +141,6 @@ struct DArgs {
   int msplit;                       // row blocks of 16*MT (adjacent on one XCD: the W lines are shared in L2)
   int packed;                       // W in the unit-packed layout (grag_gemm_decode doc)
   unsigned long long* stamps;       // diagnostics (grag_gemm_decode_stamps): per workgroup {start, end, xcc} or null
-  int wnt;                          // W loads non-temporal (grag_gemm_decode_wnt)
 };
 
 // NTW 16-row n-tiles per wave (32 or 64 W rows): the A fragment read from LDS feeds NTW MFMAs, so NTW = 4
@@ -250,10 +242,7 @@ void gemm_dec_kernel(DArgs p) {
 #pragma unroll
     for (int i = 0; i < GA; ++i) glds16(p.A + (ao[i] + so), adst[i] + slot * ABYTES);
 #pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-      if (p.wnt) ldw2_nt(wreg[2 * nt], wreg[2 * nt + 1], live ? wp[nt] + step * kstride : p.W);
-      else ldw2(wreg[2 * nt], wreg[2 * nt + 1], live ? wp[nt] + step * kstride : p.W);
-    }
+    for (int nt = 0; nt < NTW; ++nt) ldw2(wreg[2 * nt], wreg[2 * nt + 1], live ? wp[nt] + step * kstride : p.W);
   };
 
   // A fragment of rows 16 mt + li, logical chunk 4 s + h4 (swizzle depends on li only)
@@ -418,7 +407,6 @@ int launch_v(const DArgs& a, int epi, int act, int nwg, hipStream_t s) {
 // more than the 256 registers a wave gets at two waves per SIMD);  (nwv 8, ntw 2): mt 12.  ntw = 4 measured no faster than 2 at M = 192 (profiles/gemm_decode_ab_v3.jsonl) and is
 // not instantiated.
 static unsigned long long* g_dec_stamps = nullptr;
-static int g_dec_wnt = 0;  // 1: weight loads with the non-temporal hint (A/B, grag_gemm_decode_wnt)
 static int g_dec_depth = 0;  // 0: kDepth; 6 / 8: deeper rings where the LDS takes them (A/B, grag_gemm_decode_depth)
 
 // K-steps issued ahead for later launches (A/B of the ring depth): 0 = the default (kDepth = 4); 6 for mt 4 / 8
@@ -428,13 +416,6 @@ static int g_dec_depth = 0;  // 0: kDepth; 6 / 8: deeper rings where the LDS tak
 GRAG_API int grag_gemm_decode_depth(int d) {
   const int prev = g_dec_depth;
   g_dec_depth = d;
-  return prev;
-}
-
-// Weight loads of later launches with the non-temporal hint (1) or the default policy (0); returns the previous.
-GRAG_API int grag_gemm_decode_wnt(int v) {
-  const int prev = g_dec_wnt;
-  g_dec_wnt = v;
   return prev;
 }
 
@@ -506,7 +487,6 @@ GRAG_API int grag_gemm_decode_t(const void* A, const void* W, const void* bias, 
   a.msplit = msplit;
   a.packed = packed;
   a.stamps = g_dec_stamps;
-  a.wnt = g_dec_wnt;
   a.ksplit = ksplit;
   a.kt_split = kts;
   const int nwg = gs * ksplit * msplit;

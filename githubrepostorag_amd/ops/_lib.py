@@ -68,7 +68,6 @@ _SIGS = {
     "grag_gemm_decode_has_t": [I, I, I, I],
     "grag_gemm_decode_stamps": [P],
     "grag_gemm_decode_depth": [I],
-    "grag_gemm_decode_wnt": [I],
     "grag_gemm_w4": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_w4_has": [I, I],
 }

@@ -66,7 +66,6 @@ def main():
     ap.add_argument("--depths", default="", help="ring depths to A/B on the dispatched decode plan (e.g. 6,8)")
     ap.add_argument("--plan", default="", help="mt,nwv,ntw,ksplit[,gs] for the packed A/B (default dec_plan)")
     ap.add_argument("--hot", type=int, default=0, help="1: also every arm on one weight copy (cache-hot)")
-    ap.add_argument("--wnt", type=int, default=0, help="1: also the decode kernel with non-temporal weight loads")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     enable_tuned_gemms()
@@ -135,17 +134,6 @@ def main():
                             finally:
                                 lib().grag_gemm_decode_depth(prev)
                         arms[f"depth{d}_packed"] = deep_pk
-                if a.wnt and plan is not None:  # the weight stream with the non-temporal hint, same plan
-                    epi = G.EPI_SILU if silu else G.EPI_STORE
-
-                    def wnt(w, plan=plan, epi=epi):
-                        prev = lib().grag_gemm_decode_wnt(1)
-                        try:
-                            return G.gemm_decode(x, w, epi=epi, plan=plan)
-                        finally:
-                            lib().grag_gemm_decode_wnt(prev)
-                    arms["dec_default"] = lambda w, plan=plan, epi=epi: G.gemm_decode(x, w, epi=epi, plan=plan)
-                    arms["dec_wnt"] = wnt
                 if a.hot:  # the same weight every launch: served from the 256 MB MALL / L2 when it fits
                     for k in list(arms):
                         arms[k + "_hot"] = (lambda f: (lambda w, f=f: f(ws[0])))(arms[k])
