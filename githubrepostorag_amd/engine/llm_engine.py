@@ -31,6 +31,7 @@ import numpy as np
 import torch
 
 from ..ops.attention import KV_TILE, AttnMetadata
+from ..ops.gemm import WS
 from ..ops.sampling import SamplerState, reset_slots, sample, sample_tp
 from .scheduler import KVCacheManager, Scheduler
 from .sequence import Completion, SamplingParams, Sequence, SeqStatus
@@ -153,6 +154,9 @@ class LLMEngine:
         self.trace: list | None = None
         self._eos = set(getattr(tokenizer, "eos_token_ids", set()))
         self._lock = threading.RLock()
+        # split-K / stream-K workspaces of this engine's steps and graphs (ops/gemm.py WS.owned_by): owned by
+        # the engine, whichever thread steps it
+        self._ws: dict = {}
         max_split = -(-cfg.max_model_len // KV_TILE)
         self._max_b = max(cfg.graph_batch_sizes) if cfg.use_cuda_graph else cfg.max_num_seqs
         self._max_b = max(self._max_b, cfg.max_num_seqs)
@@ -256,7 +260,7 @@ class LLMEngine:
         step's prefill tokens (Scheduler.schedule)."""
         t0 = time.perf_counter()
         try:
-            with self._on_stream():
+            with self._on_stream(), WS.owned_by(self._ws):
                 return self._step(max_window, prefill_budget, bulk_budget)
         finally:
             self.stats["step_s"] += time.perf_counter() - t0
@@ -757,6 +761,10 @@ class LLMEngine:
             self._graph_pool = torch.cuda.graph_pool_handle()
 
     def _capture(self, B, nsplit, split_len, K=1) -> _DecodeGraph:
+        with WS.owned_by(self._ws):
+            return self._capture_ws(B, nsplit, split_len, K)
+
+    def _capture_ws(self, B, nsplit, split_len, K=1) -> _DecodeGraph:
         t0 = time.perf_counter()
         try:
             with gpu_guard():  # no other thread may sync / allocate while the capture is open

@@ -16,6 +16,7 @@ covers the chip.
 from __future__ import annotations
 
 import bisect
+import contextlib
 import json
 import os
 import threading
@@ -228,10 +229,40 @@ class _Workspace:
         self._tls = threading.local()
         self.retired: list = []
 
-    def get(self, dev: torch.device, floats: int) -> torch.Tensor:
+    def _bufs(self) -> dict:
+        o = getattr(self._tls, "owner", None)  # an engine's own workspace while it runs (WS.owned_by)
+        if o is not None:
+            return o.setdefault("bufs", {})
         bufs = getattr(self._tls, "bufs", None)
         if bufs is None:
             bufs = self._tls.bufs = {}
+        return bufs
+
+    def _cnts(self) -> dict:
+        o = getattr(self._tls, "owner", None)
+        if o is not None:
+            return o.setdefault("cnts", {})
+        cs = getattr(self._tls, "cnts", None)
+        if cs is None:
+            cs = self._tls.cnts = {}
+        return cs
+
+    @contextlib.contextmanager
+    def owned_by(self, owner: dict):
+        """Route this thread's workspace requests to ``owner`` (a dict the caller keeps) for the block.  An
+        engine runs its steps and graph captures under its own dict: a captured decode graph then points at
+        memory the ENGINE owns -- not at the capturing thread's buffers, which another thread's eager GEMMs
+        may be using when the graph replays (the harness captures on the main thread, an EngineRunner thread
+        replays) and which a thread-local dict would free when that thread exits."""
+        prev = getattr(self._tls, "owner", None)
+        self._tls.owner = owner
+        try:
+            yield
+        finally:
+            self._tls.owner = prev
+
+    def get(self, dev: torch.device, floats: int) -> torch.Tensor:
+        bufs = self._bufs()
         b = bufs.get(dev.index)
         if b is None or b.numel() < floats:
             if torch.cuda.is_current_stream_capturing():
@@ -243,14 +274,15 @@ class _Workspace:
         return b
 
     def ready(self, dev: torch.device, floats: int) -> bool:
-        b = getattr(self._tls, "bufs", {}).get(dev.index)
+        b = self._bufs().get(dev.index)
         return b is not None and b.numel() >= floats
+
+    def has_counters(self, dev: torch.device) -> bool:
+        return self._cnts().get(dev.index) is not None
 
     def counters(self, dev: torch.device) -> torch.Tensor:
         """Stream-K arrival tickets: zero at rest (each tile's last arriver resets its word)."""
-        cs = getattr(self._tls, "cnts", None)
-        if cs is None:
-            cs = self._tls.cnts = {}
+        cs = self._cnts()
         c = cs.get(dev.index)
         if c is None:
             if torch.cuda.is_current_stream_capturing():
@@ -560,7 +592,7 @@ def capture_ok(dev: torch.device, M: int, N: int, K: int, silu: bool = False) ->
     ks, sk = schedule(M, N, K, silu)
     fl = _ws_floats(M, N, ks, sk)
     return fl == 0 or not torch.cuda.is_current_stream_capturing() or (WS.ready(dev, fl) and (
-        not sk or getattr(WS._tls, "cnts", {}).get(dev.index) is not None))
+        not sk or WS.has_counters(dev)))
 
 
 def mlp_gate_up(x: torch.Tensor, w_gu: torch.Tensor, b_gu: torch.Tensor | None = None) -> torch.Tensor:

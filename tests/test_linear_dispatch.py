@@ -161,3 +161,30 @@ def test_config4_per_rank_projections_are_measured_and_owned_unless_the_library_
         assert all(G.prefill_plan(M, 2 * inter, H, silu=True) is not None for M in range(384, 16385, 512))
     finally:
         G._num_cus = ncu
+
+
+def test_workspace_owned_by_engine_not_thread(monkeypatch):
+    """ops/gemm.py WS.owned_by: inside the block a thread's split-K workspace requests go to the owner's dict
+    (an engine's, kept for its lifetime: its captured decode graphs point at it), outside to the thread's
+    own; another thread never sees the owner's buffer."""
+    import threading
+
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
+    dev = torch.device("cpu")
+    own = {}
+    with G.WS.owned_by(own):
+        b = G.WS.get(dev, 10)
+        assert G.WS.ready(dev, 10) and G.WS.get(dev, 5) is b
+    assert own["bufs"][None] is b
+    assert G.WS.get(dev, 10) is not b  # the thread's own buffer outside the block
+    seen = []
+
+    def other():
+        seen.append(G.WS.get(dev, 10) is b)
+        with G.WS.owned_by(own):
+            seen.append(G.WS.get(dev, 10) is b)
+
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert seen == [False, True]
