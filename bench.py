@@ -1109,7 +1109,9 @@ def concurrent_phase(args, model, tok, emb, prepare, sp, u, dev, group, world, d
             n += 1
         t_ing = time.perf_counter() - t0
         th.join()
-        tt = [pump.get()[0] for _ in range(n)]
+        got = [pump.get() for _ in range(n)]
+        tt, te = [g[0] for g in got], sorted(g[1] for g in got)
+        retr = sorted(pump.retrieval)
         pump.drain_and_stop(completed=n)
     finally:
         runner.shutdown()
@@ -1125,6 +1127,9 @@ def concurrent_phase(args, model, tok, emb, prepare, sp, u, dev, group, world, d
            "p50_ttft_ms": None if p50 is None else round(p50, 2), "p90_ttft_ms": None if p90 is None else round(p90, 2),
            "ingest_free": {"load": base["load"], "p50_ttft_ms": base["p50_ttft_ms"], "p90_ttft_ms": base["p90_ttft_ms"]},
            "ttft_p50_vs_ingest_free": None if p50 is None else round(p50 / base["p50_ttft_ms"], 3),
+           # TTFT = retrieval (embed + search + prompt, on the GPU beside the engine) + submit -> first token
+           "retrieval_p50_ms": round(1000 * retr[len(retr) // 2], 2) if retr else None,
+           "submit_to_first_token_p50_ms": round(1000 * te[len(te) // 2], 2) if te else None,
            "engine": (st or {}).get("engine"),
            "setup": "one LLMEngine + EngineRunner (max_model_len 8192) shared by the ingest pipeline and the "
                     "serving loop's per-query arrivals (Poisson at the ingest-free open loop's load, until the "
