@@ -103,9 +103,21 @@ class _StreamWorkspace:
     outside graph capture; GEMMs on one stream reuse it in stream order."""
 
     def __init__(self):
-        self.slab = {}
-        self.counters = {}
+        self._slab = {}
+        self._counters = {}
         self._retired = []  # outgrown slabs stay alive: captured hipGraphs may still point at them
+
+    # an engine's steps and graph captures use its own slab / tickets (ops/gemm.py WS.owned_by): a decode
+    # graph's LM head must not share them with another engine's or thread's eager stream-K launches
+    @property
+    def slab(self) -> dict:
+        o = getattr(_tile.WS._tls, "owner", None)
+        return self._slab if o is None else o.setdefault("stream_slab", {})
+
+    @property
+    def counters(self) -> dict:
+        o = getattr(_tile.WS._tls, "owner", None)
+        return self._counters if o is None else o.setdefault("stream_cnt", {})
 
     def ready(self, dev: torch.device, M: int, N: int, K: int) -> bool:
         """True when a graph capture can use the stream kernel for this shape
