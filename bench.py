@@ -158,6 +158,8 @@ def parse():
     ap.add_argument("--bulk-prefill", type=int, default=1024,
                     help="of --interactive-prefill, the prefill tokens per step bulk work (ingest) may take while "
                          "interactive arrivals keep coming (EngineRunner bulk_prefill; 0: no separate cap)")
+    ap.add_argument("--heartbeat", type=float, default=0.0,
+                    help="seconds between rank 0's progress lines (engine step counters); 0: none")
     ap.add_argument("--low-load", type=int, default=1,
                     help="1: the reference's own regime (vLLM --max-num-seqs 4 --max-model-len 11712): single-prompt "
                          "TTFT at 1K / 4K / 11.6K tokens, decode TPOT at 1 / 4 / 16 live sequences x those contexts "
@@ -337,6 +339,19 @@ def main():
                                              mixed_batches=bool(args.mixed), kv_cache_gb=args.kv_cache_gb,
                                              max_model_len=max_len, use_cuda_graph=not args.no_graph,
                                              seed=dp_rank, graph_batch_sizes=gsizes))
+    if args.heartbeat > 0 and rank == 0:
+        import threading
+
+        # a line every --heartbeat seconds from rank 0 (engine step counters): long multi-rank rehearsals
+        # (Qwen2-72B at TP=8 over gloo on one card) show progress between phase lines
+        def _beat():
+            t_hb = time.perf_counter()
+            while True:
+                time.sleep(args.heartbeat)
+                st = eng.stats
+                print(f"[bench] alive {time.perf_counter() - t_hb:.0f} s: engine steps {st['steps']}, prefill "
+                      f"tokens {st['prefill_tokens']}, decode tokens {st['decode_tokens']}", file=sys.stderr, flush=True)
+        threading.Thread(target=_beat, name="bench-heartbeat", daemon=True).start()
     sp = (SamplingParams(max_tokens=args.gen_len, temperature=0.0, ignore_eos=True) if args.greedy else
           SamplingParams(max_tokens=args.gen_len, temperature=0.4, top_p=0.8, repetition_penalty=1.2,
                          ignore_eos=True))

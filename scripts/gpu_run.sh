@@ -65,7 +65,8 @@ for step in "$@"; do
     c4tp8) run 1100 c4tp8 env GRAG_DIST_BACKEND=gloo python -u bench.py --gpus 8 --tp 8 --model qwen2-72b \
              --index-size 2000000 --nlist 1024 --nprobe 32 --batch 8 --inflight 2 --arrival-groups 2 --steps 2 \
              --warmup 1 --kv-cache-gb 6 --max-batched-tokens 480 --no-ingest --agent-jobs 4 \
-             --agent-concurrency 4 --serving-steps 0 ${val//,/ } ;;
+             --agent-concurrency 4 --serving-steps 0 --prompt-len 256 --gen-len 16 --agent-gen-len 8 \
+             --agent-synth-len 16 --low-load 0 --recall-queries 8 --heartbeat 30 ${val//,/ } ;;
     sweep) run 1100 sweep python -u bench.py --no-ingest --agent-sweep "${val:-64,256,512,1024}" --steps 2 --warmup 1 \
              ${SWEEP_ARGS//,/ } ;;
     prof) run 700 prof bash scripts/profile_bench.sh ;;
