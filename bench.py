@@ -155,7 +155,7 @@ def parse():
                     help="after the closed loop: open-loop Poisson arrivals of query groups at these fractions of "
                          "the closed loop's throughput through the same serving loop (serving_runner.open_loop: "
                          "TTFT p50 / p90 at each load; empty: skip)")
-    ap.add_argument("--bulk-prefill", type=int, default=1024,
+    ap.add_argument("--bulk-prefill", type=int, default=512,
                     help="of --interactive-prefill, the prefill tokens per step bulk work (ingest) may take while "
                          "interactive arrivals keep coming (EngineRunner bulk_prefill; 0: no separate cap)")
     ap.add_argument("--heartbeat", type=float, default=0.0,

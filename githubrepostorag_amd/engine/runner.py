@@ -109,7 +109,7 @@ class EngineRunner:
     # of that budget, the tokens bulk work (ingest: submitted with interactive=False) may take per step while
     # interactive arrivals keep coming: the step an arrival waits for and the step carrying its prompt stay
     # short; 0 = no separate cap
-    BULK_PREFILL = int(os.environ.get("GRAG_BULK_PREFILL", "1024"))
+    BULK_PREFILL = int(os.environ.get("GRAG_BULK_PREFILL", "512"))
 
     def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005, watchdog_s: float = 120.0,
                  on_health=None, tp=None, start: bool = True, interactive_prefill: int | None = None,

@@ -232,7 +232,7 @@ class Scheduler:
         passes a smaller one while interactive arrivals queue, so one step never carries a burst's worth
         of prompts and the first of them reach their first token sooner).  ``bulk_budget``: of that, at most
         this many tokens for requests below INTERACTIVE_PRIORITY (ingest beside the serving loop: the step an
-        arrival waits for, and the step that carries its prompt, stay short)."""
+        arrival waits for stays short), and none in a step that carries an interactive prompt."""
         with self.lock:
             budget = min(budget or self.max_num_batched_tokens, self.max_num_batched_tokens)
             items = []
@@ -250,6 +250,10 @@ class Scheduler:
             i = 0
             admit_ok = True
             bulk_left = bulk_budget if bulk_budget is not None else 1 << 30
+            if bulk_budget is not None and (
+                    (self.waiting and self.waiting[0].params.priority >= INTERACTIVE_PRIORITY)
+                    or any(q.params.priority >= INTERACTIVE_PRIORITY for q in pf)):
+                bulk_left = 0  # a step that carries an interactive prompt carries no bulk prefill: it stays short
 
             def cap(seq, n):  # the bulk share of this step's budget
                 return n if seq.params.priority >= INTERACTIVE_PRIORITY else min(n, bulk_left)

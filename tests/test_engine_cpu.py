@@ -299,8 +299,10 @@ def test_bulk_budget_caps_low_priority_prefill(model, tok):
     bulk = SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True)
     hi = SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True, priority=INTERACTIVE_PRIORITY)
     rb = eng.add_request([(5 * i) % 200 + 3 for i in range(100)], bulk)
+    eng.step(prefill_budget=64, bulk_budget=8)  # bulk alone: its 8-token share
+    assert eng.get(rb).num_computed == 8
     rh = eng.add_request([(3 * i) % 200 + 3 for i in range(40)], hi)
-    eng.step(prefill_budget=64, bulk_budget=8)
+    eng.step(prefill_budget=64, bulk_budget=8)  # a step carrying an interactive prompt carries no bulk
     assert eng.get(rh).num_computed == 40 and eng.get(rb).num_computed == 8
     eng.step(prefill_budget=64, bulk_budget=8)  # the interactive prompt decodes; bulk gets 8 more
     assert eng.get(rb).num_computed <= 16
