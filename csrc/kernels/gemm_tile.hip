@@ -171,7 +171,7 @@ __device__ __forceinline__ void acc_zero(typename Shape<MF>::Acc& acc) {
   for (int c = 0; c < 8; ++c) chunk_set<MF>(acc, c, f32x4_t{0.f, 0.f, 0.f, 0.f});
 }
 
-template <int EPI, int ACT, int MF>
+template <int EPI, int ACT, int MF, int SCHED>
 __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
   using Acc = typename Shape<MF>::Acc;
   using FragA = typename Shape<MF>::FA;
@@ -271,6 +271,89 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
     acc_zero<MF>(acc01);
     acc_zero<MF>(acc11);
     acc_zero<MF>(acc10);
+    if constexpr (SCHED == 1) {
+      // Balanced schedule: 8 / 4 / 8 / 4 fragment reads per phase instead of 12 / 4 / 8 / 0.  P4 of
+      // K-tile t reads the B quadrant that tile t+1 starts with (its own MFMAs use the other one), so
+      // the quadrant order alternates with the tile's parity e (qe = the B held at tile start:
+      // 1 on even tiles, 0 on odd):
+      //   P1 (0,qe)  A q0        refill B qe of t+2   (its slot was last read in P4 of t-1)
+      //   P2 (0,ql)  B ql        refill A q0 of t+2
+      //   P3 (1,ql)  A q1        refill B ql of t+2
+      //   P4 (1,qe)  B ql of t+1 refill A q1 of t+2
+      // Every slot is refilled in the phase after its only read and read 7 phases after the refill
+      // (>= 6 needed with the counted vmcnt(8) per phase and the one-interval stagger, see above).
+      // The tail needs no variant: the refills of the last two K-tiles re-load the segment's last
+      // K-tile (clamped index, valid addresses) into slots nobody reads again, so every phase issues
+      // 2 LDS-DMA and one vmcnt(8) count serves all of them; the loop drains before it returns.
+      const int klast = nk - 1;
+      issueB(1, 0, 0);
+      issueA(0, 0, 0);
+      issueB(0, 0, 0);
+      issueA(1, 0, 0);
+      issueB(0, min(1, klast), 1);
+      issueA(0, min(1, klast), 1);
+      issueB(1, min(1, klast), 1);
+      issueA(1, min(1, klast), 1);
+      wait_vm<8>();
+      bar();
+      readB(b1, 1, 0);  // tile 0 starts holding B q1; its slot is refilled in P1(0), after the next barrier
+      wait_lgkm0();
+      bar();
+      if (lag) bar();
+      auto ktile2 = [&](int kt, auto odd_c) {
+        constexpr bool ODD = decltype(odd_c)::value;
+        constexpr int qe = ODD ? 0 : 1, ql = 1 - qe;
+        FragB& be = ODD ? b0 : b1;
+        FragB& bl = ODD ? b1 : b0;
+        Acc& acc0e = ODD ? acc00 : acc01;
+        Acc& acc0l = ODD ? acc01 : acc00;
+        Acc& acc1e = ODD ? acc10 : acc11;
+        Acc& acc1l = ODD ? acc11 : acc10;
+        const int buf = kt & 1;
+        const int kn = min(kt + 2, klast);
+        // P1
+        readA(a, 0, buf);
+        issueB(qe, kn, buf);
+        wait_lgkm0();
+        bar();
+        mma_cluster<MF>(acc0e, a, be);
+        wait_vm<8>();
+        bar();
+        // P2
+        readB(bl, ql, buf);
+        issueA(0, kn, buf);
+        wait_lgkm0();
+        bar();
+        mma_cluster<MF>(acc0l, a, bl);
+        wait_vm<8>();
+        bar();
+        // P3
+        readA(a, 1, buf);
+        issueB(ql, kn, buf);
+        wait_lgkm0();
+        bar();
+        mma_cluster<MF>(acc1l, a, bl);
+        wait_vm<8>();
+        bar();
+        // P4
+        if (kt < klast) readB(bl, ql, buf ^ 1);
+        issueA(1, kn, buf);
+        wait_lgkm0();
+        bar();
+        mma_cluster<MF>(acc1e, a, be);
+        wait_vm<8>();
+        bar();
+      };
+      int kt = 0;
+      for (; kt < klast; kt += 2) {
+        ktile2(kt, std::integral_constant<bool, false>{});
+        ktile2(kt + 1, std::integral_constant<bool, true>{});
+      }
+      if (kt == klast) ktile2(kt, std::integral_constant<bool, false>{});
+      wait_vm<0>();  // the clamped re-loads land before the LDS is reused (next segment / stream-K flag)
+      if (!lag) bar();
+      return;
+    }
     // prologue: tile 0 (all 4 slots) + tile 1 (A q0, B q0, B q1); tile 1's A q1 goes out in P1(0)
     issueA(0, 0, 0);
     issueB(0, 0, 0);
@@ -630,12 +713,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 int g_mfma = 16;  // grag_gemm_tile_mfma()
+int g_sched = 0;  // grag_gemm_tile_sched(): 0 the 12/4/8/0-read phase schedule, 1 the balanced 8/4/8/4 one
 
 template <int EPI, int ACT>
 int launch(const Args& a, hipStream_t stream) {
   const int nwg = a.dp_tiles + a.sk_grid;
-  if (g_mfma == 32) gemm_tile_kernel<EPI, ACT, 32><<<nwg, kThreads, 0, stream>>>(a);
-  else gemm_tile_kernel<EPI, ACT, 16><<<nwg, kThreads, 0, stream>>>(a);
+  if (g_mfma == 32) gemm_tile_kernel<EPI, ACT, 32, 0><<<nwg, kThreads, 0, stream>>>(a);
+  else if (g_sched == 1) gemm_tile_kernel<EPI, ACT, 16, 1><<<nwg, kThreads, 0, stream>>>(a);
+  else gemm_tile_kernel<EPI, ACT, 16, 0><<<nwg, kThreads, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
 
@@ -646,6 +731,14 @@ int launch(const Args& a, hipStream_t stream) {
 GRAG_API int grag_gemm_tile_mfma(int mf) {
   const int prev = g_mfma;
   if (mf == 16 || mf == 32) g_mfma = mf;
+  return prev;
+}
+
+// Phase schedule of the 16x16x32 tile kernel for later launches (0 or 1, see gemm_tile_kernel's
+// mainloop); any other value only queries.  Returns the previous schedule.
+GRAG_API int grag_gemm_tile_sched(int sched) {
+  const int prev = g_sched;
+  if (sched == 0 || sched == 1) g_sched = sched;
   return prev;
 }
 

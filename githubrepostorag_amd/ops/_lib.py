@@ -62,6 +62,7 @@ _SIGS = {
     "grag_gemm_tile": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "grag_splitk_reduce": [P, P, P, I, I, I, I, I, I, P],
     "grag_gemm_tile_mfma": [I],
+    "grag_gemm_tile_sched": [I],
     "grag_gemm_decode": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_decode_has": [I, I, I],
     "grag_gemm_decode_t": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, I, P, P],
@@ -103,6 +104,9 @@ def lib():
         mf = os.environ.get("GRAG_GEMM_MFMA")
         if mf and getattr(handle, "grag_gemm_tile_mfma", None) is not None:
             handle.grag_gemm_tile_mfma(int(mf))  # tile GEMM MFMA shape (16 default, 32)
+        sc = os.environ.get("GRAG_GEMM_SCHED")
+        if sc and getattr(handle, "grag_gemm_tile_sched", None) is not None:
+            handle.grag_gemm_tile_sched(int(sc))  # tile GEMM phase schedule (0, 1 balanced reads)
         _lib = handle
         return _lib
 

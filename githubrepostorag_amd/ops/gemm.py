@@ -214,6 +214,14 @@ def set_mfma(mf: int) -> int:
     return int(lib().grag_gemm_tile_mfma(int(mf)))
 
 
+def set_sched(sched: int) -> int:
+    """Select the 16x16x32 tile kernel's phase schedule (0: 12/4/8/0 fragment reads per phase; 1: the
+    balanced 8/4/8/4 order, csrc/kernels/gemm_tile.hip ``SCHED``).  Returns the previous schedule."""
+    from ._lib import lib
+
+    return int(lib().grag_gemm_tile_sched(int(sched)))
+
+
 def _ws_floats(M: int, N: int, ksplit: int, sk: int) -> int:
     return ksplit * M * N if ksplit > 1 else (2 * abs(sk) * 65536 if sk else 0)
 

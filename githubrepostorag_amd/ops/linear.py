@@ -228,7 +228,7 @@ def splitk_parts(M: int, N: int, K: int) -> int:
     projections (down_proj: K = 18944 = 5.3 N) at decode batches: hipBLASLt
     has only N/tile x M/tile output tiles (~56 workgroups for 256 CUs) and no
     split-K solution in the tuned table.  Cold-weight hipGraph timings
-    (scripts/bench_splitk.py, profiles/splitk_decode_gemm.jsonl), down_proj
+    (round-1 microbench, profiles/splitk_decode_gemm.jsonl), down_proj
     N=3584: 8 slices at M=160 105.7 -> 62.7 us, 192 75.9 -> 66.3, 224 117.4 ->
     70.0, 256 77.0 -> 56.7; 2 slices at M=96 63.5 -> 52.4, M=64 46.5 -> 43.0.
     At M=128 and for o/qkv/gate_up the library wins.  Decode batch range only,

@@ -418,3 +418,50 @@ def test_gemm_decode_small_rows(dev, depth, M, N, K, silu):
         check(y1, want.reshape(M, -1), K)
     else:
         check(y1, ref(x, w, b), K)
+
+
+# ---------------------------------------------------------------- balanced phase schedule (gemm_tile.hip SCHED 1)
+@pytest.fixture
+def sched1():
+    prev = G.set_sched(1)
+    yield
+    G.set_sched(prev)
+
+
+@pytest.mark.parametrize("M,N,K,ks,sk", [(256, 256, 128, 1, 0), (300, 520, 192, 1, 0), (777, 3584, 640, 1, 0),
+                                         (4096, 4608, 3584, 1, 0), (200, 1024, 1024, 4, 0), (192, 3584, 18944, 8, 0),
+                                         (512, 1536, 512, 1, 20), (2560, 1024, 384, 1, 16),
+                                         (7040, 3584, 2048, 1, -408), (1280, 4608, 1024, 1, -270)])
+def test_gemm_balanced_schedule(dev, M, N, K, ks, sk):
+    # every K-tile count parity, 2- and 3-tile segments, split-K planes and stream-K shares; each accumulator
+    # sees the same K order under both schedules, so the results are bitwise equal to schedule 0's
+    x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+    prev = G.set_sched(0)
+    try:
+        y0 = G.gemm(x, w, b, ksplit=ks, sk=sk)
+        G.set_sched(1)
+        y1 = G.gemm(x, w, b, ksplit=ks, sk=sk)
+    finally:
+        G.set_sched(prev)
+    check(y1, ref(x, w, b), K)
+    assert torch.equal(y0, y1)
+
+
+@pytest.mark.parametrize("M,I,K,sk", [(700, 512, 384, 0), (768, 2048, 1024, -20), (192, 4096, 1024, 48)])
+def test_gemm_silu_balanced_schedule(dev, sched1, M, I, K, sk):
+    x = rnd(M, K, dev=dev, scale=0.5)
+    wg, wu = rnd(I, K, dev=dev, seed=1, scale=0.3), rnd(I, K, dev=dev, seed=2, scale=0.3)
+    h = G.gemm_silu(x, G.interleave_gate_up(wg, wu), ksplit=1, sk=sk)
+    check(h, torch.nn.functional.silu(ref(x, wg)) * ref(x, wu), K)
+
+
+def test_gemm_balanced_identity_gelu(dev, sched1):
+    K = 256
+    x = torch.eye(K, dtype=torch.bfloat16, device=dev)
+    w = (torch.arange(K * 264, dtype=torch.float32).reshape(264, K) % 251 - 125).to(torch.bfloat16).to(dev)
+    b = rnd(264, dev=dev, seed=3)
+    assert torch.equal(G.gemm(x, w, b, ksplit=1).cpu(), (w.float().T + b.float()).to(torch.bfloat16).cpu())
+    M, N, K = 333, 1024, 384
+    x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
+    r = torch.nn.functional.gelu(ref(x, w, b))
+    check(G.gemm(x, w, b, act=G.ACT_GELU, ksplit=1), r, K)
