@@ -12,9 +12,9 @@
 #   tp2              shared-GPU TP rehearsal: bench --gpus 2 --tp 2 (IPC all-reduce + vocab-parallel
 #                    sampler in the decode graphs, lockstep ingest and agent)
 #   c4tp8            BASELINE config 4's per-rank shapes rehearsed on ONE GPU: Qwen2-72B at TP=8 as 8 rank
-#                    processes sharing the card (18 GB of weights each), small batch / index / KV; prefill
-#                    chunks of 480 tokens keep every all-reduce on the one-shot IPC path (gloo would stage
-#                    the large ones through the host)
+#                    processes sharing the card (18 GB of weights each), small batch / index / KV; ranks
+#                    sharing a device run process-group (gloo-staged) collectives and eager decode, so
+#                    the agent phase is one job (4 took > 400 s, profiles/rehearse_c4tp8_shared_gpu_r5.log)
 #   sweep=LEVELS     bench with --agent-sweep LEVELS (agent saturation curve); SWEEP_ARGS=a,b,.. extra bench args
 #   prof             rocprofv3 --kernel-trace --stats over a 2-step bench (scripts/profile_bench.sh)
 #   mb=WHAT          scripts/microbench.py --what WHAT (json in gpurun_out/<TAG>_mb_WHAT.json)
@@ -64,8 +64,8 @@ for step in "$@"; do
     tp2) run 900 tp2 env GRAG_DIST_BACKEND=gloo python -u bench.py --gpus 2 --tp 2 $REH ${val//,/ } ;;
     c4tp8) run 1100 c4tp8 env GRAG_DIST_BACKEND=gloo python -u bench.py --gpus 8 --tp 8 --model qwen2-72b \
              --index-size 2000000 --nlist 1024 --nprobe 32 --batch 8 --inflight 2 --arrival-groups 2 --steps 2 \
-             --warmup 1 --kv-cache-gb 6 --max-batched-tokens 480 --no-ingest --agent-jobs 4 \
-             --agent-concurrency 4 --serving-steps 0 --prompt-len 256 --gen-len 16 --agent-gen-len 8 \
+             --warmup 1 --kv-cache-gb 6 --max-batched-tokens 480 --no-ingest --agent-jobs 1 \
+             --agent-concurrency 1 --serving-steps 0 --prompt-len 256 --gen-len 16 --agent-gen-len 8 \
              --agent-synth-len 16 --low-load 0 --recall-queries 8 --heartbeat 30 ${val//,/ } ;;
     sweep) run 1100 sweep python -u bench.py --no-ingest --agent-sweep "${val:-64,256,512,1024}" --steps 2 --warmup 1 \
              ${SWEEP_ARGS//,/ } ;;
