@@ -94,6 +94,7 @@ struct Args {
   int sk_grid;     // blockIdx >= dp_tiles: stream-K workgroups over the remaining tiles
   float* slab;     // split-K partial planes, or 2 x 256 KB stream-K slots per SK workgroup
   unsigned* cnt;   // stream-K arrival tickets, one per SK tile (zero at rest)
+  int a_bytes, w_bytes;  // buffer-resource extents of A / W (SCHED 1; both < 2 GB)
 };
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
@@ -232,6 +233,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
     }
   };
 
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.W, 0, p.w_bytes, 0x00020000);
   Acc acc00, acc01, acc11, acc10;
   FragA a;
   FragB b0, b1;
@@ -240,8 +243,12 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
   auto mainloop = [&](int m0, int n0, int kb, int nk) {
     // LDS-DMA sources: piece q = 2w + i fills slot rows [8q, 8q+8); lane -> row 8q + L/8,
     // physical chunk L%8 = logical chunk c ^ ((row >> 1) & 7)
+    // SCHED 1 addresses through buffer resources: a 32-bit byte offset per (quadrant, piece) and the
+    // K-tile step in the scalar offset (half the address VGPRs of 64-bit pointers; the launcher keeps
+    // both operands under 2 GB for it).  Rows are clamped either way, so every access is in range.
     const bf16* srcA[2][2];
     const bf16* srcB[2][2];
+    unsigned offA[2][2], offB[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int rs = (2 * w + i) * 8 + (L >> 3);
@@ -251,21 +258,37 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
       for (int q = 0; q < 2; ++q) {
         int gm = m0 + (rs >> 6) * 128 + q * 64 + (rs & 63);
         gm = gm < p.M ? gm : p.M - 1;
-        srcA[q][i] = p.A + (size_t)gm * p.lda + koff;
         int gn = n0 + (rs >> 5) * 64 + q * 32 + (rs & 31);
         gn = gn < p.N ? gn : p.N - 1;
-        srcB[q][i] = p.W + (size_t)gn * p.ldw + koff;
+        if constexpr (SCHED == 1) {
+          offA[q][i] = (unsigned)(gm * p.lda + koff) * 2u;
+          offB[q][i] = (unsigned)(gn * p.ldw + koff) * 2u;
+        } else {
+          srcA[q][i] = p.A + (size_t)gm * p.lda + koff;
+          srcB[q][i] = p.W + (size_t)gn * p.ldw + koff;
+        }
       }
     }
     // slot order inside a buffer: 0 A q0, 1 A q1, 2 B q0, 3 B q1
     auto issueA = [&](int q, int kt, int buf) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) glds16(srcA[q][i] + kt * 64, smem + buf * kBuf + q * kSlot + (2 * w + i) * 1024);
+      for (int i = 0; i < 2; ++i) {
+        char* dst = smem + buf * kBuf + q * kSlot + (2 * w + i) * 1024;
+        if constexpr (SCHED == 1)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void_t*)dst, 16, offA[q][i], kt * 128, 0, 0);
+        else
+          glds16(srcA[q][i] + kt * 64, dst);
+      }
     };
     auto issueB = [&](int q, int kt, int buf) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        glds16(srcB[q][i] + kt * 64, smem + buf * kBuf + (2 + q) * kSlot + (2 * w + i) * 1024);
+      for (int i = 0; i < 2; ++i) {
+        char* dst = smem + buf * kBuf + (2 + q) * kSlot + (2 * w + i) * 1024;
+        if constexpr (SCHED == 1)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void_t*)dst, 16, offB[q][i], kt * 128, 0, 0);
+        else
+          glds16(srcB[q][i] + kt * 64, dst);
+      }
     };
     acc_zero<MF>(acc00);
     acc_zero<MF>(acc01);
@@ -713,13 +736,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 int g_mfma = 16;  // grag_gemm_tile_mfma()
-int g_sched = 0;  // grag_gemm_tile_sched(): 0 the 12/4/8/0-read phase schedule, 1 the balanced 8/4/8/4 one
+int g_sched = 1;  // grag_gemm_tile_sched(): 1 the balanced 8/4/8/4-read phase schedule (default: +5-10 % on
+                  // the prefill shapes, profiles/ab_tile_sched_r5.json), 0 the 12/4/8/0 one
 
 template <int EPI, int ACT>
 int launch(const Args& a, hipStream_t stream) {
   const int nwg = a.dp_tiles + a.sk_grid;
   if (g_mfma == 32) gemm_tile_kernel<EPI, ACT, 32, 0><<<nwg, kThreads, 0, stream>>>(a);
-  else if (g_sched == 1) gemm_tile_kernel<EPI, ACT, 16, 1><<<nwg, kThreads, 0, stream>>>(a);
+  else if (g_sched == 1 && a.a_bytes > 0 && a.w_bytes > 0) gemm_tile_kernel<EPI, ACT, 16, 1><<<nwg, kThreads, 0, stream>>>(a);
   else gemm_tile_kernel<EPI, ACT, 16, 0><<<nwg, kThreads, 0, stream>>>(a);
   return (int)hipGetLastError();
 }
@@ -817,6 +841,11 @@ GRAG_API int grag_gemm_tile(const void* A, const void* W, const void* bias, void
   a.cnt = (unsigned*)cnt;
   a.lda = lda; a.ldw = ldw; a.ldc = ldc;
   a.M = M; a.N = N; a.K = K;
+  {  // SCHED 1's 32-bit offsets: operands of 2 GB or more take schedule 0 (64-bit pointers)
+    const long ab = (long)M * lda * 2, wb = (long)N * ldw * 2;
+    a.a_bytes = ab < (1L << 31) ? (int)ab : 0;
+    a.w_bytes = wb < (1L << 31) ? (int)wb : 0;
+  }
   a.tiles_m = (M + 255) / 256;
   a.tiles_n = (N + 255) / 256;
   a.ksplit = ksplit;
