@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--depths", default="", help="ring depths to A/B on the dispatched decode plan (e.g. 6,8)")
     ap.add_argument("--plan", default="", help="mt,nwv,ntw,ksplit[,gs] for the packed A/B (default dec_plan)")
     ap.add_argument("--hot", type=int, default=0, help="1: also every arm on one weight copy (cache-hot)")
+    ap.add_argument("--tile", default="", help="stream-K grids of the 256x256 tile kernel to A/B (e.g. 256:192; "
+                                               "k2 = 2-way split-K with the reduce)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     enable_tuned_gemms()
@@ -134,13 +136,24 @@ def main():
                             finally:
                                 lib().grag_gemm_decode_depth(prev)
                         arms[f"depth{d}_packed"] = deep_pk
+                for t in [v for v in a.tile.replace(":", ",").split(",") if v.strip()]:
+                    ks_t, sk_t = (int(t[1:]), 0) if t.startswith("k") else (1, int(t))
+                    G.WS.reserve(dev, G._ws_floats(M, N, ks_t, sk_t))
+                    if silu:
+                        arms[f"tile_{t}"] = lambda w, ks_t=ks_t, sk_t=sk_t: G.gemm_silu(x, w, ksplit=ks_t, sk=sk_t)
+                    else:
+                        arms[f"tile_{t}"] = lambda w, ks_t=ks_t, sk_t=sk_t: G.gemm(x, w, ksplit=ks_t, sk=sk_t)
                 if a.hot:  # the same weight every launch: served from the 256 MB MALL / L2 when it fits
                     for k in list(arms):
                         arms[k + "_hot"] = (lambda f: (lambda w, f=f: f(ws[0])))(arms[k])
                 r = {"kernel": "mlp_gate_up" if silu else kernel_for(M, N, K), "plan": plan}
                 gb = N * K * 2 / 1e9
                 for k, fn in arms.items():
-                    us = graph_time(fn, ws, a.reps)
+                    try:
+                        us = graph_time(fn, ws, a.reps)
+                    except RuntimeError as e:  # a schedule the launcher refuses for this shape
+                        r[k] = {"error": str(e)[:120]}
+                        continue
                     r[k] = {"us": round(us, 2), "TB_s": round(gb / (us * 1e-6) / 1e3, 3)}
                 out[f"{name}_M{M}"] = r
                 print(name, M, json.dumps(r), flush=True)
