@@ -602,9 +602,9 @@ def main():
     # ---- the same workload through the serving loop (reported next to the harness numbers)
     serving_res = None
     n_srv = args.steps if args.serving_steps < 0 else args.serving_steps
-    if n_srv > 0 and tp == 1 and pool is not None:
+    if n_srv > 0 and pool is not None:
         serving_res = serving_runner_phase(args, eng, prepare, sp, U, u, A, S, n_srv, dev, dp_size, group,
-                                           world, log)
+                                           world, log, tp_group)
     if pool is not None:
         pool.shutdown(wait=True)
     log("per-step phases (ms, timed steps): " + ", ".join(f"{k}={v / args.steps * 1000:.1f}"
@@ -684,10 +684,10 @@ def main():
         concurrent = concurrent_phase(args, model, tok, emb, prepare, sp, u, dev, group, world, dp_rank, base, log)
 
     if rank == 0:
-        # headline loop: the product's serving loop (EngineRunner, per-query arrivals) when it ran (TP = 1): its
-        # closed-loop queries/s is `value`, its TTFT is the open-loop TTFT at the highest load <= 90 % of that
-        # rate (BASELINE: POST -> first token of a server at a set load); the harness loop is kept as
-        # harness_loop.  Under TP the harness loop is the headline.
+        # headline loop: the product's serving loop (EngineRunner, per-query arrivals; under TP the leader's
+        # runner with its peers mirroring): its closed-loop queries/s is `value`, its TTFT is the open-loop
+        # TTFT at the highest load <= 90 % of that rate (BASELINE: POST -> first token of a server at a set
+        # load); the harness loop is kept as harness_loop (and is the headline with --serving-steps 0)
         harness = {"value": round(qps, 3), "p50_ttft_ms": round(p50, 2), "ms_per_step": round(ms_step, 2),
                    "steps": args.steps, "warmup": args.warmup,
                    "ttft_admission_policy": ("decode window capped to 1 step while an arrival's retrieval is in flight"
@@ -795,12 +795,16 @@ class _ArrivalPump:
     stop) all-gather first; a round no rank has queries for is skipped; a rank with none joins the search
     with an empty batch; the pumps exit together once every rank asks to stop."""
 
-    def __init__(self, runner, prepare, sp, u, group, dev, tick: float = 0.002):
+    def __init__(self, runner, prepare, sp, u, group, dev, tick: float = 0.002, follower: bool = False):
         import queue
         import threading
 
         self.runner, self.prepare, self.sp, self.u, self.group, self.dev, self.tick = \
             runner, prepare, sp, u, group, dev, tick
+        # a TP follower rank: no arrivals of its own (its TP leader submits, its engine mirrors the leader's
+        # steps); it joins every retrieval round's search collectives with an empty batch, never holds a
+        # barrier back, and stops when every rank has asked to
+        self.follower = follower
         self.q = collections.deque()
         self.cv = threading.Condition()
         self.done = queue.SimpleQueue()  # (handle, t_arrival, t_submitted) per completed query
@@ -810,7 +814,8 @@ class _ArrivalPump:
         self.batches = []    # queries per retrieval micro-batch
         self.retrieval = []  # per micro-batch: first arrival -> prompts submitted (s)
         self.error = None
-        self.sync_req = False
+        self.sync_req = follower
+        self.stop_req = follower
         self.sync_ev = threading.Event()
         self.th = threading.Thread(target=self._run, name="bench-pump", daemon=True)
         self.th.start()
@@ -847,7 +852,7 @@ class _ArrivalPump:
                                                                device=self.dev)).view(-1, 3).cpu()
                     if int(f[:, 2].min()) == 1:  # every rank is at barrier(): release them together
                         with self.cv:
-                            self.sync_req = False
+                            self.sync_req = self.follower
                         self.sync_ev.set()
                     if int(f[:, 1].min()) == 1:
                         return
@@ -875,6 +880,12 @@ class _ArrivalPump:
         except BaseException as e:  # surfaced by the phase's waits
             self.error = e
             self.done.put(None)
+
+    def join_follower(self, timeout: float = 3600.0) -> None:
+        """A follower's pump: serve the rounds until every rank has stopped."""
+        self.th.join(timeout=timeout)
+        if self.error is not None:
+            raise RuntimeError("serving phase: follower pump failed") from self.error
 
     def barrier(self, timeout: float = 600.0) -> None:
         """A barrier of all ranks' main threads taken inside the pumps' round stream (the pump is the only
@@ -924,7 +935,7 @@ class _ArrivalPump:
         return n
 
 
-def serving_runner_phase(args, eng, prepare, sp, U, u, A, S, steps, dev, dp_size, group, world, log):
+def serving_runner_phase(args, eng, prepare, sp, U, u, A, S, steps, dev, dp_size, group, world, log, tp_group=None):
     """The headline workload through the product's serving loop: the engine steps on its own EngineRunner
     thread (engine/runner.py, as ``serve`` runs it); queries arrive ONE AT A TIME (a POST each) and go
     through a retrieval micro-batcher (_ArrivalPump: the queries that arrived meanwhile, up to u, share one
@@ -934,7 +945,9 @@ def serving_runner_phase(args, eng, prepare, sp, U, u, A, S, steps, dev, dp_size
     completions per rank after one untimed turnover of the pipeline; qps = completed queries / wall time
     (max over ranks); TTFT = arrival -> first token.  Then ``--serving-open-load``: Poisson arrivals of
     single queries at fractions of the closed loop's rate (``open_loop``) -- the TTFT a server sees at a set
-    load.  ``--interactive-prefill`` caps the prefill tokens per step while arrivals are pending."""
+    load.  ``--interactive-prefill`` caps the prefill tokens per step while arrivals are pending.
+    TP > 1: the TP leader's runner takes the arrivals and every TP peer's runner mirrors its engine steps
+    (engine/runner.py follow); the peers' pumps join each retrieval round's sharded search with no queries."""
     import torch
 
     from githubrepostorag_amd.engine.runner import EngineRunner
@@ -943,8 +956,23 @@ def serving_runner_phase(args, eng, prepare, sp, U, u, A, S, steps, dev, dp_size
     B = u * A
     pg = group if world > 1 else None
     runner = EngineRunner(eng, watchdog_s=0, interactive_prefill=args.interactive_prefill,
-                          bulk_prefill=args.bulk_prefill)
+                          bulk_prefill=args.bulk_prefill, tp=tp_group)
     res_open = []
+    loads = [float(x) for x in str(args.serving_open_load).split(",") if x.strip()]
+    if not runner.leader:
+        try:  # the closed loop's pump, then one per open-loop level, each followed by the leaders' barrier
+            for _ in range(1 + len(loads)):
+                _ArrivalPump(runner, prepare, sp, u, pg, dev, follower=True).join_follower()
+                comm.barrier()
+        finally:
+            runner.shutdown()
+        t = torch.tensor([0.0], dtype=torch.float64, device=dev)
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            comm.world_group().all_gather(torch.full((steps * B,), float("nan"), dtype=torch.float64, device=dev))
+        return None
     try:
         pump = _ArrivalPump(runner, prepare, sp, u, pg, dev)
         d0 = eng.stats["decode_steps"]
@@ -983,7 +1011,6 @@ def serving_runner_phase(args, eng, prepare, sp, U, u, A, S, steps, dev, dp_size
         batches, retr = pump.batches[nb0:], pump.retrieval[nr0:]
         pump.drain_and_stop(completed=U * u + steps * B)
         comm.barrier()
-        loads = [float(x) for x in str(args.serving_open_load).split(",") if x.strip()]
         n_open = max(4 * B, min(steps * B, 768))  # arrivals per load level (bounds the bench's wall time)
         for load in loads:
             res_open.append({"load": load, **_open_loop(runner, prepare, sp, u, pg, dev, load * B * steps / elapsed,
@@ -1000,7 +1027,7 @@ def serving_runner_phase(args, eng, prepare, sp, U, u, A, S, steps, dev, dp_size
         allt = comm.world_group().all_gather(torch.tensor(ttfts, dtype=torch.float64, device=dev)).cpu().tolist()
     elapsed = float(t.item())
     qps = B * steps * dp_size / elapsed
-    flat = sorted(x for r in allt for x in r)
+    flat = sorted(x for r in allt for x in r if x == x)  # TP peers send NaN rows
     p50 = statistics.median(flat) * 1000.0
     p90 = flat[min(len(flat) - 1, int(0.9 * len(flat)))] * 1000.0
     log(f"serving loop (EngineRunner, per-query arrivals): {qps:.3f} queries/s, closed-loop TTFT p50 {p50:.1f} ms")

@@ -59,6 +59,9 @@ def test_bench_tensor_parallel_two_ranks_gloo():
                 "--tp", "2", *TINY], env)
     assert res["config"]["parallelism"] == "tp2dp1" and res["config"]["global_batch"] == 3
     assert res["value"] > 0 and "TP=2" in res["config"]["model"]
+    # the serving loop under TP: the leader's runner takes the arrivals, the peer's mirrors its steps
+    assert res["headline_loop"].startswith("serving loop") and res["serving_runner"]["value"] == res["value"]
+    assert all(o["p50_ttft_ms"] > 0 for o in res["serving_runner"]["open_loop"])
     # ingest on the TP group (leader runs the pipeline, the peer mirrors its engine) and the agent
     # phase (TP leader runs jobs, the peer answers index rounds for its shard as a shard-only replica)
     assert res["ingest_docs_per_s"] > 0 and res["retrieval_prefetch"] is True
