@@ -811,6 +811,7 @@ class _ArrivalPump:
         self.stop_req = False
         self.taken = 0      # arrivals taken into a retrieval micro-batch (each completes once submitted)
         self.submitted = 0
+        self.abs_times = []  # (submitted, first token) perf_counter stamps of the completions taken by get()
         self.batches = []    # queries per retrieval micro-batch
         self.retrieval = []  # per micro-batch: first arrival -> prompts submitted (s)
         self.error = None
@@ -909,6 +910,7 @@ class _ArrivalPump:
             raise RuntimeError("serving phase: arrival pump failed") from self.error
         h, t0, t_in = item
         c = h.wait(0)  # a failed request raises here
+        self.abs_times.append((t_in, c.first_token_at))
         return c.first_token_at - t0, c.first_token_at - t_in
 
     def drain_and_stop(self, completed: int, timeout: float = 600.0) -> int:
@@ -1137,6 +1139,7 @@ def concurrent_phase(args, model, tok, emb, prepare, sp, u, dev, group, world, d
 
         pump = _ArrivalPump(runner, prepare, q_sp, u, pg, dev)
         comm.barrier()
+        eng.trace = []  # the engine steps of the concurrent window (kind, rows, tokens, seconds)
         th = threading.Thread(target=ingest, name="bench-concurrent-ingest", daemon=True)
         rng = random.Random(8642 + (dist.get_rank() if dist.is_available() and dist.is_initialized() else 0))
         t0 = time.perf_counter()
@@ -1154,9 +1157,11 @@ def concurrent_phase(args, model, tok, emb, prepare, sp, u, dev, group, world, d
         got = [pump.get() for _ in range(n)]
         tt, te = [g[0] for g in got], sorted(g[1] for g in got)
         retr = sorted(pump.retrieval)
+        abs_times = list(pump.abs_times)
         pump.drain_and_stop(completed=n)
     finally:
         runner.shutdown()
+        trace, eng.trace = eng.trace, None
         del eng
         if dev.type == "cuda":
             torch.cuda.empty_cache()
@@ -1173,12 +1178,43 @@ def concurrent_phase(args, model, tok, emb, prepare, sp, u, dev, group, world, d
            "retrieval_p50_ms": round(1000 * retr[len(retr) // 2], 2) if retr else None,
            "submit_to_first_token_p50_ms": round(1000 * te[len(te) // 2], 2) if te else None,
            "engine": (st or {}).get("engine"),
+           "engine_steps": _trace_summary(trace),
+           "submit_to_first_token_anatomy": _wait_anatomy(trace, abs_times),
            "setup": "one LLMEngine + EngineRunner (max_model_len 8192) shared by the ingest pipeline and the "
                     "serving loop's per-query arrivals (Poisson at the ingest-free open loop's load, until the "
                     "ingest ends); queries at priority 2, ingest roll-ups 1, extractor waves 0"}
     log(f"concurrent ingest + queries: ingest {res['ingest_docs_per_s']} docs/s, {n} queries at {rate:.1f}/s, TTFT "
         f"p50 {res['p50_ttft_ms']} ms (ingest-free {base['p50_ttft_ms']} ms), p90 {res['p90_ttft_ms']} ms")
     return res
+
+
+def _wait_anatomy(trace, abs_times) -> dict:
+    """Where a query's submit -> first token goes, from the engine trace: the rest of the step in flight when
+    it was submitted, and the steps that started before its first token (its own prefill step included),
+    by kind.  Medians over the queries."""
+    steps = sorted((t[0], t[1], t[4]) for t in trace or [] if t[1] in ("prefill", "mixed", "decode"))
+    if not steps or not abs_times:
+        return {}
+    import bisect
+
+    starts = [t for t, _, _ in steps]
+    inflight, n_steps, kinds = [], [], collections.Counter()
+    for t_in, t_first in abs_times:
+        i = bisect.bisect_left(starts, t_in)
+        if i > 0 and starts[i - 1] + steps[i - 1][2] > t_in:
+            inflight.append(starts[i - 1] + steps[i - 1][2] - t_in)
+        else:
+            inflight.append(0.0)
+        j = bisect.bisect_left(starts, t_first)
+        n_steps.append(j - i)
+        for _, kind, _ in steps[i:j]:
+            kinds[kind] += 1
+    inflight.sort()
+    n_steps.sort()
+    nq = len(abs_times)
+    return {"inflight_step_rest_p50_ms": round(1000 * inflight[nq // 2], 2),
+            "steps_started_before_first_token_p50": n_steps[nq // 2],
+            "steps_started_per_query_by_kind": {k: round(v / nq, 2) for k, v in kinds.items()}}
 
 
 def _trace_summary(trace) -> dict:

@@ -95,7 +95,11 @@ def _ingest_on(runner, eng, tok, emb, n_files, seed, summary_tokens, token_cap, 
             for f in files]
     if dev.type == "cuda":
         torch.cuda.synchronize()
-    eng.trace = []  # per-step timeline for the critical-path summary below
+    own_trace = eng.trace is None  # a caller's trace (bench.py concurrent phase) is kept and shared
+    if own_trace:
+        eng.trace = []  # per-step timeline for the critical-path summary below
+    trace = eng.trace
+    i0 = len(trace)
     t0 = time.perf_counter()
     res = ctl.ingest_component(repo=f"bench-repo-{seed}", namespace="bench", documents=docs, force=True)
     if dev.type == "cuda":
@@ -105,8 +109,9 @@ def _ingest_on(runner, eng, tok, emb, n_files, seed, summary_tokens, token_cap, 
     st["engine"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()
                     if isinstance(v, (int, float))}
     st["llm_calls"] = ctl.extractors.wave.calls + ctl.hier.wave.calls + ctl.hier.extract.wave.calls
-    st["timeline"] = critical_path(eng.trace, t0, dt)
-    eng.trace = None
+    st["timeline"] = critical_path(trace[i0:], t0, dt)
+    if own_trace:
+        eng.trace = None
     return res["documents"], dt, st
 
 

@@ -32,6 +32,9 @@ def test_bench_single_process_cpu():
     assert res["scaling"] == "weak" and res["config"]["global_batch"] == 3
     assert res["ingest_docs_per_s"] > 0 and res["p50_ttft_ms"] > 0 and res["p90_ttft_ms"] >= res["p50_ttft_ms"]
     assert res["headline_loop"].startswith("serving loop") and res["harness_loop"]["value"] > 0
+    ci = res["concurrent_ingest"]  # ingest + open-loop queries on one engine, with the wait anatomy
+    assert ci["queries"] > 0 and "decode" in ci["engine_steps"] or "prefill" in ci["engine_steps"]
+    assert "inflight_step_rest_p50_ms" in ci["submit_to_first_token_anatomy"]
     ref = res["ingest_ref_cap"]  # the one-cap-for-every-call ingest pass (2048 by default)
     assert res["ingest_docs_per_s_ref_cap"] > 0 and ref["token_cap"] == 48 and ref["files"] == 3
 
