@@ -311,7 +311,8 @@ def main():
     # ---- index shard: N / world rows of d-dim clustered vectors
     n_local = args.index_size // world + (1 if rank < args.index_size % world else 0)
     t0 = time.perf_counter()
-    X = synthetic.clustered_vectors(n_local, emb.dim, seed=1000 + rank, device=dev)
+    # one corpus: the same cluster centres on every shard, each rank's own draws around them
+    X = synthetic.clustered_vectors(n_local, emb.dim, seed=1000 + rank, device=dev, center_seed=1000)
     # the product table (index/store.py) per shard: IVF lists + metadata filter columns; the
     # corpus rows (row id, chunk text, repo/module/file metadata) are a deterministic recipe
     corpus = synthetic.SyntheticCorpus(args.index_size, seed=7)

@@ -82,11 +82,16 @@ def question(i: int) -> str:
 
 @torch.inference_mode()
 def clustered_vectors(n: int, d: int, n_centers: int = 4096, noise: float = 0.35, seed: int = 0,
-                      device="cuda", chunk: int = 1 << 20) -> torch.Tensor:
-    """bf16 [n, d] unit vectors drawn around random unit centres."""
+                      device="cuda", chunk: int = 1 << 20, center_seed: int | None = None) -> torch.Tensor:
+    """bf16 [n, d] unit vectors drawn around random unit centres.  ``center_seed``: draw the centres from
+    their own seed, so the shards of one corpus (one ``seed`` per rank) share ONE set of clusters -- with
+    per-shard centres a W-way sharded corpus would hold W x n_centers clusters and a fixed nlist would
+    cover W times as many clusters per list as on one GPU."""
     g = torch.Generator(device=device)
-    g.manual_seed(seed)
+    g.manual_seed(seed if center_seed is None else center_seed)
     C = torch.randn(n_centers, d, generator=g, device=device)
+    if center_seed is not None and center_seed != seed:  # (center_seed == seed: one stream, as without it)
+        g.manual_seed(seed)
     C = C / C.norm(dim=1, keepdim=True)
     out = torch.empty(n, d, dtype=torch.bfloat16, device=device)
     for s in range(0, n, chunk):

@@ -353,3 +353,30 @@ def test_tp_ffn_zero_padding_matches_unpadded(monkeypatch):
     for toks, real, padded in res:
         assert (real, padded) == (176, 192)
         assert toks == ref
+
+
+def _sharded_recall_worker(rank, world, n, nlist):
+    from githubrepostorag_amd.index.sharded import ShardedIndex
+    from githubrepostorag_amd.parallel.comm import Group, world_group
+    from githubrepostorag_amd.utils import synthetic
+
+    # the bench's corpus recipe: one set of cluster centres, each rank its own draws around them
+    X = synthetic.clustered_vectors(n // world, 64, n_centers=256, seed=1000 + rank, device="cpu", center_seed=1000)
+    corpus = synthetic.SyntheticCorpus(n, seed=7)
+    idx = ShardedIndex(64, world_group() if world > 1 else Group([0]), "cpu", kind="ivf", nlist=nlist, nprobe=8)
+    idx.build_corpus(corpus, X, seed=7)
+    Q = torch.nn.functional.normalize(torch.randn(32, 64, generator=torch.Generator().manual_seed(5)), dim=1)
+    r = idx.recall(Q.to(torch.bfloat16), 10, {"namespace": corpus.namespace}, nprobes=[8, nlist])
+    return [x["recall_at_k"] for x in r["by_nprobe"]]
+
+
+def test_sharded_ivf_recall_matches_one_shard():
+    """recall@10 of the sharded IVF against the sharded exact scan: at nprobe = nlist it is exact, and at a
+    small nprobe a 2-way sharded corpus keeps the one-shard recall (the shards share one set of clusters;
+    with per-rank cluster centres a W-way corpus held W x the clusters and recall fell from 0.97 to 0.15
+    at the bench's nprobe on a 2-rank GPU rehearsal)."""
+    one = _sharded_recall_worker(0, 1, 40000, 256)
+    two = run_ranks(_sharded_recall_worker, 2, 40000, 256)
+    assert one[1] == 1.0 and all(r[1] == 1.0 for r in two)
+    assert all(r[0] >= one[0] - 0.06 for r in two), (one, two)
+    assert one[0] >= 0.85
