@@ -418,8 +418,21 @@ __global__ __launch_bounds__(64 * NW) void attn_prefill_kernel(AttnParams p) {
         for (int c = 0; c < NC; ++c) s[j][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], qf[j][c], s[j][tt], 0, 0, 0);
       }
     }
-    // masking is needed only on tiles that reach the wave's diagonal / the context end
-    const bool need_mask = kt0 + KT > wave_lim_min;
+    // masking is needed only on tiles that reach the wave's diagonal / the context end.  The empty
+    // volatile asm keeps this a real wave-uniform branch: without it hipcc if-converted the selects
+    // into ~100 compares / cndmasks per tile on EVERY tile (the prefill loop was VALU-bound)
+    if (kt0 + KT > wave_lim_min) {
+      asm volatile("");
+#pragma unroll
+      for (int j = 0; j < RPW; ++j)
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kt0 + 16 * tt + 4 * h4 + r;
+            s[j][tt][r] = (key >= key_lim[j] || key >= kv_hi) ? -INFINITY : s[j][tt][r];
+          }
+    }
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       // raw scores: the softmax scale (log2 domain) is folded into the exponent's FMA, and the
@@ -428,13 +441,7 @@ __global__ __launch_bounds__(64 * NW) void attn_prefill_kernel(AttnParams p) {
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (need_mask) {
-            const int key = kt0 + 16 * tt + 4 * h4 + r;
-            s[j][tt][r] = (key >= key_lim[j] || key >= kv_hi) ? -INFINITY : s[j][tt][r];
-          }
-          tmax = __builtin_fmaxf(tmax, s[j][tt][r]);
-        }
+        for (int r = 0; r < 4; ++r) tmax = __builtin_fmaxf(tmax, s[j][tt][r]);
       tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       // deferred rescale (cdna guide §5.5 T13): the running max m (scaled units) moves only when a
@@ -686,17 +693,20 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
     // O (held in accumulator registers) is touched only on tiles where some row's max moved by more
     // than kRescaleLog2
     float tmax = -INFINITY;
-    const bool tail = kt0 + TK > kv_hi;
+    if (kt0 + TK > kv_hi) {  // the context's last tile only; a real branch (see attn_prefill_kernel)
+      asm volatile("");
 #pragma unroll
-    for (int tt = 0; tt < NT16; ++tt)
+      for (int tt = 0; tt < NT16; ++tt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (tail) {
+        for (int r = 0; r < 4; ++r) {
           const int key = kt0 + 16 * tt + 4 * h4 + r;
           s[tt][r] = key >= kv_hi ? -INFINITY : s[tt][r];
         }
-        tmax = fmaxf(tmax, s[tt][r]);
-      }
+    }
+#pragma unroll
+    for (int tt = 0; tt < NT16; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[tt][r]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_cand = fmaxf(m, tmax * p.scale_log2);
@@ -898,17 +908,20 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, 
       }
     }
     float tmax = -INFINITY;
-    const bool tail = kt0 + TK > kv_hi;
+    if (kt0 + TK > kv_hi) {  // the context's last tile only; a real branch (see attn_prefill_kernel)
+      asm volatile("");
 #pragma unroll
-    for (int tt = 0; tt < NT16; ++tt)
+      for (int tt = 0; tt < NT16; ++tt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (tail) {
+        for (int r = 0; r < 4; ++r) {
           const int key = kt0 + 16 * tt + 4 * h4 + r;
           sc[tt][r] = key >= kv_hi ? -INFINITY : sc[tt][r];
         }
-        tmax = fmaxf(tmax, sc[tt][r]);
-      }
+    }
+#pragma unroll
+    for (int tt = 0; tt < NT16; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, sc[tt][r]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_cand = fmaxf(m, tmax * p.scale_log2);
