@@ -129,6 +129,10 @@ def test_sharded_replicas_answer_from_every_shard(cluster):
         assert ev[-1][0] == "final" and not final.get("error"), ev[-3:]
         paths = {s["metadata"]["file_path"] for s in final["sources"]}
         assert paths == {"a.py", "b.py", "c.py"}, paths
+        # the job's result record lands just after its final event is published: wait for it
+        t_end = time.time() + 10
+        while "result" not in hub.queue.results.get(jid, {}) and time.time() < t_end:
+            time.sleep(0.01)
         seen_replicas.add(hub.queue.results[jid]["result"]["replica"])
     assert seen_replicas == {0, 1}
     h = client.get("/health").json()["components"]["vector_index"]["details"]["replicas"]
