@@ -345,11 +345,19 @@ def main():
 
         # a line every --heartbeat seconds from rank 0 (engine step counters): long multi-rank rehearsals
         # (Qwen2-72B at TP=8 over gloo on one card) show progress between phase lines
+        import weakref
+
+        eng_ref = weakref.ref(eng)  # the phases free the serving engine later (del eng): no strong reference here
+
         def _beat():
             t_hb = time.perf_counter()
             while True:
                 time.sleep(args.heartbeat)
-                st = eng.stats
+                e = eng_ref()
+                if e is None:
+                    return
+                st = dict(e.stats)
+                del e
                 print(f"[bench] alive {time.perf_counter() - t_hb:.0f} s: engine steps {st['steps']}, prefill "
                       f"tokens {st['prefill_tokens']}, decode tokens {st['decode_tokens']}", file=sys.stderr, flush=True)
         threading.Thread(target=_beat, name="bench-heartbeat", daemon=True).start()
