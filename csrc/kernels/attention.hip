@@ -103,6 +103,23 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
   }
 }
 
+// The same LDS-DMA with the address as a wave-uniform 64-bit base in SGPRs plus a 32-bit per-lane byte
+// offset (global_load_lds saddr form): no 64-bit VALU address arithmetic per load.
+__device__ __forceinline__ void glds16_s(const void* sbase, uint32_t voff, void* lds_dst) {
+  const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds_dst;
+  const uint32_t lu = __builtin_amdgcn_readfirstlane(lds);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lu)
+      : "memory");
+}
+
 template <int D, int NW, bool PAGED>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   constexpr int CPR = D / 8;      // 16-B chunks per K/V row
@@ -374,18 +391,27 @@ __global__ __launch_bounds__(64 * NW) void attn_prefill_kernel(AttnParams p) {
   const int wave_lim_min = min(kv_hi, p.causal ? ctx - qlen + min(wrow0, nrows - 1) / G + 1 : ctx);
 
   const int lrow = lane / CPR, lch = lane % CPR;
+  // A wave's PPW pieces are PPW * RPP consecutive keys inside one KV block (tiles start on block
+  // boundaries), so the block lookup and the base address are wave-uniform (SGPRs) and each lane adds a
+  // 32-bit byte offset.  Keys past the context end re-read its last key (finite V for the masked keys,
+  // as a per-key clamp would): the wave's block is clamped to the last valid one and so is the slot.
+  static_assert(BS % (PPW * RPP) == 0 && KT % BS == 0, "a wave's DMA rows sit in one KV block");
+  const int last_blk = (kv_hi - 1) / BS, last_slot = (kv_hi - 1) % BS;
+  const int wrow = __builtin_amdgcn_readfirstlane(wave) * PPW * RPP;
   auto issue = [&](int kt0, int stage) {
     char* kdst = smem + stage * 2 * TILE;
     char* vdst = kdst + TILE;
+    const int blk = __builtin_amdgcn_readfirstlane(bt_lds[min((kt0 + wrow) / BS, last_blk)]);
+    const size_t base = ((size_t)blk * p.Hkv + kvh) * BS * D;
+    const bf16* kb = p.k + base;
+    const bf16* vb = p.v + base;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int piece = wave * PPW + i;
       const int row = piece * RPP + lrow;
-      const int key = min(kt0 + row, kv_hi - 1);
-      const int blk = bt_lds[key / BS];
-      const size_t off = (((size_t)blk * p.Hkv + kvh) * BS + (key % BS)) * D;
-      glds16(p.k + off + ((lch ^ kswz<D>(row)) << 3), kdst + piece * 1024);
-      glds16(p.v + off + ((lch ^ vswz<D>(row)) << 3), vdst + piece * 1024);
+      const int slot = kt0 + row < kv_hi ? row % BS : last_slot;
+      glds16_s(kb, (uint32_t)(slot * D + ((lch ^ kswz<D>(row)) << 3)) * 2u, kdst + piece * 1024);
+      glds16_s(vb, (uint32_t)(slot * D + ((lch ^ vswz<D>(row)) << 3)) * 2u, vdst + piece * 1024);
     }
   };
 
