@@ -164,6 +164,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
     }
   }
   const int key_lim = p.causal ? (ctx - qlen + pq + 1) : ctx;  // keys j < key_lim visible
+  // the smallest limit among the wave's valid rows (its first row's): tiles ending at or below it need no mask
+  const int wrow0 = min(row_base + __builtin_amdgcn_readfirstlane(wave) * 16, nrows - 1);
+  const int wave_lim_min = min(kv_hi, p.causal ? ctx - qlen + wrow0 / G + 1 : ctx);
 
   float m = -INFINITY, lsum = 0.f;
   f32x4_t o[ND];
@@ -207,19 +210,27 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
         s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[c], s[t], 0, 0, 0);
       }
     }
-    // scale + mask; this lane holds keys kt0 + 16t + 4*h4 + r of query row li
+    // scale + mask; this lane holds keys kt0 + 16t + 4*h4 + r of query row li.  The mask runs only on
+    // tiles that reach the wave's first row's limit (a real wave-uniform branch, see attn_prefill_kernel)
     float tmax = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kt0 + 16 * t + 4 * h4 + r;
-        float x = s[t][r] * p.scale_log2;
-        if (key >= key_lim || key >= kv_hi) x = -INFINITY;
-        s[t][r] = x;
-        tmax = fmaxf(tmax, x);
-      }
+      for (int r = 0; r < 4; ++r) s[t][r] *= p.scale_log2;
+    if (kt0 + KT > wave_lim_min) {
+      asm volatile("");
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kt0 + 16 * t + 4 * h4 + r;
+          if (key >= key_lim || key >= kv_hi) s[t][r] = -INFINITY;
+        }
     }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[t][r]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_new = fmaxf(m, tmax);
