@@ -269,11 +269,13 @@ int grid_for(size_t total) {
 
 }  // namespace
 
-// Blocks of qkv_rope_kernel: rope_block(T) threads per block, one block per rope_block(T) units of each token
-// (64 under 32 tokens, else 128): at decode batches of 64-256 tokens a block per token left CUs idle and
-// kept too few plane loads in flight (9.9 us at 176 tokens, ~2.3 TB/s of split-K planes).
-static int rope_block(int T) { return T < 32 ? 64 : 128; }
+// Blocks of qkv_rope_kernel: rope_block(T) threads per block.  Under 32 tokens one 64-thread block per 64
+// units of each token; at decode batches of 32-511 tokens one 128-thread block per 128 units (a block per
+// token left CUs idle and kept too few plane loads in flight: 9.9 -> 7.9 us at 176 tokens); at prefill
+// sizes one 256-thread block per token (the split grid measured slower there: 35 vs 21 us per call).
+static int rope_block(int T) { return T < 32 ? 64 : T < 512 ? 128 : kThreads; }
 static dim3 rope_grid(int T, int Hq, int Hkv, int D) {
+  if (T >= 512) return dim3(T, 1);
   const int units = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
   const int b = rope_block(T);
   return dim3(T, (units + b - 1) / b);
