@@ -24,6 +24,8 @@
 // log2 domain (exp2).
 #include "common.h"
 
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
 using namespace grag;
 
 namespace {
@@ -495,16 +497,26 @@ __global__ __launch_bounds__(64 * NW) void attn_prefill_kernel(AttnParams p) {
         for (int n = 0; n < ND; ++n) o[j][n] *= alpha;
       }
       const float nm = m[j] == -INFINITY ? 0.f : -m[j];
+      // exponent arguments and the row-sum adds as packed f32 pairs (v_pk_fma_f32 / v_pk_add_f32: one issue
+      // per two lanes' worth of work -- the softmax VALU, not the MFMA pipe, paces this loop)
+      const f32x2_t sc2 = {p.scale_log2, p.scale_log2}, nm2 = {nm, nm};
+      f32x2_t ls2 = {0.f, 0.f};
 #pragma unroll
       for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][2 * cc][r], p.scale_log2, nm));
-          const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][2 * cc + 1][r], p.scale_log2, nm));
-          lsum[j] += p0 + p1;
-          bp[j][cc][r] = f2bits(p0);
-          bp[j][cc][4 + r] = f2bits(p1);
+        for (int rp = 0; rp < 2; ++rp) {
+          const f32x2_t x0 = __builtin_elementwise_fma(f32x2_t{s[j][2 * cc][2 * rp], s[j][2 * cc][2 * rp + 1]}, sc2, nm2);
+          const f32x2_t x1 =
+              __builtin_elementwise_fma(f32x2_t{s[j][2 * cc + 1][2 * rp], s[j][2 * cc + 1][2 * rp + 1]}, sc2, nm2);
+          const f32x2_t p0 = {__builtin_amdgcn_exp2f(x0[0]), __builtin_amdgcn_exp2f(x0[1])};
+          const f32x2_t p1 = {__builtin_amdgcn_exp2f(x1[0]), __builtin_amdgcn_exp2f(x1[1])};
+          ls2 += p0 + p1;
+          bp[j][cc][2 * rp] = f2bits(p0[0]);
+          bp[j][cc][2 * rp + 1] = f2bits(p0[1]);
+          bp[j][cc][4 + 2 * rp] = f2bits(p1[0]);
+          bp[j][cc][4 + 2 * rp + 1] = f2bits(p1[1]);
         }
+      lsum[j] += ls2[0] + ls2[1];
     }
   };
   // phase B: O^T += V^T P^T from the V image at v_lds
