@@ -386,7 +386,7 @@ def main():
 
     from concurrent.futures import ThreadPoolExecutor
 
-    from githubrepostorag_amd.utils.gpu_guard import side_stream
+    from githubrepostorag_amd.utils.gpu_guard import gpu_shared, side_stream
 
     # the end of every prompt (answer cue + assistant turn), kept when the context is cut to --prompt-len
     tail_ids = tok.encode(tok.apply_chat_template([{"role": "user", "content": "\n\nAnswer:"}])
@@ -405,8 +405,9 @@ def main():
             qv = emb.embed_queries(qs) if B else torch.zeros(0, emb.dim, dtype=torch.bfloat16, device=dev)
             t_e = time.perf_counter()
             # every reference retrieval carries the namespace filter (agent_graph.py:249): fused in the scan
-            scores, ids = index.search(qv, args.top_k, {"namespace": corpus.namespace})
-            ids = ids.cpu().tolist()
+            with gpu_shared():  # the .cpu() is a host sync: never inside another thread's graph capture
+                scores, ids = index.search(qv, args.top_k, {"namespace": corpus.namespace})
+                ids = ids.cpu().tolist()
             t_s = time.perf_counter()
         prompts = []
         for q, row in zip(qs, ids):

@@ -35,7 +35,7 @@ from ..ops.gemm import WS
 from ..ops.sampling import SamplerState, reset_slots, sample, sample_tp
 from .scheduler import KVCacheManager, Scheduler
 from .sequence import Completion, SamplingParams, Sequence, SeqStatus
-from ..utils.gpu_guard import gpu_guard, no_gc
+from ..utils.gpu_guard import gpu_guard, gpu_shared, no_gc
 from .tokenizer import IncrementalDetokenizer
 
 log = logging.getLogger(__name__)
@@ -260,7 +260,9 @@ class LLMEngine:
         step's prefill tokens (Scheduler.schedule)."""
         t0 = time.perf_counter()
         try:
-            with self._on_stream(), WS.owned_by(self._ws):
+            # shared capture guard for the whole step (utils/gpu_guard.py): the step's host reads sync, and
+            # a sync while another thread captures (the embedder's query-bucket graphs) breaks that capture
+            with self._on_stream(), WS.owned_by(self._ws), (gpu_shared() if self.on_gpu else contextlib.nullcontext()):
                 return self._step(max_window, prefill_budget, bulk_budget)
         finally:
             self.stats["step_s"] += time.perf_counter() - t0

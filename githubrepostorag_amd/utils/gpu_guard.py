@@ -13,7 +13,9 @@ Captures hold the guard exclusively (``with gpu_guard():``); a thread's GPU
 section that synchronises holds it shared (``with gpu_shared():`` or the
 ``@guarded`` decorator), so retrieval / embedding / ingest sections run
 concurrently with each other and only wait while a capture is open.  ``side_stream`` keeps such
-latency-bound sections off the engine's stream.
+latency-bound sections off the engine's stream (its closing sync is a shared section too).  The
+engine holds the guard shared for every step (its host reads sync while the embedder may capture a
+query-bucket graph on a retrieval thread) and upgrades to exclusive for its own lazy captures.
 """
 from __future__ import annotations
 
@@ -74,16 +76,22 @@ class _CaptureGuard:
             finally:
                 self._tls.ex -= 1
             return
-        if self._depth("sh"):
-            raise RuntimeError("gpu_guard: cannot take the capture guard inside a shared section")
+        # a thread inside a shared section (the engine thread holds one for its whole step and captures
+        # lazily inside it) gives its read hold up while it waits and captures, and takes it back after:
+        # two upgrading threads then wait as plain writers instead of each holding the other's read count
+        sh = self._depth("sh")
         me = threading.get_ident()
         with self._cond:
+            if sh:
+                self._readers -= 1
+                if self._readers == 0:
+                    self._cond.notify_all()
             self._waiting += 1
             while self._writer is not None or self._readers:
                 self._cond.wait()
             self._waiting -= 1
             self._writer = me
-        self._tls.ex = 1
+        self._tls.ex, self._tls.sh = 1, 0
         try:
             yield
         finally:
@@ -91,6 +99,11 @@ class _CaptureGuard:
             with self._cond:
                 self._writer = None
                 self._cond.notify_all()
+                if sh:
+                    while self._writer is not None or self._waiting:
+                        self._cond.wait()
+                    self._readers += 1
+            self._tls.sh = sh
 
 
 _GUARD = _CaptureGuard()
@@ -168,7 +181,8 @@ def side_stream(device, wait_caller: bool = False, join: str = "sync"):
     if join == "event":
         prev.wait_stream(s)
     else:
-        s.synchronize()
+        with _GUARD.shared():  # a host sync: never while another thread's capture is open
+            s.synchronize()
 
 
 def set_device_of(dev) -> None:
