@@ -967,6 +967,18 @@ def serving_runner_phase(args, eng, prepare, sp, U, u, A, S, steps, dev, dp_size
 
     B = u * A
     pg = group if world > 1 else None
+    if dev.type == "cuda" and not args.no_graph:
+        # the loop fills from an empty engine, so its first steps meet small decode buckets / split plans and
+        # 1..u-query encoder buckets the harness never used: capture them here, on this thread with nothing
+        # else running, not lazily on the runner / retrieval threads while the other one works (every rank
+        # runs this in the same order: the sharded search and TP captures are collective)
+        hi = next((b for b in eng.cfg.graph_batch_sizes if b >= (U + 1) * u), eng.cfg.graph_batch_sizes[-1])
+        ctxs = sorted({args.prompt_len + k for k in range(1, args.gen_len + 2, 32)} | {args.prompt_len + args.gen_len})
+        n_cap = eng.warmup_graphs([b for b in eng.cfg.graph_batch_sizes if b <= hi], ctxs, windows=(1, 2, 4, 8),
+                                  params=sp)
+        for n in range(1, u + 1):
+            prepare(n)
+        log(f"serving loop: {n_cap} more decode graphs and the 1-{u}-query retrieval buckets warmed")
     runner = EngineRunner(eng, watchdog_s=0, interactive_prefill=args.interactive_prefill,
                           bulk_prefill=args.bulk_prefill, tp=tp_group)
     res_open = []
