@@ -784,6 +784,17 @@ def main():
             "index_recall": recall,
             "concurrent_ingest": concurrent,
             "recall_at_10": None if recall is None else recall.get("recall_at_10"),
+            # the two operating points the headline combines, side by side: the closed loop's saturating rate
+            # with its own TTFT, and each open-loop level's achieved rate with its TTFT
+            "operating_points": ([{"loop": "closed (saturating)", "queries_per_s": srv["value"],
+                                   "ttft_p50_ms": srv["p50_ttft_ms"], "ttft_p90_ms": srv["p90_ttft_ms"]}]
+                                 + [{"loop": f"open, Poisson at {o['load']:.0%}",
+                                     "queries_per_s": round(o["achieved_queries_per_s"] * dp_size, 3),
+                                     "ttft_p50_ms": o["p50_ttft_ms"], "ttft_p90_ms": o["p90_ttft_ms"]}
+                                    for o in srv.get("open_loop") or []]) if srv else None,
+            # kernels' out-of-range index reports over the whole run (csrc/kernels/common.h index guard): the
+            # engine raises on the first at its next step, so a clean run reports 0
+            "device_index_reports": __import__("githubrepostorag_amd.ops._lib", fromlist=["x"]).device_errors()[2],
         }
         line = json.dumps(res)
         print(line, flush=True)
@@ -967,11 +978,13 @@ def serving_runner_phase(args, eng, prepare, sp, U, u, A, S, steps, dev, dp_size
 
     B = u * A
     pg = group if world > 1 else None
-    if dev.type == "cuda" and not args.no_graph:
+    if dev.type == "cuda" and not args.no_graph and os.environ.get("GRAG_SERVING_WARMUP", "1") != "0":
         # the loop fills from an empty engine, so its first steps meet small decode buckets / split plans and
-        # 1..u-query encoder buckets the harness never used: capture them here, on this thread with nothing
-        # else running, not lazily on the runner / retrieval threads while the other one works (every rank
-        # runs this in the same order: the sharded search and TP captures are collective)
+        # 1..u-query encoder buckets the harness never used: capture them here, outside the timed window (every
+        # rank runs this in the same order: the sharded search and TP captures are collective).  Not
+        # load-bearing for correctness: GRAG_SERVING_WARMUP=0 leaves every capture to the runner / retrieval
+        # threads while the other one works (the round-5 fault's setting; the workspaces those threads' kernels
+        # use are owned per engine / embedder / thread and the index guard reports bad indices)
         hi = next((b for b in eng.cfg.graph_batch_sizes if b >= (U + 1) * u), eng.cfg.graph_batch_sizes[-1])
         ctxs = sorted({args.prompt_len + k for k in range(1, args.gen_len + 2, 32)} | {args.prompt_len + args.gen_len})
         n_cap = eng.warmup_graphs([b for b in eng.cfg.graph_batch_sizes if b <= hi], ctxs, windows=(1, 2, 4, 8),

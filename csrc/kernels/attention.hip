@@ -49,6 +49,7 @@ struct AttnParams {
   int tiles_per_seq, num_splits, split_len, total_q;
   float scale_log2;
   int causal;
+  int nblocks;  // KV blocks in the cache: the index guard's bound for block-table entries (common.h)
 };
 
 // Chunk (16 B) swizzle for the K image read as row fragments by ds_read_b128.
@@ -186,7 +187,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       if (j < kv_hi) {
         size_t off;
         if constexpr (PAGED) {
-          const int blk = p.block_tables[(size_t)seq * p.bt_stride + j / p.BS];
+          int blk = p.block_tables[(size_t)seq * p.bt_stride + j / p.BS];
+          if (!index_ok(blk, p.nblocks, ERR_BLOCK_PREFILL)) blk = 0;
           off = (((size_t)blk * p.Hkv + kvh) * p.BS + (j % p.BS)) * D + ch * 8;
         } else {
           off = (size_t)(q0 + j) * p.kv_stride + (size_t)kvh * D + ch * 8;
@@ -372,7 +374,11 @@ __global__ __launch_bounds__(64 * NW) void attn_prefill_kernel(AttnParams p) {
   // pieces in flight.  The launcher guarantees bt_stride <= MAXB.
   const int nb = (kv_hi + BS - 1) / BS;
   const int32_t* bt = p.block_tables + (size_t)seq * p.bt_stride;
-  for (int i = threadIdx.x; i < nb; i += 64 * NW) bt_lds[i] = bt[i];
+  for (int i = threadIdx.x; i < nb; i += 64 * NW) {
+    int b = bt[i];
+    if (!index_ok(b, p.nblocks, ERR_BLOCK_PREFILL)) b = 0;  // reported; block 0 read instead of faulting
+    bt_lds[i] = b;
+  }
 
   bf16x8_t qf[RPW][NC];
   int key_lim[RPW];  // this lane's row limit
@@ -676,6 +682,7 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
   const int nblk_seq = (ctx + p.BS - 1) / p.BS;
   int win = (kv_lo / p.BS) >> 6;
   int bvec = bt[min((win << 6) + lane, nblk_seq - 1)];
+  if (!index_ok(bvec, p.nblocks, ERR_BLOCK_DECODE)) bvec = 0;
   // Retire the Q and block-id loads with a wait hipcc understands, so its
   // scoreboard is empty when the asm-issued LDS-DMA pipeline starts (else it
   // re-waits vmcnt(0) for them inside every iteration).
@@ -691,6 +698,7 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
     if (w != win) {
       win = w;
       bvec = bt[min((w << 6) + lane, nblk_seq - 1)];
+      if (!index_ok(bvec, p.nblocks, ERR_BLOCK_DECODE)) bvec = 0;
     }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -900,6 +908,7 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, 
   const int nblk_seq = (ctx + p.BS - 1) / p.BS;
   int win = ((kv_lo + w * TK) / p.BS) >> 6;
   int bvec = bt[min((win << 6) + lane, nblk_seq - 1)];
+  if (!index_ok(bvec, p.nblocks, ERR_BLOCK_DECODE)) bvec = 0;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): Q and block ids retired before the counted DMA pipeline
 #pragma unroll
   for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(qf[c]));
@@ -913,6 +922,7 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, 
     if (wn != win) {
       win = wn;
       bvec = bt[min((wn << 6) + lane, nblk_seq - 1)];
+      if (!index_ok(bvec, p.nblocks, ERR_BLOCK_DECODE)) bvec = 0;
     }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -1068,6 +1078,7 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned* cnt = counters + (size_t)seq * p.Hkv + kvh;
     const unsigned tk = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk >= (unsigned)nvalid) report_index_error(ERR_TICKET, tk);  // a stale or shared ticket word
     const unsigned last = tk == (unsigned)(nvalid - 1) ? 1u : 0u;
     if (last) {
       __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1221,7 +1232,7 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
                                   const int32_t* q_start, const int32_t* ctx_len, int nseq,
                                   int total_q, int max_q_len, int Hq, int Hkv, int D, int BS,
                                   float scale, int causal, int num_splits, int split_len,
-                                  float* part_o, float* part_ml, int nw, hipStream_t stream) {
+                                  float* part_o, float* part_ml, int nw, int nblocks, hipStream_t stream) {
   if (nseq <= 0) return 0;
   if (Hq % Hkv != 0 || BS <= 0 || nw < 1 || (nw > 8 && nw != 11 && nw != 12)) return (int)hipErrorInvalidValue;
   if ((nw == 5 || nw == 6) && num_splits > 1) return (int)hipErrorInvalidValue;
@@ -1256,6 +1267,7 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
   prm.total_q = total_q;
   prm.scale_log2 = scale * 1.4426950408889634f;
   prm.causal = causal;
+  prm.nblocks = nblocks;
   switch (D) {
     case 128: return dispatch_nw<128>(prm, nseq, nw, true, stream);
     case 64: return dispatch_nw<64>(prm, nseq, nw, true, stream);
@@ -1272,7 +1284,7 @@ GRAG_API int grag_paged_decode_mw(const void* q, int q_stride, const void* k_cac
                                   int out_stride, const int32_t* block_tables, int bt_stride, const int32_t* q_start,
                                   const int32_t* ctx_len, int nseq, int total_q, int Hq, int Hkv, int D, int BS,
                                   float scale, int num_splits, int split_len, float* part_o, float* part_ml,
-                                  unsigned* counters, int nw, hipStream_t stream) {
+                                  unsigned* counters, int nw, int nblocks, hipStream_t stream) {
   if (nseq <= 0) return 0;
   if (Hq % Hkv != 0 || Hq / Hkv > 16 || BS <= 0 || BS % 16 != 0 || (nw != 2 && nw != 4) || (D != 64 && D != 128))
     return (int)hipErrorInvalidValue;
@@ -1303,6 +1315,7 @@ GRAG_API int grag_paged_decode_mw(const void* q, int q_stride, const void* k_cac
   prm.total_q = total_q;
   prm.scale_log2 = scale * 1.4426950408889634f;
   prm.causal = 1;
+  prm.nblocks = nblocks;
   if (D == 128) return nw == 4 ? launch_decode_mw<128, 4>(prm, nseq, counters, stream)
                                : launch_decode_mw<128, 2>(prm, nseq, counters, stream);
   return nw == 4 ? launch_decode_mw<64, 4>(prm, nseq, counters, stream)
@@ -1344,3 +1357,5 @@ GRAG_API int grag_varlen_attention(const void* q, const void* k, const void* v, 
     default: return (int)hipErrorInvalidValue;
   }
 }
+
+GRAG_ERR_UNIT(attention)

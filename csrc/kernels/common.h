@@ -94,4 +94,55 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return base + orig / 8;
 }
 
+// ---- device-side index guard --------------------------------------------------------------------
+// Kernels whose addresses come from index INPUTS (token ids, KV slot ids, block-table entries, row ids,
+// cross-workgroup tickets) check them.  An out-of-range index skips its access and records (code, value)
+// in a small host-mapped error block instead of faulting the device: an illegal address poisons every
+// stream of the process and names no kernel, a recorded code names the kernel and the bad value, and the
+// host raises on it at its next sync point (ops/_lib.py check_device_errors).  The block pointer is one
+// per translation unit (no relocatable device code here), bound once at library load by
+// grag_err_bind_<unit>; it is read with plain (scalar) loads and written only with vector atomics.
+enum : unsigned {
+  ERR_EMBED_TOKEN = 1u << 0,   // decoder embedding gather: token id >= vocab
+  ERR_KV_SLOT = 1u << 1,       // RoPE + KV store: slot id >= KV slots
+  ERR_ROPE_POS = 1u << 2,      // RoPE: position >= cos/sin table rows
+  ERR_BLOCK_PREFILL = 1u << 3, // prefill attention: block-table entry >= KV blocks
+  ERR_BLOCK_DECODE = 1u << 4,  // decode attention: block-table entry >= KV blocks
+  ERR_TICKET = 1u << 5,        // a split-merge / stream-K ticket past its part count (shared or stale word)
+  ERR_SAMPLER_SLOT = 1u << 6,  // sampler / seen-bit row >= sampler slots
+  ERR_TOPK_ROW = 1u << 7,      // top-k merge / IVF scan: candidate row or list range out of range
+  ERR_BERT_TOKEN = 1u << 8,    // encoder embedding: token / position id out of range
+};
+
+static __device__ unsigned* g_err_block = nullptr;  // [0] codes (OR), [1] last bad value, [2] count, [3] code of [1]
+
+// The block is pinned host memory mapped into the device address space: plain (non-RMW) system-scope
+// stores only -- they travel as posted writes on any host link, where read-modify-write atomics to host
+// memory would need link atomics.  Two reporters racing may lose one code bit or count: this is a
+// diagnostic that something went wrong and where, not a tally.
+__device__ __noinline__ void report_index_error(unsigned code, unsigned value) {
+  unsigned* e = g_err_block;
+  if (e == nullptr) return;
+  const unsigned prev = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(e, prev | code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(e + 1, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned cnt = __hip_atomic_load(e + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(e + 2, cnt + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(e + 3, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// true when 0 <= v < n; otherwise reports (code, v) and returns false
+__device__ __forceinline__ bool index_ok(long v, long n, unsigned code) {
+  if (__builtin_expect(v >= 0 && v < n, 1)) return true;
+  report_index_error(code, (unsigned)v);
+  return false;
+}
+
 }  // namespace grag
+
+// exported per translation unit: bind this unit's error-block pointer (host-mapped memory)
+#define GRAG_ERR_UNIT(unit)                                                                 \
+  GRAG_API int grag_err_bind_##unit(void* p) {                                              \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(grag::g_err_block), &p, sizeof(p), 0,          \
+                                  hipMemcpyHostToDevice);                                   \
+  }

@@ -37,7 +37,7 @@ __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
     const int32_t* __restrict__ positions, const float* __restrict__ cos_sin,
     const int32_t* __restrict__ slot_mapping, bf16* __restrict__ q_out, bf16* __restrict__ k_cache,
     bf16* __restrict__ v_cache, int Hq, int Hkv, int D, int BS, const float* __restrict__ planes, int S,
-    size_t plane) {
+    size_t plane, int nslots, int npos) {
   const int t = blockIdx.x;
   const float* prow = PL ? planes + (size_t)t * ld : nullptr;
   // 8 consecutive projection outputs of this token as bf16-rounded floats
@@ -62,8 +62,12 @@ __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
   const int upp = half >> 3;  // rotary units per head
   const int n_rot = (Hq + Hkv) * upp;
   const int n_v = Hkv * (D >> 3);
-  const int pos = positions[t];
-  const int slot = slot_mapping ? slot_mapping[t] : -1;
+  int pos = positions[t];
+  int slot = slot_mapping ? slot_mapping[t] : -1;
+  // index inputs checked (common.h index guard): a bad position reads row 0 of the table, a bad slot skips
+  // the K/V store; either is reported and raised on the host at its next sync
+  if (cos_sin && !index_ok(pos, npos, ERR_ROPE_POS)) pos = 0;
+  if (slot >= 0 && !index_ok(slot, nslots, ERR_KV_SLOT)) slot = -1;
   // cos_sin == nullptr: no rotary (absolute-position decoders, GPT-2) — the
   // kernel is then the fused bias add + q split + paged K/V store
   const float* cs = cos_sin ? cos_sin + (size_t)pos * D : nullptr;
@@ -284,14 +288,15 @@ static dim3 rope_grid(int T, int Hq, int Hkv, int D) {
 GRAG_API int grag_qkv_rope_kvstore(const void* qkv, int ld, const void* bias,
                                    const int32_t* positions, const float* cos_sin,
                                    const int32_t* slot_mapping, void* q_out, void* k_cache,
-                                   void* v_cache, int T, int Hq, int Hkv, int D, int BS,
-                                   hipStream_t stream) {
+                                   void* v_cache, int T, int Hq, int Hkv, int D, int BS, int nslots,
+                                   int npos, hipStream_t stream) {
   if (T <= 0) return 0;
   if (D % 16 != 0 || ld % 8 != 0) return (int)hipErrorInvalidValue;
   const dim3 g = rope_grid(T, Hq, Hkv, D);
   qkv_rope_kernel<false><<<g, rope_block(T), 0, stream>>>((const bf16*)qkv, ld, (const bf16*)bias, positions,
                                                      cos_sin, slot_mapping, (bf16*)q_out,
-                                                     (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, D, BS, nullptr, 1, 0);
+                                                     (bf16*)k_cache, (bf16*)v_cache, Hq, Hkv, D, BS, nullptr, 1, 0,
+                                                     nslots, npos);
   return (int)hipGetLastError();
 }
 
@@ -300,14 +305,14 @@ GRAG_API int grag_qkv_rope_kvstore(const void* qkv, int ld, const void* bias,
 GRAG_API int grag_qkv_rope_kvstore_planes(const float* planes, int S, int N, const void* bias,
                                           const int32_t* positions, const float* cos_sin,
                                           const int32_t* slot_mapping, void* q_out, void* k_cache,
-                                          void* v_cache, int T, int Hq, int Hkv, int D, int BS,
-                                          hipStream_t stream) {
+                                          void* v_cache, int T, int Hq, int Hkv, int D, int BS, int nslots,
+                                          int npos, hipStream_t stream) {
   if (T <= 0) return 0;
   if (D % 16 != 0 || N % 8 != 0 || S < 1 || N != (Hq + 2 * Hkv) * D) return (int)hipErrorInvalidValue;
   const dim3 g = rope_grid(T, Hq, Hkv, D);
   qkv_rope_kernel<true><<<g, rope_block(T), 0, stream>>>(nullptr, N, (const bf16*)bias, positions, cos_sin,
                                                     slot_mapping, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache,
-                                                    Hq, Hkv, D, BS, planes, S, (size_t)T * N);
+                                                    Hq, Hkv, D, BS, planes, S, (size_t)T * N, nslots, npos);
   return (int)hipGetLastError();
 }
 
@@ -340,3 +345,5 @@ GRAG_API int grag_pool_l2norm(const void* hidden, const int32_t* starts, const i
                                                  (bf16*)outb, S, H, mode, normalize);
   return (int)hipGetLastError();
 }
+
+GRAG_ERR_UNIT(elementwise)

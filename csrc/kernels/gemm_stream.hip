@@ -202,6 +202,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(const bf16* __restrict
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned tk = __hip_atomic_fetch_add(&counters[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tk >= (unsigned)ncontrib) report_index_error(ERR_TICKET, tk);  // stale / shared ticket word
       const unsigned last = tk == (unsigned)(ncontrib - 1) ? 1u : 0u;
       if (last) {
         __hip_atomic_store(&counters[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -339,3 +340,5 @@ GRAG_API int grag_gemm_stream(const void* A, const void* W, const void* bias, vo
   GO(8, 256, 3);
 #undef GO
 }
+
+GRAG_ERR_UNIT(gemm_stream)

@@ -636,6 +636,7 @@ auto slab_store = [&](const Acc& acc, int q) {
       __syncthreads();
       if (tid == 0) {
         const unsigned tk = __hip_atomic_fetch_add(&p.cnt[ts], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tk > (unsigned)(last - first)) report_index_error(ERR_TICKET, tk);  // stale / shared ticket word
         const unsigned is_last = tk == (unsigned)(last - first) ? 1u : 0u;
         if (is_last) {
           __hip_atomic_store(&p.cnt[ts], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -887,3 +888,5 @@ GRAG_API int grag_gemm_tile(const void* A, const void* W, const void* bias, void
   if (act == ACT_GELU_TANH) return launch<EPI_STORE, ACT_GELU_TANH>(a, stream);
   return launch<EPI_STORE, ACT_NONE>(a, stream);
 }
+
+GRAG_ERR_UNIT(gemm_tile)

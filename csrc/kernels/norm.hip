@@ -9,6 +9,7 @@
 // written (+7 KB residual each way when fused), which is why the residual add
 // is folded in instead of being a separate pass.
 #include "common.h"
+#include <string.h>
 
 using namespace grag;
 
@@ -227,12 +228,15 @@ __global__ __launch_bounds__(kThreads) void bert_embed_ln_kernel(
     const int32_t* __restrict__ ids, const int32_t* __restrict__ pos_ids,
     const int32_t* __restrict__ type_ids, const bf16* __restrict__ word,
     const bf16* __restrict__ pos, const bf16* __restrict__ type, const bf16* __restrict__ gamma,
-    const bf16* __restrict__ beta, bf16* __restrict__ out, int H, float eps) {
+    const bf16* __restrict__ beta, bf16* __restrict__ out, int H, int V, int P, float eps) {
   __shared__ float red[kThreads / 64];
   const int t = blockIdx.x;
   const int nvec = H >> 3;
-  const bf16x8_t* wr = reinterpret_cast<const bf16x8_t*>(word + (size_t)ids[t] * H);
-  const bf16x8_t* pr = reinterpret_cast<const bf16x8_t*>(pos + (size_t)pos_ids[t] * H);
+  int tid = ids[t], pid = pos_ids[t];
+  if (!index_ok(tid, V, ERR_BERT_TOKEN)) tid = 0;  // (workgroup-uniform) reported; row 0 read instead
+  if (!index_ok(pid, P, ERR_BERT_TOKEN)) pid = 0;
+  const bf16x8_t* wr = reinterpret_cast<const bf16x8_t*>(word + (size_t)tid * H);
+  const bf16x8_t* pr = reinterpret_cast<const bf16x8_t*>(pos + (size_t)pid * H);
   const bf16x8_t* tr =
       reinterpret_cast<const bf16x8_t*>(type + (size_t)(type_ids ? type_ids[t] : 0) * H);
   float v[VPT][8];
@@ -289,14 +293,16 @@ __global__ __launch_bounds__(kThreads) void bert_embed_ln_kernel(
 __global__ __launch_bounds__(kThreads) void embed_gather_kernel(const int32_t* __restrict__ ids,
                                                                 const bf16* __restrict__ table,
                                                                 bf16* __restrict__ out, int T,
-                                                                int H) {
+                                                                int H, int V) {
   const int nvec = H >> 3;
   const size_t total = (size_t)T * nvec;
   for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
        i += (size_t)gridDim.x * kThreads) {
     const int t = (int)(i / nvec), v = (int)(i % nvec);
+    int id = ids[t];
+    if (!index_ok(id, V, ERR_EMBED_TOKEN)) id = 0;  // reported (ops/_lib.py raises at the next sync)
     reinterpret_cast<bf16x8_t*>(out + (size_t)t * H)[v] =
-        reinterpret_cast<const bf16x8_t*>(table + (size_t)ids[t] * H)[v];
+        reinterpret_cast<const bf16x8_t*>(table + (size_t)id * H)[v];
   }
 }
 
@@ -368,6 +374,7 @@ __global__ __launch_bounds__(64) void splitk_rmsnorm_small_kernel(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned tk = __hip_atomic_fetch_add(&counters[row], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk >= (unsigned)nch) report_index_error(ERR_TICKET, tk);  // stale / shared ticket word
     last = tk == (unsigned)(nch - 1) ? 1u : 0u;
     if (last) {
       __hip_atomic_store(&counters[row], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -462,13 +469,13 @@ GRAG_API int grag_add_layernorm(const void* x, const void* bias, void* residual,
 GRAG_API int grag_bert_embed_ln(const int32_t* ids, const int32_t* pos_ids,
                                 const int32_t* type_ids, const void* word, const void* pos,
                                 const void* type, const void* gamma, const void* beta, void* out,
-                                int T, int H, float eps, hipStream_t stream) {
+                                int T, int H, int V, int P, float eps, hipStream_t stream) {
   if (T <= 0) return 0;
   if (H % 8 != 0 || H > 8 * 8 * kThreads) return (int)hipErrorInvalidValue;
   auto args = [&](auto kern) {
     kern<<<T, kThreads, 0, stream>>>(ids, pos_ids, type_ids, (const bf16*)word, (const bf16*)pos,
                                      (const bf16*)type, (const bf16*)gamma, (const bf16*)beta,
-                                     (bf16*)out, H, eps);
+                                     (bf16*)out, H, V, P, eps);
   };
   switch (vpt_for(H)) {
     case 1: args(bert_embed_ln_kernel<1>); break;
@@ -479,13 +486,28 @@ GRAG_API int grag_bert_embed_ln(const int32_t* ids, const int32_t* pos_ids,
   return (int)hipGetLastError();
 }
 
-GRAG_API int grag_embed_gather(const int32_t* ids, const void* table, void* out, int T, int H,
+GRAG_API int grag_embed_gather(const int32_t* ids, const void* table, void* out, int T, int H, int V,
                                hipStream_t stream) {
   if (T <= 0) return 0;
   if (H % 8 != 0) return (int)hipErrorInvalidValue;
   const size_t total = (size_t)T * (H / 8);
   int grid = (int)((total + kThreads - 1) / kThreads);
   if (grid > 4096) grid = 4096;
-  embed_gather_kernel<<<grid, kThreads, 0, stream>>>(ids, (const bf16*)table, (bf16*)out, T, H);
+  embed_gather_kernel<<<grid, kThreads, 0, stream>>>(ids, (const bf16*)table, (bf16*)out, T, H, V);
   return (int)hipGetLastError();
+}
+
+GRAG_ERR_UNIT(norm)
+
+// The index guard's error block (common.h): pinned, device-mapped, coherent host memory, so a kernel's
+// report is visible to the host without a copy.  Returns the host address (nullptr when no device);
+// *dev_out receives the device address every unit's grag_err_bind_* takes.
+GRAG_API void* grag_err_alloc(void** dev_out) {
+  void* h = nullptr;
+  if (hipHostMalloc(&h, 256, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+  memset(h, 0, 256);
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) d = h;
+  *dev_out = d;
+  return h;
 }

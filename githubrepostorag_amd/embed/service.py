@@ -5,12 +5,14 @@ batches (varlen: no padding compute), truncated to the model's
 ``max_seq_length`` like sentence-transformers does."""
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
 
 import torch
 
 from ..engine.tokenizer import WordPieceTokenizer
+from ..ops.gemm import WS
 from ..utils.gpu_guard import gpu_guard, gpu_shared, set_device_of, side_stream
 from ..models.configs import EncoderConfig, encoder_config
 from ..models.encoder import BertEncoder, EncoderGraphs
@@ -30,6 +32,12 @@ class Embedder:
         # query-sized batches replay captured encoder graphs (GRAG_ENCODER_GRAPHS=0: eager)
         self.graphs = (EncoderGraphs(encoder) if encoder.device.type == "cuda"
                        and os.environ.get("GRAG_ENCODER_GRAPHS", "1") != "0" else None)
+        # The encoder's launches -- eager batches, graph captures and replays, from whichever thread embeds --
+        # all go to ONE stream the embedder owns, with split-K slabs / stream-K tickets it owns (ops/gemm.py
+        # WS.owned_by): a captured bucket graph and the eager batches that share its workspace are then
+        # ordered by that stream instead of racing on two callers' streams.  Callers' streams wait on an event.
+        self._ws: dict = {}
+        self._stream = None
 
     @classmethod
     def from_name(cls, name: str, device="cuda", seed: int = 0, **kw) -> "Embedder":
@@ -40,39 +48,69 @@ class Embedder:
         L = min(self.cfg.max_seq_length, self.cfg.max_position)
         return [self.tok.encode(prefix + (t or ""), L) for t in texts]
 
+    @contextlib.contextmanager
+    def _on_encoder(self):
+        """The embedder's stream and workspace owner for the block (the caller holds ``self.lock``); the
+        caller's stream waits for the block's work on exit (an event, no host sync)."""
+        dev = self.encoder.device
+        if dev.type != "cuda":
+            yield None
+            return
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        if self._stream is None:
+            lo, hi = torch.cuda.Stream.priority_range()  # latency-bound query embedding: high priority
+            self._stream = torch.cuda.Stream(device=dev, priority=min(lo, hi))
+        caller = torch.cuda.current_stream(dev)
+        with torch.cuda.stream(self._stream), WS.owned_by(self._ws):
+            yield self._stream
+        if caller != self._stream:
+            caller.wait_stream(self._stream)
+
     @torch.inference_mode()
     def embed_ids(self, ids: list[list[int]]) -> torch.Tensor:
-        """-> bf16 [n, d] L2-normalised on the encoder's device (input order)."""
+        """-> bf16 [n, d] L2-normalised on the encoder's device (input order), ready on the caller's stream."""
         n = len(ids)
-        out = torch.empty(n, self.dim, dtype=torch.bfloat16, device=self.encoder.device)
         if n == 0:
-            return out
+            return torch.empty(0, self.dim, dtype=torch.bfloat16, device=self.encoder.device)
         if self.graphs is not None and n <= EncoderGraphs.B_BUCKETS[-1]:
             bk = self.graphs.bucket_for(ids)
             if bk is not None and not self.graphs.has(bk):
-                with gpu_guard(), self.lock, side_stream(self.encoder.device):  # capture: exclusive
+                with gpu_guard(), self.lock, self._on_encoder():  # capture: exclusive
                     self.graphs.capture(*bk)
-            with gpu_shared(), self.lock, side_stream(self.encoder.device):
-                r = self.graphs.run(ids, allow_capture=False)
+            with gpu_shared(), self.lock:
+                with self._on_encoder():
+                    r = self.graphs.run(ids, allow_capture=False)
+                    if r is not None:
+                        # allocated on the embedder's stream, which also writes it; the caller's stream waits
+                        # for that stream, and record_stream keeps the block from being reused on the
+                        # embedder's stream before the caller is done with it
+                        out = r[1].clone()
                 if r is not None:
-                    out.copy_(r[1])
+                    if out.is_cuda:
+                        out.record_stream(torch.cuda.current_stream(out.device))
                     self.stats["graph_batches"] += 1
                     self.stats["tokens"] += sum(len(x) for x in ids)
                     self.stats["texts"] += n
                     return out
         order = sorted(range(n), key=lambda i: len(ids[i]))
-        with gpu_shared(), self.lock, side_stream(self.encoder.device):
-            i = 0
-            while i < n:
-                j, tok = i, 0
-                while j < n and j - i < self.max_batch and (tok + len(ids[order[j]]) <= self.max_tokens or j == i):
-                    tok += len(ids[order[j]])
-                    j += 1
-                idx = order[i:j]
-                _, vb = self.encoder.encode_ids([ids[t] for t in idx], want_bf16=True)
-                out[torch.as_tensor(idx, device=out.device)] = vb
-                self.stats["tokens"] += tok
-                i = j
+        with gpu_shared(), self.lock:
+            with self._on_encoder():
+                out = torch.empty(n, self.dim, dtype=torch.bfloat16, device=self.encoder.device)
+                i = 0
+                while i < n:
+                    j, tok = i, 0
+                    while j < n and j - i < self.max_batch and (tok + len(ids[order[j]]) <= self.max_tokens
+                                                                or j == i):
+                        tok += len(ids[order[j]])
+                        j += 1
+                    idx = order[i:j]
+                    _, vb = self.encoder.encode_ids([ids[t] for t in idx], want_bf16=True)
+                    out[torch.as_tensor(idx, device=out.device)] = vb
+                    self.stats["tokens"] += tok
+                    i = j
+            if out.is_cuda:
+                out.record_stream(torch.cuda.current_stream(out.device))
         self.stats["texts"] += n
         return out
 

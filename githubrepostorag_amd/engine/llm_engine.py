@@ -31,6 +31,7 @@ import numpy as np
 import torch
 
 from ..ops.attention import KV_TILE, AttnMetadata
+from ..ops._lib import check_device_errors
 from ..ops.gemm import WS
 from ..ops.sampling import SamplerState, reset_slots, sample, sample_tp
 from .scheduler import KVCacheManager, Scheduler
@@ -168,11 +169,17 @@ class LLMEngine:
             # sampler scratch for the largest decode batch up front: graphs captured later all see one buffer
             self.sampler.workspace(self._max_b)
             from ..ops.attention import decode_counters  # small-batch decode tickets: before any capture
-
-            decode_counters(self.device)
             from ..ops.norm import norm_ws
 
-            norm_ws(self.device)
+            with WS.owned_by(self._ws):  # this engine's own ticket words (ops/gemm.py WS.scratch)
+                decode_counters(self.device)
+                norm_ws(self.device)
+            # kernels report out-of-range index inputs (block tables, slots, token ids, tickets) to a
+            # host-mapped block instead of faulting; every step's host read checks it (_read_host)
+            from ..ops._lib import bind_error_guard, lib
+
+            lib()
+            bind_error_guard(self.device.index if self.device.index is not None else torch.cuda.current_device())
             # the engine's own (non-default) stream: retrieval / API threads issue their copies and syncs
             # on other streams; with the engine on the legacy default stream their runtime calls stalled
             # the engine thread (profiles/timeline_r2_*.txt).  Weights and the KV cache were written on
@@ -357,6 +364,7 @@ class LLMEngine:
         dst.copy_(t, non_blocking=True)
         self._pinned_ev.record()
         self._pinned_ev.synchronize()
+        check_device_errors("engine step")
         return dst.numpy().copy()
 
     def _to_dev(self, arr: np.ndarray) -> torch.Tensor:
@@ -689,6 +697,7 @@ class LLMEngine:
             out = self._decode_forward(self._views(dev, n, width, 1), n, nsplit, split_len, out, 1)
             self.model.tp.stage_health()
             toks = out.cpu().numpy()
+            check_device_errors("engine step")
             self.model.tp.check_health()
         now = time.perf_counter()
         finished = []
@@ -769,15 +778,22 @@ class LLMEngine:
     def _capture_ws(self, B, nsplit, split_len, K=1) -> _DecodeGraph:
         t0 = time.perf_counter()
         try:
+            # The eager warm-up step of the shape runs real TP collectives (all-reduces, the sampler's
+            # exchanges): it runs under the SHARED guard.  Only the capture itself -- local work, its
+            # collectives are recorded, not run -- holds the guard exclusively.  An exclusive section that
+            # waited on a peer rank could deadlock against a retrieval thread holding the shared guard in a
+            # cross-rank search collective on either rank.
+            with gpu_shared():
+                prep = self._capture_prepare(B, nsplit, split_len, K)
             with gpu_guard():  # no other thread may sync / allocate while the capture is open
-                return self._capture_locked(B, nsplit, split_len, K)
+                return self._capture_locked(B, nsplit, split_len, K, prep)
         finally:
             dt = time.perf_counter() - t0
             self.stats["capture_s"] += dt
             if self.trace is not None:
                 self.trace.append((t0, "capture", B, K, dt))
 
-    def _capture_locked(self, B, nsplit, split_len, K=1) -> _DecodeGraph:
+    def _capture_prepare(self, B, nsplit, split_len, K=1):
         self._ensure_static()
         W = self.max_blocks_per_seq
         # a benign batch: every row is a padding row (scratch block, scratch slot)
@@ -792,6 +808,10 @@ class LLMEngine:
         with torch.cuda.stream(s):  # one warm-up step of this shape (every window step has the same shapes)
             self._decode_forward(v, B, nsplit, split_len, out, 1)
         torch.cuda.current_stream().wait_stream(s)
+        return v, out, rng_save, seen_save
+
+    def _capture_locked(self, B, nsplit, split_len, K, prep) -> _DecodeGraph:
+        v, out, rng_save, seen_save = prep
         graph = torch.cuda.CUDAGraph()
         # thread_local: API / retrieval threads keep launching (and syncing) on
         # their own streams while the engine thread captures

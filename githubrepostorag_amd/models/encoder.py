@@ -199,8 +199,10 @@ class EncoderGraphs:
         starts.copy_(torch.arange(B + 1, dtype=torch.int32, device=dev) * L)
         lens.fill_(1)
         host.copy_(dbuf.cpu())
-        if self.pool is None:
-            self.pool = torch.cuda.graph_pool_handle()
+        # a private memory pool per bucket: with one pool shared by every bucket, a bucket captured later
+        # may place its intermediates in memory an earlier bucket's graph also writes on replay -- safe only
+        # while replays never overlap, which a pool of its own does not depend on
+        pool = torch.cuda.graph_pool_handle()
         cur = torch.cuda.current_stream(dev)
         s = cur if cur != torch.cuda.default_stream(dev) else torch.cuda.Stream(device=dev)  # capture needs a side stream
         s.wait_stream(cur)
@@ -208,7 +210,7 @@ class EncoderGraphs:
             self.enc.forward(ids, pos, starts, lens, L, want_bf16=True)  # eager warm-up sizes workspaces
             s.synchronize()
             g = torch.cuda.CUDAGraph()
-            with no_gc(), torch.cuda.graph(g, pool=self.pool, stream=s, capture_error_mode="thread_local"):
+            with no_gc(), torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode="thread_local"):
                 outf, outb = self.enc.forward(ids, pos, starts, lens, L, want_bf16=True)
         cur.wait_stream(s)
         self.stats["captures"] += 1

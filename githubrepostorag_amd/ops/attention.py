@@ -34,7 +34,6 @@ _DEC_NT = os.environ.get("GRAG_DECODE_NT", "auto")
 DECODE_MW = {22: 2, 24: 4}
 DECODE_MW_CODE = int(os.environ.get("GRAG_DECODE_MW_CODE", "24"))
 DECODE_MW_ROWS = int(os.environ.get("GRAG_DECODE_MW", "16"))
-_COUNTERS: dict = {}
 MW_SPLITS = int(os.environ.get("GRAG_DECODE_MW_SPLITS", "20"))  # target parts per sequence at B = 1
 
 
@@ -60,15 +59,13 @@ def decode_mw_plan(B: int, Hkv: int, max_ctx: int, max_model_len: int, force: bo
 
 def decode_counters(dev: torch.device) -> torch.Tensor:
     """The small-batch decode kernel's per-(sequence, kv head) tickets (zeroed once; every last arriver resets
-    its word, so hipGraph replays need no memset).  Allocate before any capture (LLMEngine does)."""
-    dev = torch.device(dev)
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
-    c = _COUNTERS.get(key)
-    if c is None:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("decode ticket counters must be allocated before hipGraph capture")
-        c = _COUNTERS[key] = torch.zeros(1 << 16, dtype=torch.int32, device=torch.device("cuda", key))
-    return c
+    its word, so hipGraph replays need no memset).  Owned by the caller's workspace owner (ops/gemm.py
+    WS.scratch: an engine's, so two engines' decodes on two streams never share a ticket word); allocate
+    before any capture (LLMEngine does, under its owner)."""
+    from .gemm import WS
+
+    return WS.scratch("decode_tickets", torch.device(dev),
+                      lambda d: torch.zeros(1 << 16, dtype=torch.int32, device=d))
 
 
 def decode_variant(nsplit: int, split_len: int, waves: int | None = None) -> int:
@@ -196,7 +193,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                  ptr(meta.block_tables), meta.block_tables.stride(0), ptr(meta.q_start), ptr(meta.ctx_len),
                  meta.num_seqs, T, Hq, Hkv, D, BS, float(scale), nsplit, meta.split_len if nsplit > 1 else 0,
                  ptr(meta.part_o) if nsplit > 1 else None, ptr(meta.part_ml) if nsplit > 1 else None,
-                 ptr(decode_counters(q.device)), DECODE_MW[nw])
+                 ptr(decode_counters(q.device)), DECODE_MW[nw], k_cache.shape[0])
             return out
         if nw in DECODE_MW:
             nw = decode_variant(nsplit, meta.split_len, meta.num_seqs * Hkv * nsplit)
@@ -208,7 +205,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
          ptr(meta.block_tables), meta.block_tables.stride(0), ptr(meta.q_start), ptr(meta.ctx_len),
          meta.num_seqs, T, meta.max_q_len, Hq, Hkv, D, BS, float(scale), 1 if causal else 0, nsplit,
          meta.split_len if nsplit > 1 else 0, ptr(meta.part_o) if nsplit > 1 else None,
-         ptr(meta.part_ml) if nsplit > 1 else None, nw)
+         ptr(meta.part_ml) if nsplit > 1 else None, nw, k_cache.shape[0])
     return out
 
 

@@ -61,7 +61,7 @@ def qkv_rope_kvstore(qkv, bias, positions, cos_sin, slot_mapping, k_cache, v_cac
             q = torch.empty(T, Hq, D, dtype=qkv.dtype, device=qkv.device)
             call("grag_qkv_rope_kvstore_planes", ptr(qkv.planes), qkv.S, qkv.N, ptr(bias), ptr(positions),
                  ptr(cos_sin), ptr(slot_mapping), ptr(q), ptr(k_cache), ptr(v_cache), T, Hq, Hkv, D,
-                 k_cache.shape[2])
+                 k_cache.shape[2], *_bounds(k_cache, cos_sin, D))
             return q
     if not qkv.is_cuda:
         return qkv_rope_kvstore_ref(qkv, bias, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, D)
@@ -69,8 +69,15 @@ def qkv_rope_kvstore(qkv, bias, positions, cos_sin, slot_mapping, k_cache, v_cac
     q = torch.empty(T, Hq, D, dtype=qkv.dtype, device=qkv.device)
     BS = k_cache.shape[2]
     call("grag_qkv_rope_kvstore", ptr(qkv), qkv.stride(0), ptr(bias), ptr(positions), ptr(cos_sin),
-         ptr(slot_mapping), ptr(q), ptr(k_cache), ptr(v_cache), T, Hq, Hkv, D, BS)
+         ptr(slot_mapping), ptr(q), ptr(k_cache), ptr(v_cache), T, Hq, Hkv, D, BS, *_bounds(k_cache, cos_sin, D))
     return q
+
+
+def _bounds(k_cache, cos_sin, D) -> tuple[int, int]:
+    """(KV slots, cos/sin rows): the kernel's index-guard limits for slot_mapping / positions."""
+    nslots = 0 if k_cache is None else k_cache.shape[0] * k_cache.shape[2]
+    npos = 0 if cos_sin is None else cos_sin.numel() // D
+    return nslots, npos
 
 
 def silu_mul(gu: torch.Tensor) -> torch.Tensor:

@@ -301,6 +301,31 @@ class _Workspace:
     def reserve(self, dev: torch.device, floats: int) -> None:
         self.get(dev, floats)
 
+    def owner(self) -> dict | None:
+        """The owner dict this thread's launches are routed to (None: thread-local scratch)."""
+        return getattr(self._tls, "owner", None)
+
+    def scratch(self, name: str, dev: torch.device, make):
+        """A persistent per-owner scratch tensor (ticket arrays, small merge buffers) under ``name``: the
+        owner's (an engine's, an embedder's) while one is set, else this thread's.  Every kernel that keeps
+        cross-workgroup state between launches (stream-K / split-merge tickets, a last arriver's chunk sums)
+        takes its buffer from here, so two owners' launches on different streams never share a word -- a
+        process-global ticket array touched by two concurrent launches would leave a word non-zero and make
+        a later launch merge partials that are not written yet.  Created outside hipGraph capture only."""
+        o = getattr(self._tls, "owner", None)
+        if o is None:
+            o = getattr(self._tls, "misc", None)
+            if o is None:
+                o = self._tls.misc = {}
+        tab = o.setdefault(name, {})
+        key = dev.index if dev.index is not None else torch.cuda.current_device()
+        t = tab.get(key)
+        if t is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(f"{name} scratch must be allocated before hipGraph capture")
+            t = tab[key] = make(torch.device("cuda", key))
+        return t
+
 
 WS = _Workspace()
 

@@ -103,21 +103,28 @@ class _StreamWorkspace:
     outside graph capture; GEMMs on one stream reuse it in stream order."""
 
     def __init__(self):
-        self._slab = {}
-        self._counters = {}
         self._retired = []  # outgrown slabs stay alive: captured hipGraphs may still point at them
 
-    # an engine's steps and graph captures use its own slab / tickets (ops/gemm.py WS.owned_by): a decode
-    # graph's LM head must not share them with another engine's or thread's eager stream-K launches
+    # the workspace owner's (ops/gemm.py WS.owned_by: an engine's, an embedder's) or this thread's own: a
+    # decode graph's LM head or an encoder graph's FFN must never share a slab or a ticket word with another
+    # owner's launches on another stream (a process-wide fallback did, for every ownerless thread)
+    @staticmethod
+    def _home() -> dict:
+        t = _tile.WS._tls
+        o = getattr(t, "owner", None)
+        if o is None:
+            o = getattr(t, "misc", None)
+            if o is None:
+                o = t.misc = {}
+        return o
+
     @property
     def slab(self) -> dict:
-        o = getattr(_tile.WS._tls, "owner", None)
-        return self._slab if o is None else o.setdefault("stream_slab", {})
+        return self._home().setdefault("stream_slab", {})
 
     @property
     def counters(self) -> dict:
-        o = getattr(_tile.WS._tls, "owner", None)
-        return self._counters if o is None else o.setdefault("stream_cnt", {})
+        return self._home().setdefault("stream_cnt", {})
 
     def ready(self, dev: torch.device, M: int, N: int, K: int) -> bool:
         """True when a graph capture can use the stream kernel for this shape

@@ -27,21 +27,16 @@ def rmsnorm_ref(x, w, eps, residual=None):
 # the chunked ticket-merge kernel measured slower than one workgroup per row at B = 1 (8.6 vs 5.6 us: the
 # agent-scope release / acquire round trips outweigh the parallel plane reads; profiles/decode_step_b1_r5.txt)
 SMALL_ROWS = int(os.environ.get("GRAG_NORM_SMALL_ROWS", "0"))
-_NORM_WS: dict = {}
 
 
 def norm_ws(dev) -> tuple[torch.Tensor, torch.Tensor]:
-    """(tickets [64] int32, zeroed; chunk sums [64 * 64] fp32) of the small-batch split-K RMSNorm; allocated
-    before any hipGraph capture (LLMEngine does) -- every last arriver resets its ticket."""
-    dev = torch.device(dev)
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
-    ws = _NORM_WS.get(key)
-    if ws is None:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("norm ticket workspace must be allocated before hipGraph capture")
-        d = torch.device("cuda", key)
-        ws = _NORM_WS[key] = (torch.zeros(64, dtype=torch.int32, device=d), torch.zeros(64 * 64, device=d))
-    return ws
+    """(tickets [64] int32, zeroed; chunk sums [64 * 64] fp32) of the small-batch split-K RMSNorm, owned by
+    the caller's workspace owner (ops/gemm.py WS.scratch); allocated before any hipGraph capture (LLMEngine
+    does, under its owner) -- every last arriver resets its ticket."""
+    from .gemm import WS
+
+    return WS.scratch("norm_tickets", torch.device(dev),
+                      lambda d: (torch.zeros(64, dtype=torch.int32, device=d), torch.zeros(64 * 64, device=d)))
 
 
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None,
@@ -130,7 +125,7 @@ def bert_embed_ln(ids, pos_ids, type_ids, word, pos, typ, gamma, beta, eps):
     pos_ids = pos_ids.to(torch.int32).contiguous()
     type_ids = None if type_ids is None else type_ids.to(torch.int32).contiguous()
     call("grag_bert_embed_ln", ptr(ids), ptr(pos_ids), ptr(type_ids), ptr(word), ptr(pos), ptr(typ),
-         ptr(gamma), ptr(beta), ptr(out), T, H, float(eps))
+         ptr(gamma), ptr(beta), ptr(out), T, H, word.shape[0], pos.shape[0], float(eps))
     return out
 
 
@@ -140,5 +135,5 @@ def embed_gather(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
     ids = ids.to(torch.int32).contiguous()
     T, H = ids.numel(), table.shape[1]
     out = torch.empty(T, H, dtype=table.dtype, device=table.device)
-    call("grag_embed_gather", ptr(ids), ptr(table), ptr(out), T, H)
+    call("grag_embed_gather", ptr(ids), ptr(table), ptr(out), T, H, table.shape[0])
     return out

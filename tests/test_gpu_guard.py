@@ -93,3 +93,79 @@ def test_writer_waits_for_a_shared_step():
 
     _run([threading.Thread(target=step), threading.Thread(target=capture)])
     assert order == ["step done", "capture"]
+
+
+def _lazy_capture_beside_search(rank, world):
+    """One rank of test_lazy_capture_during_cross_rank_search_does_not_deadlock: the engine thread steps
+    under the shared guard with a TP collective per step and, at a rank-dependent step, runs the engine's
+    real capture path (LLMEngine._capture_ws: warm-up step with its TP collective, then the exclusive
+    capture); the retrieval thread runs a cross-rank search collective on another group inside the shared
+    guard, as the bench's pump and the service's shard rounds do."""
+    import torch
+    import torch.distributed as dist
+
+    from githubrepostorag_amd.engine.llm_engine import LLMEngine
+    from githubrepostorag_amd.utils.gpu_guard import gpu_shared
+
+    tp = dist.new_group(list(range(world)))
+    idx = dist.new_group(list(range(world)))
+    captured = []
+
+    class FakeEngine:
+        stats = {"capture_s": 0.0}
+        trace = None
+
+        def _capture_prepare(self, B, nsplit, split_len, K):
+            t = torch.ones(1)
+            dist.all_reduce(t, group=tp)  # the warm-up step's TP all-reduce
+            return t
+
+        def _capture_locked(self, B, nsplit, split_len, K, prep):
+            time.sleep(0.01)  # the capture itself: local work only
+            captured.append(B)
+            return None
+
+    eng = FakeEngine()
+    errors = []
+
+    def engine():
+        try:
+            for i in range(40):
+                with gpu_shared():  # LLMEngine.step holds the guard shared
+                    t = torch.ones(1)
+                    dist.all_reduce(t, group=tp)
+                    if i in (7 + 5 * rank, 20):  # lazy captures at steps that differ between the ranks
+                        LLMEngine._capture_ws(eng, 8 + i, 1, 128, 1)
+        except BaseException as e:
+            errors.append(e)
+
+    def pump():
+        try:
+            for _ in range(60):
+                with gpu_shared():  # a sharded search: collective inside the shared section
+                    t = torch.ones(4)
+                    dist.all_reduce(t, group=idx)
+                time.sleep(0.001 * (1 + rank))
+        except BaseException as e:
+            errors.append(e)
+
+    th = [threading.Thread(target=engine), threading.Thread(target=pump)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    if any(t.is_alive() for t in th):
+        return "deadlock"
+    if errors:
+        raise errors[0]
+    return len(captured)
+
+
+def test_lazy_capture_during_cross_rank_search_does_not_deadlock():
+    """a lazy decode capture used to run its eager warm-up step (real TP collectives) inside the
+    exclusive guard, while the retrieval thread held the shared guard across a cross-rank search; two
+    ranks could then wait on each other for ever.  The warm-up now runs under the shared guard, the
+    exclusive section is local."""
+    from tests.dist_utils import run_ranks
+
+    assert run_ranks(_lazy_capture_beside_search, 2, timeout=150) == [2, 2]
