@@ -33,6 +33,15 @@ _CODEY = ("stacktrace", "traceback", "exception", "error", "class ", "function "
           "undefined", "timeout", "reconnect", "retry", "activemq", "jms")
 _CONSERVATIVE = ("insufficient", "don't see enough", "can't answer", "not enough information")
 NEXT_SCOPE = {"project": "package", "package": "file", "file": "code"}
+# synthesize / synthesize-retry: one above the engine's interactive priority (engine/scheduler.py
+# INTERACTIVE_PRIORITY = 2), so an answer's prefill is admitted ahead of other jobs' plan / judge calls
+SYNTH_PRIORITY = 3
+# Context-first prompt layout (prompts.context_prefix), opt-in: on the bench's agent mix the reference order
+# measured fewer prefill tokens (its system text is a prefix shared by every job's synthesize: 1.133M vs 1.159M
+# ideal prefill tokens over 256 jobs, profiles/agent_token_audit_r6.json); the context-first form lets a
+# synthesize-retry reuse the synthesize call's KV of the documents
+_SHARED_CONTEXT = __import__("os").environ.get("GRAG_AGENT_SHARED_CONTEXT", "0") == "1"
+_SHARED_JUDGE = __import__("os").environ.get("GRAG_AGENT_SHARED_JUDGE", "0") == "1"
 
 
 class Cancelled(Exception):
@@ -80,6 +89,17 @@ def doc_to_source(i: int, doc: Any) -> dict:
             "text": _content(doc)[:1200]}
 
 
+def _context_blocks(docs: list) -> list[str]:
+    """The synthesize call's numbered context blocks (agent_graph.py:467-476: top 5 documents, 800 chars
+    each) -- also the shared prefix of the judge prompt over the same retrieval."""
+    blocks = []
+    for i, d in enumerate(docs[:5], start=1):
+        md = getattr(d, "metadata", {}) or {}
+        blocks.append(f"[{i}] repo={md.get('repo', '')} module={md.get('module', '')} "
+                      f"file={md.get('file_path', '')}\n{_content(d)[:800]}")
+    return blocks
+
+
 def _json_object(raw: str) -> dict:
     raw = raw[raw.find("{"): raw.rfind("}") + 1]
     data = json.loads(raw)
@@ -118,9 +138,12 @@ class RunContext:
 
 class GraphAgent:
     def __init__(self, llm, retrievers: dict, namespace: str = "default", max_iters: int = 3,
-                 router_top_k: int = 5, embed_fn=None, synth_max_tokens: int | None = None):
+                 router_top_k: int = 5, embed_fn=None, synth_max_tokens: int | None = None,
+                 shared_context: bool | None = None):
         self.llm = llm
         self.synth_max_tokens = synth_max_tokens
+        # judge / synthesize / synthesize-retry prompts lead with the same context blocks (prompts.context_prefix)
+        self.shared_context = _SHARED_CONTEXT if shared_context is None else bool(shared_context)
         self.retrievers = retrievers
         self.namespace = namespace
         self.max_iters = max_iters
@@ -265,8 +288,21 @@ class GraphAgent:
         elif inv and any("auth" in it["content_preview"].lower() or "cache" in it["content_preview"].lower()
                          for it in inv):
             quality = "semantically_relevant"
+        # Judge over the shared context prefix (GRAG_AGENT_SHARED_JUDGE=1): the full top-5 blocks cost the judge
+        # ~700 tokens more than the reference's 200-char previews and save the following synthesize ~1100 only
+        # when a synthesize over the SAME documents follows.  On the bench's agent mix (random weights: every
+        # judge falls back, 1.8 judges per job, most send the job back to retrieval) the ideal prefill went UP:
+        # 1.133M -> 1.194M tokens for every judge, 1.153M for the last-attempt judge only
+        # (scripts/agent_token_audit.py, profiles/agent_token_audit_r6.json) -- so off by default; synthesize
+        # and its retry always share (the retry then prefills only its own instruction)
+        last = int(st.get("attempt", 0)) >= self.max_iters - 1
+        blocks = _context_blocks(docs) if self.shared_context and _SHARED_JUDGE and last else None
+        if blocks:  # the top documents lead the prompt (shared with synthesize): point at them, no preview
+            inv = [{**it, "content_preview": f"(context block [{it['i']}])"} if it["i"] <= len(blocks) else it
+                   for it in inv]
         try:
-            data = _json_object((yield from self._complete(prompts.judge(q, quality, inv), ctx, "judge")).strip())
+            data = _json_object((yield from self._complete(prompts.judge(q, quality, inv, blocks), ctx,
+                                                           "judge")).strip())
         except Cancelled:
             raise
         except Exception as e:
@@ -329,26 +365,27 @@ class GraphAgent:
     def synthesize(self, st: dict, ctx: RunContext) -> dict:
         q = st["query"]
         docs = st.get("docs") or []
-        blocks, sources = [], []
-        for i, d in enumerate(docs[:5], start=1):
-            md = getattr(d, "metadata", {}) or {}
-            blocks.append(f"[{i}] repo={md.get('repo', '')} module={md.get('module', '')} "
-                          f"file={md.get('file_path', '')}\n{_content(d)[:800]}")
-            sources.append(doc_to_source(i, d))
+        blocks = _context_blocks(docs)
+        sources = [doc_to_source(i, d) for i, d in enumerate(docs[:5], start=1)]
         qtype = "overview" if any(w in q.lower() for w in ("projects", "repositories", "overview", "tell me about",
                                                             "what is", "describe")) else "specific"
         has_content = any(len(b.split("\n", 1)[-1].strip()) > 50 for b in blocks)
         system = prompts.SYNTH_OVERVIEW if qtype == "overview" and has_content else prompts.SYNTH_SPECIFIC
         dbg_issue = None
         try:
+            # the answer's first token is what the job's client waits for: the synthesize call goes ahead of
+            # other jobs' planning / judging prefills in admission (engine/scheduler.py priorities)
             kw = {"on_token": ctx.on_answer_token} if ctx.on_answer_token else {}
+            kw["priority"] = SYNTH_PRIORITY
             if self.synth_max_tokens:
                 kw["max_tokens"] = self.synth_max_tokens
-            text = yield from self._complete(prompts.synthesize(system, q, blocks), ctx, "synthesize", **kw)
+            sh = self.shared_context
+            text = yield from self._complete(prompts.synthesize(system, q, blocks, sh), ctx, "synthesize", **kw)
             if has_content and len(docs) >= 3 and any(p in text.lower() for p in _CONSERVATIVE):
                 try:
                     retry = yield from self._complete(
-                        prompts.synthesize(prompts.SYNTH_RETRY, q, blocks), ctx, "synthesize_retry",
+                        prompts.synthesize(prompts.SYNTH_RETRY, q, blocks, sh), ctx, "synthesize_retry",
+                        priority=SYNTH_PRIORITY,
                         **({"max_tokens": self.synth_max_tokens} if self.synth_max_tokens else {}))
                     if not any(p in retry.lower() for p in _CONSERVATIVE[:3]):
                         text = retry

@@ -32,14 +32,26 @@ def expand_query(question: str, repo: str | None, scope: str | None) -> str:
             "JSON array:")
 
 
-def judge(question: str, context_quality: str, inventory: list[dict]) -> str:
-    # agent_graph.py:325-341
-    rubric = ("Judge if the retrieved content is semantically relevant and sufficient to answer the question. "
-              "Consider both metadata relevance AND content preview relevance. Return JSON: "
-              "{coverage:0..1, needs_more:boolean, suggest_filters?:{repo?,module?,topics?}, "
-              "stage_down?: 'package'|'file'|'code'|null, rewrite?:string, semantic_match:boolean}")
-    return (f"{rubric}\n\nQuestion: {question}\nContext quality: {context_quality}\n"
+JUDGE_RUBRIC = ("Judge if the retrieved content is semantically relevant and sufficient to answer the question. "
+                "Consider both metadata relevance AND content preview relevance. Return JSON: "
+                "{coverage:0..1, needs_more:boolean, suggest_filters?:{repo?,module?,topics?}, "
+                "stage_down?: 'package'|'file'|'code'|null, rewrite?:string, semantic_match:boolean}")
+
+
+def context_prefix(blocks: list[str]) -> str:
+    """The job's retrieved documents as one text block that the judge, synthesize and synthesize-retry
+    prompts all START with, so the engine's prefix cache computes their KV once per retrieval and the later
+    calls prefill only their own instruction + question (shared prefixes)."""
+    return "Context:\n" + "\n\n".join(blocks) + "\n\n"
+
+
+def judge(question: str, context_quality: str, inventory: list[dict], blocks: list[str] | None = None) -> str:
+    # agent_graph.py:325-341 (same rubric and fields).  With ``blocks`` the top documents lead the prompt as
+    # the shared context prefix (their inventory entries then point at their block instead of repeating a
+    # preview of the same text)
+    body = (f"{JUDGE_RUBRIC}\n\nQuestion: {question}\nContext quality: {context_quality}\n"
             f"Retrieved items: {json.dumps(inventory, ensure_ascii=False)}\nJSON:")
+    return context_prefix(blocks) + body if blocks else body
 
 
 def rewrite(base_query: str, context: str) -> str:
@@ -61,9 +73,13 @@ SYNTH_RETRY = ("You are a helpful developer assistant. The user is asking about 
                "if you have project descriptions, share them! Cite sources as [1], [2].")
 
 
-def synthesize(system: str, question: str, blocks: list[str]) -> str:
-    # agent_graph.py:467-476 / 485-488
-    return f"{system}\n\nQuestion: {question}\n\nContext:\n" + "\n\n".join(blocks) + "\n\nAnswer:"
+def synthesize(system: str, question: str, blocks: list[str], shared_prefix: bool = False) -> str:
+    # agent_graph.py:467-476 / 485-488: the same system text, question, numbered context blocks and answer
+    # cue; the context blocks come first (context_prefix) so this call reuses the judge's KV of them and the
+    # retry reuses this one's.  shared_prefix=False: the reference's order (system, question, context)
+    if not shared_prefix:
+        return f"{system}\n\nQuestion: {question}\n\nContext:\n" + "\n\n".join(blocks) + "\n\nAnswer:"
+    return context_prefix(blocks) + f"{system}\n\nQuestion: {question}\n\nAnswer:"
 
 
 # ---- ingest prompts -------------------------------------------------------

@@ -82,6 +82,9 @@ DECODERS = {
     # tiny configs for tests / CPU plumbing
     "qwen2-tiny": DecoderConfig("qwen2-tiny", 512, 256, 512, 2, 4, 2, 64, max_position=4096),
     "qwen2-small": DecoderConfig("qwen2-small", 4096, 512, 1408, 4, 8, 2, 64, max_position=8192),
+    # Qwen2-72B's head layout scaled down (GQA 8:1 -> 16 q / 8 kv heads): TP = 8 leaves each rank 2 q heads and
+    # one kv head, as the 72B's 8 / 1 at TP = 8 (BASELINE config 4's command form, rehearsed on the host)
+    "qwen2-tiny-tp8": DecoderConfig("qwen2-tiny-tp8", 512, 512, 1024, 2, 16, 8, 32, max_position=4096),
     # GPT-2 family (BASELINE config 1: "GPT-2-small greedy answer"): pre-LN,
     # learned absolute positions, GELU(tanh) MLP, MHA, tied LM head
     "gpt2": DecoderConfig("gpt2", 50257, 768, 3072, 12, 12, 12, 64, 1e-5, 0.0, 1024, True, True, "gpt2"),

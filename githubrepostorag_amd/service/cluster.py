@@ -772,7 +772,7 @@ def demo_runtime(settings):
             time.sleep(delay)
         if p.startswith("Choose the best search scope"):
             return '{"scope": "code"}'
-        if p.startswith("Judge if"):
+        if "Judge if the retrieved" in p:
             return '{"coverage": 0.9, "needs_more": false}'
         if p.startswith("Generate 3-4"):
             return '["alt query"]'

@@ -39,7 +39,7 @@ PURPOSE = (("Choose the best search scope", "plan"), ("Generate 3-4", "expand"),
 
 def purpose_of(prompt: str) -> str:
     for pre, name in PURPOSE:
-        if pre in prompt[:200]:
+        if pre in prompt:  # (judge / synthesize prompts lead with the shared context blocks)
             return name
     return "other"
 

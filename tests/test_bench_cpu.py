@@ -15,8 +15,23 @@ TINY = ["--model", "qwen2-tiny", "--encoder", "encoder-tiny", "--index-size", "4
         "--ingest-ref-cap-files", "0"]
 
 
-def _run(cmd, env):
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+def _run(cmd, env, timeout=600):
+    # a stuck rank dumps every thread's stack (bench.py GRAG_DUMP_STACKS_AFTER, repeated) well before the
+    # test's own limit, and a timed-out run fails with those stacks instead of a bare TimeoutExpired
+    env = dict(env, GRAG_DUMP_STACKS_AFTER=str(int(timeout * 0.6)), GRAG_DUMP_STACKS_REPEAT="1")
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, 9)
+        out, err = p.communicate()
+        raise AssertionError(f"bench run hung (> {timeout} s); stacks:\n{err[-12000:]}") from None
+
+    class R:
+        returncode, stdout, stderr = p.returncode, out, err
+
+    r = R
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -109,3 +124,26 @@ def test_bench_self_launch_eight_ranks():
     assert ae["front_door"] == "front door + 8 sharded replicas" and ae["errors"] == 0 and ae["jobs"] == 32
     assert ae["degraded_jobs"] == 0
     assert sorted(r["shard"] for r in ae["replicas"]) == [f"{r}/8" for r in range(8)]
+
+
+def test_bench_self_launch_tp8_config4_form():
+    """BASELINE config 4's exact command form on the host: ``python bench.py --gpus 8 --tp 8`` (one TP group
+    of 8 ranks over gloo, a tiny decoder with Qwen2-72B's 8:1 GQA head layout): the TP leader's runner takes
+    the serving loop's arrivals while 7 peers mirror its steps, ingest runs on the TP group, and the agent
+    phase runs on the leader with 7 shard-only replicas answering index rounds for their shards."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               GRAG_DIST_BACKEND="gloo")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    args = list(TINY)
+    args[args.index("--model") + 1] = "qwen2-tiny-tp8"
+    args[args.index("--agent-jobs") + 1] = "6"
+    args[args.index("--ingest-files") + 1] = "2"
+    res = _run([sys.executable, "bench.py", "--gpus", "8", "--tp", "8", *args], env, timeout=900)
+    assert res["n_gpus"] == 8 and res["config"]["parallelism"] == "tp8dp1"
+    assert res["value"] > 0 and "TP=8" in res["config"]["model"] and res["ingest_docs_per_s"] > 0
+    assert res["headline_loop"].startswith("serving loop") and res["serving_runner"]["value"] == res["value"]
+    ae = res["agent_e2e"]
+    assert ae["errors"] == 0 and ae["jobs"] == 6 and "7 shard-only replicas, 8 shards" in ae["front_door"]
+    assert ae["degraded_jobs"] == 0
+

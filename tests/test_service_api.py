@@ -24,7 +24,7 @@ from githubrepostorag_amd.service.worker import JobQueue
 def _router(p):
     if p.startswith("Choose the best search scope"):
         return '{"scope": "code"}'
-    if p.startswith("Judge if"):
+    if "Judge if the retrieved" in p:
         return '{"coverage": 0.9, "needs_more": false}'
     if p.startswith("Generate 3-4"):
         return '["alt query"]'
@@ -109,7 +109,7 @@ def test_cancel_mid_run(embedder):
     started = {"t": None}
 
     def slow(p):
-        if p.startswith("Judge if"):
+        if "Judge if the retrieved" in p:
             started["t"] = time.time()
             time.sleep(0.5)
         return _router(p)
