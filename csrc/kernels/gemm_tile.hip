@@ -260,7 +260,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
         gm = gm < p.M ? gm : p.M - 1;
         int gn = n0 + (rs >> 5) * 64 + q * 32 + (rs & 31);
         gn = gn < p.N ? gn : p.N - 1;
-        if constexpr (SCHED == 1) {
+        if constexpr (SCHED >= 1) {
           offA[q][i] = (unsigned)(gm * p.lda + koff) * 2u;
           offB[q][i] = (unsigned)(gn * p.ldw + koff) * 2u;
         } else {
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         char* dst = smem + buf * kBuf + q * kSlot + (2 * w + i) * 1024;
-        if constexpr (SCHED == 1)
+        if constexpr (SCHED >= 1)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void_t*)dst, 16, offA[q][i], kt * 128, 0, 0);
         else
           glds16(srcA[q][i] + kt * 64, dst);
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         char* dst = smem + buf * kBuf + (2 + q) * kSlot + (2 * w + i) * 1024;
-        if constexpr (SCHED == 1)
+        if constexpr (SCHED >= 1)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void_t*)dst, 16, offB[q][i], kt * 128, 0, 0);
         else
           glds16(srcB[q][i] + kt * 64, dst);
@@ -294,6 +294,67 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tile_kernel(Args p) {
     acc_zero<MF>(acc01);
     acc_zero<MF>(acc11);
     acc_zero<MF>(acc10);
+    if constexpr (SCHED == 2) {
+      // Two-phase schedule: 32 MFMAs per barrier interval instead of 16 (half the barriers per MFMA; the
+      // interval's fixed cost -- barrier skew over 8 waves, setprio hand-off, wait -- is what kept the 4-phase
+      // schedules at 71-74 % MFMA busy, profiles/pmc_tile_r5.txt).  Per K-tile t (buffer b = t & 1):
+      //   L1 reads A q0, B q0, B q1 (16 b128)  refill A q1 of tile t+1 (buffer b^1; read there in L2(t-1))
+      //   M1 acc00 = A0 B0, acc01 = A0 B1       (32 MFMAs)
+      //   L2 reads A q1 (8 b128)                refill A q0, B q0, B q1 of tile t+2 (buffer b; read in L1(t))
+      //   M2 acc10 = A1 B0, acc11 = A1 B1       (32 MFMAs; B q0 / q1 held from L1)
+      // Every load segment ends with a counted vmcnt(8) (its own 2 or 6 refills plus the other segment's are
+      // the 8 youngest), which retires the batch the NEXT load segment reads -- for the lagging half too,
+      // whose load segments coincide with the leading half's MFMA segments.  A refill is issued one segment
+      // after the barrier that closes the last read of its slot by either half.  Refills past the last
+      // K-tile re-load it (clamped index) into slots nobody reads again, so the counts never change.
+      const int klast = nk - 1;
+      issueA(0, 0, 0);
+      issueB(0, 0, 0);
+      issueB(1, 0, 0);
+      issueA(1, 0, 0);
+      issueA(0, min(1, klast), 1);
+      issueB(0, min(1, klast), 1);
+      issueB(1, min(1, klast), 1);
+      wait_vm<6>();  // tile 0 landed (tile 1's A0 / B0 / B1 are the 6 youngest)
+      bar();
+      if (lag) bar();
+      auto ktile2 = [&](int kt, auto odd_c) {
+        constexpr int buf = decltype(odd_c)::value ? 1 : 0;
+        // L1
+        readA(a, 0, buf);
+        readB(b0, 0, buf);
+        readB(b1, 1, buf);
+        issueA(1, min(kt + 1, klast), buf ^ 1);
+        wait_vm<8>();
+        wait_lgkm0();
+        bar();
+        // M1
+        mma_cluster<MF>(acc00, a, b0);
+        mma_cluster<MF>(acc01, a, b1);
+        bar();
+        // L2
+        readA(a, 1, buf);
+        issueA(0, min(kt + 2, klast), buf);
+        issueB(0, min(kt + 2, klast), buf);
+        issueB(1, min(kt + 2, klast), buf);
+        wait_vm<8>();
+        wait_lgkm0();
+        bar();
+        // M2
+        mma_cluster<MF>(acc10, a, b0);
+        mma_cluster<MF>(acc11, a, b1);
+        bar();
+      };
+      int kt = 0;
+      for (; kt < klast; kt += 2) {
+        ktile2(kt, std::integral_constant<bool, false>{});
+        ktile2(kt + 1, std::integral_constant<bool, true>{});
+      }
+      if (kt == klast) ktile2(kt, std::integral_constant<bool, false>{});
+      wait_vm<0>();  // the clamped re-loads land before the LDS is reused (next segment / stream-K flag)
+      if (!lag) bar();
+      return;
+    }
     if constexpr (SCHED == 1) {
       // Balanced schedule: 8 / 4 / 8 / 4 fragment reads per phase instead of 12 / 4 / 8 / 0.  P4 of
       // K-tile t reads the B quadrant that tile t+1 starts with (its own MFMAs use the other one), so
@@ -744,6 +805,7 @@ template <int EPI, int ACT>
 int launch(const Args& a, hipStream_t stream) {
   const int nwg = a.dp_tiles + a.sk_grid;
   if (g_mfma == 32) gemm_tile_kernel<EPI, ACT, 32, 0><<<nwg, kThreads, 0, stream>>>(a);
+  else if (g_sched == 2 && a.a_bytes > 0 && a.w_bytes > 0) gemm_tile_kernel<EPI, ACT, 16, 2><<<nwg, kThreads, 0, stream>>>(a);
   else if (g_sched == 1 && a.a_bytes > 0 && a.w_bytes > 0) gemm_tile_kernel<EPI, ACT, 16, 1><<<nwg, kThreads, 0, stream>>>(a);
   else gemm_tile_kernel<EPI, ACT, 16, 0><<<nwg, kThreads, 0, stream>>>(a);
   return (int)hipGetLastError();
@@ -763,7 +825,7 @@ GRAG_API int grag_gemm_tile_mfma(int mf) {
 // mainloop); any other value only queries.  Returns the previous schedule.
 GRAG_API int grag_gemm_tile_sched(int sched) {
   const int prev = g_sched;
-  if (sched == 0 || sched == 1) g_sched = sched;
+  if (sched >= 0 && sched <= 2) g_sched = sched;
   return prev;
 }
 

@@ -70,6 +70,10 @@ class EngineConfig:
     # misses the tuned library solutions and costs more than the saved decode steps
     mixed_batches: bool = False
     seed: int = 0
+    # slots / KV tokens bulk (below interactive priority) admissions leave free while interactive traffic is on
+    # (engine/scheduler.py Scheduler reserve): a query beside ingest waves is admitted at the next step
+    interactive_reserve_seqs: int = 16
+    interactive_reserve_tokens: int = 16384
 
 
 def _split_len_for(batch: int) -> int:
@@ -133,7 +137,9 @@ class LLMEngine:
         self.kv = KVCacheManager(nblocks, bs, cfg.enable_prefix_caching)
         self.kv_caches = model.allocate_kv_cache(nblocks, bs)
         self.sched = Scheduler(self.kv, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len,
-                               mixed_batches=cfg.mixed_batches)
+                               mixed_batches=cfg.mixed_batches,
+                               reserve_seqs=min(cfg.interactive_reserve_seqs, cfg.max_num_seqs // 4),
+                               reserve_tokens=min(cfg.interactive_reserve_tokens, nblocks * bs // 8))
         self.scratch_slot = cfg.max_num_seqs
         self.sampler = SamplerState(cfg.max_num_seqs + 1, model.cfg.vocab_size, self.device, seed=cfg.seed)
         self.max_blocks_per_seq = -(-cfg.max_model_len // bs)

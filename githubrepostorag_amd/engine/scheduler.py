@@ -141,8 +141,14 @@ class KVCacheManager:
 
 class Scheduler:
     def __init__(self, kv: KVCacheManager, max_num_seqs: int, max_num_batched_tokens: int, max_model_len: int,
-                 mixed_batches: bool = True):
+                 mixed_batches: bool = True, reserve_seqs: int = 0, reserve_tokens: int = 0):
         self.kv = kv
+        # While interactive traffic is on (schedule() called with a bulk budget), bulk admissions leave this
+        # many sequence slots and KV tokens for interactive arrivals: a query that finds the slots / blocks
+        # taken by ingest waves waits through decode steps until some bulk sequence finishes (concurrent
+        # ingest: 1.46 decode steps before a query's first token, bench concurrent_ingest r5)
+        self.reserve_seqs = reserve_seqs
+        self.reserve_blocks = -(-reserve_tokens // kv.block_size) if reserve_tokens else 0
         self.mixed_batches = mixed_batches
         self.max_num_seqs = max_num_seqs
         self.max_num_batched_tokens = max_num_batched_tokens
@@ -212,7 +218,8 @@ class Scheduler:
         victims = [s for s in self.running if s is not keep]
         if not victims:
             return False
-        v = max(victims, key=lambda s: s.arrival)
+        # lowest priority first (a bulk ingest sequence before an interactive query), newest within it
+        v = max(victims, key=lambda s: (-s.params.priority, s.arrival))
         self.running.remove(v)
         if v in self.prefilling:
             self.prefilling.remove(v)
@@ -258,6 +265,8 @@ class Scheduler:
             def cap(seq, n):  # the bulk share of this step's budget
                 return n if seq.params.priority >= INTERACTIVE_PRIORITY else min(n, bulk_left)
 
+            reserve = bulk_budget is not None  # interactive traffic: hold the reserve back from bulk admissions
+
             while budget > 0:
                 can_admit = (admit_ok and self.waiting and self.free_slots
                              and len(self.running) < self.max_num_seqs)
@@ -284,7 +293,8 @@ class Scheduler:
                     self._finish(seq)
                     admitted.append(("rejected", seq))
                     continue
-                if seq.params.priority < INTERACTIVE_PRIORITY and bulk_left <= 0:
+                bulk = seq.params.priority < INTERACTIVE_PRIORITY
+                if bulk and (bulk_left <= 0 or (reserve and len(self.running) >= self.max_num_seqs - self.reserve_seqs)):
                     admit_ok = False  # (waiting is priority-ordered: only bulk requests follow)
                     continue
                 if not seq.blocks:
@@ -296,7 +306,7 @@ class Scheduler:
                 # blocks and preempting at the next decode step recomputes whole prompts: at 1024 agent jobs
                 # on one GPU that thrash dominated, profiles/agent_saturation_r4.json)
                 if self.running and self.kv.num_free - self.kv.blocks_needed(seq, seq.num_computed + max(n, 0)) \
-                        < len(self.running) + 1:
+                        < len(self.running) + 1 + (self.reserve_blocks if reserve and bulk else 0):
                     admit_ok = False
                     continue
                 if n <= 0 or not self.kv.ensure(seq, seq.num_computed + n):

@@ -216,7 +216,8 @@ def set_mfma(mf: int) -> int:
 
 def set_sched(sched: int) -> int:
     """Select the 16x16x32 tile kernel's phase schedule (0: 12/4/8/0 fragment reads per phase; 1: the
-    balanced 8/4/8/4 order, csrc/kernels/gemm_tile.hip ``SCHED``).  Returns the previous schedule."""
+    balanced 8/4/8/4 order; 2: two phases of 32 MFMAs per K-tile -- csrc/kernels/gemm_tile.hip ``SCHED``).
+    Returns the previous schedule."""
     from ._lib import lib
 
     return int(lib().grag_gemm_tile_sched(int(sched)))

@@ -33,7 +33,7 @@ def main():
 
     def use(arm):
         G.set_mfma(32 if arm == "mf32" else 16)
-        G.set_sched(1 if arm == "s1" else 0)
+        G.set_sched(2 if arm == "s2" else 1 if arm == "s1" else 0)
     dev = torch.device("cuda")
     res = {}
     for M in a.M:

@@ -465,3 +465,37 @@ def test_engine_llm_acomplete_many_coroutines_and_cancel(model, tok):
             asyncio.run(cancelled())
     finally:
         runner.shutdown()
+
+
+def test_interactive_reserve_beside_bulk_admissions():
+    """While interactive traffic is on (a bulk budget is passed), bulk admissions leave the reserve of slots
+    and KV blocks free, so an interactive arrival is admitted at the next step instead of waiting for bulk
+    sequences to finish; without interactive traffic bulk work may use every slot.  Preemption takes a bulk
+    sequence before an interactive one."""
+    from githubrepostorag_amd.engine.scheduler import KVCacheManager, Scheduler
+    from githubrepostorag_amd.engine.sequence import SamplingParams, Sequence
+
+    def mk(n_slots, reserve):
+        kv = KVCacheManager(num_blocks=400, block_size=16)
+        return Scheduler(kv, n_slots, 16384, 4096, mixed_batches=False, reserve_seqs=reserve,
+                         reserve_tokens=16 * 16 if reserve else 0)
+
+    bulk = [Sequence(f"b{i}", list(range(100 + i, 164 + i)), SamplingParams(priority=0)) for i in range(12)]
+    sch = mk(8, 2)
+    for s in bulk:
+        sch.add(s)
+    kind, items = sch.schedule(4096, bulk_budget=4096)
+    assert kind == "prefill" and len(items) == 6  # 8 slots - 2 reserved
+    q = Sequence("q", list(range(7, 71)), SamplingParams(priority=2))
+    sch.add(q)
+    kind, items = sch.schedule(4096, bulk_budget=512)
+    assert [it[0].req_id for it in items] == ["q"]  # admitted at once, and the step carries no bulk prefill
+    # no interactive traffic: bulk work takes every slot
+    sch2 = mk(8, 2)
+    for s in [Sequence(f"c{i}", list(range(64)), SamplingParams(priority=0)) for i in range(12)]:
+        sch2.add(s)
+    kind, items = sch2.schedule(4096)
+    assert len(items) == 8
+    # preemption victim: lowest priority first
+    sch.running.sort(key=lambda s: s.arrival)
+    assert sch._preempt_one(keep=sch.running[0]) and q in sch.running

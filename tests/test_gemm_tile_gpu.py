@@ -421,9 +421,9 @@ def test_gemm_decode_small_rows(dev, depth, M, N, K, silu):
 
 
 # ---------------------------------------------------------------- balanced phase schedule (gemm_tile.hip SCHED 1)
-@pytest.fixture
-def sched1():
-    prev = G.set_sched(1)
+@pytest.fixture(params=[1, 2])
+def sched1(request):
+    prev = G.set_sched(request.param)
     yield
     G.set_sched(prev)
 
@@ -432,14 +432,16 @@ def sched1():
                                          (4096, 4608, 3584, 1, 0), (200, 1024, 1024, 4, 0), (192, 3584, 18944, 8, 0),
                                          (512, 1536, 512, 1, 20), (2560, 1024, 384, 1, 16),
                                          (7040, 3584, 2048, 1, -408), (1280, 4608, 1024, 1, -270)])
-def test_gemm_balanced_schedule(dev, M, N, K, ks, sk):
+@pytest.mark.parametrize("sched", [1, 2])
+def test_gemm_balanced_schedule(dev, M, N, K, ks, sk, sched):
     # every K-tile count parity, 2- and 3-tile segments, split-K planes and stream-K shares; each accumulator
-    # sees the same K order under both schedules, so the results are bitwise equal to schedule 0's
+    # sees the same K order under every schedule (1: balanced 4-phase, 2: two-phase, 32 MFMAs per barrier
+    # interval), so the results are bitwise equal to schedule 0's
     x, w, b = rnd(M, K, dev=dev, scale=0.3), rnd(N, K, dev=dev, seed=1, scale=0.3), rnd(N, dev=dev, seed=2)
     prev = G.set_sched(0)
     try:
         y0 = G.gemm(x, w, b, ksplit=ks, sk=sk)
-        G.set_sched(1)
+        G.set_sched(sched)
         y1 = G.gemm(x, w, b, ksplit=ks, sk=sk)
     finally:
         G.set_sched(prev)
