@@ -95,6 +95,9 @@ def parse():
                          "(ingest/src/app/llm_init.py:56) over this many files: ingest_docs_per_s_ref_cap (0: skip)")
     ap.add_argument("--ingest-ref-cap", type=int, default=2048, help="the cap of that pass (tests shrink it)")
     ap.add_argument("--ingest-seqs", type=int, default=256, help="concurrent sequences of the ingest engine")
+    ap.add_argument("--ingest-multi", default="auto",
+                    help="RxF: R synthetic repos of F files through ingest_many, all at once on one engine "
+                         "(auto: 8x48 on a GPU, 2x2 on the host; 0: skip)")
     ap.add_argument("--ingest-mixed", type=int, default=0,
                     help="1: the ingest engine piggybacks decode tokens on prefill steps (mixed batches)")
     ap.add_argument("--mixed", type=int, default=0,
@@ -687,6 +690,26 @@ def main():
                           "llm_calls": st2.get("llm_calls")}
             log(f"ingest at a {args.ingest_ref_cap}-token cap on every call: {n2} docs/rank in {float(tt2.item()):.2f}s")
 
+    ingest_multi = None
+    spec = args.ingest_multi
+    if spec == "auto":
+        spec = "8x48" if dev.type == "cuda" else "2x2"
+    if not args.no_ingest and spec not in ("0", "", "none") and tp == 1:
+        from githubrepostorag_amd.ingest.bench_ingest import run_ingest_multi
+
+        nr, nf = (int(x) for x in spec.lower().split("x"))
+        comm.barrier()
+        ingest_multi = run_ingest_multi(model, tok, emb, nr, nf, seed=dp_rank, max_num_seqs=args.ingest_seqs,
+                                        use_graph=not args.no_graph, kv_cache_gb=args.ingest_kv_gb,
+                                        max_model_len=min(8192, dcfg.max_position))
+        tm = torch.tensor([ingest_multi["seconds"]], dtype=torch.float64, device=dev)
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        ingest_multi["docs_per_s"] = round(ingest_multi["docs"] * dp_size / float(tm.item()), 3)
+        log(f"multi-repo ingest ({nr} repos x {nf} files, ingest_many at once): {ingest_multi['docs_per_s']} docs/s")
+
     concurrent = None
     if (args.concurrent_ingest and not args.no_ingest and args.ingest_files > 0 and tp == 1 and serving_res
             and serving_res.get("open_loop")):
@@ -774,6 +797,9 @@ def main():
             "serving_runner": serving_res,
             "ingest_stage_s": ingest_stages,
             "ingest_ref_cap": ingest_ref,
+            # several repositories through ingest_many at once on one engine (the next repo's extractor waves
+            # fill a repo's roll-up tail); ingest_docs_per_s above is one repository at a time
+            "ingest_multi_repo": ingest_multi,
             "e2e_ttft_p50_ms": None if agent_res is None else agent_res["e2e_ttft_p50_ms"],
             "e2e_ttft_p90_ms": None if agent_res is None else agent_res["e2e_ttft_p90_ms"],
             "agent_jobs_per_s": None if agent_res is None else agent_res["agent_jobs_per_s"],

@@ -798,8 +798,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 int g_mfma = 16;  // grag_gemm_tile_mfma()
-int g_sched = 1;  // grag_gemm_tile_sched(): 1 the balanced 8/4/8/4-read phase schedule (default: +5-10 % on
-                  // the prefill shapes, profiles/ab_tile_sched_r5.json), 0 the 12/4/8/0 one
+int g_sched = 2;  // grag_gemm_tile_sched(): 2 the two-phase schedule, 32 MFMAs per barrier interval (default:
+                  // +0.9-4.1 % over 1 at 7104 rows, bitwise equal, profiles/ab_tile_sched_r6.json); 1 the balanced
+                  // 8/4/8/4-read phase schedule (+5-10 % over 0, profiles/ab_tile_sched_r5.json); 0 the 12/4/8/0 one
 
 template <int EPI, int ACT>
 int launch(const Args& a, hipStream_t stream) {

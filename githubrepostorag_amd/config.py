@@ -72,6 +72,9 @@ class Settings:
                                                           _env("EMBEDDINGS_TABLE", "embeddings")))
     pushgateway_address: str = field(default_factory=lambda: _env("PUSHGATEWAY_ADDRESS", "pushgateway:9091"))
     # --- MI355X engine / index knobs (new)
+    # repositories ingest_many runs at once on the one engine (the reference: one after another,
+    # ingest_controller.py:506-516): repo N+1's extractor waves fill repo N's roll-up tail
+    ingest_concurrency: int = field(default_factory=lambda: _int("INGEST_CONCURRENCY", 4))
     model_dir: str | None = field(default_factory=lambda: os.environ.get("MODEL_DIR"))
     encoder_dir: str | None = field(default_factory=lambda: os.environ.get("ENCODER_DIR"))
     index_dir: str | None = field(default_factory=lambda: os.environ.get("INDEX_DIR"))

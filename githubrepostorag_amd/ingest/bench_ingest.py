@@ -115,6 +115,56 @@ def _ingest_on(runner, eng, tok, emb, n_files, seed, summary_tokens, token_cap, 
     return res["documents"], dt, st
 
 
+def run_ingest_multi(model, tok, emb, n_repos: int, n_files: int, seed: int = 0, concurrency: int | None = None,
+                     max_num_seqs: int = 256, max_model_len: int = 8192, use_graph: bool = True,
+                     summary_tokens: int = 128, kv_cache_gb: float | None = None) -> dict:
+    """Multi-repository ingest (the reference's DEV_MODE batch: every repo of a user) through
+    ``IngestController.ingest_many`` on ONE engine: ``n_repos`` synthetic repositories of ``n_files`` files,
+    ``concurrency`` of them at once (default: all).  Returns docs/s with the sequential figure's setup."""
+    dev = torch.device(getattr(model, "device", "cpu"))
+    sizes = tuple(sorted({*EngineConfig.graph_batch_sizes, *range(256, max_num_seqs + 1, 128), max_num_seqs}))
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=max_num_seqs, max_num_batched_tokens=16384,
+                                             max_model_len=max_model_len, use_cuda_graph=use_graph, seed=seed,
+                                             kv_cache_gb=kv_cache_gb,
+                                             graph_batch_sizes=tuple(b for b in sizes if b <= max_num_seqs)))
+    if use_graph and dev.type == "cuda":
+        ctxs = sorted({c for c in (2048, 4096, max_model_len) if c <= max_model_len})
+        eng.warmup_graphs(max_ctx=ctxs, windows=(1, 2, 4, 8),
+                          params=SamplingParams(temperature=EngineLLM.INGEST["temperature"],
+                                                top_p=EngineLLM.INGEST["top_p"]))
+    runner = EngineRunner(eng)
+    try:
+        llm = EngineLLM(runner, tok, max_tokens=summary_tokens, mode="ingest", timeout_s=3600.0, retries=0)
+        store = VectorStore(emb.dim, dev)
+        ctl = IngestController(llm=llm, store=store, embedder=emb, settings=Settings(data_dir=None),
+                               summary_tokens=summary_tokens)
+        items, n_docs = [], 0
+        for r in range(n_repos):
+            name = f"bench-multi-{seed}-{r}"
+            _, files = synthetic_repo(seed * 1000 + r, n_files, name)
+            docs = [Document(f["text"], {"file_path": f["file_path"], "file_name": f["file_path"].split("/")[-1]})
+                    for f in files]
+            n_docs += len(docs)
+            items.append({"repo": name, "namespace": "bench", "documents": docs, "force": True})
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = ctl.ingest_many(items, concurrency=concurrency or n_repos)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        return {"repos": n_repos, "files_per_repo": n_files, "concurrency": concurrency or n_repos,
+                "docs": n_docs, "seconds": round(dt, 2), "docs_per_s": round(n_docs / dt, 3),
+                "ok": all(r.get("ok") for r in res),
+                "engine": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()
+                           if isinstance(v, (int, float))}}
+    finally:
+        runner.shutdown()
+        del eng
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+
+
 def critical_path(trace: list, t0: float, total: float, bucket: float = 1.0) -> dict:
     """Where the ingest wall time went, from the engine's per-step trace (engine/llm_engine.py ``trace``):
     totals per step kind, the engine-idle remainder (host work, waits between dependent waves), and a

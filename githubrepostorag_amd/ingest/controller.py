@@ -259,7 +259,13 @@ class IngestController:
 
     # ---- batch driver (ingest_controller.py:490-542) ---------------------
     def ingest_many(self, components, *, branch: str | None = None, dev_force_standalone: bool | None = None,
-                    source: str = "synthetic", path: str | None = None) -> list[dict]:
+                    source: str = "synthetic", path: str | None = None, concurrency: int | None = None) -> list[dict]:
+        """Every component of the batch (the reference's DEV_MODE: every public repo of the user), up to
+        ``concurrency`` (settings INGEST_CONCURRENCY) at once on the one engine: each repository's pipeline
+        ends in a dependent roll-up chain (file -> module -> repo -> catalog) of small decode batches, and
+        the next repository's extractor waves fill those steps (the reference ingests one repository after
+        another, ingest_controller.py:506-516).  Results in input order; a failed component raises after
+        the others finished, as the sequential loop would have stopped at it."""
         default_branch = branch or self.s.default_branch
         items = []
         if dev_force_standalone and source == "github":
@@ -280,9 +286,12 @@ class IngestController:
                          "dev_force_standalone": it[5] if len(it) > 5 else dev_force_standalone,
                          "branch": default_branch}
                 items.append(p)
-        out = []
         for p in items:
             p.setdefault("source", source)
             p.setdefault("path", path)
-            out.append(self.ingest_component(**p))
-        return out
+        R = max(1, int(concurrency if concurrency is not None else getattr(self.s, "ingest_concurrency", 1)))
+        if R == 1 or len(items) <= 1:
+            return [self.ingest_component(**p) for p in items]
+        with ThreadPoolExecutor(max_workers=min(R, len(items)), thread_name_prefix="ingest-repo") as ex:
+            futs = [ex.submit(self.ingest_component, **p) for p in items]
+            return [f.result() for f in futs]
