@@ -1227,6 +1227,10 @@ def concurrent_phase(args, model, tok, emb, prepare, sp, u, dev, group, world, d
         if dev.type == "cuda":
             torch.cuda.empty_cache()
     docs, secs, st = out["ingest"]
+    if os.environ.get("GRAG_DUMP_TRACE"):  # the raw step trace + each query's (submitted, first token) stamps
+        with open(os.environ["GRAG_DUMP_TRACE"], "w") as f:
+            json.dump({"trace": [list(t) for t in trace or []], "abs_times": abs_times,
+                       "ttft": [g[0] for g in got], "submit_to_first": [g[1] for g in got]}, f)
     tt.sort()
     p50 = 1000 * tt[len(tt) // 2] if tt else None
     p90 = 1000 * tt[min(len(tt) - 1, int(0.9 * len(tt)))] if tt else None
@@ -1387,9 +1391,10 @@ def agent_phase(args, rank, world, dev, eng, tok, emb, index, corpus, log, tp_gr
             dist.broadcast_object_list(obj, src=0)
             addr, key = obj[0]
             rgroup = None
-            if os.environ.get("GRAG_SHARD_TRANSPORT") == "collective":
-                # opt-in: the replicas' shard rounds as lockstep collectives (service/collective.py) on a
-                # communicator of their own; the default stays the socket mesh
+            if os.environ.get("GRAG_SHARD_TRANSPORT", "collective") == "collective":
+                # the replicas' shard rounds as lockstep collectives (service/collective.py: RCCL over xGMI, the
+                # score exchange a device all-gather) on a communicator of their own; GRAG_SHARD_TRANSPORT=mesh
+                # keeps the socket mesh
                 from githubrepostorag_amd.parallel import comm
 
                 rgroup = comm.Group(list(range(world)), pg=dist.new_group(list(range(world))))

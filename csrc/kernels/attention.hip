@@ -50,7 +50,16 @@ struct AttnParams {
   float scale_log2;
   int causal;
   int nblocks;  // KV blocks in the cache: the index guard's bound for block-table entries (common.h)
+  int xcd_group;  // decode: consecutive sequences of one (kv head, split) run on one XCD (g_decode_xcd)
 };
+
+// grag_attn_decode_xcd(1): decode workgroups remapped so that sequences adjacent in the batch run on the same
+// XCD at about the same time (their shared prefix K/V from that XCD's L2).  Off by default: measured
+// (scripts/mb_shared_prefix.py, profiles/mb_shared_prefix_r6.json) prefix-sharing rows already read their
+// shared blocks mostly from the Infinity Cache in any order (B192 ctx 1792: 122.7 us unshared -> 105.8 us
+// shared, adjacent or shuffled alike), and the remap deals whole split columns to XCD halves: B256 with a
+// 2048 + 512-key split plan 233 -> 292 us
+int g_decode_xcd = 0;
 
 // Chunk (16 B) swizzle for the K image read as row fragments by ds_read_b128.
 template <int D>
@@ -656,7 +665,15 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
 
   const int lane = threadIdx.x;
   const int h4 = lane >> 4, li = lane & 15;
-  const int seq = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
+  int seq = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
+  if (p.xcd_group) {  // logical ids dealt to one XCD are contiguous, sequence index fastest (common.h xcd_remap)
+    const int nseq = gridDim.x;
+    const int lg = xcd_remap(blockIdx.x + nseq * (blockIdx.y + gridDim.y * blockIdx.z),
+                             nseq * gridDim.y * gridDim.z);
+    seq = lg % nseq;
+    kvh = (lg / nseq) % gridDim.y;
+    split = lg / (nseq * gridDim.y);
+  }
   const int ctx = p.ctx_len[seq];
   const int kv_lo = split * p.split_len;
   const int kv_hi = min(ctx, kv_lo + p.split_len);
@@ -1160,7 +1177,9 @@ int launch(const AttnParams& prm, int nseq, hipStream_t stream) {
 }
 
 template <int D>
-int launch_decode(const AttnParams& prm, int nseq, int tk, int ns, bool nt, hipStream_t stream) {
+int launch_decode(const AttnParams& prm_in, int nseq, int tk, int ns, bool nt, hipStream_t stream) {
+  AttnParams prm = prm_in;
+  prm.xcd_group = g_decode_xcd;
   dim3 grid(nseq, prm.Hkv, prm.num_splits);
   if (nt && tk == 32 && ns == 3)
     paged_decode_kernel<D, 32, 3, true><<<grid, 64, 0, stream>>>(prm);
@@ -1274,6 +1293,14 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
     case 32: return dispatch_nw<32>(prm, nseq, nw, true, stream);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// Decode workgroup placement for later launches (1: sequences adjacent in the batch on one XCD, 0: the
+// dispatcher's round robin); any other value only queries.  Returns the previous setting.
+GRAG_API int grag_attn_decode_xcd(int on) {
+  const int prev = g_decode_xcd;
+  if (on == 0 || on == 1) g_decode_xcd = on;
+  return prev;
 }
 
 // Small-batch decode (paged_decode_mw_kernel): nw = 2 or 4 waves per (sequence, kv head, split), the splits

@@ -106,6 +106,15 @@ def _decode_plan(model, B: int, max_ctx: int, max_model_len: int, graph: bool = 
     return max(1, need), split_len
 
 
+# prefix-sharing decode rows side by side (GRAG_DECODE_GROUP_ROWS=1): off by default -- the shared blocks
+# already come from the Infinity Cache in any row order (profiles/mb_shared_prefix_r6.json)
+_GROUP_ROWS = __import__("os").environ.get("GRAG_DECODE_GROUP_ROWS", "0") == "1"
+
+
+def _prefix_blocks(s) -> list:
+    return s.blocks[:32]
+
+
 def _pow2_at_least(n: int) -> int:
     p = 1
     while p < n:
@@ -671,6 +680,12 @@ class LLMEngine:
     def _run_decode(self, seqs, max_window: int | None = None) -> list[Sequence]:
         t0 = time.perf_counter()
         n = len(seqs)
+        if _GROUP_ROWS and n >= 32:
+            # rows that share a cached prompt prefix (ingest's summary / title / keyword calls of one chunk,
+            # the roll-ups over the same content) side by side: with the decode kernel's XCD placement
+            # (csrc/kernels/attention.hip g_decode_xcd) their shared K/V blocks are read on one XCD at about
+            # the same time and come from its L2 for all but the first
+            seqs = sorted(seqs, key=_prefix_blocks)
         # under TP the graphs hold the decode's collectives (one-shot IPC all-reduce, RCCL logits gather);
         # replicated scheduling makes every TP rank pick, capture and replay the same graph in lockstep
         use_graph = (self.on_gpu and self.cfg.use_cuda_graph and n <= max(self.cfg.graph_batch_sizes)

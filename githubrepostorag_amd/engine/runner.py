@@ -91,13 +91,17 @@ class EngineRunner:
     # submitted during one waits for the rest of it (up to 8 steps: ~220 ms at 1024 live rows) before its
     # prefill.  GRAG_ARRIVAL_WINDOW:
     #   "auto" (default): paced by the arrival rate -- while arrivals keep coming (one within the last two
-    #          mean gaps), a replay lasts at most half the mean gap between arrival events (EWMA; submits
-    #          within 2 ms are one event), at least one step: an arrival waits ~1/4 gap on average instead
-    #          of half a window.  No arrivals -> full windows.
+    #          mean gaps or PACE_HOLD_S, whichever is longer), a replay lasts at most half the mean gap between
+    #          arrival events (EWMA; submits within 2 ms are one event), at least one step: an arrival waits
+    #          ~1/4 gap on average instead of half a window.  No arrivals -> full windows.  (The hold: Poisson
+    #          arrivals leave a two-gap quiet spell about one time in seven, and a full 8-step window of a
+    #          ~340-row ingest batch then ran ~97 ms with the next queries waiting behind it -- the concurrent
+    #          ingest trace, bench.py GRAG_DUMP_TRACE.)
     #   N > 0: fixed cap of N steps while requests keep arriving (one within ARRIVAL_RECENT_S);
     #   0:     off (full windows).  profiles/ab_arrival_window_r2.txt: fixed N = 2 on the agent phase
     #          cost 4-6 % jobs/s; the paced form is measured in docs/STATUS.md (round 4).
     ARRIVAL_RECENT_S = 0.05
+    PACE_HOLD_S = float(os.environ.get("GRAG_PACE_HOLD_S", "0.5"))
     _AW = os.environ.get("GRAG_ARRIVAL_WINDOW", "auto")
     ARRIVAL_WINDOW = -1 if _AW == "auto" else int(_AW)
     MAX_WINDOW = 8
@@ -206,7 +210,7 @@ class EngineRunner:
         if self.ARRIVAL_WINDOW > 0:
             return self.ARRIVAL_WINDOW if now - self._last_submit < self.ARRIVAL_RECENT_S else None
         g, d = self._gap, self._step_s
-        if g is None or d is None or now - self._last_event > 2 * g:
+        if g is None or d is None or now - self._last_event > max(2 * g, self.PACE_HOLD_S):
             return None
         return max(1, min(self.MAX_WINDOW, int(0.5 * g / d)))
 
@@ -216,7 +220,7 @@ class EngineRunner:
         if not self.interactive_prefill or self.tp is not None:
             return None, None
         g = self._gap
-        if self._expecting > 0 or (g is not None and time.monotonic() - self._last_event <= 2 * g):
+        if self._expecting > 0 or (g is not None and time.monotonic() - self._last_event <= max(2 * g, self.PACE_HOLD_S)):
             return self.interactive_prefill, (self.bulk_prefill or None)
         return None, None
 

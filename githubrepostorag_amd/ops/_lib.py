@@ -72,6 +72,7 @@ _SIGS = {
     "grag_gemm_w4": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_w4_has": [I, I],
     "grag_err_alloc": [P],
+    "grag_attn_decode_xcd": [I],
 }
 
 
@@ -106,6 +107,9 @@ def lib():
         mf = os.environ.get("GRAG_GEMM_MFMA")
         if mf and getattr(handle, "grag_gemm_tile_mfma", None) is not None:
             handle.grag_gemm_tile_mfma(int(mf))  # tile GEMM MFMA shape (16 default, 32)
+        xc = os.environ.get("GRAG_DECODE_XCD")
+        if xc and getattr(handle, "grag_attn_decode_xcd", None) is not None:
+            handle.grag_attn_decode_xcd(int(xc))  # decode workgroups of adjacent rows on one XCD (1) or not (0)
         sc = os.environ.get("GRAG_GEMM_SCHED")
         if sc and getattr(handle, "grag_gemm_tile_sched", None) is not None:
             handle.grag_gemm_tile_sched(int(sc))  # tile GEMM phase schedule (0, 1 balanced reads)

@@ -710,8 +710,9 @@ def spawn_replicas(n: int, address, authkey: bytes, extra_args=(), gpus: list[in
                    env: dict | None = None, shards: int = 1) -> list[subprocess.Popen]:
     """Start one replica child process per GPU (HIP_VISIBLE_DEVICES pins it; never an exec of this
     process).  The authkey travels in the environment, not on the command line.  With
-    GRAG_SHARD_TRANSPORT=collective the replicas also form a torch.distributed group (rank = replica)
-    for their shard rounds (service/collective.py)."""
+    sharded replicas (the default transport, GRAG_SHARD_TRANSPORT=collective; =mesh / =hub keep the socket
+    transports) the replicas also form a torch.distributed group (rank = replica) for their shard rounds
+    (service/collective.py)."""
     import socket
 
     with socket.socket() as sk:
@@ -724,7 +725,7 @@ def spawn_replicas(n: int, address, authkey: bytes, extra_args=(), gpus: list[in
         if gpus is not None:
             e["HIP_VISIBLE_DEVICES"] = str(gpus[r])
         e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        if shards > 1 and e.get("GRAG_SHARD_TRANSPORT") == "collective":
+        if shards > 1 and e.setdefault("GRAG_SHARD_TRANSPORT", "collective") == "collective":
             # the replicas' process group (service/collective.py): RCCL when each has its own GPU
             e.update(RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                      MASTER_PORT=str(pg_port))

@@ -61,6 +61,13 @@ class CollectiveShardTransport:
         # rounds / degraded_rounds: this replica's fan-outs (as the mesh counts them); ticks: lockstep rounds
         self.stats = {"rounds": 0, "degraded_rounds": 0, "ticks": 0, "busy_rounds": 0, "requests": 0, "served": 0, "stacked_searches": 0,
                       "bytes_out": 0, "device_exchanges": 0}
+        # plain-search answers pruned to each query's global winners through a score all-gather (C3 as a
+        # tensor exchange, _prune_searches); GRAG_SHARD_PRUNE=0 sends every shard's top-k
+        import os
+
+        self.prune = os.environ.get("GRAG_SHARD_PRUNE", "1") != "0"
+        self.prune_min = int(os.environ.get("GRAG_SHARD_PRUNE_MIN", "128"))  # candidate hits in the round
+        self._broken = False  # the group failed: rounds go to the fallback transport (fanout)
         self._ipc_bad = False  # this rank's device exchange timed out (reported in the next round's header)
         self._ipc_off = False  # every rank left the device exchange at the same round
         self._lat: list[float] = []
@@ -71,11 +78,18 @@ class CollectiveShardTransport:
     def fanout(self, origin: int, scope: str, op: str, payload, timeout: float = 60.0):
         from .mesh import Parts
 
+        r = None
         with self._cv:
-            self._ids += 1
-            r = _Req(self._ids, scope, op, payload)
-            self._q.append(r)
-            self._cv.notify()
+            if not (self._broken and self.fallback is not None):
+                self._ids += 1
+                r = _Req(self._ids, scope, op, payload)
+                self._q.append(r)
+                self._cv.notify()
+        if r is None:
+            # the replicas' process group broke (a replica died: a collective cannot leave one rank out):
+            # the socket mesh carries the rounds from here on and reports the lost shard as missing
+            self.stats["fallback_rounds"] = self.stats.get("fallback_rounds", 0) + 1
+            return self.fallback.fanout(origin, scope, op, payload, timeout)
         t0 = time.monotonic()
         ok = r.ev.wait(timeout)
         self._lat.append(time.monotonic() - t0)
@@ -170,7 +184,7 @@ class CollectiveShardTransport:
         return [got[s, : int(all_lens[s, self.rank])].numpy().tobytes() for s in range(g.size)]
 
     def _loop(self) -> None:
-        from ..utils.gpu_guard import set_device_of, side_stream
+        from ..utils.gpu_guard import gpu_shared, set_device_of, side_stream
 
         g = self.group
         # the round header (and the fallback payload path) on the group's control device: RCCL -> the GPU,
@@ -185,11 +199,15 @@ class CollectiveShardTransport:
                 with self._cv:
                     if not self._q:  # (a closing rank keeps the tick until every rank has closed)
                         # lockstep rounds: a busy system turns every tick; an idle one backs off (x4 after
-                        # 64 empty rounds) -- a new request then waits at most that long for the round
-                        self._cv.wait(self.tick if idle < 64 else 4 * self.tick)
+                        # 64 empty rounds, x20 after 1024) -- a new request then waits at most that long
+                        self._cv.wait(self.tick if idle < 64 else 4 * self.tick if idle < 1024 else 20 * self.tick)
                     mine, self._q = self._q, []
                     stop = self._stop
-                with side_stream(self.device) if self.device.type == "cuda" else _null():
+                # the round's host syncs (.cpu() of its collectives) never run inside another thread's hipGraph
+                # capture: the round holds the capture guard shared -- "urgent", i.e. not queued behind a
+                # capture that is only waiting, since job threads holding the guard wait on this round
+                with (gpu_shared(urgent=True) if self.device.type == "cuda" else _null()), \
+                        (side_stream(self.device) if self.device.type == "cuda" else _null()):
                     blob = pickle.dumps([(r.rid, r.scope, r.op, r.payload) for r in mine],
                                         protocol=pickle.HIGHEST_PROTOCOL) if mine else b""
                     hdr = torch.tensor([len(mine), int(stop), int(not self._ipc_bad), len(blob)], dtype=torch.int64)
@@ -216,13 +234,18 @@ class CollectiveShardTransport:
                     failed_before = self._ipc_bad
                     allreq = [_loads(b) for b in self._gather_bytes(blob, head[:, 3].tolist())]
                     # answer every other replica's reads on this shard (stacked plain searches)
-                    answers = []
+                    results = {}
                     for src, items in enumerate(allreq):
                         if src == self.rank or not items:
-                            answers.append(b"")
                             continue
                         self.stats["served"] += len(items)
-                        answers.append(pickle.dumps(self._run_reads(items), protocol=pickle.HIGHEST_PROTOCOL))
+                        results[src] = self._run_reads(items)
+                    if self.prune:  # C3 as a tensor exchange: only each query's global winners travel back
+                        _t = time.perf_counter()
+                        results = self._prune_searches(allreq, results)
+                        self.stats["prune_s"] = self.stats.get("prune_s", 0.0) + time.perf_counter() - _t
+                    answers = [pickle.dumps(results[src], protocol=pickle.HIGHEST_PROTOCOL) if src in results
+                               else b"" for src in range(g.size)]
                     back = self._exchange(answers)
                     round_bad = self._ipc_bad and not failed_before
                 by_id = {r.rid: r for r in mine}
@@ -237,8 +260,9 @@ class CollectiveShardTransport:
                 for r in mine:
                     r.ev.set()
         except Exception:  # a broken group: every waiter learns it at once (missing shards -> degraded)
-            log.exception("collective shard transport: round failed; rounds stop")
+            log.exception("collective shard transport: round failed; later rounds go to the fallback transport")
             with self._cv:
+                self._broken = True
                 pending, self._q = self._q, []
             for r in pending:
                 r.ev.set()
@@ -249,6 +273,86 @@ class CollectiveShardTransport:
         from .mesh import run_reads
 
         return run_reads(self.store, items, self.stats)
+
+    def _prune_searches(self, allreq, results: dict) -> dict:
+        """C3 of the round's plain searches as one tensor collective: every shard's per-query top-k SCORES
+        ([rows, K] fp32, -inf padded; rows = every plain-search query row of the round in request order,
+        the same layout on every rank since every rank holds every request) are all-gathered; each rank
+        then computes, for every row, the global top-k over the shards other than the row's origin (the
+        origin merges its own shard locally) -- identically on every rank (stable sort by score, ties by
+        shard, then position) -- and sends back only ITS winning hits.  Without this every shard returned k
+        hits per query, (W - 1) k per query to merge at the origin; now at most k travel in total.  The
+        score exchange is a device all-gather on RCCL (host gloo on one shared card)."""
+        import numpy as np
+
+        g = self.group
+        layout = []
+        for o, items in enumerate(allreq):
+            for rid, scope, op, payload in items or ():
+                if op == "search":
+                    Q, k, _ = payload
+                    q = np.asarray(Q)
+                    layout.append((o, rid, 1 if q.ndim == 1 else int(q.shape[0]), int(k)))
+        if not layout:
+            return results
+        R = sum(x[2] for x in layout)
+        K = max(1, max(x[3] for x in layout))
+        # the score exchange is one more collective in the round: it pays when the candidates it keeps off
+        # the answer exchange are many (decided from the gathered requests, so identically on every rank)
+        if R * K * (g.size - 1) < self.prune_min:
+            return results
+        row0, r = {}, 0
+        for o, rid, nq, _ in layout:
+            row0[(o, rid)] = r
+            r += nq
+        S = torch.full((R, K), float("-inf"), dtype=torch.float32)
+        for src, res in results.items():
+            for rid, ok, val in res:
+                base = row0.get((src, rid))
+                if base is None or not ok or not isinstance(val, list):
+                    continue
+                for qi, hits in enumerate(val):
+                    for j, h in enumerate(hits[:K]):
+                        sc = getattr(h, "score", None)
+                        S[base + qi, j] = float(sc) if sc is not None else float("inf")  # unscored: always kept
+        allS = (g.all_gather(S.to(self._cdev)).cpu() if self._cdev.type == "cuda"
+                else _host_gather(g, S)).view(g.size, R, K)
+        self.stats["score_exchanges"] = self.stats.get("score_exchanges", 0) + 1
+        keep = {}  # (origin, rid) -> [per row: set of this shard's winning positions]
+        shard_of = torch.arange(g.size).view(-1, 1).expand(g.size, K).reshape(-1)
+        pos_of = torch.arange(K).view(1, -1).expand(g.size, K).reshape(-1)
+        for o, rid, nq, k in layout:
+            base = row0[(o, rid)]
+            cand = allS[:, base:base + nq, :].clone()  # [W, nq, K]
+            cand[o] = float("-inf")  # the origin's own shard is merged at the origin
+            flat = cand.permute(1, 0, 2).reshape(nq, g.size * K)
+            order = torch.sort(-flat, dim=1, stable=True).indices[:, :k]
+            rows = []
+            for qi in range(nq):
+                idx = order[qi]
+                ok = flat[qi, idx] > float("-inf")
+                sel = idx[ok & (shard_of[idx] == self.rank)]
+                rows.append(set(pos_of[sel].tolist()))
+            keep[(o, rid)] = rows
+        sent = pruned = 0
+        out = {}
+        for src, res in results.items():
+            new = []
+            for rid, ok, val in res:
+                rows = keep.get((src, rid))
+                if rows is not None and ok and isinstance(val, list):
+                    kept = [[h for j, h in enumerate(hits) if qi < len(rows) and j in rows[qi]]
+                            for qi, hits in enumerate(val)]
+                    n_all = sum(len(h) for h in val)
+                    n_kept = sum(len(h) for h in kept)
+                    sent += n_kept
+                    pruned += n_all - n_kept
+                    val = kept
+                new.append((rid, ok, val))
+            out[src] = new
+        self.stats["hits_sent"] = self.stats.get("hits_sent", 0) + sent
+        self.stats["hits_pruned"] = self.stats.get("hits_pruned", 0) + pruned
+        return out
 
 
 def _own_group(group):

@@ -45,7 +45,10 @@ class _CaptureGuard:
         return getattr(self._tls, kind, 0)
 
     @contextlib.contextmanager
-    def shared(self):
+    def shared(self, urgent: bool = False):
+        """``urgent``: enter while a capture is only WAITING (not running).  For a thread other shared
+        holders depend on -- the shard-round thread: a job thread holds the guard while it waits for a round's
+        answer, and that round must not queue behind a capture that waits for the job thread."""
         if self._depth("ex") or self._depth("sh"):
             self._tls.sh = self._depth("sh") + 1
             try:
@@ -54,7 +57,7 @@ class _CaptureGuard:
                 self._tls.sh -= 1
             return
         with self._cond:
-            while self._writer is not None or self._waiting:
+            while self._writer is not None or (self._waiting and not urgent):
                 self._cond.wait()
             self._readers += 1
         self._tls.sh = 1
@@ -114,9 +117,9 @@ def gpu_guard():
     return _GUARD.exclusive()
 
 
-def gpu_shared():
-    """Shared section (may synchronise; must not overlap a capture)."""
-    return _GUARD.shared()
+def gpu_shared(urgent: bool = False):
+    """Shared section (may synchronise; must not overlap a capture).  ``urgent``: see _CaptureGuard.shared."""
+    return _GUARD.shared(urgent)
 
 
 def guarded(fn):

@@ -110,6 +110,9 @@ def _check(rank, world, device="cpu", ipc=False, n_rows=300):
         if name == "collective":
             out["concurrent_ok"] = not errs and not bad
             out["busy_rounds"] = coll.stats["busy_rounds"] - b0
+            # the 32 fan-outs' rounds are big enough for the score exchange (C3 as a tensor all-gather): each
+            # query got back at most k = 5 hits in total from the other shards, not 5 per shard
+            out["pruned"] = {k: coll.stats.get(k, 0) for k in ("score_exchanges", "hits_sent", "hits_pruned")}
     # round latency of each transport (sequential single-query fan-outs)
     lat = {}
     for name, st in (("mesh", via_mesh), ("collective", via_coll)):
@@ -139,6 +142,10 @@ def test_collective_transport_matches_flat_and_mesh_cpu():
         assert o["busy_rounds"] < 32, o["busy_rounds"]  # 32 fan-outs shared rounds
         assert o["closed"]
         assert o["stats"]["degraded_rounds"] == 0 and o["stats"]["served"] > 0
+        p = o["pruned"]
+        assert p["score_exchanges"] >= 1 and p["hits_pruned"] > 0, p
+        # 3 ranks x 32 single-query fan-outs, k = 5: at most 5 winners per query leave the other two shards
+        assert p["hits_sent"] <= 5 * 32 * 2, p
         print(f"replica {r}: round p50 mesh {o['p50_ms']['mesh']:.3f} ms, collective "
               f"{o['p50_ms']['collective']:.3f} ms; 32 concurrent fan-outs in {o['busy_rounds']} rounds")
 
