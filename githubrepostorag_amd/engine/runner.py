@@ -102,6 +102,7 @@ class EngineRunner:
     #          cost 4-6 % jobs/s; the paced form is measured in docs/STATUS.md (round 4).
     ARRIVAL_RECENT_S = 0.05
     PACE_HOLD_S = float(os.environ.get("GRAG_PACE_HOLD_S", "0.5"))
+    BULK_RECENT_S = 5.0
     _AW = os.environ.get("GRAG_ARRIVAL_WINDOW", "auto")
     ARRIVAL_WINDOW = -1 if _AW == "auto" else int(_AW)
     MAX_WINDOW = 8
@@ -141,6 +142,7 @@ class EngineRunner:
         self._ar_failed = False
         self._expecting = 0  # admission hints in flight (arrival())
         self._gap = None      # EWMA of the gap between arrival events (s)
+        self._last_bulk = -1e9  # last submit of bulk (non-interactive) work: the pacing hold applies beside it
         self._last_event = -1e9
         self._step_s = None   # EWMA of one decode step's time (s), from the replays
         self.ctrl_stats = {"iterations": 0, "bytes": 0, "payloads": 0}
@@ -174,6 +176,8 @@ class EngineRunner:
         with self._cv:
             self._handles[rid] = h
             self._pending.append((rid, prompt, params, on_token))
+            if not interactive:
+                self._last_bulk = time.monotonic()
             if interactive:
                 now = time.monotonic()
                 self._last_submit = now
@@ -210,19 +214,38 @@ class EngineRunner:
         if self.ARRIVAL_WINDOW > 0:
             return self.ARRIVAL_WINDOW if now - self._last_submit < self.ARRIVAL_RECENT_S else None
         g, d = self._gap, self._step_s
-        if g is None or d is None or now - self._last_event > max(2 * g, self.PACE_HOLD_S):
+        if g is None or d is None or now - self._last_event > max(2 * g, self._hold(now)):
             return None
         return max(1, min(self.MAX_WINDOW, int(0.5 * g / d)))
 
     def _prefill_budget(self) -> tuple[int | None, int | None]:
         """This step's (prefill token cap, bulk share of it): the interactive budget while arrivals are
-        pending or paced, and then at most BULK_PREFILL tokens of it for bulk requests."""
+        pending or paced (within two mean gaps of the last), and at most BULK_PREFILL tokens of bulk work
+        for PACE_HOLD_S beyond that too -- the bulk cap (and the scheduler's interactive reserve) only holds
+        back ingest, while the interactive cap also splits a saturating closed loop's prefill into smaller
+        steps (measured: -10 % queries/s when it was held as long, profiles/pace_hold_ab_r6.json).  The hold applies
+        only beside bulk work (_hold)."""
         if not self.interactive_prefill or self.tp is not None:
             return None, None
         g = self._gap
-        if self._expecting > 0 or (g is not None and time.monotonic() - self._last_event <= max(2 * g, self.PACE_HOLD_S)):
+        if self._expecting > 0:
             return self.interactive_prefill, (self.bulk_prefill or None)
+        if g is None:
+            return None, None
+        now = time.monotonic()
+        quiet = now - self._last_event
+        if quiet <= 2 * g:
+            return self.interactive_prefill, (self.bulk_prefill or None)
+        if quiet <= self._hold(now) and self.bulk_prefill:
+            return None, self.bulk_prefill
         return None, None
+
+    def _hold(self, now: float) -> float:
+        """PACE_HOLD_S while bulk work shares the engine (a bulk submit within BULK_RECENT_S), else 0: with
+        only interactive traffic (a saturating closed loop, whose arrivals come in bursts at window ends)
+        the hold would shorten decode windows for nothing -- measured -7 % queries/s
+        (profiles/pace_hold_ab_r6.json)."""
+        return self.PACE_HOLD_S if now - self._last_bulk < self.BULK_RECENT_S else 0.0
 
     def generate(self, prompt, params: SamplingParams | None = None, on_token=None,
                  timeout: float | None = None) -> Completion:
