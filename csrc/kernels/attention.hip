@@ -51,6 +51,14 @@ struct AttnParams {
   int causal;
   int nblocks;  // KV blocks in the cache: the index guard's bound for block-table entries (common.h)
   int xcd_group;  // decode: consecutive sequences of one (kv head, split) run on one XCD (g_decode_xcd)
+  // shared-prefix decode (paged_decode_prefix_kernel): batch rows [grp_start[g], grp_start[g + 1]) share
+  // their first pre_len[row] keys (whole KV blocks, one set of block ids); null pre_len = no sharing
+  const int32_t* pre_len;    // [nseq]
+  const int32_t* grp_start;  // [ngroups, 2]: (first row, end row) of each group
+  float* pre_o;              // [pre planes, T, Hq, D]: the prefix parts' unnormalised O
+  float* pre_ml;             // [pre planes, T, Hq, 2]: their (m, l)
+  int pre_nsplit;            // prefix parts per group (the prefix kernel's grid z; planes of pre_o / pre_ml)
+  int pre_min_part;          // shortest prefix part (keys, a multiple of 32)
 };
 
 // grag_attn_decode_xcd(1): decode workgroups remapped so that sequences adjacent in the batch run on the same
@@ -630,6 +638,50 @@ __global__ __launch_bounds__(64 * NW) void attn_prefill_kernel(AttnParams p) {
   }
 }
 
+// Keys per part of a P-key shared prefix (paged_decode_prefix_kernel's split of it; the merges' plane count)
+__device__ __forceinline__ int prefix_part(const AttnParams& p, int P) {
+  const int part = (((P + p.pre_nsplit - 1) / p.pre_nsplit) + 31) & ~31;
+  return max(part, p.pre_min_part);
+}
+
+// Keys [0, pre) of decode row `seq` that a shared-prefix part covers (paged_decode_prefix_kernel); 0 without
+// sharing.  A value outside [0, ctx) is reported and treated as 0: the row then attends to all its keys
+// itself and merges nothing, which is still the exact result.
+__device__ __forceinline__ int prefix_of(const AttnParams& p, int seq, int ctx) {
+  if (p.pre_len == nullptr) return 0;
+  const int pre = p.pre_len[seq];
+  return (pre == 0 || index_ok(pre, ctx, ERR_PREFIX_GROUP)) ? pre : 0;
+}
+
+// Merge the prefix parts of (tok, head) into a decode wave's running state (m, l, O) -- lane (li, h4) holds
+// O[16 n + 4 h4 + r], the layout the prefix kernel wrote its parts in.  m stays the reference of l and O.
+template <int D>
+__device__ __forceinline__ void merge_prefix(const AttnParams& p, int tok, int head, int pre, int h4, float& m,
+                                             float& l, f32x4_t (&o)[D / 16]) {
+  constexpr int ND = D / 16;
+  const int part = prefix_part(p, pre);
+  const int nv = (pre + part - 1) / part;
+  float M = m;
+  for (int s = 0; s < nv; ++s) M = fmaxf(M, p.pre_ml[(((size_t)s * p.total_q + tok) * p.Hq + head) * 2]);
+  if (M == -INFINITY) return;
+  const float a = exp2f(m - M);
+  l *= a;
+#pragma unroll
+  for (int n = 0; n < ND; ++n) o[n] *= a;
+  for (int s = 0; s < nv; ++s) {
+    const size_t base = ((size_t)s * p.total_q + tok) * p.Hq + head;
+    const float w = exp2f(p.pre_ml[base * 2] - M);
+    l += p.pre_ml[base * 2 + 1] * w;
+    const float* po = p.pre_o + base * D + 4 * h4;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+      const float4 v = *reinterpret_cast<const float4*>(po + 16 * n);
+      o[n] += f32x4_t{v.x, v.y, v.z, v.w} * w;
+    }
+  }
+  m = M;
+}
+
 // ---------------------------------------------------------------------------
 // Decode (q_len == 1) specialisation: one wave per (sequence, kv head, split).
 // The GQA group's G <= 16 query heads are the 16 MFMA columns.  K/V tiles are
@@ -675,7 +727,8 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
     split = lg / (nseq * gridDim.y);
   }
   const int ctx = p.ctx_len[seq];
-  const int kv_lo = split * p.split_len;
+  const int pre = prefix_of(p, seq, ctx);  // keys a shared-prefix part already covered (0: none)
+  const int kv_lo = pre + split * p.split_len;
   const int kv_hi = min(ctx, kv_lo + p.split_len);
   if (kv_lo >= kv_hi) return;
   const int G = p.G;
@@ -841,6 +894,7 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
       pm[1] = lsum;
     }
   } else {
+    if (pre > 0) merge_prefix<D>(p, tok, head, pre, h4, m, lsum, o);
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     bf16* op = p.out + (size_t)tok * p.out_stride + (size_t)head * D;
 #pragma unroll
@@ -853,16 +907,21 @@ __global__ __launch_bounds__(64) void paged_decode_kernel(AttnParams p) {
   }
 }
 
-// Combine split-KV partials of decode (q_len == 1 per sequence: token == seq).
+// Combine split-KV partials of decode (q_len == 1 per sequence: token == seq), and the shared-prefix parts
+// of a sequence whose first keys paged_decode_prefix_kernel covered.
 template <int D>
 __global__ __launch_bounds__(D) void attn_combine_kernel(AttnParams p) {
   const int tok = blockIdx.x, head = blockIdx.y, d = threadIdx.x;
   const int ctx = p.ctx_len[tok];
-  int nvalid = (ctx + p.split_len - 1) / p.split_len;
+  const int pre = prefix_of(p, tok, ctx);
+  int nvalid = (ctx - pre + p.split_len - 1) / p.split_len;
   nvalid = max(1, min(nvalid, p.num_splits));
+  const int npre = pre > 0 ? (pre + prefix_part(p, pre) - 1) / prefix_part(p, pre) : 0;
   float M = -INFINITY;
   for (int s = 0; s < nvalid; ++s)
     M = fmaxf(M, p.part_ml[(((size_t)s * p.total_q + tok) * p.Hq + head) * 2]);
+  for (int s = 0; s < npre; ++s)
+    M = fmaxf(M, p.pre_ml[(((size_t)s * p.total_q + tok) * p.Hq + head) * 2]);
   const float Mu = M == -INFINITY ? 0.f : M;
   float L = 0.f, acc = 0.f;
   for (int s = 0; s < nvalid; ++s) {
@@ -871,7 +930,216 @@ __global__ __launch_bounds__(D) void attn_combine_kernel(AttnParams p) {
     L += p.part_ml[base * 2 + 1] * w;
     acc += p.part_o[base * D + d] * w;
   }
+  for (int s = 0; s < npre; ++s) {
+    const size_t base = ((size_t)s * p.total_q + tok) * p.Hq + head;
+    const float w = exp2f(p.pre_ml[base * 2] - Mu);
+    L += p.pre_ml[base * 2 + 1] * w;
+    acc += p.pre_o[base * D + d] * w;
+  }
   p.out[(size_t)tok * p.out_stride + (size_t)head * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+}
+
+// ---------------------------------------------------------------------------
+// Shared-prefix ("cascade") decode.  Sequences that share a cached prompt prefix -- ingest's summary /
+// title / keyword calls over one chunk, an agent job's calls over the same documents -- hold the SAME KV
+// block ids for it, and the per-sequence decode kernel above would read those blocks once per sequence.
+// Here the batch's rows are grouped (engine: adjacent rows with a common leading run of block ids) and:
+//   1. paged_decode_prefix_kernel: one wave per (group, kv head, prefix part) reads the group's prefix K/V
+//      ONCE and computes every member's G query heads against it: the rows (member, head) are the MFMA
+//      columns, RG row groups of 16 per wave (RG = 2 covers 4 members at GQA 7), each K / V^T fragment read
+//      from LDS feeding RG MFMAs.  It writes per-part (m, l, O) to the prefix planes.
+//   2. the per-sequence decode kernel runs over each row's own keys [pre_len, ctx) only and merges the
+//      prefix planes into its state before normalising (one part), or the combine pass merges them with
+//      the split parts.
+// The math is the decode kernel's (swapped QK^T, exp2 online softmax in the log2 domain, deferred rescale);
+// K/V go through the same 2-stage LDS-DMA ring of 32-key tiles.
+template <int D, int RG>
+__global__ __launch_bounds__(64) void paged_decode_prefix_kernel(AttnParams p) {
+  constexpr int TK = 32, NS = 2;
+  constexpr int NT16 = TK / 16;
+  constexpr int RB = 2 * D;
+  constexpr int CPR = D / 8;
+  constexpr int NC = D / 32;
+  constexpr int ND = D / 16;
+  constexpr int TILE = TK * RB;
+  constexpr int NI = TILE / 1024;
+  constexpr int RPI = 1024 / RB;
+  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * TILE];
+
+  const int lane = threadIdx.x;
+  const int h4 = lane >> 4, li = lane & 15;
+  const int grp = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
+  const int r0 = p.grp_start[2 * grp], r1 = p.grp_start[2 * grp + 1];
+  if (r1 - r0 < 2) return;  // padding pair (or a lone row: the per-sequence kernel covers it)
+  if (!index_ok(r0, p.total_q, ERR_PREFIX_GROUP) || !index_ok(r1, p.total_q + 1, ERR_PREFIX_GROUP)) return;
+  const int nmem = r1 - r0;
+  const int P = p.pre_len[r0];
+  if (P <= 0 || !index_ok(P, p.ctx_len[r0], ERR_PREFIX_GROUP)) return;
+  const int part = prefix_part(p, P);
+  const int kv_lo = split * part;
+  const int kv_hi = min(P, kv_lo + part);
+  if (kv_lo >= kv_hi) return;
+  const int G = p.G;
+
+  // column li of row group j is the pair (member, head) = divmod(16 j + li, G)
+  bf16x8_t qf[RG][NC];
+  int tok[RG], head[RG];
+  bool valid[RG];
+#pragma unroll
+  for (int j = 0; j < RG; ++j) {
+    const int row = 16 * j + li;
+    const int mem = row / G;
+    valid[j] = mem < nmem;
+    tok[j] = p.q_start[r0 + (valid[j] ? mem : 0)];
+    head[j] = kvh * G + (valid[j] ? row % G : 0);
+    if (valid[j] && h4 == 0 && kvh == 0 && split == 0 && row % G == 0 && p.pre_len[r0 + mem] != P)
+      report_index_error(ERR_PREFIX_GROUP, r0 + mem);  // a member whose merge would read other planes
+    const bf16* qp = p.q + (size_t)tok[j] * p.q_stride + (size_t)head[j] * D + 8 * h4;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) qf[j][c] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * c);
+  }
+  const int32_t* bt = p.block_tables + (size_t)r0 * p.bt_stride;  // the leader's ids cover the prefix
+  const int lrow = lane / CPR, lch = lane % CPR;
+  const int nblk = (P + p.BS - 1) / p.BS;
+  int win = (kv_lo / p.BS) >> 6;
+  int bvec = bt[min((win << 6) + lane, nblk - 1)];
+  if (!index_ok(bvec, p.nblocks, ERR_BLOCK_DECODE)) bvec = 0;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): Q and block ids retired before the counted DMA pipeline
+#pragma unroll
+  for (int j = 0; j < RG; ++j)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(qf[j][c]));
+  asm volatile("" : "+v"(bvec));
+
+  auto issue = [&](int kt0, int stage) {
+    char* kdst = smem + stage * 2 * TILE;
+    char* vdst = kdst + TILE;
+    const int w = (kt0 / p.BS) >> 6;
+    if (w != win) {
+      win = w;
+      bvec = bt[min((w << 6) + lane, nblk - 1)];
+      if (!index_ok(bvec, p.nblocks, ERR_BLOCK_DECODE)) bvec = 0;
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int key0 = min(kt0 + i * RPI, P - 1);
+      const int blk = __builtin_amdgcn_readlane(bvec, (key0 / p.BS) & 63);
+      const int row = i * RPI + lrow;
+      const int key = min(kt0 + row, P - 1);
+      const size_t off = (((size_t)blk * p.Hkv + kvh) * p.BS + (key % p.BS)) * D;
+      glds16(p.k + off + ((lch ^ kswz<D>(row)) << 3), kdst + i * 1024);
+      glds16(p.v + off + ((lch ^ vswz<D>(row)) << 3), vdst + i * 1024);
+    }
+  };
+
+  float m[RG], lsum[RG];
+  f32x4_t o[RG][ND];
+#pragma unroll
+  for (int j = 0; j < RG; ++j) {
+    m[j] = -INFINITY;
+    lsum[j] = 0.f;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) o[j][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  const int ntiles = (kv_hi - kv_lo + TK - 1) / TK;
+  issue(kv_lo, 0);
+  for (int t = 0; t < ntiles; ++t) {
+    const int stage = t & 1;
+    const int kt0 = kv_lo + t * TK;
+    if (t + 1 < ntiles) {
+      issue(kt0 + TK, stage ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");  // tile t landed, t + 1 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const char* k_lds = smem + stage * 2 * TILE;
+    const char* v_lds = k_lds + TILE;
+    f32x4_t s[RG][NT16];
+#pragma unroll
+    for (int tt = 0; tt < NT16; ++tt) {
+#pragma unroll
+      for (int j = 0; j < RG; ++j) s[j][tt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int row = 16 * tt + li;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const bf16x8_t a =
+            *reinterpret_cast<const bf16x8_t*>(k_lds + row * RB + (((4 * c + h4) ^ kswz<D>(row)) << 4));
+#pragma unroll
+        for (int j = 0; j < RG; ++j) s[j][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[j][c], s[j][tt], 0, 0, 0);
+      }
+    }
+    if (kt0 + TK > kv_hi) {  // the part's last tile only
+      asm volatile("");
+#pragma unroll
+      for (int j = 0; j < RG; ++j)
+#pragma unroll
+        for (int tt = 0; tt < NT16; ++tt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kt0 + 16 * tt + 4 * h4 + r;
+            s[j][tt][r] = key >= kv_hi ? -INFINITY : s[j][tt][r];
+          }
+    }
+    bf16x8_t bp[RG];
+#pragma unroll
+    for (int j = 0; j < RG; ++j) {
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int tt = 0; tt < NT16; ++tt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[j][tt][r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float m_cand = fmaxf(m[j], tmax * p.scale_log2);
+      if (__any(m_cand > m[j] + kRescaleLog2)) {
+        const float m_use = m_cand == -INFINITY ? 0.f : m_cand;
+        const float alpha = exp2f(m[j] - m_use);
+        m[j] = m_cand;
+        lsum[j] *= alpha;
+#pragma unroll
+        for (int n = 0; n < ND; ++n) o[j][n] *= alpha;
+      }
+      const float nm = m[j] == -INFINITY ? 0.f : -m[j];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][0][r], p.scale_log2, nm));
+        const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][1][r], p.scale_log2, nm));
+        lsum[j] += p0 + p1;
+        bp[j][r] = f2bits(p0);
+        bp[j][4 + r] = f2bits(p1);
+      }
+    }
+    const int tq = li >> 2, tp = li & 3;
+    const int rr0 = 4 * h4 + tq, rr1 = rr0 + 16;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+      const int unit = 4 * n + tp;
+      const int b0 = rr0 * RB + ((unit ^ (vswz<D>(rr0) << 1)) << 3);
+      const int b1 = rr1 * RB + ((unit ^ (vswz<D>(rr1) << 1)) << 3);
+      const bf16x4_t a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(v_lds + b0));
+      const bf16x4_t a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(v_lds + b1));
+      const bf16x8_t a = bf16x8_t{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+#pragma unroll
+      for (int j = 0; j < RG; ++j) o[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bp[j], o[j][n], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this stage's LDS reads done before its refill
+  }
+#pragma unroll
+  for (int j = 0; j < RG; ++j) {
+    float l = lsum[j];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (!valid[j]) continue;
+    const size_t base = ((size_t)split * p.total_q + tok[j]) * p.Hq + head[j];
+    float* po = p.pre_o + base * D;
+#pragma unroll
+    for (int n = 0; n < ND; ++n)
+      *reinterpret_cast<float4*>(po + 16 * n + 4 * h4) = make_float4(o[j][n][0], o[j][n][1], o[j][n][2], o[j][n][3]);
+    if (h4 == 0) {
+      p.pre_ml[base * 2] = m[j];
+      p.pre_ml[base * 2 + 1] = l;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1204,6 +1472,16 @@ int launch_decode(const AttnParams& prm_in, int nseq, int tk, int ns, bool nt, h
 }
 
 template <int D>
+int launch_decode_prefix(const AttnParams& prm, int ngroups, int pre_nsplit, int rg, hipStream_t stream) {
+  dim3 grid(ngroups, prm.Hkv, pre_nsplit);
+  if (rg == 4)
+    paged_decode_prefix_kernel<D, 4><<<grid, 64, 0, stream>>>(prm);
+  else
+    paged_decode_prefix_kernel<D, 2><<<grid, 64, 0, stream>>>(prm);
+  return (int)hipGetLastError();
+}
+
+template <int D>
 int launch_prefill(const AttnParams& prm, int nseq, int nw, hipStream_t stream) {
   dim3 grid(nseq * prm.tiles_per_seq, prm.Hkv, 1);
   if (nw == 6)
@@ -1293,6 +1571,70 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
     case 32: return dispatch_nw<32>(prm, nseq, nw, true, stream);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// Shared-prefix decode (q_len == 1): paged_decode_prefix_kernel over the groups' common prefixes, then the
+// per-sequence decode kernel (nw 1 / 3 / 7 / 8 / 11 / 12 as grag_paged_attention) over each row's own keys
+// [pre_len, ctx), merging the prefix parts.  pre_len [nseq]: keys shared (0 = none; every row of a group
+// holds its group's value); grp_start [ngroups, 2]: (first row, end row) of each group of adjacent rows
+// (pairs spanning < 2 rows are padding); rows of one group share their first pre_len block-table entries.  pre_o / pre_ml:
+// [pre_nsplit, total_q, Hq, D | 2] f32: a group's prefix of P keys is cut into parts of
+// max(pre_min_part, ceil(P / pre_nsplit) rounded up to 32) keys, so one launch shape serves every prefix
+// length (longer prefixes get longer parts, short ones fewer parts).  rg = 2 or 4
+// row groups of 16 (member, head) pairs per wave: a group has at most 16 * rg / G members.
+GRAG_API int grag_paged_decode_cascade(const void* q, int q_stride, const void* k_cache, const void* v_cache,
+                                       void* out, int out_stride, const int32_t* block_tables, int bt_stride,
+                                       const int32_t* q_start, const int32_t* ctx_len, int nseq, int total_q,
+                                       int Hq, int Hkv, int D, int BS, float scale, int num_splits, int split_len,
+                                       float* part_o, float* part_ml, int nw, int nblocks, const int32_t* pre_len,
+                                       const int32_t* grp_start, int ngroups, int pre_nsplit, int pre_min_part,
+                                       float* pre_o, float* pre_ml, int rg, hipStream_t stream) {
+  if (nseq <= 0) return 0;
+  if (Hq % Hkv != 0 || Hq / Hkv > 16 || BS <= 0 || BS % 16 != 0 || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
+  if (!(nw == 1 || nw == 3 || nw == 7 || nw == 8 || nw == 11 || nw == 12)) return (int)hipErrorInvalidValue;
+  if (num_splits < 1) num_splits = 1;
+  if (num_splits > 1 && (!part_o || !part_ml || split_len % KT != 0)) return (int)hipErrorInvalidValue;
+  if (!pre_len || !grp_start || !pre_o || !pre_ml || ngroups < 0 || pre_nsplit < 1 || pre_min_part <= 0 ||
+      pre_min_part % 32 != 0 || (rg != 2 && rg != 4) || 2 * (Hq / Hkv) > 16 * rg)
+    return (int)hipErrorInvalidValue;
+  AttnParams prm{};
+  prm.q = (const bf16*)q;
+  prm.k = (const bf16*)k_cache;
+  prm.v = (const bf16*)v_cache;
+  prm.out = (bf16*)out;
+  prm.part_o = part_o;
+  prm.part_ml = part_ml;
+  prm.block_tables = block_tables;
+  prm.q_start = q_start;
+  prm.ctx_len = ctx_len;
+  prm.q_stride = q_stride;
+  prm.out_stride = out_stride;
+  prm.Hq = Hq;
+  prm.Hkv = Hkv;
+  prm.G = Hq / Hkv;
+  prm.BS = BS;
+  prm.bt_stride = bt_stride;
+  prm.tiles_per_seq = 1;
+  prm.num_splits = num_splits;
+  prm.split_len = num_splits > 1 ? split_len : (1 << 30);
+  prm.total_q = total_q;
+  prm.scale_log2 = scale * 1.4426950408889634f;
+  prm.causal = 1;
+  prm.nblocks = nblocks;
+  prm.pre_len = pre_len;
+  prm.grp_start = grp_start;
+  prm.pre_o = pre_o;
+  prm.pre_ml = pre_ml;
+  prm.pre_nsplit = pre_nsplit;
+  prm.pre_min_part = pre_min_part;
+  int err = 0;
+  if (ngroups > 0)
+    err = D == 128 ? launch_decode_prefix<128>(prm, ngroups, pre_nsplit, rg, stream)
+                   : launch_decode_prefix<64>(prm, ngroups, pre_nsplit, rg, stream);
+  if (err) return err;
+  const int tk = nw == 1 ? 64 : 32, ns = nw == 7 ? 4 : (nw == 8 || nw == 12) ? 3 : 2;
+  return D == 128 ? launch_decode<128>(prm, nseq, tk, ns, nw >= 11, stream)
+                  : launch_decode<64>(prm, nseq, tk, ns, nw >= 11, stream);
 }
 
 // Decode workgroup placement for later launches (1: sequences adjacent in the batch on one XCD, 0: the

@@ -112,6 +112,7 @@ enum : unsigned {
   ERR_SAMPLER_SLOT = 1u << 6,  // sampler / seen-bit row >= sampler slots
   ERR_TOPK_ROW = 1u << 7,      // top-k merge / IVF scan: candidate row or list range out of range
   ERR_BERT_TOKEN = 1u << 8,    // encoder embedding: token / position id out of range
+  ERR_PREFIX_GROUP = 1u << 9,  // shared-prefix decode: group row range or prefix length out of range
 };
 
 static __device__ unsigned* g_err_block = nullptr;  // [0] codes (OR), [1] last bad value, [2] count, [3] code of [1]

@@ -30,7 +30,8 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from ..ops.attention import KV_TILE, AttnMetadata
+from ..ops.attention import (CASCADE_MIN, CASCADE_MIN_PART, CASCADE_PARTS, CASCADE_RG, KV_TILE, AttnMetadata, Cascade,
+                             prefix_groups)
 from ..ops._lib import check_device_errors
 from ..ops.gemm import WS
 from ..ops.sampling import SamplerState, reset_slots, sample, sample_tp
@@ -74,6 +75,9 @@ class EngineConfig:
     # (engine/scheduler.py Scheduler reserve): a query beside ingest waves is admitted at the next step
     interactive_reserve_seqs: int = 16
     interactive_reserve_tokens: int = 16384
+    # shared-prefix decode attention (ops/attention.prefix_groups, csrc/kernels/attention.hip
+    # paged_decode_prefix_kernel): decode rows that share cached prompt blocks read them once per group
+    cascade_decode: bool = __import__("os").environ.get("GRAG_CASCADE", "1") == "1"
 
 
 def _split_len_for(batch: int) -> int:
@@ -156,6 +160,7 @@ class LLMEngine:
         self._graphs: dict[tuple, _DecodeGraph] = {}
         self._graph_pool = None
         self._static = None
+        self._cascade_plan = 0
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "prefill_s": 0.0, "decode_s": 0.0, "steps": 0,
                       "graph_replays": 0, "graph_captures": 0, "decode_steps": 0, "decode_wait_s": 0.0,
                       "step_s": 0.0, "mixed_steps": 0,
@@ -164,7 +169,10 @@ class LLMEngine:
                       "host_prefill_sample_s": 0.0, "host_prefill_post_s": 0.0, "host_decode_prep_s": 0.0,
                       "host_decode_post_s": 0.0, "capture_s": 0.0,
                       # prompt tokens submitted / taken from the prefix cache at admission (the rest is prefill)
-                      "prompt_tokens": 0, "prefix_hit_tokens": 0}
+                      "prompt_tokens": 0, "prefix_hit_tokens": 0,
+                      # shared-prefix decode: windows that took it, rows in groups, K/V keys not re-read (of
+                      # decode_keys: the context keys of the batches it was considered for)
+                      "cascade_windows": 0, "cascade_rows": 0, "cascade_saved_keys": 0, "decode_keys": 0}
         # optional per-step timeline (a list; None = off): (t_start, kind, rows, tokens, seconds) per step,
         # kind "prefill" / "decode" / "mixed" / "capture" — the ingest critical-path trace reads it
         self.trace: list | None = None
@@ -181,6 +189,10 @@ class LLMEngine:
             hq, d = model.hq, model.head_dim
             self._part_o = torch.empty(max_split * self._max_b * hq * d, dtype=torch.float32, device=self.device)
             self._part_ml = torch.empty(max_split * self._max_b * hq * 2, dtype=torch.float32, device=self.device)
+            if cfg.cascade_decode:  # prefix parts of the shared-prefix decode
+                npre = CASCADE_PARTS
+                self._pre_o = torch.empty(npre * self._max_b * hq * d, dtype=torch.float32, device=self.device)
+                self._pre_ml = torch.empty(npre * self._max_b * hq * 2, dtype=torch.float32, device=self.device)
             # sampler scratch for the largest decode batch up front: graphs captured later all see one buffer
             self.sampler.workspace(self._max_b)
             from ..ops.attention import decode_counters  # small-batch decode tickets: before any capture
@@ -483,6 +495,7 @@ class LLMEngine:
         d_ctx = dec[o:o + n_dec]; o += n_dec
         d_samp = dec[o:o + n_dec]; o += n_dec
         o += n_dec + 1  # q_start 0..n_dec
+        o += n_dec + 2 * (n_dec // 2)  # shared-prefix layout (not used by mixed steps)
         d_bt = dec[o:]
         # rows to sample: the last token of every prefill chunk that completes its prompt, then every decode row
         done = [i for i, (s, a, b) in enumerate(pitems) if b == s.total_len]
@@ -558,13 +571,15 @@ class LLMEngine:
     def _last_id(s: Sequence) -> int:
         return s.output_ids[-1] if s.output_ids else s.prompt_ids[-1]
 
-    def _decode_inputs(self, seqs, B: int, width: int, K: int = 1) -> np.ndarray:
+    def _decode_inputs(self, seqs, B: int, width: int, K: int = 1, groups: bool = False) -> np.ndarray:
         """Packed int32 control buffer for a K-step decode window:
-        ids[B] | pos[K,B] | slot[K,B] | ctx[K,B] | sampler slots[B] | q_start[B+1] | block table[B,width].
-        Rows >= len(seqs) are padding (scratch slot, slot mapping -1)."""
+        ids[B] | pos[K,B] | slot[K,B] | ctx[K,B] | sampler slots[B] | q_start[B+1] | pre[B] | groups[B//2,2] |
+        block table[B,width].  Rows >= len(seqs) are padding (scratch slot, slot mapping -1).  pre / groups:
+        the shared-prefix decode layout (ops/attention.prefix_groups) when ``groups`` and the batch's rows
+        share enough cached prefix (self._cascade_plan holds its prefix-part count, 0 = none), else zeros."""
         n = len(seqs)
         bs = self.cfg.block_size
-        buf = np.empty(B * (3 * K + 3) + 1 + B * width, dtype=np.int32)
+        buf = np.empty(B * (3 * K + 3) + 1 + B + 2 * (B // 2) + B * width, dtype=np.int32)
         o = 0
         ids = buf[o:o + B]; o += B
         pos = buf[o:o + K * B].reshape(K, B); o += K * B
@@ -572,6 +587,11 @@ class LLMEngine:
         ctx = buf[o:o + K * B].reshape(K, B); o += K * B
         sl = buf[o:o + B]; o += B
         buf[o:o + B + 1] = np.arange(B + 1, dtype=np.int32); o += B + 1
+        pre = buf[o:o + B]; o += B
+        grp = buf[o:o + 2 * (B // 2)].reshape(B // 2, 2); o += 2 * (B // 2)
+        pre.fill(0)
+        grp.fill(0)
+        self._cascade_plan = 0
         bt = buf[o:].reshape(B, width)
         bt[n:].fill(0)
         ids[n:] = 0
@@ -615,7 +635,27 @@ class LLMEngine:
             pos[:, :n] = p
             ctx[:, :n] = p + 1
             slot[:, :n] = bt[np.arange(n)[None, :], p // bs].astype(np.int64) * bs + p % bs
+            if groups and n >= 4:
+                self._plan_cascade(bt[:n], L, pre, grp)
         return buf
+
+    def _plan_cascade(self, bt, L, pre, grp) -> None:
+        """Fill the shared-prefix layout of one decode window when its groups save at least CASCADE_MIN of
+        the batch's K/V keys (a group's prefix is read once instead of once per member)."""
+        total = int(L.sum())
+        self.stats["decode_keys"] += total
+        r = prefix_groups(bt, L, self.cfg.block_size, self.model.hq // max(1, self.model.hkv), CASCADE_RG)
+        if r is None:
+            return
+        p, spans, saved = r
+        if saved < CASCADE_MIN * total:
+            return
+        pre[: len(p)] = p
+        grp[: len(spans)] = spans
+        self._cascade_plan = CASCADE_PARTS
+        self.stats["cascade_windows"] += 1
+        self.stats["cascade_rows"] += sum(b - a for a, b in spans)
+        self.stats["cascade_saved_keys"] += saved
 
     def _slot_block_table(self):
         """(table [slots, max blocks], row owner, row length) behind _decode_inputs."""
@@ -634,19 +674,29 @@ class LLMEngine:
             cnt = int(np.prod(shape))
             out[name] = buf[o:o + cnt].view(*shape)
             o += cnt
+        out["pre"] = buf[o:o + B]
+        o += B
+        out["grp"] = buf[o:o + 2 * (B // 2)]
+        o += 2 * (B // 2)
         out["bt"] = buf[o:o + B * width].view(B, width)
         return out
 
-    def _decode_forward(self, v, B, nsplit, split_len, out_tokens, K: int = 1):
-        """K chained decode steps; step j > 0 embeds the ids step j-1 sampled (on device)."""
+    def _decode_forward(self, v, B, nsplit, split_len, out_tokens, K: int = 1, npre: int = 0):
+        """K chained decode steps; step j > 0 embeds the ids step j-1 sampled (on device).  npre > 0: the
+        shared-prefix decode over v["pre"] / v["grp"] with npre prefix parts."""
         hq, d = self.model.hq, self.model.head_dim
         part_o = self._part_o[: nsplit * B * hq * d] if self.on_gpu else None
         part_ml = self._part_ml[: nsplit * B * hq * 2] if self.on_gpu else None
+        cas = None
+        if npre:
+            cas = Cascade(pre_len=v["pre"], grp_start=v["grp"], nsplit=npre, min_part=CASCADE_MIN_PART,
+                          pre_o=self._pre_o[: npre * B * hq * d] if self.on_gpu else None,
+                          pre_ml=self._pre_ml[: npre * B * hq * 2] if self.on_gpu else None, rg=CASCADE_RG)
         for j in range(K):
             ids = v["ids"] if j == 0 else out_tokens[j - 1]
             meta = AttnMetadata(q_start=v["qs"], ctx_len=v["ctx"][j], block_tables=v["bt"], slot_mapping=v["slot"][j],
                                 max_q_len=1, num_seqs=B, num_tokens=B, is_decode=True, num_splits=nsplit,
-                                split_len=split_len, part_o=part_o, part_ml=part_ml)
+                                split_len=split_len, part_o=part_o, part_ml=part_ml, cascade=cas)
             hidden = self.model.forward(ids, v["pos"][j], meta, self.kv_caches)
             self._sample(hidden, v["slots"], out=out_tokens[j])
         return out_tokens
@@ -680,9 +730,15 @@ class LLMEngine:
     def _run_decode(self, seqs, max_window: int | None = None) -> list[Sequence]:
         t0 = time.perf_counter()
         n = len(seqs)
-        if _GROUP_ROWS and n >= 32:
-            # rows that share a cached prompt prefix (ingest's summary / title / keyword calls of one chunk,
-            # the roll-ups over the same content) side by side: with the decode kernel's XCD placement
+        casc = False
+        if self.cfg.cascade_decode and n >= 8 and len({s.blocks[0] for s in seqs if s.blocks}) < n:
+            # some rows share a cached prompt prefix (ingest's summary / title / keyword calls of one chunk, an
+            # agent job's calls over the same documents): rows side by side by leading block ids, so the
+            # shared-prefix decode (ops/attention.prefix_groups) can group adjacent rows
+            seqs = sorted(seqs, key=_prefix_blocks)
+            casc = True
+        elif _GROUP_ROWS and n >= 32:
+            # rows that share a cached prompt prefix side by side: with the decode kernel's XCD placement
             # (csrc/kernels/attention.hip g_decode_xcd) their shared K/V blocks are read on one XCD at about
             # the same time and come from its L2 for all but the first
             seqs = sorted(seqs, key=_prefix_blocks)
@@ -696,10 +752,11 @@ class LLMEngine:
             width = self.max_blocks_per_seq
             B = next(b for b in self.cfg.graph_batch_sizes if b >= n)
             nsplit, split_len = _decode_plan(self.model, B, max_ctx, self.cfg.max_model_len)
-            g = self._graphs.get((B, nsplit, split_len, K, self.sampler.rounds))
+            packed = self._decode_inputs(seqs, B, width, K, groups=casc)
+            npre = self._cascade_plan
+            g = self._graphs.get((B, nsplit, split_len, K, self.sampler.rounds, npre))
             if g is None:
-                g = self._capture(B, nsplit, split_len, K)
-            packed = self._decode_inputs(seqs, B, width, K)
+                g = self._capture(B, nsplit, split_len, K, npre)
             self._static_host[: packed.size] = torch.from_numpy(packed)
             self._static_dev[: packed.size].copy_(self._static_host[: packed.size], non_blocking=True)
             g.graph.replay()
@@ -713,9 +770,10 @@ class LLMEngine:
         else:
             nsplit, split_len = _decode_plan(self.model, n, max_ctx, self.cfg.max_model_len, graph=False)
             width = max(len(s.blocks) for s in seqs)
-            dev = self._to_dev(self._decode_inputs(seqs, n, width, 1))
+            dev = self._to_dev(self._decode_inputs(seqs, n, width, 1, groups=casc))
             out = torch.empty(1, n, dtype=torch.int32, device=self.device)
-            out = self._decode_forward(self._views(dev, n, width, 1), n, nsplit, split_len, out, 1)
+            out = self._decode_forward(self._views(dev, n, width, 1), n, nsplit, split_len, out, 1,
+                                       npre=self._cascade_plan)
             self.model.tp.stage_health()
             toks = out.cpu().numpy()
             check_device_errors("engine step")
@@ -786,17 +844,17 @@ class LLMEngine:
         if self._static is None:
             W = self.max_blocks_per_seq
             Kmax = max(1, self.cfg.decode_window)
-            size = (3 * Kmax + 3) * self._max_b + 1 + self._max_b * W
+            size = (3 * Kmax + 3) * self._max_b + 1 + 2 * self._max_b + self._max_b * W
             self._static_dev = torch.zeros(size, dtype=torch.int32, device=self.device)
             self._static_host = torch.zeros(size, dtype=torch.int32).pin_memory()
             self._static = True
             self._graph_pool = torch.cuda.graph_pool_handle()
 
-    def _capture(self, B, nsplit, split_len, K=1) -> _DecodeGraph:
+    def _capture(self, B, nsplit, split_len, K=1, npre=0) -> _DecodeGraph:
         with WS.owned_by(self._ws):
-            return self._capture_ws(B, nsplit, split_len, K)
+            return self._capture_ws(B, nsplit, split_len, K, npre)
 
-    def _capture_ws(self, B, nsplit, split_len, K=1) -> _DecodeGraph:
+    def _capture_ws(self, B, nsplit, split_len, K=1, npre=0) -> _DecodeGraph:
         t0 = time.perf_counter()
         try:
             # The eager warm-up step of the shape runs real TP collectives (all-reduces, the sampler's
@@ -805,16 +863,16 @@ class LLMEngine:
             # waited on a peer rank could deadlock against a retrieval thread holding the shared guard in a
             # cross-rank search collective on either rank.
             with gpu_shared():
-                prep = self._capture_prepare(B, nsplit, split_len, K)
+                prep = self._capture_prepare(B, nsplit, split_len, K, npre)
             with gpu_guard():  # no other thread may sync / allocate while the capture is open
-                return self._capture_locked(B, nsplit, split_len, K, prep)
+                return self._capture_locked(B, nsplit, split_len, K, prep, npre)
         finally:
             dt = time.perf_counter() - t0
             self.stats["capture_s"] += dt
             if self.trace is not None:
                 self.trace.append((t0, "capture", B, K, dt))
 
-    def _capture_prepare(self, B, nsplit, split_len, K=1):
+    def _capture_prepare(self, B, nsplit, split_len, K=1, npre=0):
         self._ensure_static()
         W = self.max_blocks_per_seq
         # a benign batch: every row is a padding row (scratch block, scratch slot)
@@ -827,28 +885,29 @@ class LLMEngine:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):  # one warm-up step of this shape (every window step has the same shapes)
-            self._decode_forward(v, B, nsplit, split_len, out, 1)
+            self._decode_forward(v, B, nsplit, split_len, out, 1, npre)
         torch.cuda.current_stream().wait_stream(s)
         return v, out, rng_save, seen_save
 
-    def _capture_locked(self, B, nsplit, split_len, K, prep) -> _DecodeGraph:
+    def _capture_locked(self, B, nsplit, split_len, K, prep, npre=0) -> _DecodeGraph:
         v, out, rng_save, seen_save = prep
         graph = torch.cuda.CUDAGraph()
         # thread_local: API / retrieval threads keep launching (and syncing) on
         # their own streams while the engine thread captures
         with no_gc(), torch.cuda.graph(graph, pool=self._graph_pool, capture_error_mode="thread_local"):
-            self._decode_forward(v, B, nsplit, split_len, out, K)
+            self._decode_forward(v, B, nsplit, split_len, out, K, npre)
         torch.cuda.synchronize()
         self.sampler.rng.copy_(rng_save)
         self.sampler.seen[self.scratch_slot].copy_(seen_save)
         g = _DecodeGraph(graph, out, B, nsplit, split_len, K)
         # the sampler's launch chain depends on which sampling features live slots use
-        self._graphs[(B, nsplit, split_len, K, self.sampler.rounds)] = g
+        self._graphs[(B, nsplit, split_len, K, self.sampler.rounds, npre)] = g
         self.stats["graph_captures"] += 1
         return g
 
     @torch.inference_mode()
-    def warmup_graphs(self, batch_sizes=None, max_ctx=2048, windows=(1,), params: SamplingParams | None = None) -> int:
+    def warmup_graphs(self, batch_sizes=None, max_ctx=2048, windows=(1,), params: SamplingParams | None = None,
+                      cascade_parts=(0,)) -> int:
         """Capture the decode graphs a workload will replay ahead of time
         (batch buckets x decode windows K, split plan of ``max_ctx``) so no
         capture lands inside a latency-sensitive step.  Keyed on the
@@ -856,7 +915,9 @@ class LLMEngine:
         serving sampling parameters have been admitted.  Returns the number
         of graphs captured.  ``max_ctx`` may be a list (one split plan per context length).  ``params``:
         capture for the sampler launch chain these sampling parameters select (top-k / top-p rounds)
-        instead of the live slots' (e.g. an ingest engine warmed before its first request)."""
+        instead of the live slots' (e.g. an ingest engine warmed before its first request).  ``cascade_parts``:
+        prefix-part counts of the shared-prefix decode to capture as well (0 = the plain decode graph; batches
+        of >= 8 rows only)."""
         if not (self.on_gpu and self.cfg.use_cuda_graph and getattr(self.model.tp, "capturable", True)):
             return 0
         prev = self.sampler.rounds_override
@@ -868,21 +929,25 @@ class LLMEngine:
             with self._on_stream():
                 n = 0
                 for mc in (max_ctx if isinstance(max_ctx, (list, tuple)) else [max_ctx]):
-                    n += self._warmup_graphs(batch_sizes, mc, windows)
+                    n += self._warmup_graphs(batch_sizes, mc, windows, cascade_parts)
                 return n
         finally:
             self.sampler.rounds_override = prev
 
-    def _warmup_graphs(self, batch_sizes, max_ctx, windows) -> int:
+    def _warmup_graphs(self, batch_sizes, max_ctx, windows, cascade_parts=(0,)) -> int:
         n = 0
+        parts = [c for c in cascade_parts if c == 0 or self.cfg.cascade_decode]
         for B in batch_sizes or self.cfg.graph_batch_sizes:
             nsplit, split_len = _decode_plan(self.model, B, max_ctx, self.cfg.max_model_len)
             for K in windows:
                 if K > max(1, self.cfg.decode_window):
                     continue
-                if (B, nsplit, split_len, K, self.sampler.rounds) not in self._graphs:
-                    self._capture(B, nsplit, split_len, K)
-                    n += 1
+                for npre in parts:
+                    if npre and B < 8:
+                        continue
+                    if (B, nsplit, split_len, K, self.sampler.rounds, npre) not in self._graphs:
+                        self._capture(B, nsplit, split_len, K, npre)
+                        n += 1
         return n
 
     # ------------------------------------------------------------------ outputs

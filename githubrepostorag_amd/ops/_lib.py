@@ -41,6 +41,8 @@ _SIGS = {
     "grag_paged_attention": [P, I, P, P, P, I, P, I, P, P, I, I, I, I, I, I, I, F, I, I, I, P, P, I, I, P],
     "grag_splitk_add_rmsnorm_small": [P, I, P, P, P, I, I, F, P, P, P],
     "grag_paged_decode_mw": [P, I, P, P, P, I, P, I, P, P, I, I, I, I, I, I, F, I, I, P, P, P, I, I, P],
+    "grag_paged_decode_cascade": [P, I, P, P, P, I, P, I, P, P, I, I, I, I, I, I, F, I, I, P, P, I, I, P, P, I, I, I,
+                                  P, P, I, P],
     "grag_varlen_attention": [P, P, P, I, P, I, P, P, I, I, I, I, I, F, I, P],
     "grag_score_topk_flat": [P, I64, I64, I64, I, P, I, I, I, I, P, P, P, I, P, P, P, I, P, P, P, P, P],
     "grag_score_topk_work": [P, I, P, I, I, I, I, P, P, I, P, P, P, I, P, P, P, I, P, P, P, P, P],
@@ -146,7 +148,8 @@ ERR_CODES = {1 << 0: "embed_gather: token id >= vocab", 1 << 1: "qkv_rope_kvstor
              1 << 4: "decode attention: block-table entry >= KV blocks",
              1 << 5: "split-merge / stream-K ticket past its part count (a stale or shared ticket word)",
              1 << 6: "sampler: slot row out of range", 1 << 7: "top-k / IVF: candidate row out of range",
-             1 << 8: "encoder embedding: token / position id out of range"}
+             1 << 8: "encoder embedding: token / position id out of range",
+             1 << 9: "shared-prefix decode: group row range or prefix length out of range"}
 _ERR: dict = {"host": 0, "dev": None, "bound": set()}
 
 

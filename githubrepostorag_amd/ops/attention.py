@@ -112,6 +112,79 @@ class AttnMetadata:
     part_o: torch.Tensor | None = None
     part_ml: torch.Tensor | None = None
     extra: dict = field(default_factory=dict)
+    # shared-prefix decode (prefix_groups / csrc/kernels/attention.hip paged_decode_prefix_kernel): a Cascade or
+    # None.  The fp32 reference needs none of it (the same keys, attended in one pass)
+    cascade: "Cascade | None" = None
+
+
+@dataclass
+class Cascade:
+    """Decode rows grouped on a shared cached prefix.  pre_len [nseq] int32: keys the row's group shares (0 =
+    none); grp_start [ngroups, 2] int32: (first row, end row) of each group of adjacent rows (padding pairs
+    (0, 0)); each group's prefix is cut into up to nsplit parts of >= min_part keys (the kernel sizes them from
+    the prefix length, so one launch shape -- one captured graph -- serves every length); pre_o / pre_ml: fp32
+    workspaces of nsplit x nseq x Hq x (D | 2); rg: 16-row groups per wave of the prefix kernel (a group holds
+    <= 16 * rg // G members)."""
+
+    pre_len: torch.Tensor
+    grp_start: torch.Tensor
+    nsplit: int
+    min_part: int
+    pre_o: torch.Tensor
+    pre_ml: torch.Tensor
+    rg: int = 2
+
+
+CASCADE_PARTS = int(os.environ.get("GRAG_CASCADE_PARTS", "4"))  # prefix parts per group (prefix-kernel grid z)
+CASCADE_MIN_PART = int(os.environ.get("GRAG_CASCADE_MIN_PART", "256"))  # shortest prefix part (keys)
+CASCADE_RG = int(os.environ.get("GRAG_CASCADE_RG", "2"))
+# a decode window takes the shared-prefix path when its groups save at least this share of the batch's keys
+CASCADE_MIN = float(os.environ.get("GRAG_CASCADE_MIN", "0.1"))
+
+
+def prefix_groups(bt, L, bs: int, G: int, rg: int = CASCADE_RG, min_blocks: int = 8):
+    """Group adjacent decode rows on a common leading run of KV block ids (the prefix cache hands every
+    sequence of one cached prompt prefix the same blocks).  bt [n, W] int32 block table, L [n] each row's
+    context length (keys, the current token's included).  Only whole blocks strictly before the current
+    token's block count (that block is the row's own).  A group grows while its shared keys saved,
+    (members - 1) x prefix, do not drop, up to 16 * rg // G members.  Returns (pre [n] int32, spans [(begin,
+    end), ...] of the groups, saved keys) -- pre 0 for rows outside any group -- or None when none forms."""
+    import numpy as np
+
+    n = bt.shape[0]
+    cap = (16 * rg) // G
+    if n < 2 or cap < 2:
+        return None
+    full = (np.asarray(L, dtype=np.int64) - 1) // bs  # blocks wholly before each row's current position
+    w = int(min(full.max(), bt.shape[1]))
+    if w < min_blocks:
+        return None
+    eq = bt[1:, :w] == bt[:-1, :w]
+    run = np.where(eq.all(1), w, eq.argmin(1))
+    run = np.minimum(run, np.minimum(full[1:], full[:-1])).tolist()
+    pre = np.zeros(n, dtype=np.int32)
+    spans = []
+    saved = 0
+    i = 0
+    while i < n - 1:
+        P = run[i]
+        if P < min_blocks:
+            i += 1
+            continue
+        j = i + 1  # rows i..j share P blocks
+        while j + 1 < n and j + 1 - i < cap:
+            nP = min(P, run[j])
+            if nP < min_blocks or nP * (j + 1 - i) < P * (j - i):  # the group's saved keys would drop
+                break
+            P = nP
+            j += 1
+        pre[i:j + 1] = P * bs
+        spans.append((i, j + 1))
+        saved += (j - i) * P * bs
+        i = j + 1
+    if not saved:
+        return None
+    return pre, spans, saved
 
 
 def choose_splits(max_ctx: int, nseq: int, hkv: int, target_wgs: int = 1024, split_min: int = 256):
@@ -197,6 +270,15 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
             return out
         if nw in DECODE_MW:
             nw = decode_variant(nsplit, meta.split_len, meta.num_seqs * Hkv * nsplit)
+        c = meta.cascade
+        if c is not None:
+            call("grag_paged_decode_cascade", ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(out),
+                 out.stride(0), ptr(meta.block_tables), meta.block_tables.stride(0), ptr(meta.q_start),
+                 ptr(meta.ctx_len), meta.num_seqs, T, Hq, Hkv, D, BS, float(scale), nsplit,
+                 meta.split_len if nsplit > 1 else 0, ptr(meta.part_o) if nsplit > 1 else None,
+                 ptr(meta.part_ml) if nsplit > 1 else None, nw, k_cache.shape[0], ptr(c.pre_len), ptr(c.grp_start),
+                 c.grp_start.numel() // 2, c.nsplit, c.min_part, ptr(c.pre_o), ptr(c.pre_ml), c.rg)
+            return out
     else:
         nw = meta.extra.get("prefill_nw", PREFILL_NW)
         if nw in (5, 6) and D not in (64, 128):

@@ -1,7 +1,9 @@
 """Decode attention over prefix-sharing rows (ingest's regime: each chunk's summary / title / keyword
 calls share the chunk's KV blocks): kernel time of one decode attention launch with the rows of a group
 ADJACENT in the batch and the XCD placement on (csrc/kernels/attention.hip g_decode_xcd), adjacent with it
-off, SHUFFLED, and a batch with no sharing at all (every row its own blocks: the HBM-traffic upper bound).
+off, SHUFFLED, a batch with no sharing at all (every row its own blocks: the HBM-traffic upper bound), and the
+shared-prefix decode (paged_decode_prefix_kernel + the per-row kernel over the suffix; --cascade-parts: its
+prefix parts per group), checked against the plain kernel's output.
 
 python scripts/mb_shared_prefix.py --B 192 --group 3 --prefix 1536 --suffix 256 --out gpurun_out/mb_shared.json
 """
@@ -32,6 +34,8 @@ def main():
     ap.add_argument("--suffix", type=int, default=256)
     ap.add_argument("--reps", type=int, default=40)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--cascade-parts", default="2,4,8", help="prefix parts per group (min part 256 keys)")
+    ap.add_argument("--arms", default="adjacent_rr,no_sharing,cascade")
     a = ap.parse_args()
     dev = torch.device("cuda")
     Hq, Hkv, D, BS = 28, 4, 128, 16
@@ -75,16 +79,32 @@ def main():
     shuffled = torch.randperm(B, generator=gen)
     ident = torch.arange(B)
     ref_out = None
-    for name, shared, order, xcd in (("adjacent_xcd", True, ident, 1), ("adjacent_rr", True, ident, 0),
-                                     ("shuffled_xcd", True, shuffled, 1), ("shuffled_rr", True, shuffled, 0),
-                                     ("no_sharing", False, ident, 0)):
-        bt = table(shared, order).to(dev)
+    import numpy as np
+
+    arms = [("adjacent_xcd", True, ident, 1, 0), ("adjacent_rr", True, ident, 0, 0),
+            ("shuffled_xcd", True, shuffled, 1, 0), ("shuffled_rr", True, shuffled, 0, 0),
+            ("no_sharing", False, ident, 0, 0)]
+    arms += [(f"cascade_p{np_}", True, ident, 0, int(np_)) for np_ in a.cascade_parts.split(",") if np_]
+    want = a.arms.split(",")
+    arms = [x for x in arms if x[0] in want or ("cascade" in want and x[4])]
+    for name, shared, order, xcd, csl in arms:
+        bt_h = table(shared, order)
+        bt = bt_h.to(dev)
         m = A.AttnMetadata(q_start=torch.arange(B + 1, dtype=torch.int32, device=dev),
                            ctx_len=torch.full((B,), ctx, dtype=torch.int32, device=dev), block_tables=bt,
                            slot_mapping=torch.zeros(B, dtype=torch.int32, device=dev), max_q_len=1, num_seqs=B,
                            num_tokens=B, is_decode=True, num_splits=nsplit, split_len=split_len,
                            part_o=torch.empty(nsplit * B * Hq * D, dtype=torch.float32, device=dev),
                            part_ml=torch.empty(nsplit * B * Hq * 2, dtype=torch.float32, device=dev))
+        if csl:
+            pre, spans, saved = A.prefix_groups(bt_h.numpy(), np.full(B, ctx), BS, Hq // Hkv)
+            nsp = csl
+            grp = np.zeros((B // 2, 2), dtype=np.int32)
+            grp[:len(spans)] = spans
+            m.cascade = A.Cascade(pre_len=torch.from_numpy(pre).to(dev),
+                                  grp_start=torch.from_numpy(grp.reshape(-1)).to(dev), nsplit=nsp, min_part=256,
+                                  pre_o=torch.empty(nsp * B * Hq * D, device=dev),
+                                  pre_ml=torch.empty(nsp * B * Hq * 2, device=dev))
         prev = lib().grag_attn_decode_xcd(xcd)
         try:
             out = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=dev)
@@ -107,16 +127,23 @@ def main():
                 ts.append(e0.elapsed_time(e1) * 1000 / a.reps)
         finally:
             lib().grag_attn_decode_xcd(prev)
-        if name == "adjacent_xcd":
+        if ref_out is None and shared:
             ref_out = out.float().cpu()
-        elif name == "adjacent_rr":
+        elif shared and not csl:
             assert torch.equal(out.float().cpu(), ref_out), "placement changed the result"
+        elif csl:
+            err = (out.float().cpu() - ref_out).abs().max().item()
+            assert err < 2e-2, f"shared-prefix decode differs from the plain kernel: {err}"
         us = sorted(ts)[len(ts) // 2]
         kv_bytes = B * ctx * Hkv * D * 2 * 2
         res[name] = {"us": round(us, 2), "TB_s_if_every_row_read": round(kv_bytes / us / 1e6, 2)}
+        if csl:
+            uniq = (ngroups * npfx * BS + B * (ctx - npfx * BS)) * Hkv * D * 2 * 2
+            res[name].update(prefix_parts=nsp, TB_s_unique_kv=round(uniq / us / 1e6, 2))
         print(name, res[name], flush=True)
-    res["speedup_adjacent_xcd_vs_shuffled"] = round(res["shuffled_xcd"]["us"] / res["adjacent_xcd"]["us"], 3)
-    res["speedup_adjacent_xcd_vs_rr"] = round(res["adjacent_rr"]["us"] / res["adjacent_xcd"]["us"], 3)
+    if "shuffled_xcd" in res and "adjacent_xcd" in res:
+        res["speedup_adjacent_xcd_vs_shuffled"] = round(res["shuffled_xcd"]["us"] / res["adjacent_xcd"]["us"], 3)
+        res["speedup_adjacent_xcd_vs_rr"] = round(res["adjacent_rr"]["us"] / res["adjacent_xcd"]["us"], 3)
     print(json.dumps(res))
     if a.out:
         with open(a.out, "w") as f:
