@@ -1181,7 +1181,8 @@ def concurrent_phase(args, model, tok, emb, prepare, sp, u, dev, group, world, d
         t0 = time.perf_counter()
         n = eng.warmup_graphs(max_ctx=[c for c in (2048, 4096, mml) if c <= mml], windows=(1, 2, 4, 8),
                               params=SamplingParams(temperature=EngineLLM.INGEST["temperature"],
-                                                    top_p=EngineLLM.INGEST["top_p"]))
+                                                    top_p=EngineLLM.INGEST["top_p"]),
+                              cascade=(False, True))
         n += eng.warmup_graphs(max_ctx=[2048, 4096], windows=(1, 2, 4, 8), params=q_sp)
         log(f"concurrent phase: {n} decode graphs captured in {time.perf_counter() - t0:.1f}s")
     runner = EngineRunner(eng, watchdog_s=0, interactive_prefill=args.interactive_prefill,

@@ -51,14 +51,16 @@ struct AttnParams {
   int causal;
   int nblocks;  // KV blocks in the cache: the index guard's bound for block-table entries (common.h)
   int xcd_group;  // decode: consecutive sequences of one (kv head, split) run on one XCD (g_decode_xcd)
-  // shared-prefix decode (paged_decode_prefix_kernel): batch rows [grp_start[g], grp_start[g + 1]) share
-  // their first pre_len[row] keys (whole KV blocks, one set of block ids); null pre_len = no sharing
+  // shared-prefix decode (paged_decode_prefix_kernel): the rows of a group share their first pre_len[row]
+  // keys (whole KV blocks, one set of block ids), cut into parts of pre_part[row] keys; work item i of the
+  // prefix kernel is pre_items[i] = (first row, end row, first key, end key) of one part of one group.
+  // null pre_len = no sharing
   const int32_t* pre_len;    // [nseq]
-  const int32_t* grp_start;  // [ngroups, 2]: (first row, end row) of each group
-  float* pre_o;              // [pre planes, T, Hq, D]: the prefix parts' unnormalised O
-  float* pre_ml;             // [pre planes, T, Hq, 2]: their (m, l)
-  int pre_nsplit;            // prefix parts per group (the prefix kernel's grid z; planes of pre_o / pre_ml)
-  int pre_min_part;          // shortest prefix part (keys, a multiple of 32)
+  const int32_t* pre_part;   // [nseq]
+  const int32_t* pre_items;  // [n items, 4]
+  float* pre_o;              // [pre_planes, T, Hq, D]: the prefix parts' unnormalised O (plane = part index)
+  float* pre_ml;             // [pre_planes, T, Hq, 2]: their (m, l)
+  int pre_planes;
 };
 
 // grag_attn_decode_xcd(1): decode workgroups remapped so that sequences adjacent in the batch run on the same
@@ -638,10 +640,16 @@ __global__ __launch_bounds__(64 * NW) void attn_prefill_kernel(AttnParams p) {
   }
 }
 
-// Keys per part of a P-key shared prefix (paged_decode_prefix_kernel's split of it; the merges' plane count)
-__device__ __forceinline__ int prefix_part(const AttnParams& p, int P) {
-  const int part = (((P + p.pre_nsplit - 1) / p.pre_nsplit) + 31) & ~31;
-  return max(part, p.pre_min_part);
+// Prefix parts (planes) of decode row `seq` whose first `pre` keys a shared prefix covers; a part length or
+// count out of range is reported and gives 0 (the caller then attends to all keys itself).
+__device__ __forceinline__ int prefix_planes(const AttnParams& p, int seq, int pre) {
+  const int part = p.pre_part[seq];
+  if (part <= 0) {
+    report_index_error(ERR_PREFIX_GROUP, part);
+    return 0;
+  }
+  const int nv = (pre + part - 1) / part;
+  return index_ok(nv, p.pre_planes + 1, ERR_PREFIX_GROUP) ? nv : 0;
 }
 
 // Keys [0, pre) of decode row `seq` that a shared-prefix part covers (paged_decode_prefix_kernel); 0 without
@@ -650,7 +658,8 @@ __device__ __forceinline__ int prefix_part(const AttnParams& p, int P) {
 __device__ __forceinline__ int prefix_of(const AttnParams& p, int seq, int ctx) {
   if (p.pre_len == nullptr) return 0;
   const int pre = p.pre_len[seq];
-  return (pre == 0 || index_ok(pre, ctx, ERR_PREFIX_GROUP)) ? pre : 0;
+  if (pre == 0 || !index_ok(pre, ctx, ERR_PREFIX_GROUP)) return 0;
+  return prefix_planes(p, seq, pre) > 0 ? pre : 0;
 }
 
 // Merge the prefix parts of (tok, head) into a decode wave's running state (m, l, O) -- lane (li, h4) holds
@@ -659,8 +668,7 @@ template <int D>
 __device__ __forceinline__ void merge_prefix(const AttnParams& p, int tok, int head, int pre, int h4, float& m,
                                              float& l, f32x4_t (&o)[D / 16]) {
   constexpr int ND = D / 16;
-  const int part = prefix_part(p, pre);
-  const int nv = (pre + part - 1) / part;
+  const int nv = prefix_planes(p, tok, pre);
   float M = m;
   for (int s = 0; s < nv; ++s) M = fmaxf(M, p.pre_ml[(((size_t)s * p.total_q + tok) * p.Hq + head) * 2]);
   if (M == -INFINITY) return;
@@ -916,7 +924,7 @@ __global__ __launch_bounds__(D) void attn_combine_kernel(AttnParams p) {
   const int pre = prefix_of(p, tok, ctx);
   int nvalid = (ctx - pre + p.split_len - 1) / p.split_len;
   nvalid = max(1, min(nvalid, p.num_splits));
-  const int npre = pre > 0 ? (pre + prefix_part(p, pre) - 1) / prefix_part(p, pre) : 0;
+  const int npre = pre > 0 ? prefix_planes(p, tok, pre) : 0;
   float M = -INFINITY;
   for (int s = 0; s < nvalid; ++s)
     M = fmaxf(M, p.part_ml[(((size_t)s * p.total_q + tok) * p.Hq + head) * 2]);
@@ -968,17 +976,21 @@ __global__ __launch_bounds__(64) void paged_decode_prefix_kernel(AttnParams p) {
 
   const int lane = threadIdx.x;
   const int h4 = lane >> 4, li = lane & 15;
-  const int grp = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
-  const int r0 = p.grp_start[2 * grp], r1 = p.grp_start[2 * grp + 1];
-  if (r1 - r0 < 2) return;  // padding pair (or a lone row: the per-sequence kernel covers it)
+  const int item = blockIdx.x, kvh = blockIdx.y;
+  const int4 it = reinterpret_cast<const int4*>(p.pre_items)[item];
+  const int r0 = it.x, r1 = it.y, kv_lo = it.z, kv_hi = it.w;
+  if (r1 - r0 < 2) return;  // padding item (or a lone row: the per-sequence kernel covers it)
   if (!index_ok(r0, p.total_q, ERR_PREFIX_GROUP) || !index_ok(r1, p.total_q + 1, ERR_PREFIX_GROUP)) return;
   const int nmem = r1 - r0;
   const int P = p.pre_len[r0];
-  if (P <= 0 || !index_ok(P, p.ctx_len[r0], ERR_PREFIX_GROUP)) return;
-  const int part = prefix_part(p, P);
-  const int kv_lo = split * part;
-  const int kv_hi = min(P, kv_lo + part);
-  if (kv_lo >= kv_hi) return;
+  const int part = p.pre_part[r0];
+  if (P <= 0 || !index_ok(P, p.ctx_len[r0], ERR_PREFIX_GROUP) || part <= 0) return;
+  if (kv_lo < 0 || kv_lo >= kv_hi || kv_hi > P || kv_lo % part != 0 || kv_hi - kv_lo > part) {
+    report_index_error(ERR_PREFIX_GROUP, kv_lo);
+    return;
+  }
+  const int split = kv_lo / part;  // the plane this part writes
+  if (!index_ok(split, p.pre_planes, ERR_PREFIX_GROUP)) return;
   const int G = p.G;
 
   // column li of row group j is the pair (member, head) = divmod(16 j + li, G)
@@ -992,7 +1004,8 @@ __global__ __launch_bounds__(64) void paged_decode_prefix_kernel(AttnParams p) {
     valid[j] = mem < nmem;
     tok[j] = p.q_start[r0 + (valid[j] ? mem : 0)];
     head[j] = kvh * G + (valid[j] ? row % G : 0);
-    if (valid[j] && h4 == 0 && kvh == 0 && split == 0 && row % G == 0 && p.pre_len[r0 + mem] != P)
+    if (valid[j] && h4 == 0 && kvh == 0 && split == 0 && row % G == 0 &&
+        (p.pre_len[r0 + mem] != P || p.pre_part[r0 + mem] != part))
       report_index_error(ERR_PREFIX_GROUP, r0 + mem);  // a member whose merge would read other planes
     const bf16* qp = p.q + (size_t)tok[j] * p.q_stride + (size_t)head[j] * D + 8 * h4;
 #pragma unroll
@@ -1472,8 +1485,8 @@ int launch_decode(const AttnParams& prm_in, int nseq, int tk, int ns, bool nt, h
 }
 
 template <int D>
-int launch_decode_prefix(const AttnParams& prm, int ngroups, int pre_nsplit, int rg, hipStream_t stream) {
-  dim3 grid(ngroups, prm.Hkv, pre_nsplit);
+int launch_decode_prefix(const AttnParams& prm, int n_items, int rg, hipStream_t stream) {
+  dim3 grid(n_items, prm.Hkv);
   if (rg == 4)
     paged_decode_prefix_kernel<D, 4><<<grid, 64, 0, stream>>>(prm);
   else
@@ -1575,27 +1588,26 @@ GRAG_API int grag_paged_attention(const void* q, int q_stride, const void* k_cac
 
 // Shared-prefix decode (q_len == 1): paged_decode_prefix_kernel over the groups' common prefixes, then the
 // per-sequence decode kernel (nw 1 / 3 / 7 / 8 / 11 / 12 as grag_paged_attention) over each row's own keys
-// [pre_len, ctx), merging the prefix parts.  pre_len [nseq]: keys shared (0 = none; every row of a group
-// holds its group's value); grp_start [ngroups, 2]: (first row, end row) of each group of adjacent rows
-// (pairs spanning < 2 rows are padding); rows of one group share their first pre_len block-table entries.  pre_o / pre_ml:
-// [pre_nsplit, total_q, Hq, D | 2] f32: a group's prefix of P keys is cut into parts of
-// max(pre_min_part, ceil(P / pre_nsplit) rounded up to 32) keys, so one launch shape serves every prefix
-// length (longer prefixes get longer parts, short ones fewer parts).  rg = 2 or 4
-// row groups of 16 (member, head) pairs per wave: a group has at most 16 * rg / G members.
+// [pre_len, ctx), merging the prefix parts.  pre_len [nseq]: keys the row's group shares (0 = none);
+// pre_part [nseq]: the group's part length (keys); items [n_items, 4]: (first row, end row, first key, end key)
+// of one part of one group -- rows of a group are adjacent and share their first pre_len block-table entries,
+// a part [k0, k1) starts at a multiple of the part length and writes plane k0 / part; items spanning < 2 rows
+// are padding.  pre_o / pre_ml: [pre_planes, total_q, Hq, D | 2] f32.  rg = 2 or 4 row groups of 16
+// (member, head) pairs per wave: a group has at most 16 * rg / G members.
 GRAG_API int grag_paged_decode_cascade(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                                        void* out, int out_stride, const int32_t* block_tables, int bt_stride,
                                        const int32_t* q_start, const int32_t* ctx_len, int nseq, int total_q,
                                        int Hq, int Hkv, int D, int BS, float scale, int num_splits, int split_len,
                                        float* part_o, float* part_ml, int nw, int nblocks, const int32_t* pre_len,
-                                       const int32_t* grp_start, int ngroups, int pre_nsplit, int pre_min_part,
+                                       const int32_t* pre_part, const int32_t* items, int n_items, int pre_planes,
                                        float* pre_o, float* pre_ml, int rg, hipStream_t stream) {
   if (nseq <= 0) return 0;
   if (Hq % Hkv != 0 || Hq / Hkv > 16 || BS <= 0 || BS % 16 != 0 || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
   if (!(nw == 1 || nw == 3 || nw == 7 || nw == 8 || nw == 11 || nw == 12)) return (int)hipErrorInvalidValue;
   if (num_splits < 1) num_splits = 1;
   if (num_splits > 1 && (!part_o || !part_ml || split_len % KT != 0)) return (int)hipErrorInvalidValue;
-  if (!pre_len || !grp_start || !pre_o || !pre_ml || ngroups < 0 || pre_nsplit < 1 || pre_min_part <= 0 ||
-      pre_min_part % 32 != 0 || (rg != 2 && rg != 4) || 2 * (Hq / Hkv) > 16 * rg)
+  if (!pre_len || !pre_part || !items || !pre_o || !pre_ml || n_items < 0 || pre_planes < 1 ||
+      (reinterpret_cast<uintptr_t>(items) & 15) || (rg != 2 && rg != 4) || 2 * (Hq / Hkv) > 16 * rg)
     return (int)hipErrorInvalidValue;
   AttnParams prm{};
   prm.q = (const bf16*)q;
@@ -1622,15 +1634,15 @@ GRAG_API int grag_paged_decode_cascade(const void* q, int q_stride, const void* 
   prm.causal = 1;
   prm.nblocks = nblocks;
   prm.pre_len = pre_len;
-  prm.grp_start = grp_start;
+  prm.pre_part = pre_part;
+  prm.pre_items = items;
   prm.pre_o = pre_o;
   prm.pre_ml = pre_ml;
-  prm.pre_nsplit = pre_nsplit;
-  prm.pre_min_part = pre_min_part;
+  prm.pre_planes = pre_planes;
   int err = 0;
-  if (ngroups > 0)
-    err = D == 128 ? launch_decode_prefix<128>(prm, ngroups, pre_nsplit, rg, stream)
-                   : launch_decode_prefix<64>(prm, ngroups, pre_nsplit, rg, stream);
+  if (n_items > 0)
+    err = D == 128 ? launch_decode_prefix<128>(prm, n_items, rg, stream)
+                   : launch_decode_prefix<64>(prm, n_items, rg, stream);
   if (err) return err;
   const int tk = nw == 1 ? 64 : 32, ns = nw == 7 ? 4 : (nw == 8 || nw == 12) ? 3 : 2;
   return D == 128 ? launch_decode<128>(prm, nseq, tk, ns, nw >= 11, stream)

@@ -30,8 +30,8 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from ..ops.attention import (CASCADE_MIN, CASCADE_MIN_PART, CASCADE_PARTS, CASCADE_RG, KV_TILE, AttnMetadata, Cascade,
-                             prefix_groups)
+from ..ops.attention import (CASCADE_MAX_PLANES, CASCADE_MIN, CASCADE_MIN_WAVES, CASCADE_RG, KV_TILE, AttnMetadata, Cascade,
+                             cascade_items, cascade_layout, prefix_groups)
 from ..ops._lib import check_device_errors
 from ..ops.gemm import WS
 from ..ops.sampling import SamplerState, reset_slots, sample, sample_tp
@@ -115,6 +115,9 @@ def _decode_plan(model, B: int, max_ctx: int, max_model_len: int, graph: bool = 
 _GROUP_ROWS = __import__("os").environ.get("GRAG_DECODE_GROUP_ROWS", "0") == "1"
 
 
+_CASCADE_PROBE = 7  # block index probed for prefix sharing (ops/attention.prefix_groups min_blocks - 1)
+
+
 def _prefix_blocks(s) -> list:
     return s.blocks[:32]
 
@@ -124,6 +127,24 @@ def _pow2_at_least(n: int) -> int:
     while p < n:
         p *= 2
     return p
+
+
+def _ctrl_layout(B: int, width: int, K: int = 1) -> dict:
+    """Offsets (int32 elements) and shapes of the decode control buffer for a K-step window of B rows:
+    ids[B] | pos[K,B] | slot[K,B] | ctx[K,B] | sampler slots[B] | q_start[B+1] | pre[B] | part[B] | (pad to
+    16 B) items[NI,4] | block table[B,width].  pre / part / items: the shared-prefix decode layout
+    (ops/attention.cascade_layout; NI = cascade_items(B)); zeros when the window does not take it."""
+    lay = {}
+    o = 0
+    for name, shape in (("ids", (B,)), ("pos", (K, B)), ("slot", (K, B)), ("ctx", (K, B)), ("slots", (B,)),
+                        ("qs", (B + 1,)), ("pre", (B,)), ("part", (B,)), ("items", (cascade_items(B), 4)),
+                        ("bt", (B, width))):
+        if name == "items":
+            o += -o % 4  # int4 loads in the prefix kernel
+        lay[name] = (o, shape)
+        o += int(np.prod(shape))
+    lay["size"] = o + 4  # room for the pad of a buffer whose base is 16-B aligned
+    return lay
 
 
 class _DecodeGraph:
@@ -190,9 +211,9 @@ class LLMEngine:
             self._part_o = torch.empty(max_split * self._max_b * hq * d, dtype=torch.float32, device=self.device)
             self._part_ml = torch.empty(max_split * self._max_b * hq * 2, dtype=torch.float32, device=self.device)
             if cfg.cascade_decode:  # prefix parts of the shared-prefix decode
-                npre = CASCADE_PARTS
-                self._pre_o = torch.empty(npre * self._max_b * hq * d, dtype=torch.float32, device=self.device)
-                self._pre_ml = torch.empty(npre * self._max_b * hq * 2, dtype=torch.float32, device=self.device)
+                npl = CASCADE_MAX_PLANES
+                self._pre_o = torch.empty(npl * self._max_b * hq * d, dtype=torch.float32, device=self.device)
+                self._pre_ml = torch.empty(npl * self._max_b * hq * 2, dtype=torch.float32, device=self.device)
             # sampler scratch for the largest decode batch up front: graphs captured later all see one buffer
             self.sampler.workspace(self._max_b)
             from ..ops.attention import decode_counters  # small-batch decode tickets: before any capture
@@ -488,15 +509,13 @@ class LLMEngine:
         max_ctx = max(s.total_len for s in dseqs)
         wd = -(-max_ctx // bs)
         dec = self._decode_inputs(dseqs, n_dec, wd, 1)
-        o = 0
-        d_ids = dec[o:o + n_dec]; o += n_dec
-        d_pos = dec[o:o + n_dec]; o += n_dec
-        d_slot = dec[o:o + n_dec]; o += n_dec
-        d_ctx = dec[o:o + n_dec]; o += n_dec
-        d_samp = dec[o:o + n_dec]; o += n_dec
-        o += n_dec + 1  # q_start 0..n_dec
-        o += n_dec + 2 * (n_dec // 2)  # shared-prefix layout (not used by mixed steps)
-        d_bt = dec[o:]
+        lay = _ctrl_layout(n_dec, wd, 1)
+
+        def part(name):
+            o, shape = lay[name]
+            return dec[o:o + int(np.prod(shape))]
+
+        d_ids, d_pos, d_slot, d_ctx, d_samp, d_bt = (part(k) for k in ("ids", "pos", "slot", "ctx", "slots", "bt"))
         # rows to sample: the last token of every prefill chunk that completes its prompt, then every decode row
         done = [i for i, (s, a, b) in enumerate(pitems) if b == s.total_len]
         samp_rows = np.concatenate([np.asarray([q_start[i + 1] - 1 for i in done], dtype=np.int32),
@@ -576,24 +595,19 @@ class LLMEngine:
         ids[B] | pos[K,B] | slot[K,B] | ctx[K,B] | sampler slots[B] | q_start[B+1] | pre[B] | groups[B//2,2] |
         block table[B,width].  Rows >= len(seqs) are padding (scratch slot, slot mapping -1).  pre / groups:
         the shared-prefix decode layout (ops/attention.prefix_groups) when ``groups`` and the batch's rows
-        share enough cached prefix (self._cascade_plan holds its prefix-part count, 0 = none), else zeros."""
+        share enough cached prefix (self._cascade_plan is then 1), else zeros."""
         n = len(seqs)
         bs = self.cfg.block_size
-        buf = np.empty(B * (3 * K + 3) + 1 + B + 2 * (B // 2) + B * width, dtype=np.int32)
-        o = 0
-        ids = buf[o:o + B]; o += B
-        pos = buf[o:o + K * B].reshape(K, B); o += K * B
-        slot = buf[o:o + K * B].reshape(K, B); o += K * B
-        ctx = buf[o:o + K * B].reshape(K, B); o += K * B
-        sl = buf[o:o + B]; o += B
-        buf[o:o + B + 1] = np.arange(B + 1, dtype=np.int32); o += B + 1
-        pre = buf[o:o + B]; o += B
-        grp = buf[o:o + 2 * (B // 2)].reshape(B // 2, 2); o += 2 * (B // 2)
-        pre.fill(0)
-        grp.fill(0)
+        lay = _ctrl_layout(B, width, K)
+        buf = np.zeros(lay["size"], dtype=np.int32)
+
+        def part(name):
+            o, shape = lay[name]
+            return buf[o:o + int(np.prod(shape))].reshape(shape)
+
+        ids, pos, slot, ctx, sl, qs, bt = (part(k) for k in ("ids", "pos", "slot", "ctx", "slots", "qs", "bt"))
+        qs[:] = np.arange(B + 1, dtype=np.int32)
         self._cascade_plan = 0
-        bt = buf[o:].reshape(B, width)
-        bt[n:].fill(0)
         ids[n:] = 0
         pos[:, n:] = 0
         slot[:, n:] = -1
@@ -636,10 +650,10 @@ class LLMEngine:
             ctx[:, :n] = p + 1
             slot[:, :n] = bt[np.arange(n)[None, :], p // bs].astype(np.int64) * bs + p % bs
             if groups and n >= 4:
-                self._plan_cascade(bt[:n], L, pre, grp)
+                self._plan_cascade(bt[:n], L, part("pre"), part("part"), part("items"))
         return buf
 
-    def _plan_cascade(self, bt, L, pre, grp) -> None:
+    def _plan_cascade(self, bt, L, pre, part, items) -> None:
         """Fill the shared-prefix layout of one decode window when its groups save at least CASCADE_MIN of
         the batch's K/V keys (a group's prefix is read once instead of once per member)."""
         total = int(L.sum())
@@ -650,9 +664,13 @@ class LLMEngine:
         p, spans, saved = r
         if saved < CASCADE_MIN * total:
             return
+        pl, it, used = cascade_layout(p, spans, items.shape[0])
+        if used * max(1, self.model.hkv) < CASCADE_MIN_WAVES:
+            return
         pre[: len(p)] = p
-        grp[: len(spans)] = spans
-        self._cascade_plan = CASCADE_PARTS
+        part[: len(pl)] = pl
+        items[:] = it
+        self._cascade_plan = 1
         self.stats["cascade_windows"] += 1
         self.stats["cascade_rows"] += sum(b - a for a, b in spans)
         self.stats["cascade_saved_keys"] += saved
@@ -667,31 +685,22 @@ class LLMEngine:
         return t
 
     def _views(self, buf: torch.Tensor, B: int, width: int, K: int = 1):
-        o = 0
-        out = {}
-        for name, shape in (("ids", (B,)), ("pos", (K, B)), ("slot", (K, B)), ("ctx", (K, B)), ("slots", (B,)),
-                            ("qs", (B + 1,))):
-            cnt = int(np.prod(shape))
-            out[name] = buf[o:o + cnt].view(*shape)
-            o += cnt
-        out["pre"] = buf[o:o + B]
-        o += B
-        out["grp"] = buf[o:o + 2 * (B // 2)]
-        o += 2 * (B // 2)
-        out["bt"] = buf[o:o + B * width].view(B, width)
-        return out
+        lay = _ctrl_layout(B, width, K)
+        lay.pop("size")
+        return {name: buf[o:o + int(np.prod(shape))].view(*shape) for name, (o, shape) in lay.items()}
 
     def _decode_forward(self, v, B, nsplit, split_len, out_tokens, K: int = 1, npre: int = 0):
-        """K chained decode steps; step j > 0 embeds the ids step j-1 sampled (on device).  npre > 0: the
-        shared-prefix decode over v["pre"] / v["grp"] with npre prefix parts."""
+        """K chained decode steps; step j > 0 embeds the ids step j-1 sampled (on device).  npre: 1 = the
+        shared-prefix decode over v["pre"] / v["part"] / v["items"]."""
         hq, d = self.model.hq, self.model.head_dim
         part_o = self._part_o[: nsplit * B * hq * d] if self.on_gpu else None
         part_ml = self._part_ml[: nsplit * B * hq * 2] if self.on_gpu else None
         cas = None
         if npre:
-            cas = Cascade(pre_len=v["pre"], grp_start=v["grp"], nsplit=npre, min_part=CASCADE_MIN_PART,
-                          pre_o=self._pre_o[: npre * B * hq * d] if self.on_gpu else None,
-                          pre_ml=self._pre_ml[: npre * B * hq * 2] if self.on_gpu else None, rg=CASCADE_RG)
+            npl = CASCADE_MAX_PLANES
+            cas = Cascade(pre_len=v["pre"], pre_part=v["part"], items=v["items"], planes=npl,
+                          pre_o=self._pre_o[: npl * B * hq * d] if self.on_gpu else None,
+                          pre_ml=self._pre_ml[: npl * B * hq * 2] if self.on_gpu else None, rg=CASCADE_RG)
         for j in range(K):
             ids = v["ids"] if j == 0 else out_tokens[j - 1]
             meta = AttnMetadata(q_start=v["qs"], ctx_len=v["ctx"][j], block_tables=v["bt"], slot_mapping=v["slot"][j],
@@ -731,7 +740,11 @@ class LLMEngine:
         t0 = time.perf_counter()
         n = len(seqs)
         casc = False
-        if self.cfg.cascade_decode and n >= 8 and len({s.blocks[0] for s in seqs if s.blocks}) < n:
+        k = _CASCADE_PROBE
+        if self.cfg.cascade_decode and n >= 8 and len({s.blocks[k] for s in seqs if len(s.blocks) > k}) < sum(
+                len(s.blocks) > k for s in seqs):
+            # (the prefix cache hands out one block id per (content, prefix) chain, so two rows holding the same
+            # id at block index k share their first k + 1 blocks: a group of >= min_blocks is possible)
             # some rows share a cached prompt prefix (ingest's summary / title / keyword calls of one chunk, an
             # agent job's calls over the same documents): rows side by side by leading block ids, so the
             # shared-prefix decode (ops/attention.prefix_groups) can group adjacent rows
@@ -844,7 +857,7 @@ class LLMEngine:
         if self._static is None:
             W = self.max_blocks_per_seq
             Kmax = max(1, self.cfg.decode_window)
-            size = (3 * Kmax + 3) * self._max_b + 1 + 2 * self._max_b + self._max_b * W
+            size = _ctrl_layout(self._max_b, W, Kmax)["size"]
             self._static_dev = torch.zeros(size, dtype=torch.int32, device=self.device)
             self._static_host = torch.zeros(size, dtype=torch.int32).pin_memory()
             self._static = True
@@ -907,7 +920,7 @@ class LLMEngine:
 
     @torch.inference_mode()
     def warmup_graphs(self, batch_sizes=None, max_ctx=2048, windows=(1,), params: SamplingParams | None = None,
-                      cascade_parts=(0,)) -> int:
+                      cascade=(False,)) -> int:
         """Capture the decode graphs a workload will replay ahead of time
         (batch buckets x decode windows K, split plan of ``max_ctx``) so no
         capture lands inside a latency-sensitive step.  Keyed on the
@@ -915,9 +928,9 @@ class LLMEngine:
         serving sampling parameters have been admitted.  Returns the number
         of graphs captured.  ``max_ctx`` may be a list (one split plan per context length).  ``params``:
         capture for the sampler launch chain these sampling parameters select (top-k / top-p rounds)
-        instead of the live slots' (e.g. an ingest engine warmed before its first request).  ``cascade_parts``:
-        prefix-part counts of the shared-prefix decode to capture as well (0 = the plain decode graph; batches
-        of >= 8 rows only)."""
+        instead of the live slots' (e.g. an ingest engine warmed before its first request).  ``cascade``:
+        which decode variants to capture: False = the plain graph, True = the shared-prefix decode's (batches of
+        >= 8 rows only)."""
         if not (self.on_gpu and self.cfg.use_cuda_graph and getattr(self.model.tp, "capturable", True)):
             return 0
         prev = self.sampler.rounds_override
@@ -929,14 +942,14 @@ class LLMEngine:
             with self._on_stream():
                 n = 0
                 for mc in (max_ctx if isinstance(max_ctx, (list, tuple)) else [max_ctx]):
-                    n += self._warmup_graphs(batch_sizes, mc, windows, cascade_parts)
+                    n += self._warmup_graphs(batch_sizes, mc, windows, cascade)
                 return n
         finally:
             self.sampler.rounds_override = prev
 
-    def _warmup_graphs(self, batch_sizes, max_ctx, windows, cascade_parts=(0,)) -> int:
+    def _warmup_graphs(self, batch_sizes, max_ctx, windows, cascade=(False,)) -> int:
         n = 0
-        parts = [c for c in cascade_parts if c == 0 or self.cfg.cascade_decode]
+        parts = [int(c) for c in cascade if not c or self.cfg.cascade_decode]
         for B in batch_sizes or self.cfg.graph_batch_sizes:
             nsplit, split_len = _decode_plan(self.model, B, max_ctx, self.cfg.max_model_len)
             for K in windows:

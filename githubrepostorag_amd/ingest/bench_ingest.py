@@ -17,6 +17,7 @@ import time
 
 import torch
 
+
 from ..agent.llm import EngineLLM
 from ..config import Settings
 from ..engine.llm_engine import EngineConfig, LLMEngine
@@ -63,7 +64,8 @@ def run_ingest_bench(model, tok, emb, n_files: int, seed: int = 0, max_num_seqs:
         t_w = time.perf_counter()
         n_w = eng.warmup_graphs(max_ctx=ctxs, windows=(1, 2, 4, 8),
                                 params=SamplingParams(temperature=EngineLLM.INGEST["temperature"],
-                                                      top_p=EngineLLM.INGEST["top_p"]))
+                                                      top_p=EngineLLM.INGEST["top_p"]),
+                                cascade=(False, True))
         log.info("ingest engine: %d decode graphs captured in %.1fs", n_w, time.perf_counter() - t_w)
     tp = tp if tp is not None and not tp.trivial else None
     runner = EngineRunner(eng, tp=tp)
@@ -131,7 +133,8 @@ def run_ingest_multi(model, tok, emb, n_repos: int, n_files: int, seed: int = 0,
         ctxs = sorted({c for c in (2048, 4096, max_model_len) if c <= max_model_len})
         eng.warmup_graphs(max_ctx=ctxs, windows=(1, 2, 4, 8),
                           params=SamplingParams(temperature=EngineLLM.INGEST["temperature"],
-                                                top_p=EngineLLM.INGEST["top_p"]))
+                                                top_p=EngineLLM.INGEST["top_p"]),
+                          cascade=(False, True))
     runner = EngineRunner(eng)
     try:
         llm = EngineLLM(runner, tok, max_tokens=summary_tokens, mode="ingest", timeout_s=3600.0, retries=0)

@@ -41,7 +41,7 @@ _SIGS = {
     "grag_paged_attention": [P, I, P, P, P, I, P, I, P, P, I, I, I, I, I, I, I, F, I, I, I, P, P, I, I, P],
     "grag_splitk_add_rmsnorm_small": [P, I, P, P, P, I, I, F, P, P, P],
     "grag_paged_decode_mw": [P, I, P, P, P, I, P, I, P, P, I, I, I, I, I, I, F, I, I, P, P, P, I, I, P],
-    "grag_paged_decode_cascade": [P, I, P, P, P, I, P, I, P, P, I, I, I, I, I, I, F, I, I, P, P, I, I, P, P, I, I, I,
+    "grag_paged_decode_cascade": [P, I, P, P, P, I, P, I, P, P, I, I, I, I, I, I, F, I, I, P, P, I, I, P, P, P, I, I,
                                   P, P, I, P],
     "grag_varlen_attention": [P, P, P, I, P, I, P, P, I, I, I, I, I, F, I, P],
     "grag_score_topk_flat": [P, I64, I64, I64, I, P, I, I, I, I, P, P, P, I, P, P, P, I, P, P, P, P, P],

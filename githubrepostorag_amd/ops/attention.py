@@ -119,27 +119,67 @@ class AttnMetadata:
 
 @dataclass
 class Cascade:
-    """Decode rows grouped on a shared cached prefix.  pre_len [nseq] int32: keys the row's group shares (0 =
-    none); grp_start [ngroups, 2] int32: (first row, end row) of each group of adjacent rows (padding pairs
-    (0, 0)); each group's prefix is cut into up to nsplit parts of >= min_part keys (the kernel sizes them from
-    the prefix length, so one launch shape -- one captured graph -- serves every length); pre_o / pre_ml: fp32
-    workspaces of nsplit x nseq x Hq x (D | 2); rg: 16-row groups per wave of the prefix kernel (a group holds
-    <= 16 * rg // G members)."""
+    """Decode rows grouped on a shared cached prefix (prefix_groups + cascade_layout).  pre_len [nseq] int32:
+    keys the row's group shares (0 = none); pre_part [nseq] int32: the group's prefix-part length; items
+    [n_items, 4] int32 (16-B aligned): (first row, end row, first key, end key) of each part of each group --
+    the prefix kernel's work list, one workgroup per item and kv head (padding items (0, 0, 0, 0)); pre_o /
+    pre_ml: fp32 workspaces of planes x nseq x Hq x (D | 2), plane = part index; rg: 16-row groups per wave of
+    the prefix kernel (a group holds <= 16 * rg // G members)."""
 
     pre_len: torch.Tensor
-    grp_start: torch.Tensor
-    nsplit: int
-    min_part: int
+    pre_part: torch.Tensor
+    items: torch.Tensor
+    planes: int
     pre_o: torch.Tensor
     pre_ml: torch.Tensor
     rg: int = 2
 
 
-CASCADE_PARTS = int(os.environ.get("GRAG_CASCADE_PARTS", "4"))  # prefix parts per group (prefix-kernel grid z)
 CASCADE_MIN_PART = int(os.environ.get("GRAG_CASCADE_MIN_PART", "256"))  # shortest prefix part (keys)
+CASCADE_PARTS = int(os.environ.get("GRAG_CASCADE_PARTS", "4"))  # parts a group's prefix is cut into (at most)
+CASCADE_MAX_PLANES = max(CASCADE_PARTS, 1)
 CASCADE_RG = int(os.environ.get("GRAG_CASCADE_RG", "2"))
-# a decode window takes the shared-prefix path when its groups save at least this share of the batch's keys
-CASCADE_MIN = float(os.environ.get("GRAG_CASCADE_MIN", "0.1"))
+# when a decode window takes the shared-prefix path: its groups save at least CASCADE_MIN of the batch's K/V
+# keys AND the prefix kernel gets >= CASCADE_MIN_WAVES waves (items x kv heads).  The prefix kernel runs
+# ahead of the per-row kernel, so a thin prefix grid is a serial latency chain in front of it
+# (profiles/mb_cascade_r6.json: B192, groups of 3 sharing 1536 keys: 105 -> 61 us; a third of B256's groups
+# sharing: 122 -> 145 us; B64 fully shared, 352 prefix waves: 46 -> 53 us)
+CASCADE_MIN = float(os.environ.get("GRAG_CASCADE_MIN", "0.3"))
+CASCADE_MIN_WAVES = int(os.environ.get("GRAG_CASCADE_MIN_WAVES", "1024"))
+
+
+def cascade_items(B: int) -> int:
+    """Work-item slots of the prefix kernel for a batch of B rows (its grid: slots x kv heads)."""
+    return max(8, min(2 * B, 1024))
+
+
+def _up32(x: int) -> int:
+    return -(-x // 32) * 32
+
+
+def cascade_layout(pre, spans, n_items: int, parts: int = CASCADE_PARTS, min_part: int = CASCADE_MIN_PART):
+    """Cut each group's P-key prefix into at most ``parts`` parts of max(min_part, ceil(P / parts) rounded up
+    to 32) keys: one work item (group, part) each.  Returns (part [n] int32, items [n_items, 4] int32, items
+    used).  A group that finds no slots left is dropped from the layout (its rows' pre set to 0: they attend
+    to all their keys themselves)."""
+    import numpy as np
+
+    n = len(pre)
+    part = np.zeros(n, dtype=np.int32)
+    items = np.zeros((n_items, 4), dtype=np.int32)
+    k = 0
+    for a, b in spans:
+        P = int(pre[a])
+        pl = max(min_part, _up32(-(-P // parts)))
+        cnt = -(-P // pl)
+        if k + cnt > n_items:
+            pre[a:b] = 0
+            continue
+        part[a:b] = pl
+        for j in range(cnt):
+            items[k] = (a, b, j * pl, min(P, (j + 1) * pl))
+            k += 1
+    return part, items, k
 
 
 def prefix_groups(bt, L, bs: int, G: int, rg: int = CASCADE_RG, min_blocks: int = 8):
@@ -276,8 +316,8 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                  out.stride(0), ptr(meta.block_tables), meta.block_tables.stride(0), ptr(meta.q_start),
                  ptr(meta.ctx_len), meta.num_seqs, T, Hq, Hkv, D, BS, float(scale), nsplit,
                  meta.split_len if nsplit > 1 else 0, ptr(meta.part_o) if nsplit > 1 else None,
-                 ptr(meta.part_ml) if nsplit > 1 else None, nw, k_cache.shape[0], ptr(c.pre_len), ptr(c.grp_start),
-                 c.grp_start.numel() // 2, c.nsplit, c.min_part, ptr(c.pre_o), ptr(c.pre_ml), c.rg)
+                 ptr(meta.part_ml) if nsplit > 1 else None, nw, k_cache.shape[0], ptr(c.pre_len), ptr(c.pre_part),
+                 ptr(c.items), c.items.numel() // 4, c.planes, ptr(c.pre_o), ptr(c.pre_ml), c.rg)
             return out
     else:
         nw = meta.extra.get("prefill_nw", PREFILL_NW)

@@ -141,7 +141,7 @@ class RAGRuntime:
         n = 0
         for ctx in contexts:
             if ctx <= eng.cfg.max_model_len:
-                n += eng.warmup_graphs(buckets, ctx, windows)
+                n += eng.warmup_graphs(buckets, ctx, windows, cascade=(False, True))
         return n
 
     def _warmup_tp(self) -> int:

@@ -34,8 +34,10 @@ def main():
     ap.add_argument("--suffix", type=int, default=256)
     ap.add_argument("--reps", type=int, default=40)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--cascade-parts", default="2,4,8", help="prefix parts per group (min part 256 keys)")
+    ap.add_argument("--cascade-min-part", default="256", help="shortest prefix part (keys), one arm per value")
     ap.add_argument("--arms", default="adjacent_rr,no_sharing,cascade")
+    ap.add_argument("--share-every", type=int, default=1,
+                    help="only every Nth group shares its prefix (the rest: own blocks), a partly shared batch")
     a = ap.parse_args()
     dev = torch.device("cuda")
     Hq, Hkv, D, BS = 28, 4, 128, 16
@@ -57,14 +59,15 @@ def main():
         bt = torch.zeros(B, width, dtype=torch.int32)
         o = 0
         for gi in range(ngroups):
-            pf = perm[o:o + npfx] if shared else None
-            if shared:
+            sh = shared and gi % a.share_every == 0
+            pf = perm[o:o + npfx] if sh else None
+            if sh:
                 o += npfx
             for j in range(g):
                 r = gi * g + j
                 if r >= B:
                     break
-                if shared:
+                if sh:
                     bt[r, :npfx] = pf
                 else:
                     bt[r, :npfx] = perm[o:o + npfx]
@@ -84,7 +87,7 @@ def main():
     arms = [("adjacent_xcd", True, ident, 1, 0), ("adjacent_rr", True, ident, 0, 0),
             ("shuffled_xcd", True, shuffled, 1, 0), ("shuffled_rr", True, shuffled, 0, 0),
             ("no_sharing", False, ident, 0, 0)]
-    arms += [(f"cascade_p{np_}", True, ident, 0, int(np_)) for np_ in a.cascade_parts.split(",") if np_]
+    arms += [(f"cascade_m{mp}", True, ident, 0, int(mp)) for mp in a.cascade_min_part.split(",") if mp]
     want = a.arms.split(",")
     arms = [x for x in arms if x[0] in want or ("cascade" in want and x[4])]
     for name, shared, order, xcd, csl in arms:
@@ -98,11 +101,11 @@ def main():
                            part_ml=torch.empty(nsplit * B * Hq * 2, dtype=torch.float32, device=dev))
         if csl:
             pre, spans, saved = A.prefix_groups(bt_h.numpy(), np.full(B, ctx), BS, Hq // Hkv)
-            nsp = csl
-            grp = np.zeros((B // 2, 2), dtype=np.int32)
-            grp[:len(spans)] = spans
-            m.cascade = A.Cascade(pre_len=torch.from_numpy(pre).to(dev),
-                                  grp_start=torch.from_numpy(grp.reshape(-1)).to(dev), nsplit=nsp, min_part=256,
+            res.setdefault("saved_key_share", round(saved / (B * ctx), 3))
+            nsp = A.CASCADE_MAX_PLANES
+            part, items, used = A.cascade_layout(pre, spans, A.cascade_items(B), min_part=csl)
+            m.cascade = A.Cascade(pre_len=torch.from_numpy(pre).to(dev), pre_part=torch.from_numpy(part).to(dev),
+                                  items=torch.from_numpy(items.reshape(-1)).to(dev), planes=nsp,
                                   pre_o=torch.empty(nsp * B * Hq * D, device=dev),
                                   pre_ml=torch.empty(nsp * B * Hq * 2, device=dev))
         prev = lib().grag_attn_decode_xcd(xcd)
@@ -138,8 +141,9 @@ def main():
         kv_bytes = B * ctx * Hkv * D * 2 * 2
         res[name] = {"us": round(us, 2), "TB_s_if_every_row_read": round(kv_bytes / us / 1e6, 2)}
         if csl:
-            uniq = (ngroups * npfx * BS + B * (ctx - npfx * BS)) * Hkv * D * 2 * 2
-            res[name].update(prefix_parts=nsp, TB_s_unique_kv=round(uniq / us / 1e6, 2))
+            n_sh = len(range(0, ngroups, a.share_every))
+            uniq = (n_sh * npfx * BS + (B - n_sh * g) * npfx * BS + B * (ctx - npfx * BS)) * Hkv * D * 2 * 2
+            res[name].update(items=used, part_keys=int(part.max()), TB_s_unique_kv=round(uniq / us / 1e6, 2))
         print(name, res[name], flush=True)
     if "shuffled_xcd" in res and "adjacent_xcd" in res:
         res["speedup_adjacent_xcd_vs_shuffled"] = round(res["shuffled_xcd"]["us"] / res["adjacent_xcd"]["us"], 3)

@@ -64,7 +64,10 @@ def model():
     return Qwen2Model(decoder_config("qwen2-tiny"), device="cpu", dtype=torch.float32, seed=0, init_std=0.05)
 
 
-def test_engine_groups_rows_on_cached_prefixes(model):
+def test_engine_groups_rows_on_cached_prefixes(model, monkeypatch):
+    import githubrepostorag_amd.engine.llm_engine as LE
+
+    monkeypatch.setattr(LE, "CASCADE_MIN_WAVES", 0)  # the tiny batch's prefix grid is far below the GPU gate
     tok = ByteBPETokenizer(512)
     sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
     pa = [(3 * j) % 400 + 1 for j in range(200)]  # 12 full blocks of 16
@@ -83,3 +86,21 @@ def test_engine_groups_rows_on_cached_prefixes(model):
         else:
             assert eng.stats["cascade_windows"] == 0
     assert outs[True] == outs[False]
+
+
+def test_layout_cuts_prefixes_into_work_items():
+    from githubrepostorag_amd.ops.attention import cascade_layout
+
+    pre = np.array([640, 640, 640, 0, 160, 160, 4096, 4096], dtype=np.int32)
+    spans = [(0, 3), (4, 6), (6, 8)]
+    part, items, used = cascade_layout(pre.copy(), spans, 16, parts=4, min_part=256)
+    # 640 keys -> 256-key parts (min part) x 3; 160 -> one part; 4096 -> 4 parts of 1024
+    assert part.tolist() == [256, 256, 256, 0, 256, 256, 1024, 1024]
+    got = [tuple(r) for r in items[:used]]
+    assert got[:4] == [(0, 3, 0, 256), (0, 3, 256, 512), (0, 3, 512, 640), (4, 6, 0, 160)]
+    assert got[4:] == [(6, 8, 1024 * j, 1024 * (j + 1)) for j in range(4)]
+    assert (items[used:] == 0).all()
+    # no room for a group's parts: that group drops out (its rows attend to all their keys themselves)
+    pre2 = pre.copy()
+    part, items, used = cascade_layout(pre2, spans, 5, parts=4, min_part=256)
+    assert used == 4 and pre2[6] == 0 and pre2[7] == 0 and part[6] == 0 and part[0] == 256

@@ -50,24 +50,22 @@ def _dev_meta(meta, dev):
                           max_q_len=1, num_seqs=meta.num_seqs, num_tokens=meta.num_tokens, is_decode=True)
 
 
-def cascade_for(bt, lens, G, dev, B, parts=4, min_part=256, rg=2, ngroups=None):
+def cascade_for(bt, lens, G, dev, B, n_items=None, min_part=256, rg=2, planes=16):
     r = A.prefix_groups(bt, np.asarray(lens), 16, G, rg=rg)
     assert r is not None
     pre, spans, saved = r
-    nsp = parts
-    ng = ngroups or B // 2
-    grp = np.zeros((ng, 2), dtype=np.int32)
-    grp[:len(spans)] = spans
-    return A.Cascade(pre_len=torch.from_numpy(pre).to(dev), grp_start=torch.from_numpy(grp.reshape(-1)).to(dev),
-                     nsplit=nsp, min_part=min_part,
-                     pre_o=torch.full((nsp * B * 64 * 128,), float("nan"), device=dev),
-                     pre_ml=torch.full((nsp * B * 64 * 2,), float("nan"), device=dev), rg=rg), spans, saved
+    part, items, used = A.cascade_layout(pre, spans, n_items or A.cascade_items(B), min_part=min_part)
+    assert used > 0
+    return A.Cascade(pre_len=torch.from_numpy(pre).to(dev), pre_part=torch.from_numpy(part).to(dev),
+                     items=torch.from_numpy(items.reshape(-1)).to(dev), planes=planes,
+                     pre_o=torch.full((planes * B * 64 * 128,), float("nan"), device=dev),
+                     pre_ml=torch.full((planes * B * 64 * 2,), float("nan"), device=dev), rg=rg), spans, saved
 
 
 @pytest.mark.parametrize("Hq,Hkv,D", [(28, 4, 128), (12, 2, 64), (16, 2, 128)])
 @pytest.mark.parametrize("nsplit_len", [(1, 0), (2, 2048), (8, 256)])
 @pytest.mark.parametrize("rg", [2, 4])
-@pytest.mark.parametrize("parts", [(4, 256), (2, 512), (8, 32)])
+@pytest.mark.parametrize("parts", [(None, 256), (8, 512), (200, 32)])
 def test_cascade_decode_matches_reference(dev, Hq, Hkv, D, nsplit_len, rg, parts):
     G = Hq // Hkv
     cap = 16 * rg // G
@@ -83,7 +81,7 @@ def test_cascade_decode_matches_reference(dev, Hq, Hkv, D, nsplit_len, rg, parts
         m.num_splits, m.split_len = ns, sl
         m.part_o = torch.empty(ns * B * Hq * D, dtype=torch.float32, device=dev)
         m.part_ml = torch.empty(ns * B * Hq * 2, dtype=torch.float32, device=dev)
-    c, spans, saved = cascade_for(bt, lens, G, dev, B, parts=parts[0], min_part=parts[1], rg=rg)
+    c, spans, saved = cascade_for(bt, lens, G, dev, B, n_items=parts[0], min_part=parts[1], rg=rg)
     assert saved > 0 and all(b - a >= 2 for a, b in spans)
     m.cascade = c
     qd, kd, vd = q.to(dev), kc.to(dev), vc.to(dev)
@@ -119,10 +117,12 @@ def test_cascade_graph_replay_and_guard(dev):
     bt_d = torch.zeros(B, W, dtype=torch.int32, device=dev)
     ctx_d = torch.ones(B, dtype=torch.int32, device=dev)
     pre_d = torch.zeros(B, dtype=torch.int32, device=dev)
-    grp_d = torch.zeros(2 * (B // 2), dtype=torch.int32, device=dev)  # B // 2 pairs
-    nsp = 4
-    c = A.Cascade(pre_len=pre_d, grp_start=grp_d, nsplit=nsp, min_part=256,
-                  pre_o=torch.zeros(nsp * B * Hq * D, device=dev), pre_ml=torch.zeros(nsp * B * Hq * 2, device=dev))
+    part_d = torch.zeros(B, dtype=torch.int32, device=dev)
+    NI = A.cascade_items(B)
+    items_d = torch.zeros(NI * 4, dtype=torch.int32, device=dev)
+    npl = 16
+    c = A.Cascade(pre_len=pre_d, pre_part=part_d, items=items_d, planes=npl,
+                  pre_o=torch.zeros(npl * B * Hq * D, device=dev), pre_ml=torch.zeros(npl * B * Hq * 2, device=dev))
     m = A.AttnMetadata(q_start=torch.arange(B + 1, dtype=torch.int32, device=dev), ctx_len=ctx_d, block_tables=bt_d,
                        slot_mapping=torch.zeros(B, dtype=torch.int32, device=dev), max_q_len=1, num_seqs=B,
                        num_tokens=B, is_decode=True, cascade=c)
@@ -139,6 +139,7 @@ def test_cascade_graph_replay_and_guard(dev):
     for q, kc, vc, meta, bt, lens in batches:
         n = len(lens)
         pre, spans, _ = A.prefix_groups(bt, np.asarray(lens), 16, Hq // Hkv)
+        part, items, _ = A.cascade_layout(pre, spans, NI)
         kd.zero_()
         vd.zero_()
         kd[: kc.shape[0]].copy_(kc)
@@ -151,9 +152,9 @@ def test_cascade_graph_replay_and_guard(dev):
         ctx_d[:n].copy_(meta.ctx_len)
         pre_d.zero_()
         pre_d[:n].copy_(torch.from_numpy(pre))
-        g = np.zeros((B // 2, 2), dtype=np.int32)
-        g[:len(spans)] = spans
-        grp_d.copy_(torch.from_numpy(g.reshape(-1)))
+        part_d.zero_()
+        part_d[:n].copy_(torch.from_numpy(part))
+        items_d.copy_(torch.from_numpy(items.reshape(-1)))
         graph.replay()
         torch.cuda.synchronize()
         ref = A.paged_attention_ref(q, kc, vc, meta, scale).reshape(n, -1)
