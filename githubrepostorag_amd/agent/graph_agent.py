@@ -20,6 +20,7 @@ import json
 import logging
 import re
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Optional
 
@@ -42,6 +43,9 @@ SYNTH_PRIORITY = 3
 # synthesize-retry reuse the synthesize call's KV of the documents
 _SHARED_CONTEXT = __import__("os").environ.get("GRAG_AGENT_SHARED_CONTEXT", "0") == "1"
 _SHARED_JUDGE = __import__("os").environ.get("GRAG_AGENT_SHARED_JUDGE", "0") == "1"
+# every LLM call of a job queues by the job's start time within its priority (RunContext.order);
+# GRAG_AGENT_JOB_ORDER=0: each call by its own arrival (the engine's plain FCFS)
+_JOB_ORDER = __import__("os").environ.get("GRAG_AGENT_JOB_ORDER", "1") == "1"
 
 
 class Cancelled(Exception):
@@ -123,6 +127,10 @@ class RunContext:
     on_answer_token: Optional[Callable[[str], None]] = None
     turns: list = field(default_factory=list)
     trace: Any = NULL_TRACE  # utils.tracing.Trace: per-stage / per-LLM-call spans
+    # the job's start (time.perf_counter): every LLM call of the job queues by it within its priority
+    # (SamplingParams.order), so jobs in progress finish ahead of newer jobs' first calls instead of all
+    # jobs sharing the engine evenly
+    order: float | None = None
 
     def notify(self, payload: dict) -> None:
         if self.progress_cb:
@@ -159,6 +167,8 @@ class GraphAgent:
         ctx.check()
         if ctx.cancel_check is not None:
             kw["cancel_check"] = ctx.cancel_check
+        if ctx.order is not None and _JOB_ORDER:
+            kw.setdefault("order", ctx.order)
         with ctx.trace.span("llm", purpose=purpose) as sp:
             r = yield ("llm", prompt, kw)
             for k in ("ttft_s", "tokens", "error"):
@@ -461,7 +471,8 @@ class GraphAgent:
         ``top_k``, which the reference accepts but never reads
         (rag_shared/models.py:6-14): here ``repo`` pins the repo
         filter of every retrieval and ``top_k`` caps the retrieved documents."""
-        ctx = RunContext(progress_cb, cancel_check, on_answer_token, trace=trace or NULL_TRACE)
+        ctx = RunContext(progress_cb, cancel_check, on_answer_token, trace=trace or NULL_TRACE,
+                         order=time.perf_counter())
         return self._drive_sync(self._run_g(question, ctx, namespace, force_level, repo, top_k))
 
     async def arun(self, question: str, *, namespace: str | None = None, progress_cb=None, cancel_check=None,
@@ -476,7 +487,8 @@ class GraphAgent:
         from ..index.sharded_store import round_health
 
         loop = asyncio.get_running_loop()
-        ctx = RunContext(progress_cb, cancel_check, on_answer_token, trace=trace or NULL_TRACE)
+        ctx = RunContext(progress_cb, cancel_check, on_answer_token, trace=trace or NULL_TRACE,
+                         order=time.perf_counter())
         acomplete = getattr(self.llm, "acomplete", None)
 
         def search(scope, q, filters):

@@ -117,7 +117,7 @@ class EngineLLM:
 
     def params(self, **kw) -> SamplingParams:
         d = dict(self.defaults)
-        for k in ("temperature", "top_p", "repetition_penalty", "top_k", "seed", "priority"):
+        for k in ("temperature", "top_p", "repetition_penalty", "top_k", "seed", "priority", "order"):
             if kw.get(k) is not None:
                 d[k] = kw[k]
         mt = kw.get("max_tokens") or kw.get("max_completion_tokens") or self.max_tokens

@@ -38,6 +38,18 @@ from .sequence import Sequence, SeqStatus
 INTERACTIVE_PRIORITY = 2
 
 
+def _order(seq) -> float:
+    """A sequence's queue key within its priority (SamplingParams.order, else its arrival)."""
+    o = seq.params.order
+    return seq.arrival if o is None else o
+
+
+def _before(other, pr: int, key: float) -> bool:
+    """``other`` (already waiting) goes before a new request of priority ``pr`` and queue key ``key``."""
+    op = other.params.priority
+    return op > pr or (op == pr and _order(other) <= key)
+
+
 class KVCacheManager:
     SCRATCH_BLOCK = 0  # never handed out: padding rows of graph-captured batches point here
 
@@ -166,14 +178,17 @@ class Scheduler:
     def add(self, seq: Sequence) -> None:
         with self.lock:
             pr = seq.params.priority
-            if pr <= 0 or not self.waiting or self.waiting[-1].params.priority >= pr:
-                self.waiting.append(seq)
+            key = _order(seq)
+            w = self.waiting
+            if not w or _before(w[-1], pr, key):
+                w.append(seq)
                 return
-            # insert after the last waiting request of priority >= pr
-            i = len(self.waiting)
-            while i > 0 and self.waiting[i - 1].params.priority < pr:
+            # insert after the last waiting request that goes first: higher priority, or the same priority
+            # and an order key not above this one (FIFO among equal keys)
+            i = len(w)
+            while i > 0 and not _before(w[i - 1], pr, key):
                 i -= 1
-            self.waiting.insert(i, seq)
+            w.insert(i, seq)
 
     def has_work(self) -> bool:
         return bool(self.waiting or self.running)
@@ -218,8 +233,9 @@ class Scheduler:
         victims = [s for s in self.running if s is not keep]
         if not victims:
             return False
-        # lowest priority first (a bulk ingest sequence before an interactive query), newest within it
-        v = max(victims, key=lambda s: (-s.params.priority, s.arrival))
+        # lowest priority first (a bulk ingest sequence before an interactive query), newest within it (by the
+        # queue key: an agent job's call carries its job's start, so the newest JOB gives its blocks back first)
+        v = max(victims, key=lambda s: (-s.params.priority, _order(s)))
         self.running.remove(v)
         if v in self.prefilling:
             self.prefilling.remove(v)
@@ -253,7 +269,7 @@ class Scheduler:
             # one merged order: chunks of prompts already in prefill and new admissions, higher priority first,
             # in-flight prompts first within a priority -- an interactive arrival (priority 2) takes this step's
             # budget ahead of the remaining chunks of a bulk ingest prompt admitted earlier
-            pf = sorted(self.prefilling, key=lambda q: -q.params.priority) if self.prefilling else []
+            pf = sorted(self.prefilling, key=lambda q: (-q.params.priority, _order(q))) if self.prefilling else []
             i = 0
             admit_ok = True
             bulk_left = bulk_budget if bulk_budget is not None else 1 << 30

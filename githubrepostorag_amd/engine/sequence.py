@@ -25,6 +25,9 @@ class SamplingParams:
     seed: int | None = None
     min_tokens: int = 0
     priority: int = 0  # higher is admitted first (critical-path requests ahead of bulk waves)
+    # queue key within a priority, lower first (None: the request's arrival).  An agent job's calls carry the
+    # job's start time, so an older job's next call is admitted and prefilled before newer jobs' calls
+    order: float | None = None
 
 
 class SeqStatus(enum.Enum):

@@ -499,3 +499,23 @@ def test_interactive_reserve_beside_bulk_admissions():
     # preemption victim: lowest priority first
     sch.running.sort(key=lambda s: s.arrival)
     assert sch._preempt_one(keep=sch.running[0]) and q in sch.running
+
+
+def test_queue_order_key_puts_older_jobs_first():
+    """SamplingParams.order (an agent job's start time on each of its calls): within a priority the waiting
+    queue and the chunked-prefill pass go by the key, so an older job's next call is admitted / prefilled
+    before newer jobs' calls; requests without a key keep FCFS by arrival; priority still comes first."""
+    from githubrepostorag_amd.engine.scheduler import KVCacheManager, Scheduler
+
+    sch = Scheduler(KVCacheManager(num_blocks=400, block_size=16), 2, 4096, 4096, mixed_batches=False)
+    mk = lambda name, **kw: Sequence(name, list(range(3, 200)), SamplingParams(**kw))  # noqa: E731
+    for s in (mk("new1", order=30.0), mk("new2", order=31.0), mk("old", order=10.0), mk("mid", order=20.0),
+              mk("synth", priority=3, order=40.0), mk("plain")):
+        sch.add(s)
+    # "plain" has no key: its arrival (perf_counter, far above these keys) queues it last
+    assert [s.req_id for s in sch.waiting] == ["synth", "old", "mid", "new1", "new2", "plain"]
+    kind, items = sch.schedule(4096)  # two slots: the synthesize call and the oldest job's call
+    assert kind == "prefill" and [it[0].req_id for it in items] == ["synth", "old"]
+    # the newest job (by key) is the preemption victim among equal priorities
+    sch.running.append(sch.waiting.popleft())  # "mid" as if admitted too
+    assert sch._preempt_one(keep=sch.running[0]) and [s.req_id for s in sch.running] == ["synth", "old"]
