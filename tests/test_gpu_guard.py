@@ -115,12 +115,12 @@ def _lazy_capture_beside_search(rank, world):
         stats = {"capture_s": 0.0}
         trace = None
 
-        def _capture_prepare(self, B, nsplit, split_len, K):
+        def _capture_prepare(self, B, nsplit, split_len, K, npre=0):
             t = torch.ones(1)
             dist.all_reduce(t, group=tp)  # the warm-up step's TP all-reduce
             return t
 
-        def _capture_locked(self, B, nsplit, split_len, K, prep):
+        def _capture_locked(self, B, nsplit, split_len, K, prep, npre=0):
             time.sleep(0.01)  # the capture itself: local work only
             captured.append(B)
             return None
