@@ -80,6 +80,9 @@ class EngineConfig:
     cascade_decode: bool = __import__("os").environ.get("GRAG_CASCADE", "1") == "1"
 
 
+_SPLIT_MID = int(__import__("os").environ.get("GRAG_DECODE_SPLIT_128", "1024"))
+
+
 def _split_len_for(batch: int) -> int:
     """Keys per split-KV part of the decode attention (flash-decoding) for a batch size.  Small batches
     need splits to put enough waves on the CUs (B64 ctx1152: split 256 36.7 us < split 512 38.0 us); from
@@ -87,8 +90,10 @@ def _split_len_for(batch: int) -> int:
     combine pass and the partial round trip: B512 ctx1100 251 -> 233 / 225 / 210 us at parts of 512 /
     1024 / 2048 keys, B256 ctx1100 125 -> 105 us at 2048 (profiles/mb_decode_splits_r3.json).  The part
     length still caps one wave's keys, so a long sequence among short ones is split."""
-    if batch >= 128:  # B176 ctx1500: one 2048-key part 96.5 us vs 256-key parts 121.2 (profiles/attn_sweep_r5_mw.json)
+    if batch >= 160:  # B176 ctx1500: one 2048-key part 96.5 us vs 256-key parts 121.2 (profiles/attn_sweep_r5_mw.json)
         return 32 * KV_TILE
+    if batch >= 128:  # B128 ctx1500: 2 x 1024 keys 67.8 us vs one 2048-key part 87.7 (profiles/attn_sweep_r6.json)
+        return _SPLIT_MID
     if batch >= 8:
         return 4 * KV_TILE
     return 2 * KV_TILE

@@ -24,7 +24,12 @@ _DEC_AUTO = "GRAG_DECODE_STAGES" not in os.environ and os.environ.get("GRAG_DECO
 # TB/s), B1024 413.7 -> 382.5, B256 113.3 -> 97.7, B176 ctx3000 (3 stages) 208.0 -> 197.0, B16 ctx6000 50.2 ->
 # 48.0; grids under ~1.5K waves gain nothing (B64 ctx1152 x 5 parts: 35.8 vs 36.7, B1: equal) -> default there
 DECODE_NT = {3: 11, 8: 12}
-DECODE_NT_MIN_WAVES = 1536
+# round 6 (profiles/attn_sweep_r6.json, one box): nt pays from ~700 waves too -- B176 ctx1500 one part 94.6 ->
+# 89.3 us, B256 134.8 -> 117.9 -- so the threshold moved down from 1536 waves
+DECODE_NT_MIN_WAVES = int(os.environ.get("GRAG_DECODE_NT_MIN_WAVES", "512"))
+# multi-part plans over >= this many (sequence x kv head) rows take the 3-stage ring: B192 ctx3000 (2 parts of
+# 2048 keys) 222.7 -> 191.7 us, B128 ctx1500 (2 x 1024) 73.5 -> 67.8 (0: off)
+DECODE_NS3_ROWS = int(os.environ.get("GRAG_DECODE_NS3_ROWS", "512"))
 _DEC_NT = os.environ.get("GRAG_DECODE_NT", "auto")
 
 
@@ -80,6 +85,9 @@ def decode_variant(nsplit: int, split_len: int, waves: int | None = None) -> int
     # GRAG_DECODE_STAGES asks (the round-4 auto rule is kept behind GRAG_DECODE_RING_AUTO=1)
     auto3 = _DEC_AUTO and os.environ.get("GRAG_DECODE_RING_AUTO") == "1"
     nw = DECODE_RING_NW[3] if auto3 and nsplit > 1 and nsplit * split_len > 2048 else DECODE_NW
+    if (_DEC_AUTO and DECODE_NS3_ROWS and nsplit > 1 and waves is not None
+            and waves // nsplit >= DECODE_NS3_ROWS):
+        nw = DECODE_RING_NW[3]
     nt = _DEC_NT == "1" or (_DEC_NT == "auto" and waves is not None and waves >= DECODE_NT_MIN_WAVES)
     return DECODE_NT.get(nw, nw) if nt else nw
 
