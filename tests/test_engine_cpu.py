@@ -2,6 +2,8 @@
 prefill, prefix cache, preemption, abort, stop handling, the native block
 allocator and the tokenizers.  The GPU tier (test_engine_gpu.py) repeats the
 numerics on the HIP kernels with hipGraph decode windows."""
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -519,3 +521,28 @@ def test_queue_order_key_puts_older_jobs_first():
     # the newest job (by key) is the preemption victim among equal priorities
     sch.running.append(sch.waiting.popleft())  # "mid" as if admitted too
     assert sch._preempt_one(keep=sch.running[0]) and [s.req_id for s in sch.running] == ["synth", "old"]
+
+
+def test_pacing_hold_lasts_while_bulk_work_is_in_flight(model, tok):
+    """The arrival-pacing hold applies while bulk (ingest) requests are in flight -- not only for a few seconds
+    after their submit, which dropped it in the middle of an ingest wave's long decode -- and ends once they
+    finish and the recent-submit window has passed."""
+    from githubrepostorag_amd.engine.runner import EngineRunner
+
+    eng = LLMEngine(model, tok, EngineConfig(max_num_seqs=4, max_num_batched_tokens=64, use_cuda_graph=False))
+    runner = EngineRunner(eng)
+    try:
+        hs = [runner.submit([5, 6, 7, 8 + i], SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True),
+                            interactive=False) for i in range(3)]
+        assert runner._bulk_live == 3
+        runner._last_bulk = -1e9  # the recent-submit window is long gone: in-flight bulk work alone holds
+        assert runner._hold(time.monotonic()) == runner.PACE_HOLD_S or all(h.done.is_set() for h in hs)
+        for h in hs:
+            h.wait(60)
+        assert runner._bulk_live == 0
+        assert runner._hold(time.monotonic()) == 0.0
+        h = runner.submit([9, 9, 9], SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True))
+        h.wait(60)
+        assert runner._bulk_live == 0  # interactive requests are not counted
+    finally:
+        runner.shutdown()
