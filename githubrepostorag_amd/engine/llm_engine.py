@@ -745,11 +745,15 @@ class LLMEngine:
         t0 = time.perf_counter()
         n = len(seqs)
         casc = False
-        k = _CASCADE_PROBE
-        if self.cfg.cascade_decode and n >= 8 and len({s.blocks[k] for s in seqs if len(s.blocks) > k}) < sum(
-                len(s.blocks) > k for s in seqs):
-            # (the prefix cache hands out one block id per (content, prefix) chain, so two rows holding the same
-            # id at block index k share their first k + 1 blocks: a group of >= min_blocks is possible)
+        probe = None
+        if self.cfg.cascade_decode and n >= 8:
+            # the prefix cache hands out one block id per (content, prefix) chain, so two rows holding the same
+            # id at block index k share their first k + 1 blocks.  Probe at the index a group's prefix must
+            # reach for the window to save CASCADE_MIN of its keys (at least min_blocks): a batch whose rows
+            # share only a short system prompt is not sorted and grouped every window
+            k = max(_CASCADE_PROBE, int(CASCADE_MIN * sum(s.total_len for s in seqs) / (n * self.cfg.block_size)))
+            probe = [s.blocks[k] for s in seqs if len(s.blocks) > k]
+        if probe and len(set(probe)) < len(probe):
             # some rows share a cached prompt prefix (ingest's summary / title / keyword calls of one chunk, an
             # agent job's calls over the same documents): rows side by side by leading block ids, so the
             # shared-prefix decode (ops/attention.prefix_groups) can group adjacent rows
