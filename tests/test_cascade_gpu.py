@@ -174,3 +174,33 @@ def test_cascade_graph_replay_and_guard(dev):
     assert codes & (1 << 9)
     with pytest.raises(DeviceIndexError):
         check_device_errors("bad prefix")
+
+
+def test_engine_decode_graphs_take_the_shared_prefix_path(dev, monkeypatch):
+    """The engine end to end: rows whose prompts share cached blocks are grouped, the window takes the
+    shared-prefix variant of its decode graph (cascade_windows > 0), and every greedy token stays within bf16
+    tolerance of a prefill recompute of the full prefix."""
+    import githubrepostorag_amd.engine.llm_engine as LE
+    from githubrepostorag_amd.engine.sequence import SamplingParams
+    from githubrepostorag_amd.engine.tokenizer import ByteBPETokenizer
+    from githubrepostorag_amd.models.configs import decoder_config
+    from githubrepostorag_amd.models.qwen2 import Qwen2Model
+
+    from _logits import greedy_within_tolerance
+
+    monkeypatch.setattr(LE, "CASCADE_MIN_WAVES", 0)  # 15 rows: a prefix grid far below the production gate
+    cfg = decoder_config("qwen2-small")
+    model = Qwen2Model(cfg, device=dev, seed=0)
+    tok = ByteBPETokenizer(cfg.vocab_size)
+    base = [tok.encode(f"shared context block {g}: the widgets module retries failed jobs. " * 16) for g in range(3)]
+    eng = LE.LLMEngine(model, tok, LE.EngineConfig(max_num_seqs=32, max_model_len=2048, num_blocks=2048,
+                                                   use_cuda_graph=True))
+    eng.generate([b + [7] for b in base], SamplingParams(max_tokens=1, temperature=0.0))  # cache the prefixes
+    prompts = [b + tok.encode(f" question {i}?") for b in base for i in range(5)]
+    outs = eng.generate(prompts, SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
+    st = eng.stats
+    assert st["cascade_windows"] > 0 and st["cascade_saved_keys"] > 0.3 * st["decode_keys"], st
+    assert st["graph_replays"] > 0
+    for p, o in list(zip(prompts, outs))[::3]:
+        assert len(o.token_ids) == 8
+        greedy_within_tolerance(model, dev, p, o.token_ids)
