@@ -141,7 +141,18 @@ struct DArgs {
   int msplit;                       // row blocks of 16*MT (adjacent on one XCD: the W lines are shared in L2)
   int packed;                       // W in the unit-packed layout (grag_gemm_decode doc)
   unsigned long long* stamps;       // diagnostics (grag_gemm_decode_stamps): per workgroup {start, end, xcc} or null
+  // NRM (grag_gemm_decode_norm): A = RMSNorm(residual + sum of the producer's split-K planes) * nw, formed in the
+  // prologue (p.A unused)
+  const float* nplanes;  // [nS][M][K] fp32
+  int nS;
+  const bf16* nres_in;   // [M][K] residual stream before this add (read only)
+  bf16* nres_out;        // [M][K] residual stream after it (written by workgroup 0)
+  const bf16* nw;        // [K] norm weight
+  float neps;
 };
+
+constexpr int kNrmRows = 4;         // NRM: rows of the batch (the reference's --max-num-seqs 4)
+constexpr int kNrmLds = 64 * 1024;  // NRM: LDS image of the normalised rows, [M][K + 32] bf16
 
 // NTW 16-row n-tiles per wave (32 or 64 W rows): the A fragment read from LDS feeds NTW MFMAs, so NTW = 4
 // halves the LDS read traffic per MFMA (at NTW = 2 it equals the LDS bandwidth at full MFMA rate).
@@ -150,18 +161,25 @@ struct DArgs {
 // waves each) then carry 1.25 units of MFMA work apiece where a 5-wave workgroup put 2 units on one SIMD
 // (profiles/pmc_dec_r5.txt: Qwen2-7B gate/up at 176 rows, 4.625 units per CU on 256 CUs; the doubled SIMD
 // paced every K-step barrier).  Waves 4-7 load the shared unit's W rows alike (L1 / L2 hits after the first).
-template <int EPI, int ACT, int MT, int D, int NWV, int NTW, int TQ = 0>
+// NRM = 1 (MT = 1, TQ = 0, one K-range): the RMSNorm that feeds this projection runs in the prologue -- every
+// workgroup sums the producer's split-K planes into the residual row(s), forms the row's RMS and writes the
+// normalised rows into an LDS-resident image the whole K loop reads its A fragments from (no A LDS-DMA ring,
+// no per-K-step barrier); workgroup 0 also writes the new residual to a second buffer (no other workgroup
+// reads what it writes).  Replaces the split-K RMSNorm launch between o_proj and gate/up at 1-4 rows.
+template <int EPI, int ACT, int MT, int D, int NWV, int NTW, int TQ = 0, int NRM = 0>
 __global__ __launch_bounds__(64 * NWV, (NWV == 4 && NTW == 2 && (D + 1) * MT * 2 <= 80) ? 2 : 1)
 void gemm_dec_kernel(DArgs p) {
   static_assert(TQ == 0 || (NWV == 8 && TQ * 4 == MT), "tail split: 8 waves, MT = 4 TQ");
+  static_assert(NRM == 0 || (MT == 1 && TQ == 0), "NRM: one 16-row tile");
   constexpr int NST = D + 1;            // LDS stages = W register slots
   constexpr int ABYTES = MT * 16 * 128;  // one K-step of A
   constexpr int NPC = MT * 2;                  // A pieces (1 KiB = 8 rows x 128 B) per K-step
-  constexpr int GA = (NPC + NWV - 1) / NWV;    // per wave (the last wave may repeat its final piece)
+  constexpr int GA = NRM ? 0 : (NPC + NWV - 1) / NWV;  // per wave (the last wave may repeat its final piece)
   constexpr int GW = 2 * NTW;                  // W dwordx4 per lane per K-step
   static_assert(NTW == 2 || NTW == 4, "NTW");
   static_assert(NST * ABYTES <= 160 * 1024, "LDS ring exceeds 160 KB");
-  __shared__ __attribute__((aligned(16))) char smem[NST * ABYTES];
+  constexpr int LDSB = NRM ? kNrmLds : NST * ABYTES;
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
 
   const int tid = threadIdx.x;
   const int L = tid & 63;
@@ -213,8 +231,8 @@ void gemm_dec_kernel(DArgs p) {
 
   // A pieces: piece q = w*GA + i covers rows [8q, 8q+8); lane -> row 8q + L/8, physical chunk L%8
   // 32-bit element offsets (not 64-bit pointers): the MT = 16, 5-wave variant needs the registers
-  uint32_t ao[GA];
-  uint32_t adst[GA];
+  uint32_t ao[GA > 0 ? GA : 1];
+  uint32_t adst[GA > 0 ? GA : 1];
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
@@ -301,6 +319,106 @@ void gemm_dec_kernel(DArgs p) {
 #pragma unroll
   for (int d = 0; d < D; ++d) issue(d, d, wf[d]);
 
+  // NRM: the A rows, normalised, into the LDS image while the first W steps are in flight.  Same arithmetic
+  // as splitk_rmsnorm_kernel (norm.hip): the planes added to the bf16 residual in fp32, the sum rounded to
+  // bf16 (the residual stream's precision), the RMS over the rounded row, out = bf16(h * inv * w).
+  const int nrp = p.K * 2 + 64;  // image row pitch (bytes): rows start 64 B apart in the bank space
+  if constexpr (NRM) {
+    __shared__ float nred[NWV][kNrmRows];
+    __shared__ float ninv[kNrmRows];
+    const int nvec = p.K >> 3;
+    const int tot = p.M * nvec;  // (row, 8-column unit) pairs, all rows in one pass
+    const size_t plane = (size_t)p.M * p.K;
+    const int nthr = 64 * NWV;
+    const bool writer = blockIdx.x == 0;  // one workgroup writes the new residual (to its own buffer)
+    float ssr[kNrmRows] = {0.f, 0.f, 0.f, 0.f};
+    // two units per thread per round, every plane load of both issued before any add: the round costs one
+    // L2 round trip, not one per unit
+    for (int e0 = tid; e0 < tot; e0 += 2 * nthr) {
+      const int e1 = e0 + nthr;
+      const bool has1 = e1 < tot;
+      const int m0 = e0 / nvec, u0 = e0 - m0 * nvec;
+      const int m1 = has1 ? e1 / nvec : m0, u1 = has1 ? e1 - m1 * nvec : u0;
+      float a[8], b[8];
+      unpack8(reinterpret_cast<const bf16x8_t*>(p.nres_in + (size_t)m0 * p.K)[u0], a);
+      unpack8(reinterpret_cast<const bf16x8_t*>(p.nres_in + (size_t)m1 * p.K)[u1], b);
+      const float* q0 = p.nplanes + (size_t)m0 * p.K + u0 * 8;
+      const float* q1 = p.nplanes + (size_t)m1 * p.K + u1 * 8;
+      for (int sp = 0; sp < p.nS; ++sp) {
+        const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(q0 + sp * plane);
+        const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(q0 + sp * plane + 4);
+        const f32x4_t y0 = *reinterpret_cast<const f32x4_t*>(q1 + sp * plane);
+        const f32x4_t y1 = *reinterpret_cast<const f32x4_t*>(q1 + sp * plane + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] += x0[j];
+          a[j + 4] += x1[j];
+          b[j] += y0[j];
+          b[j + 4] += y1[j];
+        }
+      }
+      const bf16x8_t ha = pack8(a), hb = pack8(b);
+      if (writer) {
+        reinterpret_cast<bf16x8_t*>(p.nres_out + (size_t)m0 * p.K)[u0] = ha;
+        if (has1) reinterpret_cast<bf16x8_t*>(p.nres_out + (size_t)m1 * p.K)[u1] = hb;
+      }
+      *reinterpret_cast<bf16x8_t*>(smem + m0 * nrp + u0 * 16) = ha;
+      if (has1) *reinterpret_cast<bf16x8_t*>(smem + m1 * nrp + u1 * 16) = hb;
+      unpack8(ha, a);
+      unpack8(hb, b);
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sa += a[j] * a[j];
+        sb += b[j] * b[j];
+      }
+#pragma unroll
+      for (int m = 0; m < kNrmRows; ++m) ssr[m] += (m == m0 ? sa : 0.f) + (has1 && m == m1 ? sb : 0.f);
+    }
+    const int wv = tid >> 6;
+#pragma unroll
+    for (int m = 0; m < kNrmRows; ++m) {
+      const float t = wave_sum(ssr[m]);
+      if ((tid & 63) == 0) nred[wv][m] = t;
+    }
+    __syncthreads();
+    if (tid < p.M) {
+      float t = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < NWV; ++w2) t += nred[w2][tid];
+      ninv[tid] = rsqrtf(t / (float)p.K + p.neps);
+    }
+    __syncthreads();
+    const bf16x8_t* gw = reinterpret_cast<const bf16x8_t*>(p.nw);
+    for (int e = tid; e < tot; e += nthr) {
+      const int m = e / nvec, u = e - m * nvec;
+      float a[8], g[8];
+      char* cell = smem + m * nrp + u * 16;
+      unpack8(*reinterpret_cast<const bf16x8_t*>(cell), a);
+      unpack8(gw[u], g);
+      const float inv = ninv[m];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = a[j] * inv * g[j];
+      *reinterpret_cast<bf16x8_t*>(cell) = pack8(a);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the W steps in flight landed too: the loop's waits hold)
+    __syncthreads();
+  }
+  // NRM: A fragments of absolute K-step `step` from the image (rows >= M are zero, never read)
+  auto compute_nrm = [&](int step, bf16x8_t (&wreg)[GW]) {
+    bf16x8_t a0 = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0}, a1 = a0;
+    if (li < p.M) {
+      const char* r = smem + li * nrp + ((kb + step) * 64 + 8 * h4) * 2;
+      a0 = *reinterpret_cast<const bf16x8_t*>(r);
+      a1 = *reinterpret_cast<const bf16x8_t*>(r + 64);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[2 * nt], a0, acc[0][nt], 0, 0, 0);
+      acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[2 * nt + 1], a1, acc[0][nt], 0, 0, 0);
+    }
+  };
+
   // A K-step's LDS slot is read one barrier interval AFTER the wait that retires its LDS-DMA (cdna guide §5
   // "Read a staged buffer one phase AFTER the wait that retires it"): iteration t retires step t + 1 and
   // computes step t.  The round-2 schedule (retire step t, barrier, read step t) is the one that returned
@@ -313,9 +431,13 @@ void gemm_dec_kernel(DArgs p) {
 #pragma unroll
     for (int u = 0; u < NST; ++u) {
       wait_w<(D - 2) * (GA + GW)>(wf[(u + 1) % NST]);  // retire step t + 1
-      bar();  // every wave is done with slot (u + D) % NST (= step t - 1's); step t + 1 retired everywhere
+      if constexpr (!NRM) bar();  // every wave is done with slot (u + D) % NST (= step t - 1's); step t + 1 retired everywhere
       issue(t0 + u + D, (u + D) % NST, wf[(u + D) % NST]);
-      if (t0 + u < nsteps) compute(u, wf[u]);  // uniform: a split's last round may be partial
+      if constexpr (NRM) {
+        if (t0 + u < nsteps) compute_nrm(t0 + u, wf[u]);
+      } else {
+        if (t0 + u < nsteps) compute(u, wf[u]);  // uniform: a split's last round may be partial
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing re-reads land before the workgroup retires
@@ -385,6 +507,15 @@ void gemm_dec_kernel(DArgs p) {
       }
     }
   }
+}
+
+template <int D, int NWV>
+int launch_nrm(const DArgs& a, int epi, int nwg, hipStream_t s) {
+  if (epi == EPI_SILU)
+    gemm_dec_kernel<EPI_SILU, ACT_NONE, 1, D, NWV, 2, 0, 1><<<nwg, 64 * NWV, 0, s>>>(a);
+  else
+    gemm_dec_kernel<EPI_STORE, ACT_NONE, 1, D, NWV, 2, 0, 1><<<nwg, 64 * NWV, 0, s>>>(a);
+  return (int)hipGetLastError();
 }
 
 template <int MT, int D, int NWV, int NTW, int TQ = 0>
@@ -523,4 +654,48 @@ GRAG_API int grag_gemm_decode(const void* A, const void* W, const void* bias, vo
                               int packed, void* ws, hipStream_t stream) {
   return grag_gemm_decode_t(A, W, bias, C, lda, ldw, ldc, M, N, K, epi, act, mt, nwv, ntw, ksplit, gs, packed, 0, ws,
                             stream);
+}
+
+// y = epilogue(RMSNorm(res_in + sum_s planes[s]) * nw @ w^T) for M <= 4 rows (NRM kernel): the split-K RMSNorm
+// of a decoder layer folded into the projection that consumes it.  planes: the producer's fp32 split-K planes
+// [S][M][K] (16-B aligned); res_in [M][K] the residual stream before the add, res_out [M][K] after it
+// (written by one workgroup; must not alias res_in); nw [K] the norm weight.  mt must be 1, one K-range
+// (ksplit 1), epi 0 (no bias / act) or 1 (silu*mul), K <= 8160; other arguments as grag_gemm_decode_t.
+GRAG_API int grag_gemm_decode_norm(const void* planes, int S, const void* res_in, void* res_out, const void* nw,
+                                   float eps, const void* W, void* C, int ldw, int ldc, int M, int N, int K,
+                                   int epi, int mt, int nwv, int ntw, int gs, int packed, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > kNrmRows || mt != 1 || ntw != 2 || (nwv != 4 && nwv != 5) || S < 1 || !planes || !res_in || !res_out ||
+      !nw || res_in == res_out || (epi != EPI_STORE && epi != EPI_SILU))
+    return (int)hipErrorInvalidValue;
+  if (K % 64 != 0 || K < 64 || M * (K * 2 + 64) > kNrmLds || N % 32 != 0 || ldw % 8 != 0 || ldc % 4 != 0 ||
+      (epi == EPI_SILU && N % 64 != 0) || packed < 0 || packed > 2 || (packed == 2 && N % 64 != 0))
+    return (int)hipErrorInvalidValue;
+  const int units = N / 32;
+  if (gs <= 0) {
+    if (units % nwv != 0) return (int)hipErrorInvalidValue;
+    gs = units / nwv;
+  }
+  if (gs > units || (units + gs - 1) / gs > nwv) return (int)hipErrorInvalidValue;
+  DArgs a{};
+  a.A = nullptr;
+  a.W = (const bf16*)W;
+  a.bias = nullptr;
+  a.C = C;
+  a.lda = K; a.ldw = ldw; a.ldc = ldc;
+  a.M = M; a.N = N; a.K = K;
+  a.units = units;
+  a.gs = gs;
+  a.msplit = 1;
+  a.packed = packed;
+  a.stamps = nullptr;
+  a.ksplit = 1;
+  a.kt_split = K / 64;
+  a.nplanes = (const float*)planes;
+  a.nS = S;
+  a.nres_in = (const bf16*)res_in;
+  a.nres_out = (bf16*)res_out;
+  a.nw = (const bf16*)nw;
+  a.neps = eps;
+  return nwv == 4 ? launch_nrm<kDepth, 4>(a, epi, gs, stream) : launch_nrm<kDepth, 5>(a, epi, gs, stream);
 }

@@ -31,7 +31,8 @@ import torch
 
 from ..ops.attention import AttnMetadata, paged_attention
 from ..ops.elementwise import qkv_rope_kvstore, rope_cos_sin, silu_mul
-from ..ops.gemm import deinterleave_gate_up, interleave_gate_up, mlp_gate_up
+from ..ops.gemm import (EPI_SILU, SplitKPartial, deinterleave_gate_up, gemm_decode_norm, interleave_gate_up,
+                        mlp_gate_up, norm_fuse_plan)
 from ..ops.linear import linear, linear_deferred
 from ..ops.norm import embed_gather, rmsnorm
 from ..parallel.comm import Group
@@ -260,8 +261,16 @@ class Qwen2Model:
                                  self.hq, self.hkv, self.head_dim)
             a = paged_attention(q, kc, vc, meta, self.scale, causal=True)
             h = self.tp.all_reduce(self._proj(a, L, "o_w", defer=defer))
-            x = rmsnorm(h, L.post_norm, eps, residual=residual)
-            m = self._proj(x, L, "gu_w")
+            plan = None
+            if isinstance(h, SplitKPartial) and self.gu_interleaved and not self.w4_enabled:
+                plan = norm_fuse_plan(h.M, L.gu_w.shape[0], h.N, True)
+            if plan is not None:  # 1-4 rows: the post-attention norm folded into the gate/up launch
+                r_new = torch.empty_like(residual)
+                m = gemm_decode_norm(h, residual, r_new, L.post_norm, eps, L.gu_w, EPI_SILU, plan)
+                residual = r_new
+            else:
+                x = rmsnorm(h, L.post_norm, eps, residual=residual)
+                m = self._proj(x, L, "gu_w")
             h = self.tp.all_reduce(self._proj(m, L, "down_w", defer=defer))
         return rmsnorm(h, self.norm, eps, residual=residual)
 

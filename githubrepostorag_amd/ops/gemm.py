@@ -547,6 +547,44 @@ def gemm_decode(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
     return out
 
 
+# the split-K RMSNorm folded into the gate/up projection that consumes it at 1-4 rows (grag_gemm_decode_norm).
+# Off by default: measured slower (profiles/norm_fold_ab_r6.json, same box): every workgroup re-reduces the
+# o_proj planes in its prologue while only D = 4 K-steps of W are in flight, so the W stream -- the kernel's
+# bound -- starts ~6.4 us late, more than the 5.6 us norm launch it replaces (B = 1 TPOT 3.83 vs 3.81 ms, B = 4
+# 4.10 vs 3.90).  GRAG_NORM_FUSE=1 turns it on (A/B, tests/test_norm_fuse_gpu.py)
+NORM_FUSE = os.environ.get("GRAG_NORM_FUSE", "0") == "1"
+
+
+def norm_fuse_plan(M: int, N: int, K: int, silu: bool) -> tuple[int, int] | None:
+    """(nwv, gs) when grag_gemm_decode_norm takes the consumer projection of a deferred norm: the decode plan
+    of (M, N, K) is a one-tile (mt 1), one-K-range plan on the 4- / 5-wave grid and the rows fit its LDS
+    image; else None."""
+    if not NORM_FUSE or M < 1 or M > 4 or M * (K * 2 + 64) > 65536:
+        return None
+    p = dec_plan(M, N, K, silu)
+    if p is None:
+        return None
+    mt, nwv, ntw, ks, *rest = p
+    gs = rest[0] if rest else 0
+    tail = rest[1] if len(rest) > 1 else 0
+    if mt != 1 or ntw != 2 or nwv not in (4, 5) or tail or dec_ksplit(K, ks) != 1:
+        return None
+    return nwv, gs
+
+
+def gemm_decode_norm(part: "SplitKPartial", res_in: torch.Tensor, res_out: torch.Tensor, w_norm: torch.Tensor,
+                     eps: float, w: torch.Tensor, epi: int, plan: tuple[int, int]) -> torch.Tensor:
+    """epilogue(RMSNorm(res_in + reduce(part)) * w_norm @ w.T) in one launch (csrc/kernels/gemm_decode.hip NRM
+    kernel); res_out receives the new residual stream (res_in + reduce(part), bf16).  ``plan`` from
+    norm_fuse_plan.  Out [M, N/2] for EPI_SILU (interleaved gate/up weight), [M, N] for EPI_STORE."""
+    M, K, N = part.M, part.N, w.shape[0]
+    nwv, gs = plan
+    out = torch.empty(M, N // 2 if epi == EPI_SILU else N, dtype=res_in.dtype, device=res_in.device)
+    call("grag_gemm_decode_norm", ptr(part.planes), part.S, ptr(res_in), ptr(res_out), ptr(w_norm), float(eps),
+         ptr(w), ptr(out), w.stride(0), out.stride(0), M, N, K, epi, 1, nwv, 2, gs, 0)
+    return out
+
+
 class SplitKPartial:
     """The fp32 split-K planes [S, M, N] of a projection whose reduce was deferred to its consumer
     (ops/norm.py rmsnorm: split-K reduce + residual add + RMSNorm in one kernel).  The planes live in the
