@@ -149,6 +149,18 @@ struct DArgs {
   bf16* nres_out;        // [M][K] residual stream after it (written by workgroup 0)
   const bf16* nw;        // [K] norm weight
   float neps;
+  // NRM = 2 (grag_gemm_decode_scaled): A is the residual stream x; the norm weight rides in the A ring's row
+  // 15 (LDS-DMA from `nw`), each A fragment is scaled by it, and the accumulators by 1 / rms(x) (from the
+  // producer's per-group sums of squares nss[nG][kNrmRows]) before the epilogue
+  const float* nss;
+  int nG;
+  // RED = 1 (grag_gemm_decode_red, EPI_PARTIAL): the last split to finish a unit group adds the group's
+  // columns of all splits' planes into the residual stream rres [M][N] (in place, bf16) and writes the
+  // group's sums of squares per row to rss[group][kNrmRows]; rcnt: per-group tickets (zeroed; each last
+  // arriver resets its word)
+  bf16* rres;
+  float* rss;
+  unsigned* rcnt;
 };
 
 constexpr int kNrmRows = 4;         // NRM: rows of the batch (the reference's --max-num-seqs 4)
@@ -166,19 +178,20 @@ constexpr int kNrmLds = 64 * 1024;  // NRM: LDS image of the normalised rows, [M
 // normalised rows into an LDS-resident image the whole K loop reads its A fragments from (no A LDS-DMA ring,
 // no per-K-step barrier); workgroup 0 also writes the new residual to a second buffer (no other workgroup
 // reads what it writes).  Replaces the split-K RMSNorm launch between o_proj and gate/up at 1-4 rows.
-template <int EPI, int ACT, int MT, int D, int NWV, int NTW, int TQ = 0, int NRM = 0>
+template <int EPI, int ACT, int MT, int D, int NWV, int NTW, int TQ = 0, int NRM = 0, int RED = 0>
 __global__ __launch_bounds__(64 * NWV, (NWV == 4 && NTW == 2 && (D + 1) * MT * 2 <= 80) ? 2 : 1)
 void gemm_dec_kernel(DArgs p) {
   static_assert(TQ == 0 || (NWV == 8 && TQ * 4 == MT), "tail split: 8 waves, MT = 4 TQ");
   static_assert(NRM == 0 || (MT == 1 && TQ == 0), "NRM: one 16-row tile");
+  static_assert(RED == 0 || (EPI == EPI_PARTIAL && TQ == 0), "RED: the split-K planes' producer");
   constexpr int NST = D + 1;            // LDS stages = W register slots
   constexpr int ABYTES = MT * 16 * 128;  // one K-step of A
   constexpr int NPC = MT * 2;                  // A pieces (1 KiB = 8 rows x 128 B) per K-step
-  constexpr int GA = NRM ? 0 : (NPC + NWV - 1) / NWV;  // per wave (the last wave may repeat its final piece)
+  constexpr int GA = NRM == 1 ? 0 : (NPC + NWV - 1) / NWV;  // per wave (the last wave may repeat its final piece)
   constexpr int GW = 2 * NTW;                  // W dwordx4 per lane per K-step
   static_assert(NTW == 2 || NTW == 4, "NTW");
   static_assert(NST * ABYTES <= 160 * 1024, "LDS ring exceeds 160 KB");
-  constexpr int LDSB = NRM ? kNrmLds : NST * ABYTES;
+  constexpr int LDSB = NRM == 1 ? kNrmLds : NST * ABYTES;
   __shared__ __attribute__((aligned(16))) char smem[LDSB];
 
   const int tid = threadIdx.x;
@@ -233,13 +246,15 @@ void gemm_dec_kernel(DArgs p) {
   // 32-bit element offsets (not 64-bit pointers): the MT = 16, 5-wave variant needs the registers
   uint32_t ao[GA > 0 ? GA : 1];
   uint32_t adst[GA > 0 ? GA : 1];
+  bool agw[GA > 0 ? GA : 1];  // NRM 2: this lane's piece row is row 15, the norm weight's
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
     const int pc = min(w * GA + i, NPC - 1);
     const int row = pc * 8 + (L >> 3);
     const int c = (L & 7) ^ ((row >> 1) & 7);
-    ao[i] = (uint32_t)min(m0 + row, p.M - 1) * p.lda + kb * 64 + c * 8;
+    agw[i] = NRM == 2 && row == 15;
+    ao[i] = agw[i] ? (uint32_t)(kb * 64 + c * 8) : (uint32_t)min(m0 + row, p.M - 1) * p.lda + kb * 64 + c * 8;
     adst[i] = __builtin_amdgcn_readfirstlane(lds0 + pc * 1024);
   }
 
@@ -258,7 +273,7 @@ void gemm_dec_kernel(DArgs p) {
     const bool live = step < nsteps;
     const int so = live ? step * 64 : 0;
 #pragma unroll
-    for (int i = 0; i < GA; ++i) glds16(p.A + (ao[i] + so), adst[i] + slot * ABYTES);
+    for (int i = 0; i < GA; ++i) glds16((agw[i] ? p.nw : p.A) + (ao[i] + so), adst[i] + slot * ABYTES);
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) ldw2(wreg[2 * nt], wreg[2 * nt + 1], live ? wp[nt] + step * kstride : p.W);
   };
@@ -290,7 +305,16 @@ void gemm_dec_kernel(DArgs p) {
         af[(mt + APF) % (APF + 1)][1] = *reinterpret_cast<const bf16x8_t*>(As + (mt + APF) * 2048 + aoff1);
       }
       __builtin_amdgcn_sched_barrier(0);
-      const bf16x8_t a0 = af[mt % (APF + 1)][0], a1 = af[mt % (APF + 1)][1];
+      bf16x8_t a0 = af[mt % (APF + 1)][0], a1 = af[mt % (APF + 1)][1];
+      if constexpr (NRM == 2) {  // x * norm weight, per element (row 15 of the tile holds the weight)
+        const bf16x8_t g0 = *reinterpret_cast<const bf16x8_t*>(As + 15 * 128 + ((h4 ^ 7) << 4));
+        const bf16x8_t g1 = *reinterpret_cast<const bf16x8_t*>(As + 15 * 128 + (((4 + h4) ^ 7) << 4));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a0[j] = f2bits(bits2f(a0[j]) * bits2f(g0[j]));
+          a1[j] = f2bits(bits2f(a1[j]) * bits2f(g1[j]));
+        }
+      }
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
         acc[MB + mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[2 * nt], a0, acc[MB + mt][nt], 0, 0, 0);
@@ -323,7 +347,7 @@ void gemm_dec_kernel(DArgs p) {
   // as splitk_rmsnorm_kernel (norm.hip): the planes added to the bf16 residual in fp32, the sum rounded to
   // bf16 (the residual stream's precision), the RMS over the rounded row, out = bf16(h * inv * w).
   const int nrp = p.K * 2 + 64;  // image row pitch (bytes): rows start 64 B apart in the bank space
-  if constexpr (NRM) {
+  if constexpr (NRM == 1) {
     __shared__ float nred[NWV][kNrmRows];
     __shared__ float ninv[kNrmRows];
     const int nvec = p.K >> 3;
@@ -431,9 +455,9 @@ void gemm_dec_kernel(DArgs p) {
 #pragma unroll
     for (int u = 0; u < NST; ++u) {
       wait_w<(D - 2) * (GA + GW)>(wf[(u + 1) % NST]);  // retire step t + 1
-      if constexpr (!NRM) bar();  // every wave is done with slot (u + D) % NST (= step t - 1's); step t + 1 retired everywhere
+      if constexpr (NRM != 1) bar();  // every wave is done with slot (u + D) % NST (= step t - 1's); step t + 1 retired everywhere
       issue(t0 + u + D, (u + D) % NST, wf[(u + D) % NST]);
-      if constexpr (NRM) {
+      if constexpr (NRM == 1) {
         if (t0 + u < nsteps) compute_nrm(t0 + u, wf[u]);
       } else {
         if (t0 + u < nsteps) compute(u, wf[u]);  // uniform: a split's last round may be partial
@@ -452,10 +476,20 @@ void gemm_dec_kernel(DArgs p) {
   }
 
   // ---- epilogue: acc[mt][nt][r] = D[W row (wr[nt] + 4 h4 + r)][A row (16 mt + li)]
-  if (!active) return;
+  if constexpr (NRM == 2) {  // 1 / rms of this lane's row, from the producer's per-group sums of squares
+    const int m = m0 + li;
+    float rstd = 0.f;
+    if (m < p.M) {
+      float t = 0.f;
+      for (int q = 0; q < p.nG; ++q) t += p.nss[q * kNrmRows + m];  // group order: deterministic
+      rstd = rsqrtf(t / (float)p.K + p.neps);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) acc[0][nt] *= rstd;
+  }
   // row tile mt is stored when its group is this wave's (tail split) -- every tile for the own waves
   auto mine = [&](int mt) { return TQ == 0 || (mt >= g_lo * TQ && mt < g_hi * TQ); };
-  {
+  if (active) {
     constexpr int NM = MT;
     const int mr0 = m0;
     if constexpr (EPI == EPI_SILU) {
@@ -505,6 +539,66 @@ void gemm_dec_kernel(DArgs p) {
           }
         }
       }
+    }
+  }
+  if constexpr (RED) {  // the last split of this unit group folds every split's planes into the residual stream
+    __shared__ unsigned rlast;
+    __shared__ float rred[NWV][kNrmRows];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's plane stores are done
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned tk = __hip_atomic_fetch_add(p.rcnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tk >= (unsigned)p.ksplit) report_index_error(ERR_TICKET, tk);  // a stale or shared ticket word
+      const unsigned last = tk == (unsigned)(p.ksplit - 1) ? 1u : 0u;
+      if (last) {
+        __hip_atomic_store(p.rcnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      rlast = last;
+    }
+    __syncthreads();
+    if (rlast == 0u) return;
+    const int c0 = u0 * 16 * NTW, nv = cnt * 2 * NTW;  // the group's columns, 8 per vector
+    const size_t plane = (size_t)p.M * p.N;
+    float ssr[kNrmRows] = {0.f, 0.f, 0.f, 0.f};
+    for (int e = tid; e < p.M * nv; e += 64 * NWV) {
+      const int m = e / nv, n = c0 + (e - m * nv) * 8;
+      bf16x8_t* rp = reinterpret_cast<bf16x8_t*>(p.rres + (size_t)m * p.N + n);
+      float a[8];
+      unpack8(*rp, a);
+      const float* q = (const float*)p.C + (size_t)m * p.N + n;
+      for (int sp = 0; sp < p.ksplit; ++sp) {  // split order, as the split-K RMSNorm
+        const f32x4_t x0 = *reinterpret_cast<const f32x4_t*>(q + sp * plane);
+        const f32x4_t x1 = *reinterpret_cast<const f32x4_t*>(q + sp * plane + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] += x0[j];
+          a[j + 4] += x1[j];
+        }
+      }
+      const bf16x8_t hb = pack8(a);
+      *rp = hb;
+      unpack8(hb, a);
+      float sm = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sm += a[j] * a[j];
+#pragma unroll
+      for (int r = 0; r < kNrmRows; ++r) ssr[r] += r == m ? sm : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < kNrmRows; ++r) {
+      const float t = wave_sum(ssr[r]);
+      if ((tid & 63) == 0) rred[w][r] = t;
+    }
+    __syncthreads();
+    if (tid < kNrmRows) {
+      float t = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < NWV; ++w2) t += rred[w2][tid];
+      p.rss[g * kNrmRows + tid] = t;
     }
   }
 }
@@ -698,4 +792,101 @@ GRAG_API int grag_gemm_decode_norm(const void* planes, int S, const void* res_in
   a.nw = (const bf16*)nw;
   a.neps = eps;
   return nwv == 4 ? launch_nrm<kDepth, 4>(a, epi, gs, stream) : launch_nrm<kDepth, 5>(a, epi, gs, stream);
+}
+
+// Producer half of the folded RMSNorm (1-4 rows): the split-K projection (EPI_PARTIAL planes into ws) whose
+// last split per unit group adds the group's columns of all planes into `residual` [M][N] in place (bf16,
+// the split-K RMSNorm's arithmetic) and writes that group's sums of squares per row to ss [gs][4].
+// counters >= gs zeroed uint32 words (self-resetting).  mt 1, ntw 2, nwv 4 or 5, ksplit > 1, no tail.
+// Returns the group count through *groups.
+GRAG_API int grag_gemm_decode_red(const void* A, const void* W, void* residual, float* ss, unsigned* counters,
+                                  int lda, int ldw, int M, int N, int K, int mt, int nwv, int ntw, int ksplit, int gs,
+                                  void* ws, int* groups, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > kNrmRows || mt != 1 || ntw != 2 || (nwv != 4 && nwv != 5) || !A || !W || !residual || !ss ||
+      !counters || !ws || K % 64 != 0 || K < 64 || N % 32 != 0 || lda % 8 != 0 || ldw % 8 != 0)
+    return (int)hipErrorInvalidValue;
+  const int units = N / 32;
+  if (gs <= 0) {
+    if (units % nwv != 0) return (int)hipErrorInvalidValue;
+    gs = units / nwv;
+  }
+  if (gs > units || (units + gs - 1) / gs > nwv || gs > 1024) return (int)hipErrorInvalidValue;
+  const int kt = K / 64;
+  if (ksplit < 2) return (int)hipErrorInvalidValue;
+  const int kts = (kt + ksplit - 1) / ksplit;
+  ksplit = (kt + kts - 1) / kts;
+  if (ksplit < 2) return (int)hipErrorInvalidValue;
+  DArgs a{};
+  a.A = (const bf16*)A;
+  a.W = (const bf16*)W;
+  a.C = ws;
+  a.lda = lda; a.ldw = ldw; a.ldc = N;
+  a.M = M; a.N = N; a.K = K;
+  a.units = units;
+  a.gs = gs;
+  a.msplit = 1;
+  a.packed = 0;
+  a.ksplit = ksplit;
+  a.kt_split = kts;
+  a.rres = (bf16*)residual;
+  a.rss = ss;
+  a.rcnt = counters;
+  if (groups) *groups = gs;
+  const int nwg = gs * ksplit;
+  if (nwv == 4)
+    gemm_dec_kernel<EPI_PARTIAL, ACT_NONE, 1, kDepth, 4, 2, 0, 0, 1><<<nwg, 256, 0, stream>>>(a);
+  else
+    gemm_dec_kernel<EPI_PARTIAL, ACT_NONE, 1, kDepth, 5, 2, 0, 0, 1><<<nwg, 320, 0, stream>>>(a);
+  return (int)hipGetLastError();
+}
+
+// Consumer half: y = epilogue((x * nw) @ w^T / rms(x)) for M <= 4 rows, x = the residual stream the producer
+// updated, rms from its per-group sums of squares ss [G][4] (mean over K) + eps.  epi 1 (silu*mul, ksplit
+// 1) or 2 (fp32 planes into ws for a consumer that reduces them, ksplit > 1).  mt 1, ntw 2, nwv 4 / 5.
+GRAG_API int grag_gemm_decode_scaled(const void* A, const void* nw, const float* ss, int G, float eps,
+                                     const void* W, void* C, int lda, int ldw, int ldc, int M, int N, int K,
+                                     int epi, int mt, int nwv, int ntw, int ksplit, int gs, void* ws,
+                                     hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > kNrmRows || mt != 1 || ntw != 2 || (nwv != 4 && nwv != 5) || !A || !nw || !ss || G < 1 ||
+      (epi != EPI_SILU && epi != EPI_PARTIAL) || K % 64 != 0 || K < 64 || N % 32 != 0 || lda % 8 != 0 ||
+      ldw % 8 != 0 || ldc % 4 != 0 || (epi == EPI_SILU && N % 64 != 0))
+    return (int)hipErrorInvalidValue;
+  const int units = N / 32;
+  if (gs <= 0) {
+    if (units % nwv != 0) return (int)hipErrorInvalidValue;
+    gs = units / nwv;
+  }
+  if (gs > units || (units + gs - 1) / gs > nwv) return (int)hipErrorInvalidValue;
+  const int kt = K / 64;
+  if (ksplit < 1) ksplit = 1;
+  const int kts = (kt + ksplit - 1) / ksplit;
+  ksplit = (kt + kts - 1) / kts;
+  if ((epi == EPI_SILU) != (ksplit == 1) || (ksplit > 1 && !ws)) return (int)hipErrorInvalidValue;
+  DArgs a{};
+  a.A = (const bf16*)A;
+  a.W = (const bf16*)W;
+  a.C = ksplit > 1 ? ws : C;
+  a.lda = lda; a.ldw = ldw; a.ldc = ldc;
+  a.M = M; a.N = N; a.K = K;
+  a.units = units;
+  a.gs = gs;
+  a.msplit = 1;
+  a.packed = 0;
+  a.ksplit = ksplit;
+  a.kt_split = kts;
+  a.nw = (const bf16*)nw;
+  a.nss = ss;
+  a.nG = G;
+  a.neps = eps;
+  const int nwg = gs * ksplit;
+#define SC(E, NW) gemm_dec_kernel<E, ACT_NONE, 1, kDepth, NW, 2, 0, 2, 0><<<nwg, 64 * NW, 0, stream>>>(a)
+  if (epi == EPI_SILU) {
+    if (nwv == 4) SC(EPI_SILU, 4); else SC(EPI_SILU, 5);
+  } else {
+    if (nwv == 4) SC(EPI_PARTIAL, 4); else SC(EPI_PARTIAL, 5);
+  }
+#undef SC
+  return (int)hipGetLastError();
 }

@@ -222,11 +222,13 @@ class LLMEngine:
             # sampler scratch for the largest decode batch up front: graphs captured later all see one buffer
             self.sampler.workspace(self._max_b)
             from ..ops.attention import decode_counters  # small-batch decode tickets: before any capture
+            from ..ops.gemm import fold_ws
             from ..ops.norm import norm_ws
 
             with WS.owned_by(self._ws):  # this engine's own ticket words (ops/gemm.py WS.scratch)
                 decode_counters(self.device)
                 norm_ws(self.device)
+                fold_ws(self.device)
             # kernels report out-of-range index inputs (block tables, slots, token ids, tickets) to a
             # host-mapped block instead of faulting; every step's host read checks it (_read_host)
             from ..ops._lib import bind_error_guard, lib

@@ -31,8 +31,9 @@ import torch
 
 from ..ops.attention import AttnMetadata, paged_attention
 from ..ops.elementwise import qkv_rope_kvstore, rope_cos_sin, silu_mul
-from ..ops.gemm import (EPI_SILU, SplitKPartial, deinterleave_gate_up, gemm_decode_norm, interleave_gate_up,
-                        mlp_gate_up, norm_fuse_plan)
+from ..ops.gemm import (EPI_PARTIAL, EPI_SILU, FoldedNorm, SplitKPartial, deinterleave_gate_up,
+                        gemm_decode_norm, gemm_decode_red, gemm_decode_scaled, interleave_gate_up, mlp_gate_up,
+                        norm_fuse_plan)
 from ..ops.linear import linear, linear_deferred
 from ..ops.norm import embed_gather, rmsnorm
 from ..parallel.comm import Group
@@ -250,28 +251,47 @@ class Qwen2Model:
         h = embed_gather(input_ids, self.embed)
         residual = None
         defer = self.tp.trivial  # under TP the all-reduce sits between the projection and the norm
-        for L, (kc, vc) in zip(self.layers, kv_caches):
+        # 1-4 rows: each split-K RMSNorm folded into the projections around it (ops/gemm.py FOLD_NORM)
+        fold = (defer and self.gu_interleaved and not self.w4_enabled and input_ids.is_cuda
+                and input_ids.shape[0] <= 4)  # (ops/gemm.py fold_plan: GRAG_FOLD_NORM=0 turns it off)
+        nl = len(self.layers)
+        for li, (L, (kc, vc)) in enumerate(zip(self.layers, kv_caches)):
+            qkv = None
             if residual is None:
                 residual = h
                 x = rmsnorm(h, L.in_norm, eps)
+            elif isinstance(h, FoldedNorm):  # the previous down_proj already added into the residual stream
+                qkv = gemm_decode_scaled(h, L.in_norm, eps, L.qkv_w, EPI_PARTIAL)
+                if qkv is None:
+                    x = rmsnorm(residual, L.in_norm, eps)
             else:
                 x = rmsnorm(h, L.in_norm, eps, residual=residual)
-            qkv = self._proj(x, L, "qkv_w", defer=True)  # a K-split's reduce folds into the RoPE pass
+            if qkv is None:
+                qkv = self._proj(x, L, "qkv_w", defer=True)  # a K-split's reduce folds into the RoPE pass
             q = qkv_rope_kvstore(qkv, L.qkv_b, positions, self.cos_sin, meta.slot_mapping, kc, vc,
                                  self.hq, self.hkv, self.head_dim)
             a = paged_attention(q, kc, vc, meta, self.scale, causal=True)
-            h = self.tp.all_reduce(self._proj(a, L, "o_w", defer=defer))
-            plan = None
-            if isinstance(h, SplitKPartial) and self.gu_interleaved and not self.w4_enabled:
-                plan = norm_fuse_plan(h.M, L.gu_w.shape[0], h.N, True)
-            if plan is not None:  # 1-4 rows: the post-attention norm folded into the gate/up launch
-                r_new = torch.empty_like(residual)
-                m = gemm_decode_norm(h, residual, r_new, L.post_norm, eps, L.gu_w, EPI_SILU, plan)
-                residual = r_new
+            folded = gemm_decode_red(a, L.o_w, residual, 0) if fold else None
+            m = None
+            if folded is not None:
+                m = gemm_decode_scaled(folded, L.post_norm, eps, L.gu_w, EPI_SILU)
+                if m is None:
+                    m = self._proj(rmsnorm(residual, L.post_norm, eps), L, "gu_w")
             else:
-                x = rmsnorm(h, L.post_norm, eps, residual=residual)
-                m = self._proj(x, L, "gu_w")
-            h = self.tp.all_reduce(self._proj(m, L, "down_w", defer=defer))
+                h = self.tp.all_reduce(self._proj(a, L, "o_w", defer=defer))
+                plan = None
+                if isinstance(h, SplitKPartial) and self.gu_interleaved and not self.w4_enabled:
+                    plan = norm_fuse_plan(h.M, L.gu_w.shape[0], h.N, True)
+                if plan is not None:  # (A/B, off by default) the norm in the gate/up launch's prologue
+                    r_new = torch.empty_like(residual)
+                    m = gemm_decode_norm(h, residual, r_new, L.post_norm, eps, L.gu_w, EPI_SILU, plan)
+                    residual = r_new
+                else:
+                    x = rmsnorm(h, L.post_norm, eps, residual=residual)
+                    m = self._proj(x, L, "gu_w")
+            h = gemm_decode_red(m, L.down_w, residual, 1) if fold and li + 1 < nl else None
+            if h is None:
+                h = self.tp.all_reduce(self._proj(m, L, "down_w", defer=defer))
         return rmsnorm(h, self.norm, eps, residual=residual)
 
     def local_logits(self, hidden: torch.Tensor) -> torch.Tensor:

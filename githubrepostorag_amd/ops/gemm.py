@@ -623,6 +623,99 @@ def deferred_plan(M: int, N: int, K: int) -> tuple[str, int, tuple] | None:
     return None
 
 
+# The decoder's split-K RMSNorm folded into its producer and consumer projections at 1-4 rows
+# (csrc/kernels/gemm_decode.hip RED / NRM 2): the last split of each unit group of the producer (o_proj, down)
+# adds the planes into the residual stream and leaves per-group sums of squares; the consumer (gate/up, the
+# next layer's qkv) reads the residual stream as A, scales it by the norm weight on the fly and its
+# accumulators by 1 / rms.  The norm launch between them goes away -- but measured slower (profiles/
+# norm_fold_ab_r6.json: B = 1 TPOT 4.03 / 3.99 vs 3.82 / 3.82 ms): each producer's split tickets with their
+# agent-scope release / acquire fences and the last split's reduce cost ~7 us, more than the 5.6 us launch.
+# Off by default; GRAG_FOLD_NORM=1 for A/B (tests/test_norm_fuse_gpu.py keeps both halves tested).
+FOLD_NORM = os.environ.get("GRAG_FOLD_NORM", "0") == "1"
+
+
+def fold_plan(M: int, N: int, K: int, silu: bool) -> tuple[int, int, int] | None:
+    """(nwv, effective K-splits, gs) when the 1-4-row decode plan of (M, N, K) is one the folded-norm kernels
+    compile (one 16-row tile, 4- / 5-wave grid, no tail split); else None."""
+    if not FOLD_NORM or M < 1 or M > 4:
+        return None
+    p = dec_plan(M, N, K, silu)
+    if p is None:
+        return None
+    mt, nwv, ntw, ks, *rest = p
+    gs = rest[0] if rest else 0
+    tail = rest[1] if len(rest) > 1 else 0
+    if mt != 1 or ntw != 2 or nwv not in (4, 5) or tail:
+        return None
+    return nwv, dec_ksplit(K, ks), gs
+
+
+class FoldedNorm:
+    """The residual stream [M, H] after a producer projection's folded reduce (updated in place), with the
+    per-group sums of squares [groups, 4] its consumer takes 1 / rms from."""
+
+    __slots__ = ("residual", "ss", "groups")
+
+    def __init__(self, residual: torch.Tensor, ss: torch.Tensor, groups: int):
+        self.residual, self.ss, self.groups = residual, ss, groups
+
+
+def fold_ws(dev: torch.device) -> tuple[torch.Tensor, torch.Tensor]:
+    """(tickets [2 x 1024] int32, zeroed; sums of squares [2 x 1024 x 4] fp32): two slots (post-attention,
+    input norm), owned by the caller's workspace owner (WS.scratch); allocate before any capture."""
+    return WS.scratch("fold_norm", torch.device(dev),
+                      lambda d: (torch.zeros(2 * 1024, dtype=torch.int32, device=d),
+                                 torch.zeros(2 * 1024 * 4, dtype=torch.float32, device=d)))
+
+
+def gemm_decode_red(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, slot: int) -> FoldedNorm | None:
+    """The producer half: residual += x @ w.T (bf16, in place) through the split-K decode kernel whose last
+    split per unit group does the add; None when the plan does not take it (the caller falls back)."""
+    M, K = x.shape
+    N = w.shape[0]
+    plan = fold_plan(M, N, K, False)
+    if plan is None or plan[1] < 2 or residual.shape != (M, N) or not residual.is_contiguous():
+        return None
+    nwv, ks, gs = plan
+    fl = dec_ws_floats(M, N, ks)
+    if torch.cuda.is_current_stream_capturing() and not WS.ready(x.device, fl):
+        return None
+    ws = WS.get(x.device, fl)
+    cnt, ss = fold_ws(x.device)
+    groups = gs if gs > 0 else (N // 32) // nwv
+    ssb = ss[slot * 4096:(slot + 1) * 4096]
+    call("grag_gemm_decode_red", ptr(x), ptr(w), ptr(residual), ptr(ssb), ptr(cnt[slot * 1024:(slot + 1) * 1024]),
+         x.stride(0), w.stride(0), M, N, K, 1, nwv, 2, ks, gs, ptr(ws), None)
+    return FoldedNorm(residual, ssb, groups)
+
+
+def gemm_decode_scaled(fold: FoldedNorm, w_norm: torch.Tensor, eps: float, w: torch.Tensor, epi: int):
+    """The consumer half: epilogue(RMSNorm(residual) * w_norm @ w.T) with the norm folded in -- [M, N/2] for
+    EPI_SILU (interleaved gate/up), SplitKPartial planes for EPI_PARTIAL (the RoPE pass reduces them); None
+    when the plan does not take it."""
+    x = fold.residual
+    M, K = x.shape
+    N = w.shape[0]
+    plan = fold_plan(M, N, K, epi == EPI_SILU)
+    if plan is None:
+        return None
+    nwv, ks, gs = plan
+    if (epi == EPI_SILU) != (ks == 1):
+        return None
+    if epi == EPI_SILU:
+        out = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
+        call("grag_gemm_decode_scaled", ptr(x), ptr(w_norm), ptr(fold.ss), fold.groups, float(eps), ptr(w), ptr(out),
+             x.stride(0), w.stride(0), out.stride(0), M, N, K, EPI_SILU, 1, nwv, 2, ks, gs, None)
+        return out
+    fl = dec_ws_floats(M, N, ks)
+    if torch.cuda.is_current_stream_capturing() and not WS.ready(x.device, fl):
+        return None
+    ws = WS.get(x.device, fl)
+    call("grag_gemm_decode_scaled", ptr(x), ptr(w_norm), ptr(fold.ss), fold.groups, float(eps), ptr(w), None,
+         x.stride(0), w.stride(0), N, M, N, K, EPI_PARTIAL, 1, nwv, 2, ks, gs, ptr(ws))
+    return SplitKPartial(ws[:fl], ks, M, N, x.dtype)
+
+
 def gemm_deferred(x: torch.Tensor, w: torch.Tensor, how: tuple[str, int, tuple]) -> SplitKPartial:
     """Run a K-split projection (deferred_plan) and leave its fp32 planes in the workspace (epi
     EPI_PARTIAL: no splitk_reduce launch)."""
