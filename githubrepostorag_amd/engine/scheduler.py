@@ -38,6 +38,9 @@ from .sequence import Sequence, SeqStatus
 INTERACTIVE_PRIORITY = 2
 
 
+_ADAPTIVE_RESERVE = __import__("os").environ.get("GRAG_ADAPTIVE_RESERVE", "1") == "1"
+
+
 def _order(seq) -> float:
     """A sequence's queue key within its priority (SamplingParams.order, else its arrival)."""
     o = seq.params.order
@@ -171,6 +174,11 @@ class Scheduler:
         # pass walks these instead of every running sequence (a 512-row decode step has none)
         self.prefilling: list[Sequence] = []
         self.free_slots = list(range(max_num_seqs - 1, -1, -1))
+        # interactive sequences holding a slot, and an EMA of their prompt blocks: the bulk reserve grows with
+        # the interactive load (_ADAPTIVE_RESERVE), so bulk work cannot fill the slots / blocks live queries
+        # are about to need
+        self.n_interactive = 0
+        self._int_blocks = 0.0
         self.lock = threading.Lock()
         self.num_preemptions = 0
         self.last_registered: list[int] = []  # prompt blocks registered by the last schedule() (rollback)
@@ -197,6 +205,8 @@ class Scheduler:
         if seq in self.prefilling:
             self.prefilling.remove(seq)
         self.kv.free(seq)
+        if seq.slot >= 0 and seq.params.priority >= INTERACTIVE_PRIORITY:
+            self.n_interactive -= 1
         if seq.slot >= 0:
             self.free_slots.append(seq.slot)
             seq.slot = -1
@@ -240,6 +250,8 @@ class Scheduler:
         if v in self.prefilling:
             self.prefilling.remove(v)
         self.kv.free(v)
+        if v.params.priority >= INTERACTIVE_PRIORITY:
+            self.n_interactive -= 1
         self.free_slots.append(v.slot)
         v.slot = -1
         v.status = SeqStatus.WAITING
@@ -282,6 +294,13 @@ class Scheduler:
                 return n if seq.params.priority >= INTERACTIVE_PRIORITY else min(n, bulk_left)
 
             reserve = bulk_budget is not None  # interactive traffic: hold the reserve back from bulk admissions
+            res_seqs, res_blocks = self.reserve_seqs, self.reserve_blocks
+            if reserve and _ADAPTIVE_RESERVE and self.n_interactive:
+                # half the live interactive load again on top: at 40 queries/s beside ingest ~100 queries are live
+                # (128 decode steps each) and a fixed 16-slot reserve let bulk fill the rest -- a new query then
+                # waited for some sequence to finish (concurrent-ingest TTFT p90 250-413 ms)
+                res_seqs += self.n_interactive // 2
+                res_blocks += int(self.n_interactive * self._int_blocks) // 2
 
             while budget > 0:
                 can_admit = (admit_ok and self.waiting and self.free_slots
@@ -310,7 +329,7 @@ class Scheduler:
                     admitted.append(("rejected", seq))
                     continue
                 bulk = seq.params.priority < INTERACTIVE_PRIORITY
-                if bulk and (bulk_left <= 0 or (reserve and len(self.running) >= self.max_num_seqs - self.reserve_seqs)):
+                if bulk and (bulk_left <= 0 or (reserve and len(self.running) >= self.max_num_seqs - res_seqs)):
                     admit_ok = False  # (waiting is priority-ordered: only bulk requests follow)
                     continue
                 if not seq.blocks:
@@ -322,7 +341,7 @@ class Scheduler:
                 # blocks and preempting at the next decode step recomputes whole prompts: at 1024 agent jobs
                 # on one GPU that thrash dominated, profiles/agent_saturation_r4.json)
                 if self.running and self.kv.num_free - self.kv.blocks_needed(seq, seq.num_computed + max(n, 0)) \
-                        < len(self.running) + 1 + (self.reserve_blocks if reserve and bulk else 0):
+                        < len(self.running) + 1 + (res_blocks if reserve and bulk else 0):
                     admit_ok = False
                     continue
                 if n <= 0 or not self.kv.ensure(seq, seq.num_computed + n):
@@ -330,6 +349,10 @@ class Scheduler:
                     continue
                 self.waiting.popleft()
                 seq.slot = self.free_slots.pop()
+                if not bulk:
+                    self.n_interactive += 1
+                    nb = -(-seq.total_len // self.kv.block_size)
+                    self._int_blocks = nb if self._int_blocks == 0.0 else 0.9 * self._int_blocks + 0.1 * nb
                 seq.status = SeqStatus.RUNNING
                 self.running.append(seq)
                 self.prefilling.append(seq)

@@ -546,3 +546,30 @@ def test_pacing_hold_lasts_while_bulk_work_is_in_flight(model, tok):
         assert runner._bulk_live == 0  # interactive requests are not counted
     finally:
         runner.shutdown()
+
+
+def test_bulk_reserve_grows_with_live_interactive_sequences():
+    """While interactive traffic is on, bulk admissions leave free the fixed reserve PLUS half the live
+    interactive sequences (slots and their prompt blocks): bulk work cannot fill the slots the next queries
+    need.  The interactive count follows admissions, finishes and preemptions."""
+    from githubrepostorag_amd.engine.scheduler import KVCacheManager, Scheduler
+
+    sch = Scheduler(KVCacheManager(num_blocks=2000, block_size=16), 40, 1 << 20, 4096, mixed_batches=False,
+                    reserve_seqs=2, reserve_tokens=0)
+    inter = [Sequence(f"q{i}", list(range(1, 65)), SamplingParams(priority=2)) for i in range(12)]
+    for s in inter:
+        sch.add(s)
+    sch.schedule(1 << 20, bulk_budget=1 << 20)
+    assert sch.n_interactive == 12
+    for q in inter:  # their prompts ran (the engine would advance this)
+        q.num_computed = len(q.prompt_ids)
+    bulk = [Sequence(f"b{i}", list(range(100 + i, 164 + i)), SamplingParams(priority=0)) for i in range(40)]
+    for s in bulk:
+        sch.add(s)
+    sch.schedule(1 << 20, bulk_budget=1 << 20)
+    # 40 slots - (2 fixed + 12 // 2) reserved = 32 running at most with bulk admissions
+    assert len(sch.running) == 40 - 2 - 6
+    sch.finish(inter[0])
+    assert sch.n_interactive == 11
+    sch._preempt_one(keep=bulk[0])  # a bulk victim first: the interactive count is unchanged
+    assert sch.n_interactive == 11
