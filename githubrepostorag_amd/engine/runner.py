@@ -107,6 +107,8 @@ class EngineRunner:
     ARRIVAL_RECENT_S = 0.05
     PACE_HOLD_S = float(os.environ.get("GRAG_PACE_HOLD_S", "0.5"))
     BULK_RECENT_S = 5.0
+    # a paced replay lasts at most this fraction of the mean gap between arrival events
+    PACE_FRAC = float(os.environ.get("GRAG_PACE_FRAC", "0.5"))
     _AW = os.environ.get("GRAG_ARRIVAL_WINDOW", "auto")
     ARRIVAL_WINDOW = -1 if _AW == "auto" else int(_AW)
     MAX_WINDOW = 8
@@ -223,7 +225,7 @@ class EngineRunner:
         g, d = self._gap, self._step_s
         if g is None or d is None or now - self._last_event > max(2 * g, self._hold(now)):
             return None
-        return max(1, min(self.MAX_WINDOW, int(0.5 * g / d)))
+        return max(1, min(self.MAX_WINDOW, int(self.PACE_FRAC * g / d)))
 
     def _prefill_budget(self) -> tuple[int | None, int | None]:
         """This step's (prefill token cap, bulk share of it): the interactive budget while arrivals are
