@@ -61,6 +61,17 @@ struct AttnParams {
   float* pre_o;              // [pre_planes, T, Hq, D]: the prefix parts' unnormalised O (plane = part index)
   float* pre_ml;             // [pre_planes, T, Hq, 2]: their (m, l)
   int pre_planes;
+  // small-batch decode with the RoPE pass folded in (paged_decode_mw_kernel FR): q and the new token's K/V come
+  // from the qkv projection's S fp32 split-K planes [S][T][rq_ld] (rq_ld = (Hq + 2 Hkv) D), plus bias and NeoX
+  // RoPE at rq_pos[token]; the new K/V is stored to cache slot rq_slot[token] by the sequence's last split
+  const float* rq_planes;
+  size_t rq_plane;  // elements per plane
+  int rq_S, rq_ld;
+  const bf16* rq_bias;      // [(Hq + 2 Hkv) D] or null
+  const int32_t* rq_pos;    // [T]
+  const float* rq_cs;       // [npos, D]: cos | sin
+  const int32_t* rq_slot;   // [T]
+  int rq_nslots, rq_npos;
 };
 
 // grag_attn_decode_xcd(1): decode workgroups remapped so that sequences adjacent in the batch run on the same
@@ -1169,7 +1180,32 @@ __global__ __launch_bounds__(64) void paged_decode_prefix_kernel(AttnParams p) {
 //     an agent-scope ticket (release fence first, as gemm_stream.hip's split tiles), and the last arriver
 //     (acquire) reads the others' partials and writes the output; it resets its counter, so the launch
 //     replays inside hipGraphs without a memset.  No second kernel, no partial round trip for the others.
-template <int D, int NW>
+//
+// FR (the RoPE pass folded in, ops/attention.py paged_decode_mw_rope): the workgroup forms its G q heads from
+// the qkv projection's split-K planes (sum in plane order, bias, NeoX RoPE: the values qkv_rope_kernel<true>
+// stores) cooperatively -- one thread per 4-dim rotary pair, all planes' loads in flight together, while the
+// first K / V tile's DMA is in flight -- and stages them in LDS past the rings.  The new token's key never goes
+// through the cache in this launch: the sequence's last split stops its tile loop one key short, its workgroup
+// also forms the new K / V (stored to the token's cache slot for the next steps, and staged in LDS), and wave 0
+// folds that key into its (m, l, O) after the loop.  One launch (and the q round trip) fewer per layer.
+template <int D>
+constexpr int mw_rope_lds() { return 16 * D * 2 + D * 2 + D * 4; }  // q [16][D] bf16, new K [D] bf16, new V [D] f32
+
+// token t's qkv projection at column col, 4 dims: the split-K planes summed in plane order and rounded to bf16,
+// the bias added and rounded again (elementwise.hip qkv_rope_kernel<true> load8)
+__device__ __forceinline__ f32x4_t rq_load4(const AttnParams& p, int t, int col) {
+  f32x4_t x = plane_sum4(p.rq_planes + (size_t)t * p.rq_ld + col, p.rq_plane, p.rq_S);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) x[r] = bits2f(f2bits(x[r]));
+  if (p.rq_bias) {
+    const bf16x4_t b = *reinterpret_cast<const bf16x4_t*>(p.rq_bias + col);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[r] = bits2f(f2bits(x[r] + bits2f(b[r])));
+  }
+  return x;
+}
+
+template <int D, int NW, bool FR>
 __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, unsigned* counters) {
   constexpr int TK = 32, NS = 2;
   constexpr int NT16 = TK / 16, NCC = TK / 32;
@@ -1195,8 +1231,15 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, 
   const int G = p.G;
   const int tok = p.q_start[seq];
   const int nvalid = min(p.num_splits, (ctx + p.split_len - 1) / p.split_len);
+  // FR: the last split's tiles stop before the new token's key (folded in from registers after the loop)
+  const bool newkey = FR && split == nvalid - 1;
+  const int kv_end = newkey ? kv_hi - 1 : kv_hi;
   bf16x8_t qf[NC];
-  {
+  int pos = 0, slot = -1;
+  if constexpr (FR) {  // q (and the new K / V) are formed once the first K / V tile is in flight (below)
+    pos = p.rq_pos[tok];
+    if (newkey) slot = p.rq_slot[tok];
+  } else {
     const bf16* qp = p.q + (size_t)tok * p.q_stride + (size_t)(kvh * G + (li < G ? li : 0)) * D + 8 * h4;
 #pragma unroll
     for (int c = 0; c < NC; ++c) qf[c] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * c);
@@ -1224,10 +1267,10 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, 
     }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int key0 = min(kt0 + i * RPI, ctx - 1);
+      const int key0 = min(kt0 + i * RPI, kv_end - 1);
       const int blk = __builtin_amdgcn_readlane(bvec, (key0 / p.BS) & 63);
       const int row = i * RPI + lrow;
-      const int key = min(kt0 + row, ctx - 1);
+      const int key = min(kt0 + row, kv_end - 1);
       const size_t off = (((size_t)blk * p.Hkv + kvh) * p.BS + (key % p.BS)) * D;
       glds16(p.k + off + ((lch ^ kswz<D>(row)) << 3), kdst + i * 1024);
       glds16(p.v + off + ((lch ^ vswz<D>(row)) << 3), vdst + i * 1024);
@@ -1238,9 +1281,58 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, 
   f32x4_t o[ND];
 #pragma unroll
   for (int n = 0; n < ND; ++n) o[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const int ntot = (kv_hi - kv_lo + TK - 1) / TK;
+  const int ntot = (kv_end - kv_lo + TK - 1) / TK;
   const int nmine = w < ntot ? (ntot - w + NW - 1) / NW : 0;  // this wave's tiles: w, w + NW, ...
   if (nmine > 0) issue(kv_lo + w * TK, 0);
+  // FR staging past the rings (mw_rope_lds): q [16][D] bf16, the new K [D] bf16 and V [D] fp32
+  bf16* q_st = reinterpret_cast<bf16*>(smem + NW * NS * 2 * TILE);
+  bf16* k_st = q_st + 16 * D;
+  float* v_st = reinterpret_cast<float*>(k_st + D);
+  if constexpr (FR) {
+    // the planes' loads overlap the first tile's DMA and retire here (the RoPE math consumes them), before the
+    // loop's counted vmcnt
+    if (!index_ok(pos, p.rq_npos, ERR_ROPE_POS)) pos = 0;
+    if (slot >= 0 && !index_ok(slot, p.rq_nslots, ERR_KV_SLOT)) slot = -1;
+    const float* cs = p.rq_cs + (size_t)pos * D;
+    constexpr int HU = D / 8;  // rotary units (dims i0..i0+3 with i0 + D/2..) per head
+    const int nq = G * HU, nk = newkey ? HU : 0, nv = newkey ? D / 4 : 0;
+    const size_t cache_off = slot >= 0 ? (((size_t)(slot / p.BS) * p.Hkv + kvh) * p.BS + slot % p.BS) * D : 0;
+    for (int u = threadIdx.x; u < nq + nk + nv; u += 64 * NW) {
+      if (u < nq + nk) {
+        const bool isk = u >= nq;
+        const int i0 = ((isk ? u - nq : u) % HU) * 4;
+        const int col = (isk ? p.Hq + kvh : kvh * G + u / HU) * D;
+        const f32x4_t x1 = rq_load4(p, tok, col + i0), x2 = rq_load4(p, tok, col + i0 + D / 2);
+        const f32x4_t cv = *reinterpret_cast<const f32x4_t*>(cs + i0);
+        const f32x4_t sv = *reinterpret_cast<const f32x4_t*>(cs + D / 2 + i0);
+        bf16x4_t r1, r2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          r1[r] = f2bits(x1[r] * cv[r] - x2[r] * sv[r]);
+          r2[r] = f2bits(x2[r] * cv[r] + x1[r] * sv[r]);
+        }
+        bf16* dst = isk ? k_st : q_st + (u / HU) * D;
+        *reinterpret_cast<bf16x4_t*>(dst + i0) = r1;
+        *reinterpret_cast<bf16x4_t*>(dst + i0 + D / 2) = r2;
+        if (isk && slot >= 0) {
+          bf16* kd = const_cast<bf16*>(p.k) + cache_off;
+          *reinterpret_cast<bf16x4_t*>(kd + i0) = r1;
+          *reinterpret_cast<bf16x4_t*>(kd + i0 + D / 2) = r2;
+        }
+      } else {
+        const int i0 = (u - nq - nk) * 4;
+        const f32x4_t x = rq_load4(p, tok, (p.Hq + p.Hkv + kvh) * D + i0);
+        *reinterpret_cast<f32x4_t*>(v_st + i0) = x;
+        if (slot >= 0)
+          *reinterpret_cast<bf16x4_t*>(const_cast<bf16*>(p.v) + cache_off + i0) =
+              bf16x4_t{f2bits(x[0]), f2bits(x[1]), f2bits(x[2]), f2bits(x[3])};
+      }
+    }
+    __syncthreads();
+    const bf16* qr = q_st + (li < G ? li : 0) * D + 8 * h4;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) qf[c] = *reinterpret_cast<const bf16x8_t*>(qr + 32 * c);
+  }
   for (int t = 0; t < nmine; ++t) {
     const int stage = t & 1;
     const int kt0 = kv_lo + (w + t * NW) * TK;
@@ -1265,14 +1357,14 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, 
       }
     }
     float tmax = -INFINITY;
-    if (kt0 + TK > kv_hi) {  // the context's last tile only; a real branch (see attn_prefill_kernel)
+    if (kt0 + TK > kv_end) {  // the context's last tile only; a real branch (see attn_prefill_kernel)
       asm volatile("");
 #pragma unroll
       for (int tt = 0; tt < NT16; ++tt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kt0 + 16 * tt + 4 * h4 + r;
-          sc[tt][r] = key >= kv_hi ? -INFINITY : sc[tt][r];
+          sc[tt][r] = key >= kv_end ? -INFINITY : sc[tt][r];
         }
     }
 #pragma unroll
@@ -1325,6 +1417,37 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, 
   }
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
+
+  if constexpr (FR) {
+    if (newkey && w == 0) {  // (wave-uniform) the new token's key: one more online-softmax key, from the staging
+      bf16x8_t kf[NC];
+      float vn[ND][4];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) kf[c] = *reinterpret_cast<const bf16x8_t*>(k_st + 32 * c + 8 * h4);
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+        const f32x4_t x = *reinterpret_cast<const f32x4_t*>(v_st + 16 * n + 4 * h4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) vn[n][r] = bits2f(f2bits(x[r]));
+      }
+      float dot = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dot = __builtin_fmaf(bits2f(qf[c][j]), bits2f(kf[c][j]), dot);
+      dot += __shfl_xor(dot, 16, 64);
+      dot += __shfl_xor(dot, 32, 64);
+      const float s = dot * p.scale_log2;
+      const float mn = fmaxf(m, s);
+      const float alpha = exp2f(m - mn), beta = exp2f(s - mn);
+      m = mn;
+      lsum = lsum * alpha + beta;
+#pragma unroll
+      for (int n = 0; n < ND; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[n][r] = __builtin_fmaf(beta, vn[n][r], o[n][r] * alpha);
+    }
+  }
 
   // ---- the waves' states merge in LDS (the rings are free once every wave passed the barrier)
   __syncthreads();
@@ -1431,15 +1554,16 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_mw_kernel(AttnParams p, 
   }
 }
 
-template <int D, int NW>
+template <int D, int NW, bool FR = false>
 int launch_decode_mw(const AttnParams& prm, int nseq, unsigned* counters, hipStream_t stream) {
-  constexpr int lds = NW * 2 * 2 * 32 * 2 * D;
+  constexpr int lds = NW * 2 * 2 * 32 * 2 * D + (FR ? mw_rope_lds<D>() : 0);
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)paged_decode_mw_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipFuncSetAttribute((const void*)paged_decode_mw_kernel<D, NW, FR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        lds);
     attr_set = true;
   }
-  paged_decode_mw_kernel<D, NW><<<dim3(nseq, prm.Hkv, prm.num_splits), 64 * NW, lds, stream>>>(prm, counters);
+  paged_decode_mw_kernel<D, NW, FR><<<dim3(nseq, prm.Hkv, prm.num_splits), 64 * NW, lds, stream>>>(prm, counters);
   return (int)hipGetLastError();
 }
 
@@ -1701,6 +1825,64 @@ GRAG_API int grag_paged_decode_mw(const void* q, int q_stride, const void* k_cac
                                : launch_decode_mw<128, 2>(prm, nseq, counters, stream);
   return nw == 4 ? launch_decode_mw<64, 4>(prm, nseq, counters, stream)
                  : launch_decode_mw<64, 2>(prm, nseq, counters, stream);
+}
+
+// The same with the RoPE pass folded in (paged_decode_mw_kernel FR): instead of q, the qkv projection's S fp32
+// split-K planes [S][total_q][(Hq + 2 Hkv) D] with its bias (or null), the positions / cos|sin table of
+// grag_qkv_rope_kvstore_planes and the new tokens' cache slots; one query token per sequence (decode).  The
+// new K / V land in the cache as grag_qkv_rope_kvstore_planes would store them.
+GRAG_API int grag_paged_decode_mw_rope(const float* planes, int S, const void* bias, const int32_t* positions,
+                                       const float* cos_sin, const int32_t* slot_mapping, const void* k_cache,
+                                       const void* v_cache, void* out, int out_stride, const int32_t* block_tables,
+                                       int bt_stride, const int32_t* q_start, const int32_t* ctx_len, int nseq,
+                                       int total_q, int Hq, int Hkv, int D, int BS, float scale, int num_splits,
+                                       int split_len, float* part_o, float* part_ml, unsigned* counters, int nw,
+                                       int nblocks, int nslots, int npos, hipStream_t stream) {
+  if (nseq <= 0) return 0;
+  if (Hq % Hkv != 0 || Hq / Hkv > 16 || BS <= 0 || BS % 16 != 0 || (nw != 2 && nw != 4) || (D != 64 && D != 128))
+    return (int)hipErrorInvalidValue;
+  if (!planes || S < 1 || !positions || !cos_sin || !slot_mapping || npos < 1 || total_q < nseq)
+    return (int)hipErrorInvalidValue;
+  if (num_splits < 1) num_splits = 1;
+  if (num_splits > 1 && (!part_o || !part_ml || !counters || split_len <= 0 || split_len % 32 != 0))
+    return (int)hipErrorInvalidValue;
+  if ((num_splits * 32 + 16) * 4 > nw * 2 * 2 * 32 * 2 * D) return (int)hipErrorInvalidValue;  // merge scratch
+  AttnParams prm{};
+  prm.k = (const bf16*)k_cache;
+  prm.v = (const bf16*)v_cache;
+  prm.out = (bf16*)out;
+  prm.part_o = part_o;
+  prm.part_ml = part_ml;
+  prm.block_tables = block_tables;
+  prm.q_start = q_start;
+  prm.ctx_len = ctx_len;
+  prm.out_stride = out_stride;
+  prm.Hq = Hq;
+  prm.Hkv = Hkv;
+  prm.G = Hq / Hkv;
+  prm.BS = BS;
+  prm.bt_stride = bt_stride;
+  prm.tiles_per_seq = 1;
+  prm.num_splits = num_splits;
+  prm.split_len = num_splits > 1 ? split_len : (1 << 30);
+  prm.total_q = total_q;
+  prm.scale_log2 = scale * 1.4426950408889634f;
+  prm.causal = 1;
+  prm.nblocks = nblocks;
+  prm.rq_planes = planes;
+  prm.rq_ld = (Hq + 2 * Hkv) * D;
+  prm.rq_plane = (size_t)total_q * prm.rq_ld;
+  prm.rq_S = S;
+  prm.rq_bias = (const bf16*)bias;
+  prm.rq_pos = positions;
+  prm.rq_cs = cos_sin;
+  prm.rq_slot = slot_mapping;
+  prm.rq_nslots = nslots;
+  prm.rq_npos = npos;
+  if (D == 128) return nw == 4 ? launch_decode_mw<128, 4, true>(prm, nseq, counters, stream)
+                               : launch_decode_mw<128, 2, true>(prm, nseq, counters, stream);
+  return nw == 4 ? launch_decode_mw<64, 4, true>(prm, nseq, counters, stream)
+                 : launch_decode_mw<64, 2, true>(prm, nseq, counters, stream);
 }
 
 // Contiguous (varlen) self-attention over packed QKV rows, e.g. encoder

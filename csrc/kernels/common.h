@@ -35,6 +35,37 @@ __device__ __forceinline__ short f2bits(float f) {
   return __builtin_bit_cast(short, b);
 }
 
+// a += four consecutive floats of each of S fp32 split-K planes (plane stride `plane` elements), in plane order.
+// For S <= 16 the planes are walked in one fully unrolled, branch-free pass of 8 or 16 (indices past S re-read
+// plane 0 and add zero: fma(1, y, x) rounds as x + y), so every plane's load can be in flight together -- a
+// runtime-count loop under "#pragma unroll" runs its remainder iterations one plane per memory round trip.
+template <int MAXS>
+__device__ __forceinline__ void plane_acc4_fixed(f32x4_t& a, const float* p, size_t plane, int S) {
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    const bool on = s < S;
+    const f32x4_t v = *reinterpret_cast<const f32x4_t*>(p + (on ? s : 0) * plane);
+    const float m = on ? 1.f : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[r] = __builtin_fmaf(m, v[r], a[r]);
+  }
+}
+__device__ __forceinline__ void plane_acc4(f32x4_t& a, const float* p, size_t plane, int S) {
+  if (S <= 8) {
+    plane_acc4_fixed<8>(a, p, plane, S);
+  } else if (S <= 16) {
+    plane_acc4_fixed<16>(a, p, plane, S);
+  } else {
+    for (int s = 0; s < S; ++s) a += *reinterpret_cast<const f32x4_t*>(p + s * plane);
+  }
+}
+// the plane sum alone (from -0, the additive identity of every float, so the bits are the plain sum's)
+__device__ __forceinline__ f32x4_t plane_sum4(const float* p, size_t plane, int S) {
+  f32x4_t a = f32x4_t{-0.f, -0.f, -0.f, -0.f};
+  plane_acc4(a, p, plane, S);
+  return a;
+}
+
 // Unpack a 16-byte bf16x8 vector into 8 floats.
 __device__ __forceinline__ void unpack8(const bf16x8_t& v, float* f) {
 #pragma unroll

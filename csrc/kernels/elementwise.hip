@@ -43,12 +43,8 @@ __global__ __launch_bounds__(kThreads) void qkv_rope_kernel(
   // 8 consecutive projection outputs of this token as bf16-rounded floats
   auto load8 = [&](int col, float* x) {
     if constexpr (PL) {
-      f32x4_t a = *reinterpret_cast<const f32x4_t*>(prow + col), b = *reinterpret_cast<const f32x4_t*>(prow + col + 4);
-#pragma unroll 8
-      for (int s = 1; s < S; ++s) {  // (unrolled: the planes' loads issue back to back; sums stay in plane order)
-        a += *reinterpret_cast<const f32x4_t*>(prow + s * plane + col);
-        b += *reinterpret_cast<const f32x4_t*>(prow + s * plane + col + 4);
-      }
+      // (common.h plane_sum4: up to 8 planes' loads in flight at once; sums stay in plane order)
+      const f32x4_t a = plane_sum4(prow + col, plane, S), b = plane_sum4(prow + col + 4, plane, S);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         x[j] = bits2f(f2bits(a[j]));

@@ -10,6 +10,7 @@ Layer dataflow per step (T tokens, kernels in brackets):
     qkv = x W_qkv^T                                   [grag_gemm_tile at decode M, else library]
     q, K/V-cache <- bias + NeoX RoPE + paged store    [grag_qkv_rope_kvstore]
     a = paged flash attention (GQA-packed, MFMA)      [grag_paged_attention]
+      (1-16 decode rows: the two lines above in one launch, [grag_paged_decode_mw_rope])
     h = a W_o^T        (+ TP all-reduce, RCCL)
     residual += h ; x = RMSNorm(residual)            [grag_rmsnorm]
     m = SiLU(x W_g^T) * (x W_u^T)                     [grag_gemm_tile EPI_SILU: one GEMM, the
@@ -29,7 +30,7 @@ import os
 
 import torch
 
-from ..ops.attention import AttnMetadata, paged_attention
+from ..ops.attention import AttnMetadata, paged_attention, paged_decode_mw_rope
 from ..ops.elementwise import qkv_rope_kvstore, rope_cos_sin, silu_mul
 from ..ops.gemm import (EPI_PARTIAL, EPI_SILU, FoldedNorm, SplitKPartial, deinterleave_gate_up,
                         gemm_decode_norm, gemm_decode_red, gemm_decode_scaled, interleave_gate_up, mlp_gate_up,
@@ -268,9 +269,13 @@ class Qwen2Model:
                 x = rmsnorm(h, L.in_norm, eps, residual=residual)
             if qkv is None:
                 qkv = self._proj(x, L, "qkv_w", defer=True)  # a K-split's reduce folds into the RoPE pass
-            q = qkv_rope_kvstore(qkv, L.qkv_b, positions, self.cos_sin, meta.slot_mapping, kc, vc,
-                                 self.hq, self.hkv, self.head_dim)
-            a = paged_attention(q, kc, vc, meta, self.scale, causal=True)
+            # 1-16 decode rows: RoPE + K/V store inside the attention launch (ops/attention.py ROPE_FUSE)
+            a = paged_decode_mw_rope(qkv, L.qkv_b, positions, self.cos_sin, kc, vc, meta, self.scale, self.hq,
+                                     self.hkv, self.head_dim) if isinstance(qkv, SplitKPartial) else None
+            if a is None:
+                q = qkv_rope_kvstore(qkv, L.qkv_b, positions, self.cos_sin, meta.slot_mapping, kc, vc,
+                                     self.hq, self.hkv, self.head_dim)
+                a = paged_attention(q, kc, vc, meta, self.scale, causal=True)
             folded = gemm_decode_red(a, L.o_w, residual, 0) if fold else None
             m = None
             if folded is not None:

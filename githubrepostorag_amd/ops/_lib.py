@@ -41,6 +41,8 @@ _SIGS = {
     "grag_paged_attention": [P, I, P, P, P, I, P, I, P, P, I, I, I, I, I, I, I, F, I, I, I, P, P, I, I, P],
     "grag_splitk_add_rmsnorm_small": [P, I, P, P, P, I, I, F, P, P, P],
     "grag_paged_decode_mw": [P, I, P, P, P, I, P, I, P, P, I, I, I, I, I, I, F, I, I, P, P, P, I, I, P],
+    "grag_paged_decode_mw_rope": [P, I, P, P, P, P, P, P, P, I, P, I, P, P, I, I, I, I, I, I, F, I, I, P, P, P, I, I, I,
+                                  I, P],
     "grag_gemm_decode_red": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "grag_gemm_decode_scaled": [P, P, P, I, F, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P, P],
     "grag_gemm_decode_norm": [P, I, P, P, P, F, P, P, I, I, I, I, I, I, I, I, I, I, I, P],

@@ -339,6 +339,43 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
     return out
 
 
+# small-batch decode with the RoPE + KV-store pass folded into the attention launch (paged_decode_mw_kernel FR;
+# GRAG_ROPE_FUSE=0: the separate qkv_rope_kvstore launch)
+ROPE_FUSE = os.environ.get("GRAG_ROPE_FUSE", "1") != "0"
+
+
+def paged_decode_mw_rope(qkv, bias, positions, cos_sin, k_cache, v_cache, meta: AttnMetadata, scale: float,
+                         Hq: int, Hkv: int, D: int) -> torch.Tensor | None:
+    """Decode attention straight from the qkv projection's deferred split-K planes (ops/gemm.py SplitKPartial):
+    the kernel forms q with bias + NeoX RoPE in registers, folds the new token's key in from registers, and stores
+    the new K / V to meta.slot_mapping's slots -- what ops/elementwise.qkv_rope_kvstore + paged_attention do in
+    two launches (the small-kernel floor VERDICT r5 item 4 measured: RoPE 6.5 us of a B = 1 layer).  Returns
+    out [T, Hq * D], or None when the small-batch decode kernel would not take this step (the caller then runs
+    the two-launch path)."""
+    from .gemm import SplitKPartial
+
+    if not (ROPE_FUSE and isinstance(qkv, SplitKPartial) and qkv.device.type == "cuda" and cos_sin is not None
+            and meta.is_decode and meta.cascade is None and "decode_rows" not in meta.extra):
+        return None
+    BS = k_cache.shape[2]
+    nsplit = meta.num_splits
+    nw = meta.extra.get("decode_nw")
+    if nw is None and DECODE_MW_ROWS and meta.num_seqs * Hkv <= DECODE_MW_ROWS:
+        nw = DECODE_MW_CODE
+    if not (nw in DECODE_MW and D in (64, 128) and Hq // Hkv <= 16 and BS % 16 == 0 and qkv.N == (Hq + 2 * Hkv) * D
+            and (nsplit == 1 or meta.split_len % 32 == 0) and meta.num_seqs * Hkv <= (1 << 16)
+            and qkv.M == meta.num_tokens and meta.max_q_len == 1):
+        return None
+    out = torch.empty(qkv.M, Hq * D, dtype=qkv.dtype, device=qkv.device)
+    call("grag_paged_decode_mw_rope", ptr(qkv.planes), qkv.S, ptr(bias), ptr(positions), ptr(cos_sin),
+         ptr(meta.slot_mapping), ptr(k_cache), ptr(v_cache), ptr(out), out.stride(0), ptr(meta.block_tables),
+         meta.block_tables.stride(0), ptr(meta.q_start), ptr(meta.ctx_len), meta.num_seqs, qkv.M, Hq, Hkv, D, BS,
+         float(scale), nsplit, meta.split_len if nsplit > 1 else 0, ptr(meta.part_o) if nsplit > 1 else None,
+         ptr(meta.part_ml) if nsplit > 1 else None, ptr(decode_counters(qkv.device)), DECODE_MW[nw],
+         k_cache.shape[0], k_cache.shape[0] * BS, cos_sin.numel() // D)
+    return out
+
+
 def varlen_attention_ref(qkv, seq_start, H, D, scale, causal=False):
     T = qkv.shape[0]
     x = qkv.float().view(T, 3, H, D)
