@@ -137,6 +137,8 @@ def test_qwen2_decode_step_with_fused_rope(dev, monkeypatch):
     assert calls[:cfg.num_layers] == [True] * cfg.num_layers, calls
     h1, h2 = outs[True][0], outs[False][0]
     assert (h1 - h2).abs().max().item() <= 0.03 * h2.abs().max().item()
-    for (k1, v1), (k0, v0) in zip(outs[True][1], outs[False][1]):
-        torch.testing.assert_close(k1.float(), k0.float(), atol=3e-2, rtol=3e-2)
-        torch.testing.assert_close(v1.float(), v0.float(), atol=3e-2, rtol=3e-2)
+    # layer 0 stores the same K / V; later layers' inputs carry the attention's bf16-level differences
+    for li, ((k1, v1), (k0, v0)) in enumerate(zip(outs[True][1], outs[False][1])):
+        tol = 3e-2 if li == 0 else 1e-1
+        torch.testing.assert_close(k1.float(), k0.float(), atol=tol, rtol=3e-2)
+        torch.testing.assert_close(v1.float(), v0.float(), atol=tol, rtol=3e-2)
