@@ -36,7 +36,7 @@ __device__ __forceinline__ short f2bits(float f) {
 }
 
 // a += four consecutive floats of each of S fp32 split-K planes (plane stride `plane` elements), in plane order.
-// For S <= 16 the planes are walked in one fully unrolled, branch-free pass of 2, 4, 8 or 16 (indices past S re-read
+// For S <= 16 the planes are walked in one fully unrolled, branch-free pass of 2, 4, 8, 12 or 16 (indices past S re-read
 // plane 0 and add zero: fma(1, y, x) rounds as x + y), so every plane's load can be in flight together -- a
 // runtime-count loop under "#pragma unroll" runs its remainder iterations one plane per memory round trip.
 template <int MAXS>
@@ -51,12 +51,14 @@ __device__ __forceinline__ void plane_acc4_fixed(f32x4_t& a, const float* p, siz
   }
 }
 __device__ __forceinline__ void plane_acc4(f32x4_t& a, const float* p, size_t plane, int S) {
-  if (S <= 2) {  // (the pass length: the power of two >= S, so at most S - 1 wasted plane reads)
+  if (S <= 2) {  // (the pass length: the first of 2, 4, 8, 12, 16 >= S)
     plane_acc4_fixed<2>(a, p, plane, S);
   } else if (S <= 4) {
     plane_acc4_fixed<4>(a, p, plane, S);
   } else if (S <= 8) {
     plane_acc4_fixed<8>(a, p, plane, S);
+  } else if (S <= 12) {
+    plane_acc4_fixed<12>(a, p, plane, S);
   } else if (S <= 16) {
     plane_acc4_fixed<16>(a, p, plane, S);
   } else {
