@@ -726,8 +726,13 @@ def gemm_deferred(x: torch.Tensor, w: torch.Tensor, how: tuple[str, int, tuple])
     ws = WS.get(x.device, fl)
     if kind == "decode":
         mt, nwv, ntw, ksp, *rest = p
+        # the launcher gets the EFFECTIVE split count the planes were sized for (dec_ksplit of the plan's
+        # request): a raw request the 4-step rounding lowers (K = 3584, 28 -> 14) would write past the slab
+        ks = dec_ksplit(K, ksp)
+        fl = ks * M * N
+        ws = WS.get(x.device, fl)
         call("grag_gemm_decode_t", ptr(x), ptr(w), ptr(None), ptr(None), x.stride(0), w.stride(0), N,
-             M, N, K, EPI_PARTIAL, ACT_NONE, mt, nwv, ntw, ksp, rest[0] if rest else 0, 0,
+             M, N, K, EPI_PARTIAL, ACT_NONE, mt, nwv, ntw, ks, rest[0] if rest else 0, 0,
              rest[1] if len(rest) > 1 else 0, ptr(ws))
     else:
         call("grag_gemm_tile", ptr(x), ptr(w), ptr(None), ptr(None), x.stride(0), w.stride(0), N,

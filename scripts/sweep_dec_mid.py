@@ -54,9 +54,9 @@ def main():
             arms = {"current": base}
             if base is not None:
                 mt = base[0]
-                for nwv in (4, 5):
-                    for ks in (7, 14):
-                        if N % (16 * nwv * 2) == 0:
+                for nwv in (4, 5, 8):
+                    for ks in (7, 14, 28):
+                        if N % (16 * nwv * 2) == 0 and (mt, nwv, 2) in G.DEC_VARIANTS:
                             arms[f"mt{mt}_w{nwv}_ks{ks}"] = (mt, nwv, 2, ks)
             row = {}
             for arm, plan in arms.items():

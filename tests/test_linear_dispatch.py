@@ -188,3 +188,21 @@ def test_workspace_owned_by_engine_not_thread(monkeypatch):
     t.start()
     t.join()
     assert seen == [False, True]
+
+
+def test_deferred_decode_launch_gets_the_split_count_its_planes_were_sized_for(monkeypatch):
+    """gemm_deferred sizes the fp32 planes with dec_ksplit of the plan's K-split request and must launch the
+    kernel with that same count: a request the 4-step rounding lowers (K = 3584: 28 -> 14) once wrote 28 planes
+    into a 14-plane slab (a GPU fault in scripts/sweep_dec_mid.py)."""
+    seen = {}
+
+    def fake_call(name, *args):
+        seen["ks"] = args[15]  # (..., mt, nwv, ntw, ksplit, gs, ...) of grag_gemm_decode_t
+
+    monkeypatch.setattr(G, "call", fake_call)
+    monkeypatch.setattr(G.WS, "get", lambda dev, fl: torch.empty(fl))
+    x, w = torch.zeros(176, 3584, dtype=torch.bfloat16), torch.zeros(4608, 3584, dtype=torch.bfloat16)
+    for req in (7, 14, 28):
+        part = G.gemm_deferred(x, w, ("decode", G.dec_ksplit(3584, req), (12, 5, 2, req)))
+        assert seen["ks"] == part.S == G.dec_ksplit(3584, req)
+    assert G.dec_ksplit(3584, 28) == 14
